@@ -1,0 +1,252 @@
+"""Headline benchmark: ResNet-50 v2 training throughput on MI355X (BASELINE.json configs[1..2]).
+
+`python bench.py --gpus N --steps K --warmup W` (N>1 under torch.distributed.run, one rank per
+GPU, RCCL all-reduce). One step = forward(is_train) + backward + bucketed all-reduce + SGD
+update over one synthetic 224x224 batch of 256 images per GPU (data/imagenet.py:9-41 restated:
+seeded U(-1,1) data, random labels), bf16 activations/weights with fp32 master weights,
+gradients and BN statistics. Inputs are resident in HBM before the timed region.
+
+Rank 0 prints ONE JSON line (contract in the task statement), including
+  roofline     : the dominant kernel family (most time per step) -- algorithmic FLOP per launch
+                 / average launch duration from HIP events around every launch of that family
+                 inside the timed region, vs the dense bf16 MFMA peak (2.5 PFLOP/s)
+  cpu_baseline : the numpy oracle (oracle/, "port") timing a bounded sample of the same step
+                 on the host cores (rank 0, N=1 only)
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+for _p in (REPO, os.path.join(REPO, "resnet.mxnet_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "images/sec/GPU ResNet-50 224px bf16 bs256; 1→8 GPU scaling"
+PEAK_BF16_TFLOPS = 2500.0
+
+
+def conv_call_flops(name, args):
+    """Algorithmic FLOP (2/MAC) of one rn_conv_* call from its descriptor."""
+    d = args[0]._obj
+    cin = d.c_real
+    macs_fwd = d.n * d.p * d.q * d.k * cin * d.r * d.s
+    return 2 * macs_fwd
+
+
+def family_of(ex, name, args):
+    if name == "rn_conv_bwd_filter":
+        return "wgrad_kernel<bf16,128,128>" if ex.dtype == 0 else "wgrad_kernel<f32,128,128>"
+    if name in ("rn_conv_fwd", "rn_conv_bwd_data"):
+        d = args[0]._obj
+        ncol = d.k if name == "rn_conv_fwd" else d.c
+        out_f32 = name == "rn_conv_fwd" and args[4] == 1 and ex.dtype == 0
+        tile = "128x64" if ncol <= 64 else "128x128"
+        return "igemm_kernel<bf16,%s,%s>" % ("f32" if out_f32 else "bf16", tile)
+    return None
+
+
+class FamilyTimer:
+    """HIP events around every launch of one kernel family on the executor's stream."""
+
+    def __init__(self, torch, ex, family):
+        self.torch, self.ex, self.family = torch, ex, family
+        self.idx = []
+        self.flops = 0
+        for lst_name in ("_fwd_train", "_bwd"):
+            lst = getattr(ex, lst_name)
+            for i, (name, fn, args) in enumerate(lst):
+                if family_of(ex, name, args) == family:
+                    self.idx.append((lst_name, i))
+                    self.flops += conv_call_flops(name, args)
+        self.events = []
+
+    def wrap(self):
+        torch = self.torch
+        self._saved = {}
+        for lst_name, i in self.idx:
+            lst = getattr(self.ex, lst_name)
+            name, fn, args = lst[i]
+            self._saved[(lst_name, i)] = lst[i]
+
+            def timed(*a, _fn=fn):
+                s = torch.cuda.Event(enable_timing=True)
+                e = torch.cuda.Event(enable_timing=True)
+                s.record(self.ex.stream)
+                r = _fn(*a)
+                e.record(self.ex.stream)
+                self.events.append((s, e))
+                return r
+
+            lst[i] = (name, timed, args)
+
+    def unwrap(self):
+        for (lst_name, i), v in self._saved.items():
+            getattr(self.ex, lst_name)[i] = v
+
+    def result(self):
+        ms = [s.elapsed_time(e) for s, e in self.events]
+        return sum(ms), len(ms)
+
+
+def calibrate_families(torch, ex, mod):
+    """Time every MFMA-kernel launch of one step; return {family: (ms, launches, flops)}."""
+    fams = {}
+    for lst_name in ("_fwd_train", "_bwd"):
+        for name, fn, args in getattr(ex, lst_name):
+            f = family_of(ex, name, args)
+            if f and f not in fams:
+                fams[f] = FamilyTimer(torch, ex, f)
+    for t in fams.values():
+        t.wrap()
+    mod.forward(None, is_train=True)
+    mod.backward()
+    mod.update()
+    torch.cuda.synchronize()
+    out = {}
+    for f, t in fams.items():
+        ms, n = t.result()
+        out[f] = (ms, n, t.flops)
+        t.unwrap()
+    return out
+
+
+def cpu_baseline(batch=8, steps=2, image=224):
+    """Time the numpy oracle (fp32) on a bounded sample of the same training step."""
+    import numpy as np
+    from oracle import net as onet
+    g = onet.resnet50_imagenet()
+    args, aux = onet.init_params(g, dtype=np.float32)
+    moms = {k: np.zeros_like(v) for k, v in args.items()}
+    data, label = onet.synthetic_batch(batch, (3, image, image), 1000, dtype=np.float32)
+    onet.train_step(g, args, aux, moms, data, label, 0.1)  # warm-up (allocations, BLAS threads)
+    t0 = time.time()
+    for _ in range(steps):
+        onet.train_step(g, args, aux, moms, data, label, 0.1)
+    dt = time.time() - t0
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    return {"value": round(batch * steps / dt, 3), "unit": "images/sec", "cores": cores, "kind": "port",
+            "sample": "numpy fp32 oracle ResNet-50 v2 train step (fwd+bwd+SGD), batch %d at %dx%d, %d timed steps "
+                      "after 1 warm-up (%.1f s)" % (batch, image, image, steps, dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--image", type=int, default=224)
+    ap.add_argument("--precision", default="bfloat16")
+    ap.add_argument("--bucket-mb", type=float, default=25.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=8)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    a = ap.parse_args()
+
+    import numpy as np
+    import torch
+    from rn import dist as rdist
+    from rn import graphs
+    import mxnet as mx
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        rdist.init_from_env("nccl")
+    import torch.distributed as dist
+
+    sym = graphs.resnet50()
+    mod = mx.mod.Module(sym, context=[mx.gpu(local)], precision=a.precision)
+    shp = (a.batch, 3, a.image, a.image)
+    mod.bind(data_shapes=[("data", shp)], label_shapes=[("softmax_label", (a.batch,))], for_training=True)
+    mx.random.seed(2)
+    mod.init_params(mx.init.Xavier(rnd_type="gaussian", factor_type="in", magnitude=2))
+    mod.init_optimizer(kvstore="dist_sync_device" if world > 1 else "device", optimizer="sgd",
+                       optimizer_params={"learning_rate": 0.1, "wd": 1e-4, "momentum": 0.9,
+                                         "multi_precision": True})
+    ex = mod.executor
+    ex.bucket_bytes = int(a.bucket_mb * (1 << 20))
+    if mod._reducer is not None:
+        from rn.dist import BucketAllReducer
+        mod._reducer = BucketAllReducer(ex.grad, ex.buckets())
+    data = np.random.default_rng(0 + rank).uniform(-1, 1, shp).astype(np.float32)
+    label = np.random.default_rng(1 + rank).integers(0, 1000, (a.batch,)).astype(np.float32)
+    batch = mx.io.DataBatch(data=[mx.nd.array(data)], label=[mx.nd.array(label)])
+    mod.forward(batch, is_train=True)  # H2D once: inputs resident from here on
+    torch.cuda.synchronize()
+
+    def step():
+        mod.forward(None, is_train=True)
+        mod.backward()
+        mod.update()
+
+    for _ in range(max(a.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    fams = calibrate_families(torch, ex, mod)
+    dom = max(fams, key=lambda f: fams[f][0])
+    timer = FamilyTimer(torch, ex, dom)
+    timer.wrap()
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    timer.unwrap()
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    fam_ms, fam_n = timer.result()
+    prob = mod.get_outputs()[0].asnumpy()
+    finite = bool(np.isfinite(prob).all())
+
+    if rank == 0:
+        imgs = a.batch * world * a.steps
+        value = imgs / elapsed
+        ms_step = elapsed / a.steps * 1e3
+        flops_step = ex.plan.train_flops()
+        per_launch_flops = timer.flops / max(1, len(timer.idx))
+        avg_ms = fam_ms / max(fam_n, 1)
+        achieved = per_launch_flops / (avg_ms * 1e-3) / 1e12
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "images/sec", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if a.precision.startswith("bf") else "fp32",
+            "data": "synthetic (seeded U(-1,1) 224x224 images, random labels; Xavier-init ResNet-50 v2)",
+            "config": {"workload": "ResNet-50 v2 (symbol/resnet.py) train step, batch %d/GPU, %dx%d" % (
+                a.batch, a.image, a.image), "model": "resnet50_v2", "global_batch": a.batch * world,
+                "seq_len": None, "parallelism": "dp%d" % world, "per_gpu_images_per_sec": round(value / world, 2)},
+            "roofline": {"bound": "mfma", "kernel": dom, "launches_per_step": len(timer.idx),
+                         "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                         "avg_launch_ms": round(avg_ms, 4),
+                         "step_tflops": round(flops_step / (ms_step * 1e-3) / 1e12, 2),
+                         "step_frac": round(flops_step / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+                         "families_ms_per_step": {f: round(v[0], 3) for f, v in fams.items()}},
+            "outputs_finite": finite,
+        }
+        if world == 1 and not a.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(a.cpu_batch, a.cpu_steps)
+            except Exception as e:  # baseline must not hide the GPU number
+                out["cpu_baseline"] = {"error": repr(e)}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

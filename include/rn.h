@@ -1,0 +1,224 @@
+/*
+ * rn.h -- C-ABI of the MI355X-native ResNet/ResNeXt training runtime (librn.so).
+ *
+ * This is the drop-in boundary that replaces the MXNet runtime (libmxnet.so of the
+ * huangzehao/incubator-mxnet-bk fork) underneath the reference's Python training harness.
+ * The reference never calls a C API directly: every op below replaces what MXNet ran for
+ * one `mx.sym.<Op>` node of the reference graphs (symbol/resnet.py, symbol/resnext.py,
+ * symbol/resnet_int8.py) when core/solver.py drove Module.forward / backward / update.
+ * The `mxnet` shim shipped in resnet.mxnet_amd/mxnet binds these entry points with ctypes
+ * (resnet.mxnet_amd/rn/lib.py); INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *  - Every entry returns 0 on success and -1 on failure; rn_last_error() returns the
+ *    thread-local message (mirrors MXNet's `-1` + MXGetLastError C-API convention).
+ *  - No entry point allocates device memory or synchronises: all work is enqueued on the
+ *    caller's HIP stream (`rn_stream_t` = hipStream_t), so a caller may capture it in a graph.
+ *  - Activations are NHWC ("rows" = N*H*W pixels, channel-contiguous) with the channel
+ *    stride padded to a multiple of 8 elements; weights are KRSC (fwd) / CRSK (dgrad).
+ *  - dtype: RN_BF16 (bf16 storage, fp32 accumulate) or RN_F32 (exact fp32 MFMA path,
+ *    used for parity runs). Parameters, gradients, BN statistics are always fp32.
+ */
+#ifndef RN_H_
+#define RN_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* rn_stream_t; /* hipStream_t */
+
+enum rn_dtype { RN_BF16 = 0, RN_F32 = 1 };
+
+/* ---------------------------------------------------------------------------------------
+ * Convolution / FullyConnected (implicit GEMM on MFMA).
+ * Replaces mx.sym.Convolution (symbol/resnet.py:14-31,93; symbol/resnext.py:17-38,83) and
+ * mx.sym.FullyConnected (symbol/resnet.py:115) = a 1x1 convolution over a 1x1 image.
+ * ------------------------------------------------------------------------------------- */
+typedef struct rn_conv_desc {
+  int32_t dtype;                  /* rn_dtype of x, w (compute copy), y                     */
+  int32_t n, h, w;                /* input batch and spatial size                             */
+  int32_t c;                      /* input channel STRIDE (multiple of 8)                     */
+  int32_t c_real;                 /* logical input channels (<= c)                            */
+  int32_t k;                      /* output channels (num_filter / num_hidden)                */
+  int32_t k_pad;                  /* output channel stride (multiple of 8, >= k)              */
+  int32_t r, s;                   /* kernel height, width                                     */
+  int32_t stride_h, stride_w;
+  int32_t pad_h, pad_w;
+  int32_t groups;                 /* num_group (ResNeXt grouped conv)                         */
+  int32_t p, q;                   /* output spatial size, filled by rn_conv_desc_init         */
+} rn_conv_desc;
+
+/* Validate and fill p, q (MXNet 'valid' convention: p = (h + 2*pad - r)/stride + 1). */
+int rn_conv_desc_init(rn_conv_desc* d);
+
+/* y[n,p,q,k] = sum_{r,s,c} x[n,p*sh-ph+r,q*sw-pw+s,c] * w[k,r,s,c] (+ bias[k]) (+ add_src)
+ * w: compute copy, KRSC, channel stride c. y_dtype lets the FC head write fp32 logits.
+ * add_src (may alias y, or NULL) implements the residual `conv3 + shortcut` and req='add'. */
+int rn_conv_fwd(const rn_conv_desc* d, const void* x, const void* w_krsc, void* y, int32_t y_dtype,
+                const void* add_src, const float* bias, rn_stream_t stream);
+
+/* dx = conv_transpose(dy, w) (+ add_src). w_crsk is the CRSK re-layout made by
+ * rn_conv_weight_pack (row count c, K stride k_pad). */
+int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
+                     const void* add_src, rn_stream_t stream);
+
+/* dw_krsc (fp32, KRSC with channel stride c_real... see rn_conv_weight_numel) += x^T * dy.
+ * Accumulates with fp32 atomics: the caller zeroes dw once per step. */
+int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, float* dw,
+                       rn_stream_t stream);
+
+/* Number of fp32 elements of the master weight (K x R x S x c_real/groups, KRSC). */
+int64_t rn_conv_weight_numel(const rn_conv_desc* d);
+
+/* From the fp32 KRSC master weight, write the compute copies: w_krsc (dtype, channel stride
+ * c) and w_crsk (dtype, c rows, K stride k_pad). Either output may be NULL. */
+int rn_conv_weight_pack(const rn_conv_desc* d, const float* w_master, void* w_krsc, void* w_crsk,
+                        rn_stream_t stream);
+
+/* Stem: explicit im2col of an NCHW fp32 image (the `data` input, train.py:70-73) with an
+ * optional per-channel affine (bn_data, symbol/resnet.py:90) into cols[m][kc] (dtype),
+ * kc = round_up(r*s*c_real, 32). conv0 then runs as a 1x1 conv over cols. */
+int rn_im2col_nchw(const rn_conv_desc* d, const float* x_nchw, const float* scale,
+                   const float* shift, void* cols, int32_t kc, rn_stream_t stream);
+
+/* d(beta) of a BN feeding the stem conv, without the stem dgrad:
+ * dbeta[c] += sum_{k,r,s} w[k,r,s,c] * sum_{n,p,q valid(r,s)} dy[n,p,q,k].
+ * ws: float workspace of p*q*k_pad + k*r*s elements. */
+int rn_stem_shift_grad(const rn_conv_desc* d, const void* dy, const float* w_master, float* dbeta,
+                       float* ws, rn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * BatchNorm (+ fused ReLU) -- replaces mx.sym.BatchNorm + mx.sym.Activation('relu')
+ * (symbol/resnet.py:12-23,90-96,111-112).
+ * ------------------------------------------------------------------------------------- */
+typedef struct rn_bn_desc {
+  int32_t dtype;     /* dtype of x / y / dy / dx                              */
+  int64_t m;         /* rows = N*H*W                                          */
+  int32_t c;         /* channel stride (multiple of 8)                        */
+  int32_t c_real;    /* channels that carry parameters                        */
+  float eps;
+  float momentum;    /* moving = moving*momentum + batch*(1-momentum)         */
+  int32_t fix_gamma; /* gamma := 1, dgamma := 0                                */
+  int32_t relu;      /* fuse Activation(relu) on the output                   */
+} rn_bn_desc;
+
+/* Workspace (bytes) needed by rn_bn_fwd_train / rn_bn_bwd. */
+int64_t rn_bn_workspace_bytes(const rn_bn_desc* d);
+
+/* Training forward: batch stats (biased variance), moving-stat update, y = act(x*scale+shift).
+ * save_mean/save_invstd/scale/shift are fp32 [c_real] outputs kept for backward.
+ * y may be NULL (stats only). */
+int rn_bn_fwd_train(const rn_bn_desc* d, const void* x, void* y, const float* gamma,
+                    const float* beta, float* moving_mean, float* moving_var, float* save_mean,
+                    float* save_invstd, float* scale, float* shift, void* ws, rn_stream_t stream);
+
+/* Inference forward with moving statistics (use_global_stats / is_train=False). */
+int rn_bn_fwd_infer(const rn_bn_desc* d, const void* x, void* y, const float* gamma,
+                    const float* beta, const float* moving_mean, const float* moving_var,
+                    float* scale, float* shift, rn_stream_t stream);
+
+/* Apply y = act(x*scale + shift) with precomputed per-channel scale/shift. */
+int rn_bn_apply(const rn_bn_desc* d, const void* x, void* y, const float* scale,
+                const float* shift, rn_stream_t stream);
+
+/* Backward through [relu o] BN: dz = relu ? dy*(x*scale+shift > 0) : dy,
+ * dgamma = sum(dz*xhat) (0 if fix_gamma), dbeta = sum(dz),
+ * dx = gamma*invstd*(dz - mean(dz) - xhat*mean(dz*xhat)) (+ add_src). dgamma/dbeta written. */
+int rn_bn_bwd(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const void* add_src,
+              const float* gamma, const float* save_mean, const float* save_invstd,
+              const float* scale, const float* shift, float* dgamma, float* dbeta, void* ws,
+              rn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Pooling -- mx.sym.Pooling (symbol/resnet.py:97 max 3x3/s2/p1; :113 global avg).
+ * ------------------------------------------------------------------------------------- */
+enum rn_pool_type { RN_POOL_MAX = 0, RN_POOL_AVG = 1 };
+typedef struct rn_pool_desc {
+  int32_t dtype;
+  int32_t n, h, w, c;   /* c = channel stride */
+  int32_t r, s, stride_h, stride_w, pad_h, pad_w;
+  int32_t type;         /* rn_pool_type */
+  int32_t global_pool;  /* ignores r/s/stride/pad like MXNet */
+  int32_t p, q;         /* filled by rn_pool_desc_init */
+} rn_pool_desc;
+int rn_pool_desc_init(rn_pool_desc* d);
+/* argmax: uint8 tap index per output element (max pool only; may be NULL for avg). */
+int rn_pool_fwd(const rn_pool_desc* d, const void* x, void* y, uint8_t* argmax, rn_stream_t stream);
+int rn_pool_bwd(const rn_pool_desc* d, const void* dy, const uint8_t* argmax, void* dx,
+                const void* add_src, rn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * SoftmaxOutput -- mx.sym.SoftmaxOutput (symbol/resnet.py:118-120): forward = probabilities,
+ * backward = grad_scale*(p - onehot(label)) with normalization 'null'. Also accumulates
+ * stats[0] += sum CE loss, stats[1] += top-1 hits, stats[2] += top-5 hits (device side,
+ * so the metric does not force a host sync every step).
+ * ------------------------------------------------------------------------------------- */
+int rn_softmax_output(int32_t grad_dtype, int32_t batch, int32_t ncls, int32_t ld,
+                      const float* logits, const float* label, float* prob, void* dlogits,
+                      float grad_scale, float* stats, rn_stream_t stream);
+
+/* out[j] (=|+=) sum_i x[i*ld + j], j < c  (FullyConnected bias gradient). */
+int rn_col_sum(int32_t dtype, int64_t m, int32_t c, int32_t ld, const void* x, float* out,
+               int32_t accumulate, rn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Optimizer -- MXNet SGD momentum (train.py:186-194, core/solver.py:80-82):
+ *   g = rescale_grad*grad (clipped if clip > 0);  mom = momentum*mom - lr*(g + wd*w);  w += mom
+ * over a flat fp32 parameter buffer described by a per-tensor table in device memory
+ * (offset, numel, wd). lr may be taken from a device scalar (lr_dev != NULL) so that a
+ * captured graph can replay with a schedule.  w_lowp (optional, dtype lowp_dtype) receives
+ * the updated weights in the compute precision.
+ * ------------------------------------------------------------------------------------- */
+int rn_sgd_mom_update(int32_t ntensors, const int64_t* offsets, const int64_t* numels,
+                      const float* wds, float* w, const float* g, float* mom, void* w_lowp,
+                      int32_t lowp_dtype, float lr, const float* lr_dev, float momentum,
+                      float rescale_grad, float clip, rn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Data movement helpers.
+ * ------------------------------------------------------------------------------------- */
+/* NCHW fp32 -> NHWC dtype with channel stride c_pad (zero padding). */
+int rn_nchw_to_nhwc(int32_t n, int32_t c, int32_t h, int32_t w, int32_t c_pad, const float* src,
+                    void* dst, int32_t dst_dtype, rn_stream_t stream);
+/* Element-wise cast between fp32 and bf16 (n elements). */
+int rn_cast(int64_t n, const void* src, int32_t src_dtype, void* dst, int32_t dst_dtype,
+            rn_stream_t stream);
+/* dst = act(a + b) (b may be NULL: dst = act(a)); act = relu if relu != 0. Residual
+ * `bn3 + shortcut` (+ Activation) of the post-activation graphs (symbol/resnext.py:45-46,
+ * symbol/resnet.py:70-74) and the unfused elementwise add. dst may alias a or b. */
+int rn_eltwise_add(int64_t n, int32_t dtype, const void* a, const void* b, void* dst, int32_t relu,
+                   rn_stream_t stream);
+/* dx = dy * (y > 0) (+ add_src): Activation('relu') backward from its output. */
+int rn_relu_bwd(int64_t n, int32_t dtype, const void* y, const void* dy, void* dx,
+                const void* add_src, rn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Int8 fake quantization -- mx.sym.contrib.Quantization_int8 (symbol/int8_api.py:133-136),
+ * semantics from symbol/quant_ops.py:12-42 / clip_grad_quantization_int8.py:14-67.
+ * ------------------------------------------------------------------------------------- */
+/* out = round(clip(x, -t, t) / (t/qmax)) * (t/qmax) with t = max|x| (weights) or the EMA
+ * minmax state (activations, updated in place when is_train). ws: >= 4096 floats. */
+int rn_quant_int8_fwd(int32_t dtype, int64_t n, const void* x, void* out, float* minmax,
+                      int32_t is_weight, int32_t is_train, float ema_decay, int32_t first_batch,
+                      int32_t nbits, float* ws, rn_stream_t stream);
+/* STE backward: dx = dy (weights) or dy * (|x| <= t) (activations). */
+int rn_quant_int8_bwd(int32_t dtype, int64_t n, const void* x, const void* dy, void* dx,
+                      const float* minmax, int32_t is_weight, const void* add_src,
+                      rn_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Runtime.
+ * ------------------------------------------------------------------------------------- */
+const char* rn_last_error(void);
+int32_t rn_version(void);
+/* Number of compute units of the current device (for split heuristics / reporting). */
+int32_t rn_device_cu_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RN_H_ */

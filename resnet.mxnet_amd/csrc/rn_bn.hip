@@ -1,0 +1,431 @@
+// rn_bn.hip -- BatchNorm (+ fused ReLU) forward / backward on NHWC activations.
+//
+// Replaces mx.sym.BatchNorm followed by mx.sym.Activation(act_type='relu') of the reference
+// graphs (symbol/resnet.py:12-23,90-96,111-112; symbol/resnext.py:20-46). Training semantics
+// (MXNet 1.x, restated in oracle/ops.py): batch mean / biased variance over N*H*W,
+// moving = moving*momentum + batch*(1-momentum), fix_gamma => gamma := 1 and dgamma := 0.
+//
+// HBM-bound: every pass reads each element once with 16-byte (8 x bf16) loads.
+//  fwd : stats pass (per-block shifted sums) -> finalize (fp64 combine) -> apply(+relu) pass
+//  bwd : reduce pass (sum dz, sum dz*(x-mean)) -> finalize -> apply pass (+ optional add_src)
+// Workspace layout (floats): partials[nrb][c][2] | coef[c][4]
+#include <algorithm>
+
+#include "rn_common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+struct Geo {
+  int cpr;   // chunks per row
+  int ct;    // chunk lanes per block (divides cpr or == cpr)
+  int rl;    // row lanes per block
+  int gx;    // blocks along channels
+  int nrb;   // blocks along rows
+  int64_t rows_per_block;
+};
+
+template <typename T>
+Geo make_geo(int64_t m, int c) {
+  Geo g;
+  const int CE = 16 / sizeof(T);
+  g.cpr = c / CE;
+  g.ct = std::min(g.cpr, 32);
+  while (g.cpr % g.ct) --g.ct;
+  g.rl = kThreads / g.ct;
+  g.gx = g.cpr / g.ct;
+  int64_t want = std::max<int64_t>(1, 2048 / g.gx);
+  int64_t maxrb = std::max<int64_t>(1, m / (g.rl * 4));
+  g.nrb = (int)std::min(want, maxrb);
+  g.rows_per_block = ceil_div(m, g.nrb);
+  return g;
+}
+
+__device__ __forceinline__ float relu_mask(float x, float sc, float sh) { return fmaf(x, sc, sh) > 0.f ? 1.f : 0.f; }
+
+// ---- forward stats: partial shifted sums; pivot = x[0][c]
+template <typename T>
+__global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, int64_t m, int c, int ct,
+                                                       int64_t rows_per_block, float* __restrict__ part) {
+  constexpr int CE = 16 / sizeof(T);
+  const int tc = threadIdx.x % ct, tr = threadIdx.x / ct, rl = blockDim.x / ct;
+  const int cbase = (blockIdx.x * ct + tc) * CE;
+  const int64_t r0 = blockIdx.y * rows_per_block;
+  const int64_t r1 = min(m, r0 + rows_per_block);
+  float piv[CE], s[CE], q[CE];
+  {
+    uint4 u = *reinterpret_cast<const uint4*>(x + cbase);
+    chunk_to_f(u, piv, (const T*)nullptr);
+  }
+#pragma unroll
+  for (int e = 0; e < CE; ++e) s[e] = q[e] = 0.f;
+  for (int64_t r = r0 + tr; r < r1; r += rl) {
+    uint4 u = *reinterpret_cast<const uint4*>(x + r * c + cbase);
+    float f[CE];
+    chunk_to_f(u, f, (const T*)nullptr);
+#pragma unroll
+    for (int e = 0; e < CE; ++e) {
+      const float d = f[e] - piv[e];
+      s[e] += d;
+      q[e] = fmaf(d, d, q[e]);
+    }
+  }
+  __shared__ float red[kThreads * 8 * 2];
+#pragma unroll
+  for (int e = 0; e < CE; ++e) {
+    red[(tr * ct + tc) * CE * 2 + 2 * e] = s[e];
+    red[(tr * ct + tc) * CE * 2 + 2 * e + 1] = q[e];
+  }
+  __syncthreads();
+  // reduce over row lanes: thread t < ct*CE*2 sums column t
+  const int ncol = ct * CE * 2;
+  for (int col = threadIdx.x; col < ncol; col += blockDim.x) {
+    float acc = 0.f;
+    for (int r = 0; r < rl; ++r) acc += red[r * ncol + col];
+    const int cc = blockIdx.x * ct * CE + col / 2;
+    part[((int64_t)blockIdx.y * c + cc) * 2 + (col & 1)] = acc;
+  }
+}
+
+// finalize: one thread group per channel; 4 lanes per channel reduce the partials.
+template <typename T>
+__global__ void bn_fwd_finalize_kernel(const T* __restrict__ x, const float* __restrict__ part, int nrb,
+                                       int64_t m, int c, int c_real, float eps, float momentum,
+                                       int fix_gamma, const float* __restrict__ gamma,
+                                       const float* __restrict__ beta, float* moving_mean,
+                                       float* moving_var, float* save_mean, float* save_invstd,
+                                       float* scale, float* shift) {
+  const int ch = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lane4 = threadIdx.x >> 6;  // 0..3
+  double s = 0.0, q = 0.0;
+  if (ch < c)
+    for (int b = lane4; b < nrb; b += 4) {
+      s += part[((int64_t)b * c + ch) * 2];
+      q += part[((int64_t)b * c + ch) * 2 + 1];
+    }
+  __shared__ double rs[256], rq[256];
+  rs[threadIdx.x] = s;
+  rq[threadIdx.x] = q;
+  __syncthreads();
+  if (lane4 != 0 || ch >= c) return;
+  s = rs[threadIdx.x] + rs[threadIdx.x + 64] + rs[threadIdx.x + 128] + rs[threadIdx.x + 192];
+  q = rq[threadIdx.x] + rq[threadIdx.x + 64] + rq[threadIdx.x + 128] + rq[threadIdx.x + 192];
+  if (ch >= c_real) {
+    scale[ch] = 0.f;
+    shift[ch] = 0.f;
+    return;
+  }
+  const double piv = (double)to_f(x[ch]);
+  const double md = s / (double)m;
+  const double mean = piv + md;
+  double var = q / (double)m - md * md;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = fix_gamma ? 1.f : gamma[ch];
+  const float sc = g * invstd;
+  scale[ch] = sc;
+  shift[ch] = beta[ch] - (float)mean * sc;
+  save_mean[ch] = (float)mean;
+  save_invstd[ch] = invstd;
+  if (moving_mean) {
+    moving_mean[ch] = moving_mean[ch] * momentum + (float)mean * (1.f - momentum);
+    moving_var[ch] = moving_var[ch] * momentum + (float)var * (1.f - momentum);
+  }
+}
+
+__global__ void bn_infer_coef_kernel(int c, int c_real, float eps, int fix_gamma, const float* gamma,
+                                     const float* beta, const float* mm, const float* mv, float* scale,
+                                     float* shift) {
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= c) return;
+  if (ch >= c_real) {
+    scale[ch] = 0.f;
+    shift[ch] = 0.f;
+    return;
+  }
+  const float invstd = 1.f / sqrtf(mv[ch] + eps);
+  const float g = fix_gamma ? 1.f : gamma[ch];
+  scale[ch] = g * invstd;
+  shift[ch] = beta[ch] - mm[ch] * g * invstd;
+}
+
+template <typename T, bool RELU>
+__global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x, T* __restrict__ y,
+                                                       const float* __restrict__ scale,
+                                                       const float* __restrict__ shift, int64_t nchunk,
+                                                       int cpr) {
+  constexpr int CE = 16 / sizeof(T);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nchunk;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int cb = (int)(i % cpr) * CE;
+    uint4 u = reinterpret_cast<const uint4*>(x)[i];
+    float f[CE];
+    chunk_to_f(u, f, (const T*)nullptr);
+#pragma unroll
+    for (int e = 0; e < CE; ++e) {
+      float v = fmaf(f[e], scale[cb + e], shift[cb + e]);
+      f[e] = RELU ? fmaxf(v, 0.f) : v;
+    }
+    reinterpret_cast<uint4*>(y)[i] = f_to_chunk(f, (const T*)nullptr);
+  }
+}
+
+// ---- backward reduce: sum dz, sum dz*(x - mean)
+template <typename T, bool RELU>
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                            int64_t m, int c, int ct, int64_t rows_per_block,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift,
+                                                            float* __restrict__ part) {
+  constexpr int CE = 16 / sizeof(T);
+  const int tc = threadIdx.x % ct, tr = threadIdx.x / ct, rl = blockDim.x / ct;
+  const int cbase = (blockIdx.x * ct + tc) * CE;
+  const int64_t r0 = blockIdx.y * rows_per_block;
+  const int64_t r1 = min(m, r0 + rows_per_block);
+  float mu[CE], sc[CE], sh[CE], s[CE], q[CE];
+#pragma unroll
+  for (int e = 0; e < CE; ++e) {
+    mu[e] = mean[cbase + e];
+    sc[e] = scale[cbase + e];
+    sh[e] = shift[cbase + e];
+    s[e] = q[e] = 0.f;
+  }
+  for (int64_t r = r0 + tr; r < r1; r += rl) {
+    uint4 ux = *reinterpret_cast<const uint4*>(x + r * c + cbase);
+    uint4 ud = *reinterpret_cast<const uint4*>(dy + r * c + cbase);
+    float fx[CE], fd[CE];
+    chunk_to_f(ux, fx, (const T*)nullptr);
+    chunk_to_f(ud, fd, (const T*)nullptr);
+#pragma unroll
+    for (int e = 0; e < CE; ++e) {
+      const float dz = RELU ? fd[e] * relu_mask(fx[e], sc[e], sh[e]) : fd[e];
+      s[e] += dz;
+      q[e] = fmaf(dz, fx[e] - mu[e], q[e]);
+    }
+  }
+  __shared__ float red[kThreads * 8 * 2];
+#pragma unroll
+  for (int e = 0; e < CE; ++e) {
+    red[(tr * ct + tc) * CE * 2 + 2 * e] = s[e];
+    red[(tr * ct + tc) * CE * 2 + 2 * e + 1] = q[e];
+  }
+  __syncthreads();
+  const int ncol = ct * CE * 2;
+  for (int col = threadIdx.x; col < ncol; col += blockDim.x) {
+    float acc = 0.f;
+    for (int r = 0; r < rl; ++r) acc += red[r * ncol + col];
+    const int cc = blockIdx.x * ct * CE + col / 2;
+    part[((int64_t)blockIdx.y * c + cc) * 2 + (col & 1)] = acc;
+  }
+}
+
+// coef[c] = {A = g*invstd, mdz = sum dz / m, A2 = g*invstd^2*sum(dz*xhat)/m... , mean}
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int64_t m, int c,
+                                       int c_real, int fix_gamma, const float* __restrict__ gamma,
+                                       const float* __restrict__ save_mean,
+                                       const float* __restrict__ save_invstd, float* dgamma,
+                                       float* dbeta, float* __restrict__ coef) {
+  const int ch = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int lane4 = threadIdx.x >> 6;
+  double s = 0.0, q = 0.0;
+  if (ch < c)
+    for (int b = lane4; b < nrb; b += 4) {
+      s += part[((int64_t)b * c + ch) * 2];
+      q += part[((int64_t)b * c + ch) * 2 + 1];
+    }
+  __shared__ double rs[256], rq[256];
+  rs[threadIdx.x] = s;
+  rq[threadIdx.x] = q;
+  __syncthreads();
+  if (lane4 != 0 || ch >= c) return;
+  s = rs[threadIdx.x] + rs[threadIdx.x + 64] + rs[threadIdx.x + 128] + rs[threadIdx.x + 192];
+  q = rq[threadIdx.x] + rq[threadIdx.x + 64] + rq[threadIdx.x + 128] + rq[threadIdx.x + 192];
+  if (ch >= c_real) {
+    coef[ch * 4 + 0] = 0.f;
+    coef[ch * 4 + 1] = 0.f;
+    coef[ch * 4 + 2] = 0.f;
+    coef[ch * 4 + 3] = 0.f;
+    return;
+  }
+  const double invstd = save_invstd[ch];
+  const double g = fix_gamma ? 1.0 : (double)gamma[ch];
+  const double dg_raw = q * invstd;  // sum dz * xhat
+  if (dbeta) dbeta[ch] = (float)s;
+  if (dgamma) dgamma[ch] = fix_gamma ? 0.f : (float)dg_raw;
+  coef[ch * 4 + 0] = (float)(g * invstd);
+  coef[ch * 4 + 1] = (float)(s / (double)m);
+  coef[ch * 4 + 2] = (float)(g * invstd * invstd * dg_raw / (double)m);
+  coef[ch * 4 + 3] = save_mean[ch];
+}
+
+template <typename T, bool RELU>
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
+                                                           T* __restrict__ dx, const T* __restrict__ add,
+                                                           const float* __restrict__ coef,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift, int64_t nchunk,
+                                                           int cpr) {
+  constexpr int CE = 16 / sizeof(T);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nchunk;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int cb = (int)(i % cpr) * CE;
+    float fx[CE], fd[CE], fa[CE];
+    chunk_to_f(reinterpret_cast<const uint4*>(x)[i], fx, (const T*)nullptr);
+    chunk_to_f(reinterpret_cast<const uint4*>(dy)[i], fd, (const T*)nullptr);
+    if (add) chunk_to_f(reinterpret_cast<const uint4*>(add)[i], fa, (const T*)nullptr);
+#pragma unroll
+    for (int e = 0; e < CE; ++e) {
+      const int ch = cb + e;
+      const float4 cf = reinterpret_cast<const float4*>(coef)[ch];
+      const float dz = RELU ? fd[e] * relu_mask(fx[e], scale[ch], shift[ch]) : fd[e];
+      float v = cf.x * (dz - cf.y) - cf.z * (fx[e] - cf.w);
+      if (add) v += fa[e];
+      fd[e] = v;
+    }
+    reinterpret_cast<uint4*>(dx)[i] = f_to_chunk(fd, (const T*)nullptr);
+  }
+}
+
+int apply_grid(int64_t nchunk) {
+  int64_t g = (nchunk + 255) / 256;
+  return (int)std::min<int64_t>(std::max<int64_t>(g, 1), 256 * 16);
+}
+
+template <typename T>
+int bn_fwd_train_t(const rn_bn_desc* d, const void* x, void* y, const float* gamma, const float* beta,
+                   float* mm, float* mv, float* smean, float* sinv, float* scale, float* shift, void* ws,
+                   hipStream_t st) {
+  Geo g = make_geo<T>(d->m, d->c);
+  float* part = reinterpret_cast<float*>(ws);
+  hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(g.gx, g.nrb), dim3(kThreads), 0, st, (const T*)x, d->m,
+                     d->c, g.ct, g.rows_per_block, part);
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel<T>, dim3((d->c + 63) / 64), dim3(256), 0, st, (const T*)x, part,
+                     g.nrb, d->m, d->c, d->c_real, d->eps, d->momentum, d->fix_gamma, gamma, beta, mm, mv,
+                     smean, sinv, scale, shift);
+  if (y) {
+    const int CE = 16 / sizeof(T);
+    const int64_t nchunk = d->m * d->c / CE;
+    if (d->relu)
+      hipLaunchKernelGGL((bn_apply_kernel<T, true>), dim3(apply_grid(nchunk)), dim3(256), 0, st, (const T*)x,
+                         (T*)y, scale, shift, nchunk, d->c / CE);
+    else
+      hipLaunchKernelGGL((bn_apply_kernel<T, false>), dim3(apply_grid(nchunk)), dim3(256), 0, st, (const T*)x,
+                         (T*)y, scale, shift, nchunk, d->c / CE);
+  }
+  return rn_check_launch("bn_fwd_train");
+}
+
+template <typename T>
+int bn_apply_t(const rn_bn_desc* d, const void* x, void* y, const float* scale, const float* shift,
+               hipStream_t st) {
+  const int CE = 16 / sizeof(T);
+  const int64_t nchunk = d->m * d->c / CE;
+  if (d->relu)
+    hipLaunchKernelGGL((bn_apply_kernel<T, true>), dim3(apply_grid(nchunk)), dim3(256), 0, st, (const T*)x,
+                       (T*)y, scale, shift, nchunk, d->c / CE);
+  else
+    hipLaunchKernelGGL((bn_apply_kernel<T, false>), dim3(apply_grid(nchunk)), dim3(256), 0, st, (const T*)x,
+                       (T*)y, scale, shift, nchunk, d->c / CE);
+  return rn_check_launch("bn_apply");
+}
+
+template <typename T>
+int bn_bwd_t(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const void* add, const float* gamma,
+             const float* smean, const float* sinv, const float* scale, const float* shift, float* dgamma,
+             float* dbeta, void* ws, hipStream_t st) {
+  Geo g = make_geo<T>(d->m, d->c);
+  float* part = reinterpret_cast<float*>(ws);
+  float* coef = part + (int64_t)g.nrb * d->c * 2;
+  coef = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(coef) + 15) & ~uintptr_t(15));
+  if (d->relu)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(g.gx, g.nrb), dim3(kThreads), 0, st, (const T*)x,
+                       (const T*)dy, d->m, d->c, g.ct, g.rows_per_block, smean, scale, shift, part);
+  else
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(g.gx, g.nrb), dim3(kThreads), 0, st, (const T*)x,
+                       (const T*)dy, d->m, d->c, g.ct, g.rows_per_block, smean, scale, shift, part);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((d->c + 63) / 64), dim3(256), 0, st, part, g.nrb, d->m, d->c,
+                     d->c_real, d->fix_gamma, gamma, smean, sinv, dgamma, dbeta, coef);
+  if (dx) {
+    const int CE = 16 / sizeof(T);
+    const int64_t nchunk = d->m * d->c / CE;
+    if (d->relu)
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true>), dim3(apply_grid(nchunk)), dim3(256), 0, st, (const T*)x,
+                         (const T*)dy, (T*)dx, (const T*)add, coef, scale, shift, nchunk, d->c / CE);
+    else
+      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false>), dim3(apply_grid(nchunk)), dim3(256), 0, st, (const T*)x,
+                         (const T*)dy, (T*)dx, (const T*)add, coef, scale, shift, nchunk, d->c / CE);
+  }
+  return rn_check_launch("bn_bwd");
+}
+
+}  // namespace
+
+extern "C" {
+
+int64_t rn_bn_workspace_bytes(const rn_bn_desc* d) {
+  Geo g = d->dtype == RN_BF16 ? make_geo<bf16_t>(d->m, d->c) : make_geo<float>(d->m, d->c);
+  return ((int64_t)g.nrb * d->c * 2 + (int64_t)d->c * 4) * (int64_t)sizeof(float) + 64;
+}
+
+static int check_bn(const rn_bn_desc* d) {
+  RN_CHECK_ARG(d != nullptr, "null desc");
+  RN_CHECK_ARG(d->dtype == RN_BF16 || d->dtype == RN_F32, "bad dtype");
+  RN_CHECK_ARG(d->m > 0 && d->c > 0 && d->c % 8 == 0, "bad shape (c must be a multiple of 8)");
+  RN_CHECK_ARG(d->c_real > 0 && d->c_real <= d->c, "bad c_real");
+  return 0;
+}
+
+int rn_bn_fwd_train(const rn_bn_desc* d, const void* x, void* y, const float* gamma, const float* beta,
+                    float* moving_mean, float* moving_var, float* save_mean, float* save_invstd, float* scale,
+                    float* shift, void* ws, rn_stream_t stream) {
+  if (check_bn(d)) return -1;
+  RN_CHECK_ARG(x && beta && save_mean && save_invstd && scale && shift && ws, "null argument");
+  RN_CHECK_ARG(d->fix_gamma || gamma, "gamma required unless fix_gamma");
+  RN_CHECK_ARG((moving_mean == nullptr) == (moving_var == nullptr), "moving stats must both be set");
+  hipStream_t st = as_stream(stream);
+  if (d->dtype == RN_BF16)
+    return bn_fwd_train_t<bf16_t>(d, x, y, gamma, beta, moving_mean, moving_var, save_mean, save_invstd, scale,
+                                  shift, ws, st);
+  return bn_fwd_train_t<float>(d, x, y, gamma, beta, moving_mean, moving_var, save_mean, save_invstd, scale,
+                               shift, ws, st);
+}
+
+int rn_bn_fwd_infer(const rn_bn_desc* d, const void* x, void* y, const float* gamma, const float* beta,
+                    const float* moving_mean, const float* moving_var, float* scale, float* shift,
+                    rn_stream_t stream) {
+  if (check_bn(d)) return -1;
+  RN_CHECK_ARG(x && y && beta && moving_mean && moving_var && scale && shift, "null argument");
+  RN_CHECK_ARG(d->fix_gamma || gamma, "gamma required unless fix_gamma");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(bn_infer_coef_kernel, dim3((d->c + 255) / 256), dim3(256), 0, st, d->c, d->c_real, d->eps,
+                     d->fix_gamma, gamma, beta, moving_mean, moving_var, scale, shift);
+  if (d->dtype == RN_BF16) return bn_apply_t<bf16_t>(d, x, y, scale, shift, st);
+  return bn_apply_t<float>(d, x, y, scale, shift, st);
+}
+
+int rn_bn_apply(const rn_bn_desc* d, const void* x, void* y, const float* scale, const float* shift,
+                rn_stream_t stream) {
+  if (check_bn(d)) return -1;
+  RN_CHECK_ARG(x && y && scale && shift, "null argument");
+  hipStream_t st = as_stream(stream);
+  if (d->dtype == RN_BF16) return bn_apply_t<bf16_t>(d, x, y, scale, shift, st);
+  return bn_apply_t<float>(d, x, y, scale, shift, st);
+}
+
+int rn_bn_bwd(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const void* add_src,
+              const float* gamma, const float* save_mean, const float* save_invstd, const float* scale,
+              const float* shift, float* dgamma, float* dbeta, void* ws, rn_stream_t stream) {
+  if (check_bn(d)) return -1;
+  RN_CHECK_ARG(x && dy && save_mean && save_invstd && scale && shift && ws, "null argument");
+  RN_CHECK_ARG(d->fix_gamma || gamma, "gamma required unless fix_gamma");
+  hipStream_t st = as_stream(stream);
+  if (d->dtype == RN_BF16)
+    return bn_bwd_t<bf16_t>(d, x, dy, dx, add_src, gamma, save_mean, save_invstd, scale, shift, dgamma, dbeta,
+                            ws, st);
+  return bn_bwd_t<float>(d, x, dy, dx, add_src, gamma, save_mean, save_invstd, scale, shift, dgamma, dbeta, ws,
+                         st);
+}
+
+}  // extern "C"

@@ -1,0 +1,99 @@
+// rn_common.h -- shared device helpers for librn (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/rn.h"
+
+typedef uint16_t bf16_t;
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef short v8s __attribute__((ext_vector_type(8)));
+typedef short v4s __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------ error reporting
+void rn_set_error(const std::string& msg);
+#define RN_CHECK_ARG(cond, msg)                                                              \
+  do {                                                                                     \
+    if (!(cond)) {                                                                         \
+      rn_set_error(std::string(__func__) + ": " + (msg));                                  \
+      return -1;                                                                           \
+    }                                                                                      \
+  } while (0)
+int rn_check_launch(const char* where);
+
+// ------------------------------------------------------------------ bf16 <-> f32
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float((uint32_t)v << 16); }
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  // v_cvt_pk_bf16_f32: round-to-nearest-even, NaN stays NaN (MI355X_MICROARCH correctness table)
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+__device__ __forceinline__ float to_f(bf16_t v) { return bf2f(v); }
+__device__ __forceinline__ float to_f(float v) { return v; }
+template <typename T> __device__ __forceinline__ T from_f(float f);
+template <> __device__ __forceinline__ float from_f<float>(float f) { return f; }
+template <> __device__ __forceinline__ bf16_t from_f<bf16_t>(float f) { return f2bf(f); }
+
+// A 16-byte chunk: 8 bf16 or 4 f32. All vector memory traffic moves whole chunks.
+template <typename T> struct Chunk {
+  static constexpr int N = 16 / sizeof(T);
+};
+__device__ __forceinline__ void chunk_to_f(const uint4& u, float* f, const bf16_t*) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void chunk_to_f(const uint4& u, float* f, const float*) {
+  f[0] = __uint_as_float(u.x);
+  f[1] = __uint_as_float(u.y);
+  f[2] = __uint_as_float(u.z);
+  f[3] = __uint_as_float(u.w);
+}
+__device__ __forceinline__ uint4 f_to_chunk(const float* f, const bf16_t*) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    w[i] = (uint32_t)f2bf(f[2 * i]) | ((uint32_t)f2bf(f[2 * i + 1]) << 16);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+__device__ __forceinline__ uint4 f_to_chunk(const float* f, const float*) {
+  return make_uint4(__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]),
+                    __float_as_uint(f[3]));
+}
+
+// ------------------------------------------------------------------ fast division
+// n / d for 0 <= n < 2^31 via multiply-high (Granlund-Montgomery round-up variant).
+struct FastDiv {
+  uint32_t d, m, s;
+};
+static inline FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f;
+  f.d = d;
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.s = l;
+  f.m = (uint32_t)((((1ull << 32) * ((1ull << l) - d)) / d) + 1);
+  return f;
+}
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
+  return (__umulhi(n, f.m) + n) >> f.s;
+}
+
+// ------------------------------------------------------------------ wave reductions
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+static inline hipStream_t as_stream(rn_stream_t s) { return reinterpret_cast<hipStream_t>(s); }

@@ -1,0 +1,805 @@
+// rn_conv.hip -- Convolution / FullyConnected on CDNA4 MFMA (gfx950).
+//
+// Replaces the cuDNN conv fwd / bwd-data / bwd-filter that MXNet ran for mx.sym.Convolution
+// (reference symbol/resnet.py:14-31,93, symbol/resnext.py:17-38,83) and the cuBLAS GEMM of
+// mx.sym.FullyConnected (symbol/resnet.py:115). Activations are NHWC, weights KRSC.
+//
+//  * igemm_kernel   : y[M=N*P*Q][K] = gather(x)[M][R*S*C] * W^T, the implicit GEMM used for
+//                     forward AND for data-gradient (a transposed conv, split into stride
+//                     parity classes so that only valid taps are visited).
+//  * wgrad_kernel   : dW[K][R*S*C] += dy^T[K][M] * gather(x)[M][R*S*C], split over M with
+//                     fp32 atomics; both operands are read from LDS with ds_read_b64_tr_b16.
+//  * im2col / pack / stem-shift-grad helpers.
+//
+// Tile anatomy (igemm): 256 threads = 4 waves in 2x2, block tile BM x BN, one K stage is
+// 128 bytes of reduction per row (64 bf16 / 32 f32), register-staged global->LDS with the
+// write placed after the MFMA phase (async-STAGE split), LDS double buffered, one barrier
+// per stage, 16-byte chunks XOR-swizzled by (row & 7) so ds_read_b128 fragment reads are
+// bank-conflict free.  bf16: v_mfma_f32_16x16x32_bf16.  f32: v_mfma_f32_16x16x4_f32 (exact
+// fp32 products, used by the parity path).
+#include "rn_common.h"
+
+namespace {
+
+// ------------------------------------------------------------------------------ igemm
+struct IgemmCls {
+  int a, b;          // output parity class (dgrad) -- (0,0) for fwd
+  int Pc, Qc;        // class-local output extent
+  int r0, s0;        // first tap of the class
+  int nr, ns;        // taps in the class
+  int hoff0, woff0;  // gathered coordinate offset of tap 0
+  int hb0, wb0;      // row-coordinate bias
+  FastDiv fdQ, fdPQ;
+};
+
+struct IgemmArgs {
+  const void* x;
+  const void* w;
+  void* y;
+  const void* add;
+  const float* bias;
+  int N, H, W, C;      // gathered tensor; C = channel stride (multiple of the chunk)
+  int P, Q;            // output tensor spatial
+  int K, ldo;          // valid output columns, output row stride
+  int S;               // taps per weight row (for the B row offset)
+  int wrow;            // B matrix row stride = R*S*C
+  int rstep, sstep;    // tap step (1 fwd, stride dgrad)
+  int hmul, wmul;      // row coordinate multiplier (stride fwd, 1 dgrad)
+  int hinc, winc;      // gathered coordinate change per tap step (+1 fwd, -1 dgrad)
+  int ostep_h, ostep_w;
+  int ncls;
+  IgemmCls cls[4];
+};
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ (row & 7); }
+
+template <typename T>
+__device__ __forceinline__ void mfma_slab(v4f& acc, const uint4& a, const uint4& b);
+
+template <>
+__device__ __forceinline__ void mfma_slab<bf16_t>(v4f& acc, const uint4& a, const uint4& b) {
+  v8s av = __builtin_bit_cast(v8s, a);
+  v8s bv = __builtin_bit_cast(v8s, b);
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ void mfma_slab<float>(v4f& acc, const uint4& a, const uint4& b) {
+  // lane group g holds k = 4g..4g+3; MFMA step e pairs A[.][4g+e] with B[4g+e][.]
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
+}
+
+template <typename OutT>
+__device__ __forceinline__ float load_out(const void* p, int64_t i) {
+  return to_f(reinterpret_cast<const OutT*>(p)[i]);
+}
+
+template <typename T, typename OutT, int BM, int BN>
+__global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
+  constexpr int CE = 16 / sizeof(T);   // elements per chunk
+  constexpr int BKE = 128 / sizeof(T); // reduction elements per stage
+  constexpr int A_CH = BM / 32;        // chunks per thread per stage (A)
+  constexpr int B_CH = BN / 32;
+  constexpr int MI = BM / 32;          // 16x16 tiles per wave (rows)
+  constexpr int NI = BN / 32;
+  __shared__ __attribute__((aligned(16))) uint4 smem[2 * (BM + BN) * 8];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const IgemmCls& cl = p.cls[blockIdx.z];
+  const int Mc = p.N * cl.Pc * cl.Qc;
+  const int m0 = blockIdx.x * BM;
+  if (m0 >= Mc) return;
+  const int n0 = blockIdx.y * BN;
+
+  const T* __restrict__ xg = reinterpret_cast<const T*>(p.x);
+  const T* __restrict__ wg = reinterpret_cast<const T*>(p.w);
+
+  // ---- per-thread load assignment: chunk column ch, rows (tid>>3) + 32*i
+  const int ch = tid & 7;
+  int a_pix[A_CH];  // n*H*W
+  int a_hb[A_CH], a_wb[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    const int m = m0 + (tid >> 3) + 32 * i;
+    if (m < Mc) {
+      const int n = fdiv(m, cl.fdPQ);
+      const int rem = m - n * cl.Pc * cl.Qc;
+      const int ii = fdiv(rem, cl.fdQ);
+      const int jj = rem - ii * cl.Qc;
+      a_pix[i] = n * p.H * p.W;
+      a_hb[i] = ii * p.hmul + cl.hb0;
+      a_wb[i] = jj * p.wmul + cl.wb0;
+    } else {
+      a_pix[i] = 0;
+      a_hb[i] = -(1 << 28);  // never in range
+      a_wb[i] = 0;
+    }
+  }
+  int64_t b_off[B_CH];
+  bool b_ok[B_CH];
+#pragma unroll
+  for (int i = 0; i < B_CH; ++i) {
+    const int col = n0 + (tid >> 3) + 32 * i;
+    b_ok[i] = col < p.K;
+    b_off[i] = (int64_t)(b_ok[i] ? col : 0) * p.wrow;
+  }
+
+  const int ncb = (p.C + BKE - 1) / BKE;
+  const int nstage = cl.nr * cl.ns * ncb;
+
+  uint4 ra[A_CH], rb[B_CH];
+  // stage iteration state
+  int st_tr = 0, st_ts = 0, st_cb = 0;
+
+  auto load_stage = [&](int tr, int ts, int cb) {
+    const int r = cl.r0 + p.rstep * tr;
+    const int s = cl.s0 + p.sstep * ts;
+    const int hoff = cl.hoff0 + p.hinc * tr;
+    const int woff = cl.woff0 + p.winc * ts;
+    const int c = cb * BKE + ch * CE;
+    const bool cok = c < p.C;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int hin = a_hb[i] + hoff;
+      const int win = a_wb[i] + woff;
+      const bool ok = cok && (unsigned)hin < (unsigned)p.H && (unsigned)win < (unsigned)p.W;
+      if (ok) {
+        const int64_t off = ((int64_t)(a_pix[i] + hin * p.W + win)) * p.C + c;
+        ra[i] = *reinterpret_cast<const uint4*>(xg + off);
+      } else {
+        ra[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+    const int64_t toff = (int64_t)(r * p.S + s) * p.C + c;
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      if (cok && b_ok[i]) rb[i] = *reinterpret_cast<const uint4*>(wg + b_off[i] + toff);
+      else rb[i] = make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store_stage = [&](int buf) {
+    uint4* As = smem + buf * (BM + BN) * 8;
+    uint4* Bs = As + BM * 8;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      As[row * 8 + swz(row, ch)] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      Bs[row * 8 + swz(row, ch)] = rb[i];
+    }
+  };
+  auto advance = [&]() {
+    if (++st_cb == ncb) {
+      st_cb = 0;
+      if (++st_ts == cl.ns) {
+        st_ts = 0;
+        ++st_tr;
+      }
+    }
+  };
+
+  v4f acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  if (nstage > 0) {
+    load_stage(st_tr, st_ts, st_cb);
+    advance();
+    store_stage(0);
+    __syncthreads();
+  }
+  for (int t = 0; t < nstage; ++t) {
+    const bool more = t + 1 < nstage;
+    if (more) {
+      load_stage(st_tr, st_ts, st_cb);
+      advance();
+    }
+    const uint4* As = smem + (t & 1) * (BM + BN) * 8;
+    const uint4* Bs = As + BM * 8;
+#pragma unroll
+    for (int slab = 0; slab < 2; ++slab) {
+      uint4 af[MI], bfr[NI];
+      const int kc = slab * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int row = wm * (BM / 2) + i * 16 + (lane & 15);
+        af[i] = As[row * 8 + swz(row, kc)];
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int row = wn * (BN / 2) + j * 16 + (lane & 15);
+        bfr[j] = Bs[row * 8 + swz(row, kc)];
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) mfma_slab<T>(acc[i][j], af[i], bfr[j]);
+    }
+    if (more) store_stage((t + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: (+bias) (+add) -> OutT
+  OutT* __restrict__ yg = reinterpret_cast<OutT*>(p.y);
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + e;
+      if (m >= Mc) continue;
+      const int n = fdiv(m, cl.fdPQ);
+      const int rem = m - n * cl.Pc * cl.Qc;
+      const int ii = fdiv(rem, cl.fdQ);
+      const int jj = rem - ii * cl.Qc;
+      const int oh = cl.a + p.ostep_h * ii;
+      const int ow = cl.b + p.ostep_w * jj;
+      const int64_t orow = ((int64_t)(n * p.P + oh) * p.Q + ow) * p.ldo;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
+        if (col >= p.K) continue;
+        float v = acc[i][j][e];
+        if (p.bias) v += p.bias[col];
+        if (p.add) v += load_out<OutT>(p.add, orow + col);
+        yg[orow + col] = from_f<OutT>(v);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ wgrad
+struct WgradArgs {
+  const void* x;   // NHWC gathered (B operand)
+  const void* dy;  // [M][ldy] (A operand)
+  float* dw;       // [K][ldw]
+  int N, H, W, C, P, Q, K, ldy, R, S, sh, sw, ph, pw;
+  int ncol_load;   // R*S*C
+  int ncol;        // valid columns of dw (R*S*c_real)
+  int ldw;
+  int M;
+  int m_per_split;
+  FastDiv fdQ, fdPQ, fdC, fdS;
+};
+
+// 16-byte chunk swizzle of an LDS image whose rows are read 4-at-a-time by
+// ds_read_b64_tr_b16 (rows 8g+4h+q): keeps the 8 rows of a 32-lane half on distinct slots.
+__device__ __forceinline__ int swz_tr(int row) { return 2 * ((row & 3) | (((row >> 3) & 1) << 2)); }
+
+template <typename T, int BMK, int BNC>
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
+  constexpr int CE = 16 / sizeof(T);
+  constexpr int BKM = 128 / sizeof(T);        // m rows per stage
+  constexpr int A_CPR = BMK * sizeof(T) / 16; // chunks per A row
+  constexpr int B_CPR = BNC * sizeof(T) / 16;
+  constexpr int A_CH = BKM * A_CPR / 256;
+  constexpr int B_CH = BKM * B_CPR / 256;
+  constexpr int A_RSTEP = 256 / A_CPR;
+  constexpr int B_RSTEP = 256 / B_CPR;
+  constexpr int MI = BMK / 32;
+  constexpr int NI = BNC / 32;
+  constexpr int A_SZ = BKM * A_CPR;  // chunks
+  constexpr int B_SZ = BKM * B_CPR;
+  __shared__ __attribute__((aligned(16))) uint4 smem[2 * (A_SZ + B_SZ)];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int n0 = blockIdx.x * BNC;  // dw column tile
+  const int k0 = blockIdx.y * BMK;  // dw row tile (output channels)
+  const int mbeg = blockIdx.z * p.m_per_split;
+  const int mend = min(p.M, mbeg + p.m_per_split);
+  if (mbeg >= mend) return;
+
+  const T* __restrict__ xg = reinterpret_cast<const T*>(p.x);
+  const T* __restrict__ dyg = reinterpret_cast<const T*>(p.dy);
+
+  // A assignment: chunk column a_c, rows (tid / A_CPR) + A_RSTEP*i
+  const int a_c = tid % A_CPR;
+  const int a_k = k0 + a_c * CE;
+  const bool a_kok = a_k < p.ldy;
+  // B assignment: fixed column chunk -> (tap r,s ; channel c)
+  const int b_c = tid % B_CPR;
+  const int bcol = n0 + b_c * CE;
+  const bool b_cok = bcol < p.ncol_load;
+  int b_r = 0, b_s = 0, b_ch = 0;
+  if (b_cok) {
+    const int tap = fdiv(bcol, p.fdC);
+    b_ch = bcol - tap * p.C;
+    b_r = fdiv(tap, p.fdS);
+    b_s = tap - b_r * p.S;
+  }
+  const int b_hoff = b_r - p.ph, b_woff = b_s - p.pw;
+
+  uint4 ra[A_CH], rb[B_CH];
+  auto load_stage = [&](int mb) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int m = mb + tid / A_CPR + A_RSTEP * i;
+      if (a_kok && m < mend)
+        ra[i] = *reinterpret_cast<const uint4*>(dyg + (int64_t)m * p.ldy + a_k);
+      else
+        ra[i] = make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int m = mb + tid / B_CPR + B_RSTEP * i;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (b_cok && m < mend) {
+        const int n = fdiv(m, p.fdPQ);
+        const int rem = m - n * p.P * p.Q;
+        const int pp = fdiv(rem, p.fdQ);
+        const int qq = rem - pp * p.Q;
+        const int hin = pp * p.sh + b_hoff;
+        const int win = qq * p.sw + b_woff;
+        if ((unsigned)hin < (unsigned)p.H && (unsigned)win < (unsigned)p.W)
+          v = *reinterpret_cast<const uint4*>(
+              xg + ((int64_t)(n * p.H + hin) * p.W + win) * p.C + b_ch);
+      }
+      rb[i] = v;
+    }
+  };
+  auto store_stage = [&](int buf) {
+    uint4* As = smem + buf * (A_SZ + B_SZ);
+    uint4* Bs = As + A_SZ;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int row = tid / A_CPR + A_RSTEP * i;
+      As[row * A_CPR + (a_c ^ (swz_tr(row) & (A_CPR - 1)))] = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int row = tid / B_CPR + B_RSTEP * i;
+      Bs[row * B_CPR + (b_c ^ (swz_tr(row) & (B_CPR - 1)))] = rb[i];
+    }
+  };
+
+  v4f acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  const int nstage = (mend - mbeg + BKM - 1) / BKM;
+  load_stage(mbeg);
+  store_stage(0);
+  __syncthreads();
+  for (int t = 0; t < nstage; ++t) {
+    const bool more = t + 1 < nstage;
+    if (more) load_stage(mbeg + (t + 1) * BKM);
+    const uint4* As = smem + (t & 1) * (A_SZ + B_SZ);
+    const uint4* Bs = As + A_SZ;
+    if constexpr (sizeof(T) == 2) {
+      // 2 slabs of 32 m per stage; per slab each lane needs rows 8g+j (j=0..7) at its column.
+      const char* Ab = reinterpret_cast<const char*>(As);
+      const char* Bb = reinterpret_cast<const char*>(Bs);
+      const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+#pragma unroll
+      for (int slab = 0; slab < 2; ++slab) {
+        v8s af[MI], bfv[NI];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int row = slab * 32 + 8 * g + 4 * h + q;
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const int col = wm * (BMK / 2) + i * 16 + 4 * pp;  // element column
+            const int cch = (col * 2) >> 4;
+            const int byte = row * (A_CPR * 16) + ((cch ^ (swz_tr(row) & (A_CPR - 1))) << 4) + ((col * 2) & 15);
+            v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) v4s*)(Ab + byte));
+            af[i][4 * h + 0] = v[0];
+            af[i][4 * h + 1] = v[1];
+            af[i][4 * h + 2] = v[2];
+            af[i][4 * h + 3] = v[3];
+          }
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const int col = wn * (BNC / 2) + j * 16 + 4 * pp;
+            const int cch = (col * 2) >> 4;
+            const int byte = row * (B_CPR * 16) + ((cch ^ (swz_tr(row) & (B_CPR - 1))) << 4) + ((col * 2) & 15);
+            v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) v4s*)(Bb + byte));
+            bfv[j][4 * h + 0] = v[0];
+            bfv[j][4 * h + 1] = v[1];
+            bfv[j][4 * h + 2] = v[2];
+            bfv[j][4 * h + 3] = v[3];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      // f32: 16x16x4 steps; lane holds A[k=col l&15][m = 4s + (l>>4)].
+      const float* Af = reinterpret_cast<const float*>(As);
+      const float* Bf = reinterpret_cast<const float*>(Bs);
+#pragma unroll 4
+      for (int s4 = 0; s4 < BKM / 4; ++s4) {
+        const int row = 4 * s4 + (lane >> 4);
+        float a[MI], b[NI];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int col = wm * (BMK / 2) + i * 16 + (lane & 15);
+          const int cch = col >> 2;
+          a[i] = Af[(row * A_CPR + (cch ^ (swz_tr(row) & (A_CPR - 1)))) * 4 + (col & 3)];
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int col = wn * (BNC / 2) + j * 16 + (lane & 15);
+          const int cch = col >> 2;
+          b[j] = Bf[(row * B_CPR + (cch ^ (swz_tr(row) & (B_CPR - 1)))) * 4 + (col & 3)];
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i], b[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (more) store_stage((t + 1) & 1);
+    __syncthreads();
+  }
+
+  // epilogue: D[row = k][col] -> atomic add into dw
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = k0 + wm * (BMK / 2) + i * 16 + (lane >> 4) * 4 + e;
+      if (k >= p.K) continue;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = n0 + wn * (BNC / 2) + j * 16 + (lane & 15);
+        if (col < p.ncol) atomicAdd(p.dw + (int64_t)k * p.ldw + col, acc[i][j][e]);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ helpers
+template <typename T>
+__global__ void pack_krsc_kernel(const float* __restrict__ wm, T* __restrict__ out, int K, int RS,
+                                 int creal, int c) {
+  const int64_t total = (int64_t)K * RS * c;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % c);
+    const int64_t kt = i / c;  // k*RS + tap
+    const float v = ci < creal ? wm[kt * creal + ci] : 0.f;
+    out[i] = from_f<T>(v);
+  }
+}
+
+template <typename T>
+__global__ void pack_crsk_kernel(const float* __restrict__ wm, T* __restrict__ out, int K, int kpad,
+                                 int RS, int creal, int c) {
+  const int64_t total = (int64_t)c * RS * kpad;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i % kpad);
+    const int64_t ct = i / kpad;  // c*RS + tap
+    const int tap = (int)(ct % RS);
+    const int ci = (int)(ct / RS);
+    float v = 0.f;
+    if (k < K && ci < creal) v = wm[((int64_t)k * RS + tap) * creal + ci];
+    out[i] = from_f<T>(v);
+  }
+}
+
+template <typename T>
+__global__ void im2col_nchw_kernel(const float* __restrict__ x, const float* __restrict__ scale,
+                                   const float* __restrict__ shift, T* __restrict__ cols, int N,
+                                   int C, int H, int W, int P, int Q, int R, int S, int sh, int sw,
+                                   int ph, int pw, int kc) {
+  const int64_t M = (int64_t)N * P * Q;
+  const int kreal = R * S * C;
+  const int64_t total = M * kc;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int col = (int)(i % kc);
+    const int64_t m = i / kc;
+    float v = 0.f;
+    if (col < kreal) {
+      const int c = col % C;
+      const int tap = col / C;
+      const int r = tap / S, s = tap % S;
+      const int q = (int)(m % Q);
+      const int64_t t2 = m / Q;
+      const int pp = (int)(t2 % P);
+      const int n = (int)(t2 / P);
+      const int h = pp * sh - ph + r, w = q * sw - pw + s;
+      if (h >= 0 && h < H && w >= 0 && w < W) {
+        v = x[(((int64_t)n * C + c) * H + h) * W + w];
+        if (scale) v = fmaf(v, scale[c], shift[c]);
+      }
+    }
+    cols[i] = from_f<T>(v);
+  }
+}
+
+// S[p][q][k] = sum_n dy[n][p][q][k]
+template <typename T>
+__global__ void stem_sum_n_kernel(const T* __restrict__ dy, float* __restrict__ ws, int N, int PQ,
+                                  int kpad) {
+  const int64_t total = (int64_t)PQ * kpad;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float acc = 0.f;
+    for (int n = 0; n < N; ++n) acc += to_f(dy[(int64_t)n * total + i]);
+    ws[i] = acc;
+  }
+}
+// G[k][r][s] = sum_{p in V(r), q in V(s)} S[p][q][k]
+__global__ void stem_tap_sum_kernel(const float* __restrict__ ws, float* __restrict__ g, int K,
+                                    int kpad, int R, int S, int H, int W, int P, int Q, int sh,
+                                    int sw, int ph, int pw) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= K * R * S) return;
+  const int k = idx / (R * S);
+  const int tap = idx % (R * S);
+  const int r = tap / S, s = tap % S;
+  float acc = 0.f;
+  for (int pp = 0; pp < P; ++pp) {
+    const int h = pp * sh - ph + r;
+    if (h < 0 || h >= H) continue;
+    for (int q = 0; q < Q; ++q) {
+      const int w = q * sw - pw + s;
+      if (w < 0 || w >= W) continue;
+      acc += ws[((int64_t)pp * Q + q) * kpad + k];
+    }
+  }
+  g[idx] = acc;
+}
+__global__ void stem_shift_reduce_kernel(const float* __restrict__ g, const float* __restrict__ wm,
+                                         float* __restrict__ dbeta, int K, int RS, int C) {
+  const int c = blockIdx.x;
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < K * RS; i += blockDim.x) acc += g[i] * wm[(int64_t)i * C + c];
+  __shared__ float red[256];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dbeta[c] += red[0];
+}
+
+int grid_for(int64_t total, int block = 256) {
+  int64_t g = (total + block - 1) / block;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+// Build igemm args for fwd (mode 0) or dgrad (mode 1).
+// fwd : gathered = x (N,H,W,C), out = y (N,P,Q,K), B = w_krsc [K][R][S][C]
+// dgrad: gathered = dy (N,P,Q,k_pad), out = dx (N,H,W,c), B = w_crsk [c][R][S][k_pad]
+IgemmArgs make_igemm_args(const rn_conv_desc* d, int mode) {
+  IgemmArgs a{};
+  a.S = d->s;
+  if (mode == 0) {
+    a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c;
+    a.P = d->p; a.Q = d->q; a.K = d->k; a.ldo = d->k_pad;
+    a.wrow = d->r * d->s * d->c;
+    a.rstep = 1; a.sstep = 1;
+    a.hmul = d->stride_h; a.wmul = d->stride_w;
+    a.hinc = 1; a.winc = 1;
+    a.ostep_h = 1; a.ostep_w = 1;
+    a.ncls = 1;
+    IgemmCls& c = a.cls[0];
+    c.a = 0; c.b = 0; c.Pc = d->p; c.Qc = d->q; c.r0 = 0; c.s0 = 0; c.nr = d->r; c.ns = d->s;
+    c.hoff0 = 0; c.woff0 = 0; c.hb0 = -d->pad_h; c.wb0 = -d->pad_w;
+    c.fdQ = make_fastdiv(c.Qc); c.fdPQ = make_fastdiv(c.Pc * c.Qc);
+  } else {
+    a.N = d->n; a.H = d->p; a.W = d->q; a.C = d->k_pad;
+    a.P = d->h; a.Q = d->w; a.K = d->c; a.ldo = d->c;
+    a.wrow = d->r * d->s * d->k_pad;
+    a.rstep = d->stride_h; a.sstep = d->stride_w;
+    a.hmul = 1; a.wmul = 1;
+    a.hinc = -1; a.winc = -1;
+    a.ostep_h = d->stride_h; a.ostep_w = d->stride_w;
+    a.ncls = d->stride_h * d->stride_w;
+    for (int z = 0; z < a.ncls; ++z) {
+      IgemmCls& c = a.cls[z];
+      c.a = z / d->stride_w; c.b = z % d->stride_w;
+      c.Pc = (int)ceil_div(d->h - c.a, d->stride_h);
+      c.Qc = (int)ceil_div(d->w - c.b, d->stride_w);
+      if (c.Pc < 0) c.Pc = 0;
+      if (c.Qc < 0) c.Qc = 0;
+      c.r0 = (c.a + d->pad_h) % d->stride_h;
+      c.s0 = (c.b + d->pad_w) % d->stride_w;
+      c.nr = c.r0 < d->r ? (int)ceil_div(d->r - c.r0, d->stride_h) : 0;
+      c.ns = c.s0 < d->s ? (int)ceil_div(d->s - c.s0, d->stride_w) : 0;
+      c.hoff0 = (c.a + d->pad_h - c.r0) / d->stride_h;
+      c.woff0 = (c.b + d->pad_w - c.s0) / d->stride_w;
+      c.hb0 = 0; c.wb0 = 0;
+      c.fdQ = make_fastdiv(c.Qc > 0 ? c.Qc : 1);
+      c.fdPQ = make_fastdiv(c.Pc * c.Qc > 0 ? c.Pc * c.Qc : 1);
+    }
+  }
+  return a;
+}
+
+template <typename T, typename OutT>
+int launch_igemm(const IgemmArgs& a, hipStream_t st) {
+  int maxMc = 0;
+  for (int z = 0; z < a.ncls; ++z) maxMc = std::max(maxMc, a.N * a.cls[z].Pc * a.cls[z].Qc);
+  if (maxMc == 0) return 0;
+  if (a.K <= 64) {
+    dim3 grid((unsigned)ceil_div(maxMc, 128), (unsigned)ceil_div(a.K, 64), a.ncls);
+    hipLaunchKernelGGL((igemm_kernel<T, OutT, 128, 64>), grid, dim3(256), 0, st, a);
+  } else {
+    dim3 grid((unsigned)ceil_div(maxMc, 128), (unsigned)ceil_div(a.K, 128), a.ncls);
+    hipLaunchKernelGGL((igemm_kernel<T, OutT, 128, 128>), grid, dim3(256), 0, st, a);
+  }
+  return rn_check_launch("igemm");
+}
+
+}  // namespace
+
+extern "C" {
+
+int rn_conv_desc_init(rn_conv_desc* d) {
+  RN_CHECK_ARG(d != nullptr, "null desc");
+  RN_CHECK_ARG(d->dtype == RN_BF16 || d->dtype == RN_F32, "bad dtype");
+  RN_CHECK_ARG(d->n > 0 && d->h > 0 && d->w > 0 && d->k > 0, "bad shape");
+  RN_CHECK_ARG(d->r > 0 && d->s > 0 && d->stride_h > 0 && d->stride_w > 0, "bad kernel/stride");
+  RN_CHECK_ARG(d->pad_h >= 0 && d->pad_w >= 0, "bad pad");
+  if (d->groups <= 0) d->groups = 1;
+  RN_CHECK_ARG(d->groups == 1, "grouped convolution is not supported by this build");
+  if (d->c_real <= 0) d->c_real = d->c;
+  if (d->k_pad <= 0) d->k_pad = (d->k + 7) / 8 * 8;
+  RN_CHECK_ARG(d->c % 8 == 0, "channel stride must be a multiple of 8");
+  RN_CHECK_ARG(d->k_pad % 8 == 0 && d->k_pad >= d->k, "k_pad must be a multiple of 8 >= k");
+  RN_CHECK_ARG(d->c_real <= d->c, "c_real > c");
+  RN_CHECK_ARG(d->stride_h <= 2 && d->stride_w <= 2, "stride > 2 not supported");
+  d->p = (d->h + 2 * d->pad_h - d->r) / d->stride_h + 1;
+  d->q = (d->w + 2 * d->pad_w - d->s) / d->stride_w + 1;
+  RN_CHECK_ARG(d->p > 0 && d->q > 0, "empty output");
+  RN_CHECK_ARG((int64_t)d->n * d->h * d->w < (1ll << 31) && (int64_t)d->n * d->p * d->q < (1ll << 31),
+               "too many pixels");
+  return 0;
+}
+
+int64_t rn_conv_weight_numel(const rn_conv_desc* d) {
+  return (int64_t)d->k * d->r * d->s * (d->c_real / (d->groups > 0 ? d->groups : 1));
+}
+
+int rn_conv_fwd(const rn_conv_desc* d, const void* x, const void* w, void* y, int32_t y_dtype,
+                const void* add_src, const float* bias, rn_stream_t stream) {
+  RN_CHECK_ARG(d && x && w && y, "null argument");
+  IgemmArgs a = make_igemm_args(d, 0);
+  a.x = x; a.w = w; a.y = y; a.add = add_src; a.bias = bias;
+  hipStream_t st = as_stream(stream);
+  if (d->dtype == RN_BF16) {
+    if (y_dtype == RN_BF16) return launch_igemm<bf16_t, bf16_t>(a, st);
+    return launch_igemm<bf16_t, float>(a, st);
+  }
+  RN_CHECK_ARG(y_dtype == RN_F32, "f32 compute requires f32 output");
+  return launch_igemm<float, float>(a, st);
+}
+
+int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
+                     const void* add_src, rn_stream_t stream) {
+  RN_CHECK_ARG(d && dy && w_crsk && dx, "null argument");
+  IgemmArgs a = make_igemm_args(d, 1);
+  a.x = dy; a.w = w_crsk; a.y = dx; a.add = add_src; a.bias = nullptr;
+  hipStream_t st = as_stream(stream);
+  if (d->dtype == RN_BF16) return launch_igemm<bf16_t, bf16_t>(a, st);
+  return launch_igemm<float, float>(a, st);
+}
+
+int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, float* dw,
+                       rn_stream_t stream) {
+  RN_CHECK_ARG(d && x && dy && dw, "null argument");
+  RN_CHECK_ARG(d->r * d->s == 1 || d->c == d->c_real,
+               "wgrad of a padded-channel input needs the im2col (1x1) formulation");
+  WgradArgs a{};
+  a.x = x; a.dy = dy; a.dw = dw;
+  a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.P = d->p; a.Q = d->q; a.K = d->k;
+  a.ldy = d->k_pad; a.R = d->r; a.S = d->s; a.sh = d->stride_h; a.sw = d->stride_w;
+  a.ph = d->pad_h; a.pw = d->pad_w;
+  a.ncol_load = d->r * d->s * d->c;
+  a.ncol = d->r * d->s * d->c_real;
+  a.ldw = a.ncol;
+  a.M = d->n * d->p * d->q;
+  a.fdQ = make_fastdiv(d->q); a.fdPQ = make_fastdiv(d->p * d->q);
+  a.fdC = make_fastdiv(d->c); a.fdS = make_fastdiv(d->s);
+  const int bmk = 128, bnc = 128;
+  const int tiles = (int)(ceil_div(a.ncol_load, bnc) * ceil_div(a.K, bmk));
+  const int bkm = d->dtype == RN_BF16 ? 64 : 32;
+  const int64_t mstages = ceil_div(a.M, bkm);
+  // split M so that the grid covers ~4 blocks per CU, with >= 8 stages per block
+  int64_t want = std::max<int64_t>(1, (4 * 256 + tiles - 1) / tiles);
+  int64_t maxsplit = std::max<int64_t>(1, mstages / 8);
+  int64_t split = std::min(want, maxsplit);
+  int64_t stages_per = ceil_div(mstages, split);
+  a.m_per_split = (int)(stages_per * bkm);
+  split = ceil_div(a.M, a.m_per_split);
+  dim3 grid((unsigned)ceil_div(a.ncol_load, bnc), (unsigned)ceil_div(a.K, bmk), (unsigned)split);
+  hipStream_t st = as_stream(stream);
+  if (d->dtype == RN_BF16)
+    hipLaunchKernelGGL((wgrad_kernel<bf16_t, 128, 128>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((wgrad_kernel<float, 128, 128>), grid, dim3(256), 0, st, a);
+  return rn_check_launch("wgrad");
+}
+
+int rn_conv_weight_pack(const rn_conv_desc* d, const float* wm, void* w_krsc, void* w_crsk,
+                        rn_stream_t stream) {
+  RN_CHECK_ARG(d && wm, "null argument");
+  hipStream_t st = as_stream(stream);
+  const int RS = d->r * d->s;
+  if (w_krsc) {
+    const int64_t total = (int64_t)d->k * RS * d->c;
+    if (d->dtype == RN_BF16)
+      hipLaunchKernelGGL(pack_krsc_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st, wm,
+                         (bf16_t*)w_krsc, d->k, RS, d->c_real, d->c);
+    else
+      hipLaunchKernelGGL(pack_krsc_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, wm,
+                         (float*)w_krsc, d->k, RS, d->c_real, d->c);
+  }
+  if (w_crsk) {
+    const int64_t total = (int64_t)d->c * RS * d->k_pad;
+    if (d->dtype == RN_BF16)
+      hipLaunchKernelGGL(pack_crsk_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st, wm,
+                         (bf16_t*)w_crsk, d->k, d->k_pad, RS, d->c_real, d->c);
+    else
+      hipLaunchKernelGGL(pack_crsk_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, wm,
+                         (float*)w_crsk, d->k, d->k_pad, RS, d->c_real, d->c);
+  }
+  return rn_check_launch("weight_pack");
+}
+
+int rn_im2col_nchw(const rn_conv_desc* d, const float* x, const float* scale, const float* shift,
+                   void* cols, int32_t kc, rn_stream_t stream) {
+  RN_CHECK_ARG(d && x && cols, "null argument");
+  RN_CHECK_ARG(kc >= d->r * d->s * d->c_real && kc % 8 == 0, "bad kc");
+  RN_CHECK_ARG((scale == nullptr) == (shift == nullptr), "scale/shift must both be set");
+  const int64_t total = (int64_t)d->n * d->p * d->q * kc;
+  hipStream_t st = as_stream(stream);
+  if (d->dtype == RN_BF16)
+    hipLaunchKernelGGL(im2col_nchw_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st, x,
+                       scale, shift, (bf16_t*)cols, d->n, d->c_real, d->h, d->w, d->p, d->q, d->r,
+                       d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, kc);
+  else
+    hipLaunchKernelGGL(im2col_nchw_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, x,
+                       scale, shift, (float*)cols, d->n, d->c_real, d->h, d->w, d->p, d->q, d->r,
+                       d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, kc);
+  return rn_check_launch("im2col");
+}
+
+int rn_stem_shift_grad(const rn_conv_desc* d, const void* dy, const float* wm, float* dbeta,
+                       float* ws, rn_stream_t stream) {
+  RN_CHECK_ARG(d && dy && wm && dbeta && ws, "null argument");
+  hipStream_t st = as_stream(stream);
+  const int PQ = d->p * d->q;
+  const int64_t total = (int64_t)PQ * d->k_pad;
+  if (d->dtype == RN_BF16)
+    hipLaunchKernelGGL(stem_sum_n_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st,
+                       (const bf16_t*)dy, ws, d->n, PQ, d->k_pad);
+  else
+    hipLaunchKernelGGL(stem_sum_n_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st,
+                       (const float*)dy, ws, d->n, PQ, d->k_pad);
+  float* g = ws + total;
+  const int nkt = d->k * d->r * d->s;
+  hipLaunchKernelGGL(stem_tap_sum_kernel, dim3((nkt + 63) / 64), dim3(64), 0, st, ws, g, d->k,
+                     d->k_pad, d->r, d->s, d->h, d->w, d->p, d->q, d->stride_h, d->stride_w,
+                     d->pad_h, d->pad_w);
+  hipLaunchKernelGGL(stem_shift_reduce_kernel, dim3(d->c_real), dim3(256), 0, st, g, wm, dbeta,
+                     d->k, d->r * d->s, d->c_real);
+  return rn_check_launch("stem_shift_grad");
+}
+
+}  // extern "C"

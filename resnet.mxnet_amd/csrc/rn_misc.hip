@@ -1,0 +1,545 @@
+// rn_misc.hip -- pooling, SoftmaxOutput, SGD-momentum, int8 fake-quant, casts, runtime info.
+//
+// Pooling       : mx.sym.Pooling (reference symbol/resnet.py:97 max 3x3/s2/p1, :113 global avg)
+// SoftmaxOutput : mx.sym.SoftmaxOutput (symbol/resnet.py:118-120), grad = p - onehot, 'null' norm
+// SGD momentum  : optimizer 'sgd' with momentum/wd/rescale_grad (train.py:186-194)
+// Quantization  : mx.sym.contrib.Quantization_int8 (symbol/int8_api.py:133-136) with the
+//                 semantics of symbol/quant_ops.py:12-42 and clip_grad_quantization_int8.py:14-67
+#include <algorithm>
+#include <cstring>
+
+#include "rn_common.h"
+
+static thread_local std::string g_last_error;
+void rn_set_error(const std::string& msg) { g_last_error = msg; }
+int rn_check_launch(const char* where) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    rn_set_error(std::string(where) + ": " + hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+namespace {
+
+int grid1d(int64_t total, int block = 256, int cap = 8192) {
+  int64_t g = (total + block - 1) / block;
+  return (int)std::min<int64_t>(std::max<int64_t>(g, 1), cap);
+}
+
+// ------------------------------------------------------------------------------ pooling
+struct PoolArgs {
+  int n, h, w, c, r, s, sh, sw, ph, pw, p, q, type;
+};
+
+// forward: thread per (output pixel, chunk). Max: first maximal tap in (r, s) scan order,
+// which is the element MXNet's max-unpool gives the gradient to. Avg: count_include_pad
+// (divisor r*s), global pool divides by h*w.
+template <typename T>
+__global__ void pool_fwd_kernel(PoolArgs a, const T* __restrict__ x, T* __restrict__ y,
+                                uint8_t* __restrict__ argmax) {
+  constexpr int CE = 16 / sizeof(T);
+  const int cpr = a.c / CE;
+  const int64_t total = (int64_t)a.n * a.p * a.q * cpr;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % cpr);
+    const int64_t pix = i / cpr;
+    const int qq = (int)(pix % a.q);
+    const int pp = (int)((pix / a.q) % a.p);
+    const int n = (int)(pix / ((int64_t)a.q * a.p));
+    float best[CE];
+    int arg[CE];
+#pragma unroll
+    for (int e = 0; e < CE; ++e) {
+      best[e] = a.type == RN_POOL_MAX ? -INFINITY : 0.f;
+      arg[e] = 0;
+    }
+    for (int r = 0; r < a.r; ++r) {
+      const int hh = pp * a.sh - a.ph + r;
+      if (hh < 0 || hh >= a.h) continue;
+      for (int s = 0; s < a.s; ++s) {
+        const int ww = qq * a.sw - a.pw + s;
+        if (ww < 0 || ww >= a.w) continue;
+        float f[CE];
+        chunk_to_f(*reinterpret_cast<const uint4*>(x + (((int64_t)n * a.h + hh) * a.w + ww) * a.c + cc * CE), f,
+                   (const T*)nullptr);
+#pragma unroll
+        for (int e = 0; e < CE; ++e) {
+          if (a.type == RN_POOL_MAX) {
+            if (f[e] > best[e]) {
+              best[e] = f[e];
+              arg[e] = r * a.s + s;
+            }
+          } else {
+            best[e] += f[e];
+          }
+        }
+      }
+    }
+    if (a.type != RN_POOL_MAX) {
+      const float inv = 1.f / (float)(a.r * a.s);
+#pragma unroll
+      for (int e = 0; e < CE; ++e) best[e] *= inv;
+    } else if (argmax) {
+#pragma unroll
+      for (int e = 0; e < CE; ++e) argmax[pix * a.c + cc * CE + e] = (uint8_t)arg[e];
+    }
+    reinterpret_cast<uint4*>(y)[i] = f_to_chunk(best, (const T*)nullptr);
+  }
+}
+
+// backward: input-centric gather (deterministic, no atomics).
+template <typename T>
+__global__ void pool_bwd_kernel(PoolArgs a, const T* __restrict__ dy, const uint8_t* __restrict__ argmax,
+                                T* __restrict__ dx, const T* __restrict__ add) {
+  constexpr int CE = 16 / sizeof(T);
+  const int cpr = a.c / CE;
+  const int64_t total = (int64_t)a.n * a.h * a.w * cpr;
+  const float inv = 1.f / (float)(a.r * a.s);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % cpr);
+    const int64_t pix = i / cpr;
+    const int ww = (int)(pix % a.w);
+    const int hh = (int)((pix / a.w) % a.h);
+    const int n = (int)(pix / ((int64_t)a.w * a.h));
+    float acc[CE];
+    if (add) chunk_to_f(reinterpret_cast<const uint4*>(add)[i], acc, (const T*)nullptr);
+    else
+#pragma unroll
+      for (int e = 0; e < CE; ++e) acc[e] = 0.f;
+    // outputs whose window contains hh: pp*sh - ph <= hh <= pp*sh - ph + r - 1
+    int plo = hh + a.ph - a.r + 1;
+    plo = plo <= 0 ? 0 : (plo + a.sh - 1) / a.sh;
+    const int phi = min(a.p - 1, (hh + a.ph) / a.sh);
+    int qlo = ww + a.pw - a.s + 1;
+    qlo = qlo <= 0 ? 0 : (qlo + a.sw - 1) / a.sw;
+    const int qhi = min(a.q - 1, (ww + a.pw) / a.sw);
+    for (int pp = plo; pp <= phi; ++pp) {
+      const int r = hh - (pp * a.sh - a.ph);
+      for (int qq = qlo; qq <= qhi; ++qq) {
+        const int s = ww - (qq * a.sw - a.pw);
+        const int tap = r * a.s + s;
+        const int64_t obase = (((int64_t)n * a.p + pp) * a.q + qq) * a.c + cc * CE;
+        float g[CE];
+        chunk_to_f(*reinterpret_cast<const uint4*>(dy + obase), g, (const T*)nullptr);
+        if (a.type == RN_POOL_MAX) {
+#pragma unroll
+          for (int e = 0; e < CE; ++e)
+            if (argmax[obase + e] == tap) acc[e] += g[e];
+        } else {
+#pragma unroll
+          for (int e = 0; e < CE; ++e) acc[e] += g[e] * inv;
+        }
+      }
+    }
+    reinterpret_cast<uint4*>(dx)[i] = f_to_chunk(acc, (const T*)nullptr);
+  }
+}
+
+// ------------------------------------------------------------------------------ softmax
+// one wave per sample row
+template <typename GT>
+__global__ void softmax_output_kernel(int batch, int ncls, int ld, const float* __restrict__ logits,
+                                      const float* __restrict__ label, float* __restrict__ prob,
+                                      GT* __restrict__ dlogits, float grad_scale, float* __restrict__ stats) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+  if (row >= batch) return;
+  const float* z = logits + (int64_t)row * ld;
+  float mx = -INFINITY;
+  for (int j = lane; j < ncls; j += 64) mx = fmaxf(mx, z[j]);
+  mx = wave_max(mx);
+  float sum = 0.f;
+  for (int j = lane; j < ncls; j += 64) sum += __expf(z[j] - mx);
+  sum = wave_sum(sum);
+  const float inv = 1.f / sum;
+  const int lab = (int)label[row];
+  const float zl = (lab >= 0 && lab < ncls) ? z[lab] : -INFINITY;
+  float greater = 0.f, equal_before = 0.f;
+  for (int j = lane; j < ld; j += 64) {
+    if (j < ncls) {
+      const float pj = __expf(z[j] - mx) * inv;
+      if (prob) prob[(int64_t)row * ncls + j] = pj;
+      const float gj = grad_scale * (pj - (j == lab ? 1.f : 0.f));
+      if (dlogits) dlogits[(int64_t)row * ld + j] = from_f<GT>(gj);
+      greater += z[j] > zl ? 1.f : 0.f;
+      equal_before += (z[j] == zl && j < lab) ? 1.f : 0.f;
+    } else if (dlogits) {
+      dlogits[(int64_t)row * ld + j] = from_f<GT>(0.f);
+    }
+  }
+  greater = wave_sum(greater);
+  equal_before = wave_sum(equal_before);
+  if (lane == 0 && stats) {
+    const float logp = zl - mx - __logf(sum);
+    atomicAdd(stats + 0, -logp);
+    atomicAdd(stats + 1, (greater == 0.f && equal_before == 0.f) ? 1.f : 0.f);
+    atomicAdd(stats + 2, greater < 5.f ? 1.f : 0.f);
+  }
+}
+
+template <typename T>
+__global__ void col_sum_kernel(int64_t m, int c, int ld, const T* __restrict__ x, float* __restrict__ out,
+                               int accumulate) {
+  const int j = blockIdx.x;
+  float acc = 0.f;
+  for (int64_t i = threadIdx.x; i < m; i += blockDim.x) acc += to_f(x[i * ld + j]);
+  __shared__ float red[256];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[j] = accumulate ? out[j] + red[0] : red[0];
+}
+
+// ------------------------------------------------------------------------------ SGD
+template <typename LT>
+__global__ void sgd_mom_kernel(const int64_t* __restrict__ offs, const int64_t* __restrict__ numels,
+                               const float* __restrict__ wds, float* __restrict__ w, const float* __restrict__ g,
+                               float* __restrict__ mom, LT* __restrict__ wl, float lr, const float* lr_dev,
+                               float momentum, float rescale, float clip) {
+  const int t = blockIdx.y;
+  const int64_t off = offs[t], n = numels[t];
+  const float wd = wds[t];
+  const float lrv = lr_dev ? *lr_dev : lr;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = off + i;
+    float gr = rescale * g[k];
+    if (clip > 0.f) gr = fminf(fmaxf(gr, -clip), clip);
+    const float wv = w[k];
+    const float mv = momentum * mom[k] - lrv * (gr + wd * wv);
+    mom[k] = mv;
+    const float nw = wv + mv;
+    w[k] = nw;
+    if (wl) wl[k] = from_f<LT>(nw);
+  }
+}
+
+// ------------------------------------------------------------------------------ layout / casts
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(int n, int c, int h, int w, int cpad, const float* __restrict__ src,
+                                    T* __restrict__ dst) {
+  const int64_t total = (int64_t)n * h * w * cpad;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int cc = (int)(i % cpad);
+    const int64_t pix = i / cpad;
+    const int ww = (int)(pix % w);
+    const int hh = (int)((pix / w) % h);
+    const int nn = (int)(pix / ((int64_t)w * h));
+    const float v = cc < c ? src[(((int64_t)nn * c + cc) * h + hh) * w + ww] : 0.f;
+    dst[i] = from_f<T>(v);
+  }
+}
+
+template <typename S, typename D>
+__global__ void cast_kernel(int64_t n, const S* __restrict__ src, D* __restrict__ dst) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = from_f<D>(to_f(src[i]));
+}
+
+// 16-byte chunks; n must be a multiple of the chunk (activation buffers always are)
+template <typename T, bool RELU>
+__global__ void add_kernel(int64_t nchunk, const T* a, const T* b, T* dst) {
+  constexpr int CE = 16 / sizeof(T);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nchunk; i += (int64_t)gridDim.x * blockDim.x) {
+    float fa[CE], fb[CE];
+    chunk_to_f(reinterpret_cast<const uint4*>(a)[i], fa, (const T*)nullptr);
+    if (b) chunk_to_f(reinterpret_cast<const uint4*>(b)[i], fb, (const T*)nullptr);
+#pragma unroll
+    for (int e = 0; e < CE; ++e) {
+      float v = b ? fa[e] + fb[e] : fa[e];
+      fa[e] = RELU ? fmaxf(v, 0.f) : v;
+    }
+    reinterpret_cast<uint4*>(dst)[i] = f_to_chunk(fa, (const T*)nullptr);
+  }
+}
+template <typename T>
+__global__ void relu_bwd_kernel(int64_t nchunk, const T* __restrict__ y, const T* __restrict__ dy, T* __restrict__ dx,
+                                const T* __restrict__ add) {
+  constexpr int CE = 16 / sizeof(T);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nchunk; i += (int64_t)gridDim.x * blockDim.x) {
+    float fy[CE], fd[CE], fa[CE];
+    chunk_to_f(reinterpret_cast<const uint4*>(y)[i], fy, (const T*)nullptr);
+    chunk_to_f(reinterpret_cast<const uint4*>(dy)[i], fd, (const T*)nullptr);
+    if (add) chunk_to_f(reinterpret_cast<const uint4*>(add)[i], fa, (const T*)nullptr);
+#pragma unroll
+    for (int e = 0; e < CE; ++e) {
+      float v = fy[e] > 0.f ? fd[e] : 0.f;
+      fd[e] = add ? v + fa[e] : v;
+    }
+    reinterpret_cast<uint4*>(dx)[i] = f_to_chunk(fd, (const T*)nullptr);
+  }
+}
+
+// ------------------------------------------------------------------------------ int8 quant
+template <typename T>
+__global__ void absmax_kernel(int64_t n, const T* __restrict__ x, float* __restrict__ out) {
+  float m = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(to_f(x[i])));
+  m = wave_max(m);
+  // non-negative floats order like their bit patterns
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(out), __float_as_uint(m));
+}
+__global__ void quant_state_kernel(const float* __restrict__ curmax, float* minmax, int is_weight, int is_train,
+                                   float decay, int first, float* __restrict__ thr) {
+  float t;
+  if (is_weight) {
+    t = *curmax;
+    if (is_train && minmax) *minmax = t;
+  } else {
+    if (is_train) {
+      const float nv = first ? *curmax : (*minmax) * decay + (*curmax) * (1.f - decay);
+      *minmax = nv;
+    }
+    t = *minmax;
+  }
+  *thr = t;
+}
+template <typename T>
+__global__ void quant_apply_kernel(int64_t n, const T* __restrict__ x, T* __restrict__ out,
+                                   const float* __restrict__ thr, float qmax, int clip) {
+  const float t = *thr;
+  const float unit = t / qmax;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = to_f(x[i]);
+    if (clip) v = fminf(fmaxf(v, -t), t);
+    // mx.nd.round: half away from zero
+    const float qv = unit > 0.f ? roundf(v / unit) * unit : 0.f;
+    out[i] = from_f<T>(qv);
+  }
+}
+template <typename T>
+__global__ void quant_bwd_kernel(int64_t n, const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx,
+                                 const float* __restrict__ minmax, int is_weight, const T* __restrict__ add) {
+  const float t = (is_weight || !minmax) ? INFINITY : *minmax;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const float xv = to_f(x[i]);
+    float g = to_f(dy[i]);
+    if (!is_weight && !(xv > -t && xv < t)) g = 0.f;
+    if (add) g += to_f(add[i]);
+    dx[i] = from_f<T>(g);
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* rn_last_error(void) { return g_last_error.c_str(); }
+int32_t rn_version(void) { return 100; }
+int32_t rn_device_cu_count(void) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return -1;
+  return prop.multiProcessorCount;
+}
+
+int rn_pool_desc_init(rn_pool_desc* d) {
+  RN_CHECK_ARG(d != nullptr, "null desc");
+  RN_CHECK_ARG(d->dtype == RN_BF16 || d->dtype == RN_F32, "bad dtype");
+  RN_CHECK_ARG(d->n > 0 && d->h > 0 && d->w > 0 && d->c > 0 && d->c % 8 == 0, "bad shape");
+  RN_CHECK_ARG(d->type == RN_POOL_MAX || d->type == RN_POOL_AVG, "bad pool type");
+  if (d->global_pool) {
+    d->r = d->h; d->s = d->w; d->stride_h = d->stride_w = 1; d->pad_h = d->pad_w = 0;
+  }
+  RN_CHECK_ARG(d->r > 0 && d->s > 0 && d->stride_h > 0 && d->stride_w > 0, "bad window");
+  RN_CHECK_ARG(d->r * d->s <= 255, "window too large");
+  d->p = (d->h + 2 * d->pad_h - d->r) / d->stride_h + 1;
+  d->q = (d->w + 2 * d->pad_w - d->s) / d->stride_w + 1;
+  RN_CHECK_ARG(d->p > 0 && d->q > 0, "empty output");
+  return 0;
+}
+
+int rn_pool_fwd(const rn_pool_desc* d, const void* x, void* y, uint8_t* argmax, rn_stream_t stream) {
+  RN_CHECK_ARG(d && x && y, "null argument");
+  PoolArgs a{d->n, d->h, d->w, d->c, d->r, d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, d->p, d->q, d->type};
+  hipStream_t st = as_stream(stream);
+  const int64_t total = (int64_t)d->n * d->p * d->q * d->c / 8;
+  if (d->dtype == RN_BF16)
+    hipLaunchKernelGGL(pool_fwd_kernel<bf16_t>, dim3(grid1d(total)), dim3(256), 0, st, a, (const bf16_t*)x,
+                       (bf16_t*)y, argmax);
+  else
+    hipLaunchKernelGGL(pool_fwd_kernel<float>, dim3(grid1d(total * 2)), dim3(256), 0, st, a, (const float*)x,
+                       (float*)y, argmax);
+  return rn_check_launch("pool_fwd");
+}
+
+int rn_pool_bwd(const rn_pool_desc* d, const void* dy, const uint8_t* argmax, void* dx, const void* add_src,
+                rn_stream_t stream) {
+  RN_CHECK_ARG(d && dy && dx, "null argument");
+  RN_CHECK_ARG(d->type != RN_POOL_MAX || argmax, "max pool backward needs argmax");
+  PoolArgs a{d->n, d->h, d->w, d->c, d->r, d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, d->p, d->q, d->type};
+  hipStream_t st = as_stream(stream);
+  const int64_t total = (int64_t)d->n * d->h * d->w * d->c / 8;
+  if (d->dtype == RN_BF16)
+    hipLaunchKernelGGL(pool_bwd_kernel<bf16_t>, dim3(grid1d(total)), dim3(256), 0, st, a, (const bf16_t*)dy,
+                       argmax, (bf16_t*)dx, (const bf16_t*)add_src);
+  else
+    hipLaunchKernelGGL(pool_bwd_kernel<float>, dim3(grid1d(total * 2)), dim3(256), 0, st, a, (const float*)dy,
+                       argmax, (float*)dx, (const float*)add_src);
+  return rn_check_launch("pool_bwd");
+}
+
+int rn_softmax_output(int32_t grad_dtype, int32_t batch, int32_t ncls, int32_t ld, const float* logits,
+                      const float* label, float* prob, void* dlogits, float grad_scale, float* stats,
+                      rn_stream_t stream) {
+  RN_CHECK_ARG(logits && label && batch > 0 && ncls > 0 && ld >= ncls, "bad arguments");
+  hipStream_t st = as_stream(stream);
+  const int rows_per_block = 4;
+  dim3 grid((batch + rows_per_block - 1) / rows_per_block);
+  if (grad_dtype == RN_BF16)
+    hipLaunchKernelGGL(softmax_output_kernel<bf16_t>, grid, dim3(256), 0, st, batch, ncls, ld, logits, label, prob,
+                       (bf16_t*)dlogits, grad_scale, stats);
+  else
+    hipLaunchKernelGGL(softmax_output_kernel<float>, grid, dim3(256), 0, st, batch, ncls, ld, logits, label, prob,
+                       (float*)dlogits, grad_scale, stats);
+  return rn_check_launch("softmax_output");
+}
+
+int rn_col_sum(int32_t dtype, int64_t m, int32_t c, int32_t ld, const void* x, float* out, int32_t accumulate,
+               rn_stream_t stream) {
+  RN_CHECK_ARG(x && out && m > 0 && c > 0 && ld >= c, "bad arguments");
+  hipStream_t st = as_stream(stream);
+  if (dtype == RN_BF16)
+    hipLaunchKernelGGL(col_sum_kernel<bf16_t>, dim3(c), dim3(256), 0, st, m, c, ld, (const bf16_t*)x, out, accumulate);
+  else
+    hipLaunchKernelGGL(col_sum_kernel<float>, dim3(c), dim3(256), 0, st, m, c, ld, (const float*)x, out, accumulate);
+  return rn_check_launch("col_sum");
+}
+
+int rn_sgd_mom_update(int32_t ntensors, const int64_t* offsets, const int64_t* numels, const float* wds, float* w,
+                      const float* g, float* mom, void* w_lowp, int32_t lowp_dtype, float lr, const float* lr_dev,
+                      float momentum, float rescale_grad, float clip, rn_stream_t stream) {
+  RN_CHECK_ARG(ntensors > 0 && offsets && numels && wds && w && g && mom, "bad arguments");
+  RN_CHECK_ARG(ntensors <= 65535, "too many tensors");
+  hipStream_t st = as_stream(stream);
+  dim3 grid(64, ntensors);
+  if (w_lowp && lowp_dtype == RN_BF16)
+    hipLaunchKernelGGL(sgd_mom_kernel<bf16_t>, grid, dim3(256), 0, st, offsets, numels, wds, w, g, mom,
+                       (bf16_t*)w_lowp, lr, lr_dev, momentum, rescale_grad, clip);
+  else
+    hipLaunchKernelGGL(sgd_mom_kernel<float>, grid, dim3(256), 0, st, offsets, numels, wds, w, g, mom,
+                       (float*)w_lowp, lr, lr_dev, momentum, rescale_grad, clip);
+  return rn_check_launch("sgd_mom_update");
+}
+
+int rn_nchw_to_nhwc(int32_t n, int32_t c, int32_t h, int32_t w, int32_t c_pad, const float* src, void* dst,
+                    int32_t dst_dtype, rn_stream_t stream) {
+  RN_CHECK_ARG(src && dst && c_pad >= c, "bad arguments");
+  hipStream_t st = as_stream(stream);
+  const int64_t total = (int64_t)n * h * w * c_pad;
+  if (dst_dtype == RN_BF16)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16_t>, dim3(grid1d(total)), dim3(256), 0, st, n, c, h, w, c_pad, src,
+                       (bf16_t*)dst);
+  else
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3(grid1d(total)), dim3(256), 0, st, n, c, h, w, c_pad, src,
+                       (float*)dst);
+  return rn_check_launch("nchw_to_nhwc");
+}
+
+int rn_cast(int64_t n, const void* src, int32_t sd, void* dst, int32_t dd, rn_stream_t stream) {
+  RN_CHECK_ARG(src && dst && n >= 0, "bad arguments");
+  if (n == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  dim3 g(grid1d(n)), b(256);
+  if (sd == RN_F32 && dd == RN_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, bf16_t>), g, b, 0, st, n, (const float*)src, (bf16_t*)dst);
+  else if (sd == RN_BF16 && dd == RN_F32)
+    hipLaunchKernelGGL((cast_kernel<bf16_t, float>), g, b, 0, st, n, (const bf16_t*)src, (float*)dst);
+  else if (sd == RN_F32 && dd == RN_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), g, b, 0, st, n, (const float*)src, (float*)dst);
+  else
+    hipLaunchKernelGGL((cast_kernel<bf16_t, bf16_t>), g, b, 0, st, n, (const bf16_t*)src, (bf16_t*)dst);
+  return rn_check_launch("cast");
+}
+
+int rn_eltwise_add(int64_t n, int32_t dtype, const void* a, const void* b, void* dst, int32_t relu,
+                   rn_stream_t stream) {
+  RN_CHECK_ARG(a && dst && n >= 0, "bad arguments");
+  const int CE = dtype == RN_BF16 ? 8 : 4;
+  RN_CHECK_ARG(n % CE == 0, "n must be a multiple of the 16-byte chunk");
+  if (n == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  const int64_t nc = n / CE;
+  dim3 g(grid1d(nc)), bl(256);
+  if (dtype == RN_BF16) {
+    if (relu) hipLaunchKernelGGL((add_kernel<bf16_t, true>), g, bl, 0, st, nc, (const bf16_t*)a, (const bf16_t*)b, (bf16_t*)dst);
+    else hipLaunchKernelGGL((add_kernel<bf16_t, false>), g, bl, 0, st, nc, (const bf16_t*)a, (const bf16_t*)b, (bf16_t*)dst);
+  } else {
+    if (relu) hipLaunchKernelGGL((add_kernel<float, true>), g, bl, 0, st, nc, (const float*)a, (const float*)b, (float*)dst);
+    else hipLaunchKernelGGL((add_kernel<float, false>), g, bl, 0, st, nc, (const float*)a, (const float*)b, (float*)dst);
+  }
+  return rn_check_launch("eltwise_add");
+}
+
+int rn_relu_bwd(int64_t n, int32_t dtype, const void* y, const void* dy, void* dx, const void* add_src,
+                rn_stream_t stream) {
+  RN_CHECK_ARG(y && dy && dx && n >= 0, "bad arguments");
+  const int CE = dtype == RN_BF16 ? 8 : 4;
+  RN_CHECK_ARG(n % CE == 0, "n must be a multiple of the 16-byte chunk");
+  if (n == 0) return 0;
+  hipStream_t st = as_stream(stream);
+  const int64_t nc = n / CE;
+  if (dtype == RN_BF16)
+    hipLaunchKernelGGL(relu_bwd_kernel<bf16_t>, dim3(grid1d(nc)), dim3(256), 0, st, nc, (const bf16_t*)y,
+                       (const bf16_t*)dy, (bf16_t*)dx, (const bf16_t*)add_src);
+  else
+    hipLaunchKernelGGL(relu_bwd_kernel<float>, dim3(grid1d(nc)), dim3(256), 0, st, nc, (const float*)y,
+                       (const float*)dy, (float*)dx, (const float*)add_src);
+  return rn_check_launch("relu_bwd");
+}
+
+int rn_quant_int8_fwd(int32_t dtype, int64_t n, const void* x, void* out, float* minmax, int32_t is_weight,
+                      int32_t is_train, float ema_decay, int32_t first_batch, int32_t nbits, float* ws,
+                      rn_stream_t stream) {
+  RN_CHECK_ARG(x && out && ws && n > 0, "bad arguments");
+  RN_CHECK_ARG(is_weight || minmax, "activation quantization needs the minmax state");
+  RN_CHECK_ARG(nbits >= 2 && nbits <= 16, "bad nbits");
+  hipStream_t st = as_stream(stream);
+  const float qmax = (float)((1 << (nbits - 1)) - 1);
+  float* curmax = ws;
+  float* thr = ws + 1;
+  hipMemsetAsync(curmax, 0, sizeof(float), st);
+  const bool need_max = is_weight || is_train;
+  if (need_max) {
+    if (dtype == RN_BF16)
+      hipLaunchKernelGGL(absmax_kernel<bf16_t>, dim3(grid1d(n, 256, 1024)), dim3(256), 0, st, n, (const bf16_t*)x,
+                         curmax);
+    else
+      hipLaunchKernelGGL(absmax_kernel<float>, dim3(grid1d(n, 256, 1024)), dim3(256), 0, st, n, (const float*)x,
+                         curmax);
+  }
+  hipLaunchKernelGGL(quant_state_kernel, dim3(1), dim3(1), 0, st, curmax, minmax, is_weight, is_train, ema_decay,
+                     first_batch, thr);
+  const int clip = is_weight ? 0 : 1;
+  if (dtype == RN_BF16)
+    hipLaunchKernelGGL(quant_apply_kernel<bf16_t>, dim3(grid1d(n)), dim3(256), 0, st, n, (const bf16_t*)x,
+                       (bf16_t*)out, thr, qmax, clip);
+  else
+    hipLaunchKernelGGL(quant_apply_kernel<float>, dim3(grid1d(n)), dim3(256), 0, st, n, (const float*)x,
+                       (float*)out, thr, qmax, clip);
+  return rn_check_launch("quant_int8_fwd");
+}
+
+int rn_quant_int8_bwd(int32_t dtype, int64_t n, const void* x, const void* dy, void* dx, const float* minmax,
+                      int32_t is_weight, const void* add_src, rn_stream_t stream) {
+  RN_CHECK_ARG(x && dy && dx && n > 0, "bad arguments");
+  hipStream_t st = as_stream(stream);
+  if (dtype == RN_BF16)
+    hipLaunchKernelGGL(quant_bwd_kernel<bf16_t>, dim3(grid1d(n)), dim3(256), 0, st, n, (const bf16_t*)x,
+                       (const bf16_t*)dy, (bf16_t*)dx, minmax, is_weight, (const bf16_t*)add_src);
+  else
+    hipLaunchKernelGGL(quant_bwd_kernel<float>, dim3(grid1d(n)), dim3(256), 0, st, n, (const float*)x,
+                       (const float*)dy, (float*)dx, minmax, is_weight, (const float*)add_src);
+  return rn_check_launch("quant_int8_bwd");
+}
+
+}  // extern "C"

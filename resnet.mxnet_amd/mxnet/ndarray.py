@@ -1,0 +1,146 @@
+"""mx.nd: a minimal NDArray over numpy (host) or a torch tensor (device).
+
+Covers what the reference's hot path touches: mx.nd.array(..., ctx=cpu_pinned) in the synthetic
+iterator (data/imagenet.py:17-18), asnumpy() on outputs/labels in metrics, waitall(), save/load of
+parameter dicts for checkpoints. Math helpers used only inside Python CustomOps are not provided.
+"""
+import numpy as np
+
+from .context import Context, cpu
+
+
+class NDArray:
+    def __init__(self, data, ctx=None):
+        self._data = data  # numpy array or torch tensor
+        self._ctx = ctx or cpu()
+
+    # --- properties
+    @property
+    def shape(self):
+        return tuple(self._data.shape)
+
+    @property
+    def dtype(self):
+        if isinstance(self._data, np.ndarray):
+            return self._data.dtype.type
+        return np.float32
+
+    @property
+    def context(self):
+        return self._ctx
+
+    ctx = context
+
+    @property
+    def size(self):
+        return int(np.prod(self.shape))
+
+    @property
+    def ndim(self):
+        return len(self.shape)
+
+    def _torch(self):
+        import torch
+        if isinstance(self._data, np.ndarray):
+            t = torch.from_numpy(np.ascontiguousarray(self._data))
+            if self._ctx.device_type == "cpu_pinned":
+                t = t.pin_memory()
+                self._data = t
+            return t
+        return self._data
+
+    def asnumpy(self):
+        if isinstance(self._data, np.ndarray):
+            return self._data
+        return self._data.detach().float().cpu().numpy().reshape(self.shape)
+
+    def asscalar(self):
+        return self.asnumpy().reshape(-1)[0]
+
+    def astype(self, dtype, copy=True):
+        return NDArray(self.asnumpy().astype(dtype), self._ctx)
+
+    def copy(self):
+        return NDArray(np.array(self.asnumpy()), self._ctx)
+
+    def copyto(self, other):
+        if isinstance(other, Context):
+            return NDArray(np.array(self.asnumpy()), other)
+        other[:] = self
+        return other
+
+    as_in_context = copyto
+
+    def wait_to_read(self):
+        if not isinstance(self._data, np.ndarray):
+            import torch
+            torch.cuda.synchronize()
+
+    def reshape(self, *shape):
+        if len(shape) == 1 and isinstance(shape[0], (tuple, list)):
+            shape = shape[0]
+        return NDArray(self.asnumpy().reshape(shape), self._ctx)
+
+    def __getitem__(self, k):
+        return NDArray(self.asnumpy()[k], self._ctx)
+
+    def __setitem__(self, k, v):
+        v = v.asnumpy() if isinstance(v, NDArray) else v
+        if isinstance(self._data, np.ndarray):
+            self._data[k] = v
+        else:
+            import torch
+            if k == slice(None):
+                self._data.copy_(torch.as_tensor(np.asarray(v, dtype=np.float32)).reshape(self._data.shape))
+            else:
+                arr = self.asnumpy().copy()
+                arr[k] = v
+                self._data.copy_(torch.as_tensor(arr).reshape(self._data.shape))
+
+    def __len__(self):
+        return self.shape[0]
+
+    def __repr__(self):
+        return "\n%s\n<NDArray %s @%s>" % (self.asnumpy(), "x".join(map(str, self.shape)), self._ctx)
+
+
+def array(source, ctx=None, dtype=None):
+    a = source.asnumpy() if isinstance(source, NDArray) else np.asarray(source)
+    a = np.array(a, dtype=dtype if dtype is not None else (a.dtype if a.dtype != np.float64 else np.float32))
+    return NDArray(a, ctx)
+
+
+def zeros(shape, ctx=None, dtype=np.float32):
+    return NDArray(np.zeros(shape, dtype=dtype), ctx)
+
+
+def ones(shape, ctx=None, dtype=np.float32):
+    return NDArray(np.ones(shape, dtype=dtype), ctx)
+
+
+def empty(shape, ctx=None, dtype=np.float32):
+    return zeros(shape, ctx, dtype)
+
+
+def waitall():
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+    except ImportError:
+        pass
+
+
+def concatenate(arrays, axis=0):
+    return NDArray(np.concatenate([a.asnumpy() for a in arrays], axis=axis), arrays[0].context)
+
+
+def save(fname, data):
+    """Parameter dict / list -> file (an .npz container keyed like MXNet's 'arg:' / 'aux:')."""
+    from .model import _save_params
+    _save_params(fname, data)
+
+
+def load(fname):
+    from .model import _load_params
+    return _load_params(fname)

@@ -1,0 +1,923 @@
+"""Lower an mx.sym graph onto librn and run training steps on one MI355X.
+
+This replaces what MXNet's Module/executor did under core/solver.py (bind :75,
+forward :115, backward :116, update :121): shape inference, buffer allocation, op dispatch,
+gradient fan-in accumulation (req='add') and the optimizer step -- all as a static plan of
+C-ABI calls on one HIP stream.
+
+Planning (`Plan`) is pure Python and runs without a GPU (it is what the CPU tests check).
+`Executor` allocates device memory through PyTorch (plumbing only) and turns the plan into
+lists of bound C calls. Every compute op is a librn kernel; there is no fallback path.
+
+Layout: activations NHWC, channel stride padded to a multiple of 8, dtype bf16 (default) or
+fp32 (`dtype='float32'`, exact-fp32 MFMA path used for parity). Parameters live in ONE flat
+fp32 master buffer (conv / FC weights in KRSC), ordered in reverse forward order so that
+gradient buckets complete front-to-back during backward (RCCL bucketing, rn/dist.py).
+"""
+import math
+
+import numpy as np
+
+from . import lib as L
+
+F32, BF16 = L.RN_F32, L.RN_BF16
+
+
+def _pad8(c):
+    return (c + 7) // 8 * 8
+
+
+def _parse(v, default=None):
+    from mxnet.symbol import _parse as p  # the shim's attr parser
+    return p(v) if v is not None else default
+
+
+def _tup(v, n=2):
+    from mxnet.symbol import _tup as t
+    return t(v, n)
+
+
+class PlanError(RuntimeError):
+    pass
+
+
+# ============================================================================= plan (CPU)
+class TensorSpec:
+    """An activation tensor: logical NCHW (or (N,F)) shape -> NHWC buffer with padded C."""
+
+    def __init__(self, name, shape, dtype, needs_grad=True, kind="act"):
+        self.name = name
+        self.shape = tuple(shape)
+        if len(shape) == 4:
+            self.n, self.c, self.h, self.w = shape
+        elif len(shape) == 2:
+            self.n, self.c = shape
+            self.h = self.w = 1
+        else:
+            raise PlanError("unsupported activation rank for %s: %s" % (name, shape))
+        self.cp = _pad8(self.c)
+        self.dtype = dtype
+        self.needs_grad = needs_grad
+        self.kind = kind  # act | logits | prob | data_nchw | label
+
+    @property
+    def rows(self):
+        return self.n * self.h * self.w
+
+    @property
+    def numel(self):
+        if self.kind in ("data_nchw", "prob", "label"):
+            return int(np.prod(self.shape))
+        return self.rows * self.cp
+
+
+class PlanOp:
+    def __init__(self, kind, name, **kw):
+        self.kind = kind
+        self.name = name
+        self.__dict__.update(kw)
+
+    def __repr__(self):
+        return "<%s %s>" % (self.kind, self.name)
+
+
+class Plan:
+    """Fused op list for a symbol at fixed input shapes."""
+
+    def __init__(self, symbol, data_shapes, label_shapes=(), dtype="bfloat16", for_training=True):
+        self.symbol = symbol
+        self.dtype = BF16 if dtype in ("bfloat16", "bf16", BF16) else F32
+        self.for_training = for_training
+        self.data_names = [n for n, _ in data_shapes]
+        self.label_names = [n for n, _ in label_shapes]
+        known = dict(list(data_shapes) + list(label_shapes))
+        self.input_shapes = known
+        self.topo = symbol._topo()
+        self._infer(known)
+        self.arg_names = symbol.list_arguments()
+        self.aux_names = symbol.list_auxiliary_states()
+        self.param_names = [n for n in self.arg_names if n not in known]
+        self.tensors = {}
+        self.alias = {}
+        self.ops = []
+        self._lower()
+
+    # --- shapes of every node output
+    def _infer(self, known):
+        from mxnet.symbol import _infer_node, _parse as parse
+        shapes = {}
+        for n in self.topo:
+            if n.op == "null":
+                if n.name in known:
+                    shapes[(id(n), 0)] = tuple(known[n.name])
+                elif "__shape__" in n.attrs:
+                    shapes[(id(n), 0)] = tuple(parse(n.attrs["__shape__"]))
+        for n in self.topo:
+            if n.op != "null":
+                _infer_node(n, shapes, False)
+        self.shapes = shapes
+
+    def shape_of(self, node, idx=0):
+        return self.shapes[(id(node), idx)]
+
+    def param_shape(self, name):
+        for n in self.topo:
+            if n.op == "null" and n.name == name:
+                return self.shapes[(id(n), 0)]
+        raise KeyError(name)
+
+    # --- helpers
+    def _consumers(self):
+        cons = {}
+        for n in self.topo:
+            for (i, _) in n.inputs:
+                cons.setdefault(id(i), []).append(n)
+        for n, _ in self.symbol._outputs:
+            cons.setdefault(id(n), []).append(None)  # graph output
+        return cons
+
+    def tensor(self, node):
+        key = id(node)
+        while key in self.alias:
+            key = self.alias[key]
+        return self.tensors[key]
+
+    def _new_tensor(self, node, shape, dtype=None, kind="act", needs_grad=True):
+        t = TensorSpec(node.name, shape, self.dtype if dtype is None else dtype, needs_grad, kind)
+        self.tensors[id(node)] = t
+        return t
+
+    def _var_input(self, node):
+        """Follow identity/Cast/Flatten aliases back; return (node, is_variable)."""
+        while node.op in ("identity", "Cast", "Flatten"):
+            node = node.inputs[0][0]
+        return node
+
+    # --- lowering
+    def _lower(self):
+        cons = self._consumers()
+        topo = self.topo
+        done = set()
+        order = {id(n): i for i, n in enumerate(topo)}
+        data_vars = set(self.data_names)
+        # data / label inputs
+        for n in topo:
+            if n.op == "null" and n.name in data_vars:
+                shp = self.shape_of(n)
+                t = TensorSpec(n.name, shp, F32, needs_grad=False, kind="data_nchw")
+                self.tensors[id(n)] = t
+                self.data_tensor = t
+            elif n.op == "null" and n.name in self.label_names:
+                self.tensors[id(n)] = TensorSpec(n.name, (self.shape_of(n)[0], 1), F32, False, "label")
+        # pre-pass: fused residual adds (conv output consumed only by an add)
+        fused_add_into = {}  # id(conv node) -> (add node, other input node)
+        fused_add_relu = {}  # id(add node) -> relu node
+        for n in topo:
+            if n.op in ("_Plus", "elemwise_add", "ElementWiseSum") and len(n.inputs) == 2:
+                a, b = n.inputs[0][0], n.inputs[1][0]
+                cands = [x for x in (a, b) if x.op == "Convolution" and len(cons.get(id(x), [])) == 1
+                         and id(x) not in fused_add_into and not self._is_stem(x)]
+                if cands:
+                    conv = max(cands, key=lambda x: order[id(x)])
+                    other = b if conv is a else a
+                    if order[id(other)] < order[id(conv)] or other.op == "null":
+                        fused_add_into[id(conv)] = (n, other)
+                        continue
+                cl = cons.get(id(n), [])
+                if len(cl) == 1 and cl[0] is not None and cl[0].op == "Activation" and \
+                        _parse(cl[0].attrs.get("act_type")) == "relu":
+                    fused_add_relu[id(n)] = cl[0]
+        for n in topo:
+            if n.op == "null" or id(n) in done:
+                continue
+            op = n.op
+            if op in ("identity", "Flatten", "Cast"):
+                # Cast is a no-op under the runtime precision policy (bf16 / fp32 compute)
+                src = n.inputs[0][0]
+                if op == "Flatten":
+                    st = self.tensor(src)
+                    if st.kind == "act" and (st.h != 1 or st.w != 1):
+                        raise PlanError("Flatten of a spatial map (%s) is not supported" % n.name)
+                self.alias[id(n)] = id(src) if id(src) not in self.alias else self.alias[id(src)]
+                done.add(id(n))
+            elif op == "Convolution":
+                self._lower_conv(n, cons, fused_add_into.get(id(n)))
+                done.add(id(n))
+                if id(n) in fused_add_into:
+                    addn = fused_add_into[id(n)][0]
+                    self.alias[id(addn)] = id(n)
+                    done.add(id(addn))
+            elif op == "BatchNorm":
+                cl = cons.get(id(n), [])
+                relu_node = None
+                if len(cl) == 1 and cl[0] is not None and cl[0].op == "Activation" and \
+                        _parse(cl[0].attrs.get("act_type")) == "relu":
+                    relu_node = cl[0]
+                src = self._var_input(n.inputs[0][0])
+                stem_consumers = [c for c in cl if c is not None and c.op == "Convolution" and self._is_stem(c)]
+                if src.op == "null" and src.name in data_vars and stem_consumers and len(cl) == 1:
+                    done.add(id(n))  # folded into the stem conv (bn_data)
+                    continue
+                self._lower_bn(n, relu_node)
+                done.add(id(n))
+                if relu_node is not None:
+                    self.alias[id(relu_node)] = id(n)
+                    done.add(id(relu_node))
+            elif op == "Activation":
+                act = _parse(n.attrs.get("act_type"))
+                if act != "relu":
+                    raise PlanError("Activation %s is not supported" % act)
+                x = self.tensor(n.inputs[0][0])
+                y = self._new_tensor(n, self.shape_of(n))
+                self.ops.append(PlanOp("relu", n.name, x=x, y=y))
+                done.add(id(n))
+            elif op in ("_Plus", "elemwise_add", "ElementWiseSum"):
+                if len(n.inputs) != 2:
+                    raise PlanError("ElementWiseSum with %d inputs not supported" % len(n.inputs))
+                a = self.tensor(n.inputs[0][0])
+                b = self.tensor(n.inputs[1][0])
+                relu_node = fused_add_relu.get(id(n))
+                y = self._new_tensor(n, self.shape_of(n))
+                self.ops.append(PlanOp("add", n.name, a=a, b=b, y=y, relu=relu_node is not None))
+                done.add(id(n))
+                if relu_node is not None:
+                    self.alias[id(relu_node)] = id(n)
+                    done.add(id(relu_node))
+            elif op == "Pooling":
+                self._lower_pool(n)
+                done.add(id(n))
+            elif op == "FullyConnected":
+                self._lower_fc(n)
+                done.add(id(n))
+            elif op == "SoftmaxOutput":
+                x = self.tensor(n.inputs[0][0])
+                if x.kind != "logits":
+                    raise PlanError("SoftmaxOutput must follow FullyConnected")
+                lab = self.tensors[id(n.inputs[1][0])]
+                y = self._new_tensor(n, (x.n, x.c), F32, kind="prob", needs_grad=False)
+                self.ops.append(PlanOp("softmax", n.name, x=x, label=lab, y=y,
+                                       grad_scale=float(_parse(n.attrs.get("grad_scale", 1.0)))))
+                done.add(id(n))
+            else:
+                raise PlanError("operator %s (%s) is not supported by the MI355X runtime" % (op, n.name))
+        self.outputs = [self.tensor(n) for n, _ in self.symbol._outputs]
+
+    def _is_stem(self, conv_node):
+        src = conv_node.inputs[0][0]
+        shp = self.shape_of(src)
+        return len(shp) == 4 and shp[1] % 8 != 0
+
+    def _param_node(self, node, idx):
+        p = node.inputs[idx][0]
+        if p.op != "null":
+            raise PlanError("%s: computed weights are not supported" % node.name)
+        return p.name
+
+    def _conv_attrs(self, n):
+        k = _tup(n.attrs["kernel"])
+        st = _tup(n.attrs.get("stride", (1, 1))) or (1, 1)
+        pd = _tup(n.attrs.get("pad", (0, 0))) or (0, 0)
+        dl = _tup(n.attrs.get("dilate", (1, 1))) or (1, 1)
+        g = int(_parse(n.attrs.get("num_group", 1)))
+        if dl != (1, 1):
+            raise PlanError("%s: dilation not supported" % n.name)
+        return k, st, pd, g
+
+    def _lower_conv(self, n, cons, fused):
+        k, st, pd, g = self._conv_attrs(n)
+        if g != 1:
+            raise PlanError("%s: grouped convolution (num_group=%d) is not supported yet" % (n.name, g))
+        xshape = self.shape_of(n.inputs[0][0])
+        yshape = self.shape_of(n)
+        wname = self._param_node(n, 1)
+        if not _parse(n.attrs.get("no_bias", False)):
+            raise PlanError("%s: convolution bias not supported" % n.name)
+        y = self._new_tensor(n, yshape)
+        if self._is_stem(n):
+            src = self._var_input(n.inputs[0][0])
+            bn = None
+            if src.op == "BatchNorm":
+                bn = src
+                src = self._var_input(bn.inputs[0][0])
+                if not _parse(bn.attrs.get("fix_gamma", True)):
+                    raise PlanError("stem BatchNorm must have fix_gamma=True")
+            if not (src.op == "null" and src.name in self.data_names):
+                raise PlanError("%s: a conv over %d channels must read the data input" % (n.name, xshape[1]))
+            kc = _pad8(k[0] * k[1] * xshape[1])
+            kc = (kc + 31) // 32 * 32
+            op = PlanOp("stem", n.name, x=self.tensors[id(src)], y=y, weight=wname, kernel=k, stride=st, pad=pd,
+                        kc=kc, bn=None)
+            if bn is not None:
+                op.bn = dict(name=bn.name, gamma=self._param_node(bn, 1), beta=self._param_node(bn, 2),
+                             mean=bn.inputs[3][0].name, var=bn.inputs[4][0].name,
+                             eps=float(_parse(bn.attrs.get("eps", 1e-3))),
+                             momentum=float(_parse(bn.attrs.get("momentum", 0.9))),
+                             use_global_stats=bool(_parse(bn.attrs.get("use_global_stats", False))))
+            self.ops.append(op)
+            return
+        x = self.tensor(n.inputs[0][0])
+        if x.kind != "act":
+            raise PlanError("%s: convolution over the raw data input needs C %% 8 != 0 (stem) here" % n.name)
+        res = None
+        if fused is not None:
+            res = self.tensor(fused[1])
+        self.ops.append(PlanOp("conv", n.name, x=x, y=y, weight=wname, kernel=k, stride=st, pad=pd, res=res))
+
+    def _lower_bn(self, n, relu_node):
+        x = self.tensor(n.inputs[0][0])
+        shape = self.shape_of(n)
+        y = self._new_tensor(n, shape)
+        self.ops.append(PlanOp("bn", n.name, x=x, y=y, relu=relu_node is not None,
+                               gamma=self._param_node(n, 1), beta=self._param_node(n, 2),
+                               mean=n.inputs[3][0].name, var=n.inputs[4][0].name,
+                               eps=float(_parse(n.attrs.get("eps", 1e-3))),
+                               momentum=float(_parse(n.attrs.get("momentum", 0.9))),
+                               fix_gamma=bool(_parse(n.attrs.get("fix_gamma", True))),
+                               use_global_stats=bool(_parse(n.attrs.get("use_global_stats", False)))))
+
+    def _lower_pool(self, n):
+        x = self.tensor(n.inputs[0][0])
+        y = self._new_tensor(n, self.shape_of(n))
+        ptype = _parse(n.attrs.get("pool_type", "max"))
+        if ptype not in ("max", "avg"):
+            raise PlanError("pool_type %s not supported" % ptype)
+        glob = bool(_parse(n.attrs.get("global_pool", False)))
+        if _parse(n.attrs.get("pooling_convention", "valid")) != "valid" and not glob:
+            raise PlanError("pooling_convention other than 'valid' not supported")
+        k = _tup(n.attrs.get("kernel", (1, 1))) or (1, 1)
+        st = _tup(n.attrs.get("stride", (1, 1))) or (1, 1)
+        pd = _tup(n.attrs.get("pad", (0, 0))) or (0, 0)
+        self.ops.append(PlanOp("pool", n.name, x=x, y=y, type=ptype, global_pool=glob, kernel=k, stride=st, pad=pd))
+
+    def _lower_fc(self, n):
+        x = self.tensor(n.inputs[0][0])
+        if x.h != 1 or x.w != 1:
+            raise PlanError("%s: FullyConnected over a spatial map is not supported" % n.name)
+        nh = int(_parse(n.attrs["num_hidden"]))
+        no_bias = bool(_parse(n.attrs.get("no_bias", False)))
+        y = self._new_tensor(n, (x.n, nh), F32, kind="logits")
+        self.ops.append(PlanOp("fc", n.name, x=x, y=y, weight=self._param_node(n, 1),
+                               bias=None if no_bias else self._param_node(n, 2), nh=nh))
+
+    def summary(self):
+        kinds = {}
+        for op in self.ops:
+            kinds[op.kind] = kinds.get(op.kind, 0) + 1
+        return kinds
+
+    def train_flops(self):
+        """Algorithmic FLOP per step (2 FLOP/MAC): fwd + dgrad (except the stem) + wgrad."""
+        total = 0
+        for op in self.ops:
+            if op.kind in ("conv", "stem"):
+                y = op.y
+                cin = op.x.shape[1]
+                macs = y.n * y.h * y.w * y.c * cin * op.kernel[0] * op.kernel[1]
+                total += 2 * macs * (2 if op.kind == "stem" else 3)
+            elif op.kind == "fc":
+                total += 2 * op.x.n * op.x.c * op.nh * 3
+        return total
+
+
+# ============================================================================= executor (GPU)
+class _GradState:
+    """Gradient routing during backward-plan construction (req write/add, lazy fan-in)."""
+
+    def __init__(self, ex):
+        self.ex = ex
+        self.has_value = set()
+        self.pending = {}
+
+    def read(self, t):
+        key = id(t)
+        pend = self.pending.pop(key, [])
+        if key not in self.has_value:
+            if not pend:
+                return None
+            if len(pend) == 1:
+                return pend[0]
+            buf = self.ex.grad_buf(t)
+            self.ex._emit_bwd(("add", t.numel, pend[0], pend[1], buf))
+            pend = pend[2:]
+            self.has_value.add(key)
+        else:
+            buf = self.ex.grad_buf(t)
+        for p in pend:
+            self.ex._emit_bwd(("add", t.numel, buf, p, buf))
+        return buf
+
+    def contribute(self, t):
+        """(out_buffer, add_src) for a kernel with an add_src operand."""
+        key = id(t)
+        buf = self.ex.grad_buf(t)
+        if key in self.has_value:
+            return buf, buf
+        self.has_value.add(key)
+        pend = self.pending.get(key)
+        if pend:
+            return buf, pend.pop(0)
+        return buf, None
+
+    def alias(self, t, buf):
+        self.pending.setdefault(id(t), []).append(buf)
+
+
+class Executor:
+    """Device buffers + bound C calls for one Plan on one GPU."""
+
+    def __init__(self, plan, device, bucket_bytes=25 << 20):
+        import torch
+        self.torch = torch
+        self.plan = plan
+        self.device = torch.device(device)
+        self.dtype = plan.dtype
+        self.tdtype = torch.bfloat16 if self.dtype == BF16 else torch.float32
+        self.lib = L.load()
+        # device='cpu' builds the full call plan without launching anything (CPU dry-run tests)
+        self.dry_run = self.device.type == "cpu"
+        self.stream = None if self.dry_run else torch.cuda.current_stream(self.device)
+        self._acts = {}
+        self._grads = {}
+        self._fwd_train, self._fwd_infer, self._bwd = [], [], []
+        self._build_params()
+        self._alloc_acts()
+        self._build_forward()
+        self._build_backward()
+        self._build_update()
+        self.bucket_bytes = bucket_bytes
+        self.num_update = 0
+
+    # ------------------------------------------------------------------ buffers
+    def _zeros(self, numel, dtype):
+        return self.torch.zeros(int(max(numel, 1)), dtype=dtype, device=self.device)
+
+    def _tdt(self, d):
+        return self.torch.bfloat16 if d == BF16 else self.torch.float32
+
+    def act(self, t):
+        b = self._acts.get(id(t))
+        if b is None:
+            b = self._zeros(t.numel, self._tdt(t.dtype))
+            self._acts[id(t)] = b
+        return b
+
+    def grad_buf(self, t):
+        b = self._grads.get(id(t))
+        if b is None:
+            b = self._zeros(t.numel, self.tdtype)
+            self._grads[id(t)] = b
+        return b
+
+    def _build_params(self):
+        torch = self.torch
+        plan = self.plan
+        # reverse forward order: grads of late layers complete first during backward
+        order = []
+        seen = set()
+        for op in plan.ops:
+            for key in ("weight", "bias"):
+                nm = getattr(op, key, None)
+                if nm and nm not in seen:
+                    order.append(nm)
+                    seen.add(nm)
+            for key in ("gamma", "beta"):
+                nm = getattr(op, key, None)
+                if nm and nm not in seen:
+                    order.append(nm)
+                    seen.add(nm)
+            if op.kind == "stem" and op.bn:
+                for key in ("gamma", "beta"):
+                    nm = op.bn[key]
+                    if nm not in seen:
+                        order.append(nm)
+                        seen.add(nm)
+        missing = [n for n in plan.param_names if n not in seen]
+        if missing:
+            raise PlanError("parameters not consumed by any lowered op: %s" % missing[:5])
+        order = list(reversed(order))
+        self.param_order = order
+        self.param_off = {}
+        self.param_shape = {}
+        self.param_layout = {}
+        off = 0
+        conv_w = {op.weight for op in plan.ops if op.kind in ("conv", "stem")}
+        for nm in order:
+            shp = tuple(plan.param_shape(nm))
+            self.param_shape[nm] = shp
+            self.param_layout[nm] = "krsc" if (nm in conv_w and len(shp) == 4) else "plain"
+            self.param_off[nm] = off
+            off += int(np.prod(shp))
+            off = (off + 3) // 4 * 4  # 16-byte aligned tensors
+        self.nparam = off
+        self.master = self._zeros(off, torch.float32)
+        self.grad = self._zeros(off, torch.float32)
+        self.mom = self._zeros(off, torch.float32)
+        # aux (moving stats)
+        self.aux_off = {}
+        aoff = 0
+        for nm in plan.aux_names:
+            shp = tuple(plan.param_shape(nm))
+            self.aux_off[nm] = (aoff, shp)
+            aoff += int(np.prod(shp))
+        self.aux = self._zeros(aoff, torch.float32)
+        # device optimizer tables
+        offs = [self.param_off[n] for n in order]
+        nums = [int(np.prod(self.param_shape[n])) for n in order]
+        self.opt_offsets = torch.tensor(offs, dtype=torch.int64, device=self.device)
+        self.opt_numels = torch.tensor(nums, dtype=torch.int64, device=self.device)
+        self.wd_mult = np.array([1.0 if (n.endswith("_weight") or n.endswith("_gamma")) else 0.0 for n in order],
+                                dtype=np.float32)
+        self.opt_wds = torch.zeros(len(order), dtype=torch.float32, device=self.device)
+        self._wd_value = None
+
+    def pview(self, name):
+        o = self.param_off[name]
+        return self.master[o:o + int(np.prod(self.param_shape[name]))]
+
+    def gview(self, name):
+        o = self.param_off[name]
+        return self.grad[o:o + int(np.prod(self.param_shape[name]))]
+
+    def aview(self, name):
+        o, shp = self.aux_off[name]
+        return self.aux[o:o + int(np.prod(shp))]
+
+    def _alloc_acts(self):
+        for t in self.plan.tensors.values():
+            self.act(t)
+        self.stats = self._zeros(4, self.torch.float32)
+
+    # ------------------------------------------------------------------ helpers
+    def _p(self, t):
+        return None if t is None else L.ptr(t)
+
+    def _pp(self, name):
+        return L.C.c_void_p(self.master.data_ptr() + 4 * self.param_off[name])
+
+    def _gp(self, name):
+        return L.C.c_void_p(self.grad.data_ptr() + 4 * self.param_off[name])
+
+    def _ap(self, name):
+        return L.C.c_void_p(self.aux.data_ptr() + 4 * self.aux_off[name][0])
+
+    def _call(self, fname, *args):
+        fn = getattr(self.lib, fname)
+        return (fname, fn, args)
+
+    def _emit_bwd(self, item):
+        if item[0] == "add":
+            _, n, a, b, dst = item
+            self._bwd.append(self._call("rn_eltwise_add", n, self.dtype, self._p(a), self._p(b), self._p(dst), 0,
+                                        self._sp()))
+        else:
+            self._bwd.append(item)
+
+    def _sp(self):
+        return L.C.c_void_p(0 if self.stream is None else self.stream.cuda_stream)
+
+    def _conv_desc(self, n, h, w, c, c_real, k, kernel, stride, pad):
+        d = L.ConvDesc(dtype=self.dtype, n=n, h=h, w=w, c=c, c_real=c_real, k=k, k_pad=_pad8(k), r=kernel[0],
+                       s=kernel[1], stride_h=stride[0], stride_w=stride[1], pad_h=pad[0], pad_w=pad[1], groups=1)
+        L.check(self.lib.rn_conv_desc_init(L.C.byref(d)), "rn_conv_desc_init")
+        return d
+
+    # ------------------------------------------------------------------ forward
+    def _build_forward(self):
+        plan = self.plan
+        sp = self._sp()
+        ws_bytes = 64
+        self._descs = []  # keep ctypes structs alive
+        self.packs = []   # weight pack calls (after every update)
+        self.bn_state = {}
+        stem_ws = 64
+        for op in plan.ops:
+            if op.kind == "bn":
+                d = L.BNDesc(dtype=self.dtype, m=op.x.rows, c=op.x.cp, c_real=op.x.c, eps=op.eps,
+                             momentum=op.momentum, fix_gamma=int(op.fix_gamma), relu=int(op.relu))
+                ws_bytes = max(ws_bytes, self.lib.rn_bn_workspace_bytes(L.C.byref(d)))
+                op.desc = d
+            elif op.kind == "stem" and op.bn:
+                x = op.x
+                d = L.BNDesc(dtype=F32, m=x.n * x.h * x.w, c=8, c_real=x.c, eps=op.bn["eps"],
+                             momentum=op.bn["momentum"], fix_gamma=1, relu=0)
+                ws_bytes = max(ws_bytes, self.lib.rn_bn_workspace_bytes(L.C.byref(d)))
+                op.bn_desc = d
+        self.ws = self._zeros(ws_bytes // 4 + 16, self.torch.float32)
+        wsp = self._p(self.ws)
+        for op in plan.ops:
+            F, I = [], []  # train-mode, infer-mode call lists
+            if op.kind == "stem":
+                x, y = op.x, op.y
+                d1 = self._conv_desc(x.n, y.h, y.w, op.kc, op.kernel[0] * op.kernel[1] * x.c, y.c, (1, 1), (1, 1),
+                                     (0, 0))
+                dfull = self._conv_desc(x.n, x.h, x.w, 8, x.c, y.c, op.kernel, op.stride, op.pad)
+                op.d1, op.dfull = d1, dfull
+                op.cols = self._zeros(x.n * y.h * y.w * op.kc, self.tdtype)
+                op.wk = self._zeros(y.c * op.kc, self.tdtype)
+                self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(d1), self._pp(op.weight),
+                                             self._p(op.wk), None, sp))
+                stem_ws = max(stem_ws, y.h * y.w * y.cp + y.c * op.kernel[0] * op.kernel[1] + 64)
+                xnchw = self._p(self.act(x))
+                if op.bn:
+                    b = op.bn
+                    op.nhwc8 = self._zeros(x.n * x.h * x.w * 8, self.torch.float32)
+                    op.bnbuf = self._zeros(4 * 8, self.torch.float32)
+                    sm, si, sc, sh = [L.C.c_void_p(op.bnbuf.data_ptr() + 32 * i) for i in range(4)]
+                    op.bn_ptrs = (sm, si, sc, sh)
+                    F.append(self._call("rn_nchw_to_nhwc", x.n, x.c, x.h, x.w, 8, xnchw, self._p(op.nhwc8), F32, sp))
+                    if b["use_global_stats"]:
+                        F.append(self._call("rn_bn_fwd_infer", L.C.byref(op.bn_desc), self._p(op.nhwc8),
+                                            self._p(op.nhwc8), self._pp(b["gamma"]), self._pp(b["beta"]),
+                                            self._ap(b["mean"]), self._ap(b["var"]), sc, sh, sp))
+                    else:
+                        F.append(self._call("rn_bn_fwd_train", L.C.byref(op.bn_desc), self._p(op.nhwc8), None,
+                                            self._pp(b["gamma"]), self._pp(b["beta"]), self._ap(b["mean"]),
+                                            self._ap(b["var"]), sm, si, sc, sh, wsp, sp))
+                    I.append(self._call("rn_nchw_to_nhwc", x.n, x.c, x.h, x.w, 8, xnchw, self._p(op.nhwc8), F32, sp))
+                    I.append(self._call("rn_bn_fwd_infer", L.C.byref(op.bn_desc), self._p(op.nhwc8),
+                                        self._p(op.nhwc8), self._pp(b["gamma"]), self._pp(b["beta"]),
+                                        self._ap(b["mean"]), self._ap(b["var"]), sc, sh, sp))
+                    for lst in (F, I):
+                        lst.append(self._call("rn_im2col_nchw", L.C.byref(dfull), xnchw, sc, sh, self._p(op.cols),
+                                              op.kc, sp))
+                else:
+                    for lst in (F, I):
+                        lst.append(self._call("rn_im2col_nchw", L.C.byref(dfull), xnchw, None, None,
+                                              self._p(op.cols), op.kc, sp))
+                for lst in (F, I):
+                    lst.append(self._call("rn_conv_fwd", L.C.byref(d1), self._p(op.cols), self._p(op.wk),
+                                          self._p(self.act(y)), self.dtype, None, None, sp))
+            elif op.kind == "conv":
+                x, y = op.x, op.y
+                d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad)
+                assert (d.p, d.q) == (y.h, y.w), (op.name, d.p, d.q, y.h, y.w)
+                op.desc = d
+                op.wk = self._zeros(y.c * op.kernel[0] * op.kernel[1] * x.cp, self.tdtype)
+                op.wc = self._zeros(x.cp * op.kernel[0] * op.kernel[1] * y.cp, self.tdtype)
+                self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(d), self._pp(op.weight), self._p(op.wk),
+                                             self._p(op.wc), sp))
+                res = self._p(self.act(op.res)) if op.res is not None else None
+                c = self._call("rn_conv_fwd", L.C.byref(d), self._p(self.act(x)), self._p(op.wk),
+                               self._p(self.act(y)), self.dtype, res, None, sp)
+                F.append(c)
+                I.append(c)
+            elif op.kind == "bn":
+                x, y = op.x, op.y
+                c = x.cp
+                op.buf = self._zeros(4 * c, self.torch.float32)
+                op.sm, op.si, op.sc, op.sh = [L.C.c_void_p(op.buf.data_ptr() + 4 * c * i) for i in range(4)]
+                gamma = self._pp(op.gamma)
+                infer = self._call("rn_bn_fwd_infer", L.C.byref(op.desc), self._p(self.act(x)), self._p(self.act(y)),
+                                   gamma, self._pp(op.beta), self._ap(op.mean), self._ap(op.var), op.sc, op.sh, sp)
+                if op.use_global_stats:
+                    F.append(infer)
+                else:
+                    F.append(self._call("rn_bn_fwd_train", L.C.byref(op.desc), self._p(self.act(x)),
+                                        self._p(self.act(y)), gamma, self._pp(op.beta), self._ap(op.mean),
+                                        self._ap(op.var), op.sm, op.si, op.sc, op.sh, wsp, sp))
+                I.append(infer)
+            elif op.kind == "relu":
+                c = self._call("rn_eltwise_add", op.x.numel, self.dtype, self._p(self.act(op.x)), None,
+                               self._p(self.act(op.y)), 1, sp)
+                F.append(c)
+                I.append(c)
+            elif op.kind == "add":
+                c = self._call("rn_eltwise_add", op.y.numel, self.dtype, self._p(self.act(op.a)),
+                               self._p(self.act(op.b)), self._p(self.act(op.y)), int(op.relu), sp)
+                F.append(c)
+                I.append(c)
+            elif op.kind == "pool":
+                x, y = op.x, op.y
+                d = L.PoolDesc(dtype=self.dtype, n=x.n, h=x.h, w=x.w, c=x.cp, r=op.kernel[0], s=op.kernel[1],
+                               stride_h=op.stride[0], stride_w=op.stride[1], pad_h=op.pad[0], pad_w=op.pad[1],
+                               type=L.RN_POOL_MAX if op.type == "max" else L.RN_POOL_AVG,
+                               global_pool=int(op.global_pool))
+                L.check(self.lib.rn_pool_desc_init(L.C.byref(d)), "rn_pool_desc_init")
+                assert (d.p, d.q) == (y.h, y.w), (op.name, d.p, d.q, y.h, y.w)
+                op.desc = d
+                op.argmax = self.torch.zeros(max(y.rows * y.cp, 1), dtype=self.torch.uint8, device=self.device) \
+                    if op.type == "max" else None
+                c = self._call("rn_pool_fwd", L.C.byref(d), self._p(self.act(x)), self._p(self.act(y)),
+                               self._p(op.argmax), sp)
+                F.append(c)
+                I.append(c)
+            elif op.kind == "fc":
+                x, y = op.x, op.y
+                d = self._conv_desc(x.n, 1, 1, x.cp, x.c, op.nh, (1, 1), (1, 1), (0, 0))
+                op.desc = d
+                op.wk = self._zeros(op.nh * x.cp, self.tdtype)
+                op.wc = self._zeros(x.cp * _pad8(op.nh), self.tdtype)
+                self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(d), self._pp(op.weight), self._p(op.wk),
+                                             self._p(op.wc), sp))
+                bias = self._pp(op.bias) if op.bias else None
+                c = self._call("rn_conv_fwd", L.C.byref(d), self._p(self.act(x)), self._p(op.wk),
+                               self._p(self.act(y)), F32, None, bias, sp)
+                F.append(c)
+                I.append(c)
+            elif op.kind == "softmax":
+                x = op.x
+                # gradient of the logits is produced here (SoftmaxOutput's backward needs no head grad)
+                dl = self.grad_buf(x)
+                F.append(self._call("rn_softmax_output", self.dtype, x.n, x.c, x.cp, self._p(self.act(x)),
+                                    self._p(self.act(op.label)), self._p(self.act(op.y)), self._p(dl),
+                                    op.grad_scale, self._p(self.stats), sp))
+                I.append(self._call("rn_softmax_output", self.dtype, x.n, x.c, x.cp, self._p(self.act(x)),
+                                    self._p(self.act(op.label)), self._p(self.act(op.y)), None, op.grad_scale,
+                                    None, sp))
+            self._fwd_train.extend(F)
+            self._fwd_infer.extend(I)
+        self.stem_ws = self._zeros(stem_ws, self.torch.float32)
+
+    # ------------------------------------------------------------------ backward
+    def _build_backward(self):
+        plan = self.plan
+        sp = self._sp()
+        gs = _GradState(self)
+        wsp = self._p(self.ws)
+        self.param_done_at = {}  # param -> index in self._bwd after which its grad is final
+        for op in reversed(plan.ops):
+            if op.kind == "softmax":
+                gs.has_value.add(id(op.x))  # dlogits written by the forward softmax call
+                continue
+            dy = gs.read(op.y) if op.kind != "softmax" else None
+            if dy is None:
+                continue
+            if op.kind == "fc":
+                x = op.x
+                self._bwd.append(self._call("rn_conv_bwd_filter", L.C.byref(op.desc), self._p(self.act(x)),
+                                            self._p(dy), self._gp(op.weight), sp))
+                if op.bias:
+                    self._bwd.append(self._call("rn_col_sum", self.dtype, x.n, op.nh, _pad8(op.nh), self._p(dy),
+                                                self._gp(op.bias), 0, sp))
+                    self.param_done_at[op.bias] = len(self._bwd)
+                self.param_done_at[op.weight] = len(self._bwd)
+                if x.needs_grad:
+                    out, add = gs.contribute(x)
+                    self._bwd.append(self._call("rn_conv_bwd_data", L.C.byref(op.desc), self._p(dy), self._p(op.wc),
+                                                self._p(out), self._p(add), sp))
+            elif op.kind == "conv":
+                x = op.x
+                self._bwd.append(self._call("rn_conv_bwd_filter", L.C.byref(op.desc), self._p(self.act(x)),
+                                            self._p(dy), self._gp(op.weight), sp))
+                self.param_done_at[op.weight] = len(self._bwd)
+                if x.needs_grad:
+                    out, add = gs.contribute(x)
+                    self._bwd.append(self._call("rn_conv_bwd_data", L.C.byref(op.desc), self._p(dy), self._p(op.wc),
+                                                self._p(out), self._p(add), sp))
+                if op.res is not None and op.res.needs_grad:
+                    gs.alias(op.res, dy)
+            elif op.kind == "stem":
+                self._bwd.append(self._call("rn_conv_bwd_filter", L.C.byref(op.d1), self._p(op.cols), self._p(dy),
+                                            self._gp(op.weight), sp))
+                self.param_done_at[op.weight] = len(self._bwd)
+                if op.bn:
+                    self._bwd.append(self._call("rn_stem_shift_grad", L.C.byref(op.dfull), self._p(dy),
+                                                self._pp(op.weight), self._gp(op.bn["beta"]), self._p(self.stem_ws),
+                                                sp))
+                    self.param_done_at[op.bn["beta"]] = len(self._bwd)
+                    self.param_done_at[op.bn["gamma"]] = len(self._bwd)
+            elif op.kind == "bn":
+                x = op.x
+                out, add = (gs.contribute(x) if x.needs_grad else (None, None))
+                self._bwd.append(self._call("rn_bn_bwd", L.C.byref(op.desc), self._p(self.act(x)), self._p(dy),
+                                            self._p(out), self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc,
+                                            op.sh, self._gp(op.gamma), self._gp(op.beta), wsp, sp))
+                self.param_done_at[op.gamma] = len(self._bwd)
+                self.param_done_at[op.beta] = len(self._bwd)
+            elif op.kind == "relu":
+                if op.x.needs_grad:
+                    out, add = gs.contribute(op.x)
+                    self._bwd.append(self._call("rn_relu_bwd", op.y.numel, self.dtype, self._p(self.act(op.y)),
+                                                self._p(dy), self._p(out), self._p(add), sp))
+            elif op.kind == "add":
+                g = dy
+                if op.relu:
+                    gbuf = self._zeros(op.y.numel, self.tdtype)
+                    self._bwd.append(self._call("rn_relu_bwd", op.y.numel, self.dtype, self._p(self.act(op.y)),
+                                                self._p(dy), self._p(gbuf), None, sp))
+                    g = gbuf
+                for t in (op.a, op.b):
+                    if t.needs_grad:
+                        gs.alias(t, g)
+            elif op.kind == "pool":
+                x = op.x
+                if x.needs_grad:
+                    out, add = gs.contribute(x)
+                    self._bwd.append(self._call("rn_pool_bwd", L.C.byref(op.desc), self._p(dy), self._p(op.argmax),
+                                                self._p(out), self._p(add), sp))
+
+    # ------------------------------------------------------------------ update
+    def _build_update(self):
+        self.wpack_calls = list(self.packs)
+
+    # ------------------------------------------------------------------ running
+    def _run(self, calls):
+        for name, fn, args in calls:
+            r = fn(*args)
+            if r != 0:
+                raise L.RNError("%s: %s" % (name, self.lib.rn_last_error().decode()))
+
+    def set_input(self, data_np, label_np=None):
+        """H2D copy of one batch (host numpy / torch) into the data/label buffers."""
+        torch = self.torch
+        t = self.plan.data_tensor
+        dst = self.act(t)
+        src = torch.as_tensor(np.ascontiguousarray(data_np, dtype=np.float32)) if isinstance(data_np, np.ndarray) \
+            else data_np
+        dst.copy_(src.reshape(-1).to(torch.float32), non_blocking=True)
+        if label_np is not None:
+            for tt in self.plan.tensors.values():
+                if tt.kind == "label":
+                    lsrc = torch.as_tensor(np.ascontiguousarray(label_np, dtype=np.float32)) \
+                        if isinstance(label_np, np.ndarray) else label_np
+                    self.act(tt).copy_(lsrc.reshape(-1).to(torch.float32), non_blocking=True)
+
+    def forward(self, is_train=True):
+        self._run(self._fwd_train if is_train else self._fwd_infer)
+
+    def backward(self, hooks=None):
+        self.grad.zero_()
+        if not hooks:
+            self._run(self._bwd)
+            return
+        # hooks: {bwd index -> callable}, e.g. RCCL bucket all-reduce launches
+        calls = self._bwd
+        for i, (name, fn, args) in enumerate(calls):
+            r = fn(*args)
+            if r != 0:
+                raise L.RNError("%s: %s" % (name, self.lib.rn_last_error().decode()))
+            h = hooks.get(i + 1)
+            if h is not None:
+                h()
+
+    def repack_weights(self):
+        self._run(self.wpack_calls)
+
+    def sgd_update(self, lr, wd, momentum, rescale_grad, clip=-1.0):
+        if self._wd_value != wd:
+            self.opt_wds.copy_(self.torch.from_numpy(self.wd_mult * np.float32(wd)))
+            self._wd_value = wd
+        L.check(self.lib.rn_sgd_mom_update(len(self.param_order), self._p(self.opt_offsets),
+                                           self._p(self.opt_numels), self._p(self.opt_wds), self._p(self.master),
+                                           self._p(self.grad), self._p(self.mom), None, F32, float(lr), None,
+                                           float(momentum), float(rescale_grad), float(clip), self._sp()),
+                "rn_sgd_mom_update")
+        self.repack_weights()
+
+    # ------------------------------------------------------------------ param I/O (MXNet layouts)
+    def set_param(self, name, value):
+        v = np.asarray(value, dtype=np.float32)
+        if tuple(v.shape) != self.param_shape[name]:
+            raise ValueError("shape mismatch for %s: %s vs %s" % (name, v.shape, self.param_shape[name]))
+        if self.param_layout[name] == "krsc":
+            v = v.transpose(0, 2, 3, 1)
+        self.pview(name).copy_(self.torch.from_numpy(np.ascontiguousarray(v).reshape(-1)))
+
+    def get_param(self, name, grad=False):
+        src = self.gview(name) if grad else self.pview(name)
+        shp = self.param_shape[name]
+        v = src.detach().cpu().numpy()
+        if self.param_layout[name] == "krsc":
+            k, c, r, s = shp
+            return v.reshape(k, r, s, c).transpose(0, 3, 1, 2).copy()
+        return v.reshape(shp).copy()
+
+    def set_aux(self, name, value):
+        v = np.asarray(value, dtype=np.float32).reshape(-1)
+        self.aview(name).copy_(self.torch.from_numpy(v))
+
+    def get_aux(self, name):
+        o, shp = self.aux_off[name]
+        return self.aview(name).detach().cpu().numpy().reshape(shp).copy()
+
+    def output(self, i=0):
+        t = self.plan.outputs[i]
+        a = self.act(t)
+        if t.kind == "prob":
+            return a.view(t.n, t.c)
+        return a
+
+    # ------------------------------------------------------------------ gradient buckets
+    def buckets(self):
+        """[(start, end, last_bwd_index)] over the flat grad buffer, ~bucket_bytes each."""
+        out = []
+        cur_start, cur_end, cur_last = None, None, 0
+        for nm in self.param_order:
+            o = self.param_off[nm]
+            n = int(np.prod(self.param_shape[nm]))
+            last = self.param_done_at.get(nm, len(self._bwd))
+            if cur_start is None:
+                cur_start, cur_end, cur_last = o, o + n, last
+            else:
+                cur_end, cur_last = o + n, max(cur_last, last)
+            if (cur_end - cur_start) * 4 >= self.bucket_bytes:
+                out.append((cur_start, cur_end, cur_last))
+                cur_start = None
+        if cur_start is not None:
+            out.append((cur_start, self.nparam, max(cur_last, 0)))
+        # a bucket may only launch after every earlier bucket's params are final too
+        fixed, run = [], 0
+        for s, e, last in out:
+            run = max(run, last)
+            fixed.append((s, e, run))
+        return fixed

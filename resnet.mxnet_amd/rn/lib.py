@@ -1,0 +1,109 @@
+"""ctypes binding of librn.so, the C-ABI declared in include/rn.h.
+
+Loading fails loudly (RuntimeError) when the library is missing: there is no CPU or
+PyTorch fallback for any op of the training path.
+"""
+import ctypes as C
+import os
+
+from .build import LIB_PATH, build, needs_build
+
+RN_BF16 = 0
+RN_F32 = 1
+RN_POOL_MAX = 0
+RN_POOL_AVG = 1
+
+_P = C.c_void_p
+_i32 = C.c_int32
+_i64 = C.c_int64
+_f32 = C.c_float
+
+
+class ConvDesc(C.Structure):
+    _fields_ = [(n, _i32) for n in ("dtype", "n", "h", "w", "c", "c_real", "k", "k_pad", "r", "s", "stride_h",
+                                   "stride_w", "pad_h", "pad_w", "groups", "p", "q")]
+
+
+class BNDesc(C.Structure):
+    _fields_ = [("dtype", _i32), ("m", _i64), ("c", _i32), ("c_real", _i32), ("eps", _f32), ("momentum", _f32),
+                ("fix_gamma", _i32), ("relu", _i32)]
+
+
+class PoolDesc(C.Structure):
+    _fields_ = [(n, _i32) for n in ("dtype", "n", "h", "w", "c", "r", "s", "stride_h", "stride_w", "pad_h", "pad_w",
+                                   "type", "global_pool", "p", "q")]
+
+
+# name -> (restype, argtypes); every symbol declared in include/rn.h
+SIGNATURES = {
+    "rn_conv_desc_init": (_i32, [_P]),
+    "rn_conv_fwd": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P]),
+    "rn_conv_bwd_data": (_i32, [_P, _P, _P, _P, _P, _P]),
+    "rn_conv_bwd_filter": (_i32, [_P, _P, _P, _P, _P]),
+    "rn_conv_weight_numel": (_i64, [_P]),
+    "rn_conv_weight_pack": (_i32, [_P, _P, _P, _P, _P]),
+    "rn_im2col_nchw": (_i32, [_P, _P, _P, _P, _P, _i32, _P]),
+    "rn_stem_shift_grad": (_i32, [_P, _P, _P, _P, _P, _P]),
+    "rn_bn_workspace_bytes": (_i64, [_P]),
+    "rn_bn_fwd_train": (_i32, [_P] * 13),
+    "rn_bn_fwd_infer": (_i32, [_P] * 10),
+    "rn_bn_apply": (_i32, [_P] * 6),
+    "rn_bn_bwd": (_i32, [_P] * 14),
+    "rn_pool_desc_init": (_i32, [_P]),
+    "rn_pool_fwd": (_i32, [_P, _P, _P, _P, _P]),
+    "rn_pool_bwd": (_i32, [_P, _P, _P, _P, _P, _P]),
+    "rn_softmax_output": (_i32, [_i32, _i32, _i32, _i32, _P, _P, _P, _P, _f32, _P, _P]),
+    "rn_col_sum": (_i32, [_i32, _i64, _i32, _i32, _P, _P, _i32, _P]),
+    "rn_sgd_mom_update": (_i32, [_i32, _P, _P, _P, _P, _P, _P, _P, _i32, _f32, _P, _f32, _f32, _f32, _P]),
+    "rn_nchw_to_nhwc": (_i32, [_i32, _i32, _i32, _i32, _i32, _P, _P, _i32, _P]),
+    "rn_cast": (_i32, [_i64, _P, _i32, _P, _i32, _P]),
+    "rn_eltwise_add": (_i32, [_i64, _i32, _P, _P, _P, _i32, _P]),
+    "rn_relu_bwd": (_i32, [_i64, _i32, _P, _P, _P, _P, _P]),
+    "rn_quant_int8_fwd": (_i32, [_i32, _i64, _P, _P, _P, _i32, _i32, _f32, _i32, _i32, _P, _P]),
+    "rn_quant_int8_bwd": (_i32, [_i32, _i64, _P, _P, _P, _P, _i32, _P, _P]),
+    "rn_last_error": (C.c_char_p, []),
+    "rn_version": (_i32, []),
+    "rn_device_cu_count": (_i32, []),
+}
+
+_lib = None
+
+
+class RNError(RuntimeError):
+    pass
+
+
+def load(auto_build=True):
+    """Load librn.so (building it first if sources are newer and hipcc is present)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if auto_build and os.path.exists("/opt/rocm/bin/hipcc") and needs_build():
+        build()
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"librn.so not found at {LIB_PATH}: build it with "
+                           "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(ret, what=""):
+    if ret != 0:
+        msg = _lib.rn_last_error().decode() if _lib is not None else "librn not loaded"
+        raise RNError(f"{what}: {msg}")
+    return ret
+
+
+def call(name, *args):
+    lib = load()
+    return check(getattr(lib, name)(*args), name)
+
+
+def ptr(t):
+    """Device pointer of a torch tensor (or None)."""
+    return None if t is None else C.c_void_p(t.data_ptr())

@@ -1,0 +1,312 @@
+"""Per-kernel parity of librn against the numpy oracle (oracle/ops.py) on the GPU.
+
+Tolerances (max |err| / max |ref|):
+  fp32 path: 2e-5 (exact-fp32 MFMA products, fp32 accumulation order differs from fp64)
+  bf16 path: 1.5e-2 (oracle fed the same bf16-rounded inputs; output rounded to bf16 = 2^-8)
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ops
+from rn import lib as L
+from gpu_util import BF16, F32, bf16_round, conv_desc, from_nhwc, p, pad8, rel_err, stream, tdt, to_nhwc
+
+pytestmark = pytest.mark.gpu
+
+TOL = {F32: 2e-5, BF16: 1.5e-2}
+
+CONV_CASES = [
+    # n, c, h, w, k, r, stride, pad
+    (2, 64, 14, 14, 64, 1, 1, 0),
+    (2, 64, 14, 14, 128, 3, 1, 1),
+    (3, 32, 13, 11, 48, 3, 2, 1),
+    (2, 64, 14, 14, 256, 1, 2, 0),
+    (2, 128, 7, 7, 24, 3, 1, 1),
+    (4, 16, 9, 9, 40, 5, 2, 2),
+    (2, 8, 16, 16, 16, 7, 2, 3),
+    (1, 256, 4, 4, 1000, 1, 1, 0),
+]
+
+
+def _conv_data(case, seed):
+    n, c, h, w, k, r, st, pd = case
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((n, c, h, w))
+    wt = rng.standard_normal((k, c, r, r)) / np.sqrt(c * r * r)
+    return x, wt
+
+
+def _master_krsc(wt, dev):
+    return torch.from_numpy(np.ascontiguousarray(wt.transpose(0, 2, 3, 1), dtype=np.float32)).reshape(-1).to(dev)
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_fwd(gpu, dtype, case):
+    n, c, h, w, k, r, st, pd = case
+    x, wt = _conv_data(case, 1)
+    if dtype == BF16:
+        x, wt = bf16_round(x), bf16_round(wt)
+    res = np.random.default_rng(2).standard_normal((n, k) + ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd)))
+    if dtype == BF16:
+        res = bf16_round(res)
+    ref = ops.conv2d_fwd(x, wt, (st, st), (pd, pd)) + res
+    d = conv_desc(dtype, n, c, h, w, k, r, r, st, pd)
+    xd = to_nhwc(x, dtype, gpu)
+    wk = torch.zeros(k * r * r * d.c, dtype=tdt(dtype), device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), p(wk), None, stream())
+    y = torch.zeros((n, d.p, d.q, d.k_pad), dtype=tdt(dtype), device=gpu)
+    rd = to_nhwc(res, dtype, gpu)
+    L.call("rn_conv_fwd", C.byref(d), p(xd), p(wk), p(y), dtype, p(rd), None, stream())
+    torch.cuda.synchronize()
+    assert rel_err(from_nhwc(y, k), ref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_bwd(gpu, dtype, case):
+    n, c, h, w, k, r, st, pd = case
+    x, wt = _conv_data(case, 3)
+    P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+    dy = np.random.default_rng(4).standard_normal((n, k, P, Q))
+    if dtype == BF16:
+        x, wt, dy = bf16_round(x), bf16_round(wt), bf16_round(dy)
+    dx_ref, dw_ref = ops.conv2d_bwd(x, wt, dy, (st, st), (pd, pd))
+    d = conv_desc(dtype, n, c, h, w, k, r, r, st, pd)
+    xd = to_nhwc(x, dtype, gpu)
+    dyd = to_nhwc(dy, dtype, gpu)
+    wc = torch.zeros(d.c * r * r * d.k_pad, dtype=tdt(dtype), device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), None, p(wc), stream())
+    dx = torch.zeros((n, h, w, d.c), dtype=tdt(dtype), device=gpu)
+    L.call("rn_conv_bwd_data", C.byref(d), p(dyd), p(wc), p(dx), None, stream())
+    dw = torch.zeros(k * r * r * c, dtype=torch.float32, device=gpu)
+    L.call("rn_conv_bwd_filter", C.byref(d), p(xd), p(dyd), p(dw), stream())
+    torch.cuda.synchronize()
+    assert rel_err(from_nhwc(dx, c), dx_ref) < TOL[dtype]
+    dw_h = dw.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2)
+    assert rel_err(dw_h, dw_ref) < (TOL[dtype] if dtype == F32 else 5e-3)
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+def test_stem_im2col_and_shift_grad(gpu, dtype):
+    """conv0 as im2col + 1x1 GEMM (with bn_data affine) and d(beta) without the stem dgrad."""
+    n, c, h, w, k, r, st, pd = 2, 3, 20, 18, 16, 7, 2, 3
+    rng = np.random.default_rng(5)
+    x = rng.uniform(-1, 1, (n, c, h, w))
+    wt = rng.standard_normal((k, c, r, r)) * 0.1
+    scale = np.array([1.5, 0.5, 2.0])
+    shift = np.array([0.1, -0.2, 0.3])
+    xa = x * scale[None, :, None, None] + shift[None, :, None, None]
+    if dtype == BF16:
+        xa, wt = bf16_round(xa), bf16_round(wt)
+    ref = ops.conv2d_fwd(xa, wt, (st, st), (pd, pd))
+    P, Q = ref.shape[2:]
+    kc = 160
+    d1 = conv_desc(dtype, n, kc, P, Q, k, 1, 1, 1, 0, c_real=r * r * c)
+    dfull = conv_desc(dtype, n, 8, h, w, k, r, r, st, pd, c_real=c)
+    xd = torch.from_numpy(x.astype(np.float32)).to(gpu)
+    sc = torch.tensor(scale, dtype=torch.float32, device=gpu)
+    sh = torch.tensor(shift, dtype=torch.float32, device=gpu)
+    cols = torch.zeros(n * P * Q * kc, dtype=tdt(dtype), device=gpu)
+    L.call("rn_im2col_nchw", C.byref(dfull), p(xd), p(sc), p(sh), p(cols), kc, stream())
+    master = _master_krsc(wt, gpu)
+    wk = torch.zeros(k * kc, dtype=tdt(dtype), device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d1), p(master), p(wk), None, stream())
+    y = torch.zeros((n, P, Q, pad8(k)), dtype=tdt(dtype), device=gpu)
+    L.call("rn_conv_fwd", C.byref(d1), p(cols), p(wk), p(y), dtype, None, None, stream())
+    # wgrad through the cols matrix, d(shift) via rn_stem_shift_grad
+    dy = rng.standard_normal((n, k, P, Q))
+    if dtype == BF16:
+        dy = bf16_round(dy)
+    dx_ref, dw_ref = ops.conv2d_bwd(xa, wt, dy, (st, st), (pd, pd))
+    dshift_ref = dx_ref.sum(axis=(0, 2, 3))
+    dyd = to_nhwc(dy, dtype, gpu)
+    dw = torch.zeros(k * r * r * c, dtype=torch.float32, device=gpu)
+    L.call("rn_conv_bwd_filter", C.byref(d1), p(cols), p(dyd), p(dw), stream())
+    dbeta = torch.zeros(c, dtype=torch.float32, device=gpu)
+    ws = torch.zeros(P * Q * pad8(k) + k * r * r, dtype=torch.float32, device=gpu)
+    L.call("rn_stem_shift_grad", C.byref(dfull), p(dyd), p(master), p(dbeta), p(ws), stream())
+    torch.cuda.synchronize()
+    assert rel_err(from_nhwc(y, k), ref) < TOL[dtype]
+    assert rel_err(dw.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2), dw_ref) < \
+        (TOL[dtype] if dtype == F32 else 5e-3)
+    assert rel_err(dbeta.cpu().numpy(), dshift_ref) < (1e-4 if dtype == F32 else 5e-3)
+
+
+BN_CASES = [(4, 64, 9, 9, False, True), (2, 24, 5, 7, True, False), (8, 256, 4, 4, False, False),
+            (2, 2048, 2, 2, False, True)]
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("case", BN_CASES)
+def test_bn_relu(gpu, dtype, case):
+    n, c, h, w, fix_gamma, relu = case
+    rng = np.random.default_rng(6)
+    x = rng.standard_normal((n, c, h, w)) * 2 + 0.5
+    gamma = rng.uniform(0.5, 1.5, c)
+    beta = rng.standard_normal(c) * 0.1
+    dy = rng.standard_normal((n, c, h, w))
+    if dtype == BF16:
+        x, dy = bf16_round(x), bf16_round(dy)
+    eps, mom = 1e-5, 0.9
+    y_ref, cache = ops.bn_train_fwd(x, gamma, beta, eps, fix_gamma)
+    if relu:
+        dz = ops.relu_bwd(dy, ops.relu_fwd(y_ref))
+        y_ref = ops.relu_fwd(y_ref)
+    else:
+        dz = dy
+    dx_ref, dg_ref, db_ref = ops.bn_train_bwd(dz, cache, fix_gamma)
+    mm_ref, mv_ref = ops.bn_moving_update(np.zeros(c), np.ones(c), cache[3], cache[4], mom)
+    cp = pad8(c)
+    d = L.BNDesc(dtype=dtype, m=n * h * w, c=cp, c_real=c, eps=eps, momentum=mom, fix_gamma=int(fix_gamma),
+                 relu=int(relu))
+    f = lambda a: torch.tensor(np.pad(a, (0, cp - c)), dtype=torch.float32, device=gpu)
+    g_d, b_d, mm, mv = f(gamma), f(beta), f(np.zeros(c)), f(np.ones(c))
+    sm, si, sc, sh = [torch.zeros(cp, dtype=torch.float32, device=gpu) for _ in range(4)]
+    ws = torch.zeros(L.load().rn_bn_workspace_bytes(C.byref(d)) // 4 + 16, dtype=torch.float32, device=gpu)
+    xd = to_nhwc(x, dtype, gpu)
+    yd = torch.zeros_like(xd)
+    L.call("rn_bn_fwd_train", C.byref(d), p(xd), p(yd), p(g_d), p(b_d), p(mm), p(mv), p(sm), p(si), p(sc), p(sh),
+           p(ws), stream())
+    dyd = to_nhwc(dy, dtype, gpu)
+    dxd = torch.zeros_like(xd)
+    addd = to_nhwc(np.ones_like(x), dtype, gpu)
+    dg, db = torch.zeros(cp, device=gpu), torch.zeros(cp, device=gpu)
+    L.call("rn_bn_bwd", C.byref(d), p(xd), p(dyd), p(dxd), p(addd), p(g_d), p(sm), p(si), p(sc), p(sh), p(dg), p(db),
+           p(ws), stream())
+    torch.cuda.synchronize()
+    tol = TOL[dtype]
+    assert rel_err(from_nhwc(yd, c), y_ref) < tol
+    assert rel_err(mm.cpu().numpy()[:c], mm_ref) < 1e-4
+    assert rel_err(mv.cpu().numpy()[:c], mv_ref) < 1e-4
+    assert rel_err(from_nhwc(dxd, c), dx_ref + 1.0) < (tol if dtype == F32 else 3e-2)
+    assert rel_err(db.cpu().numpy()[:c], db_ref) < (1e-4 if dtype == F32 else 1e-2)
+    if fix_gamma:
+        assert np.all(dg.cpu().numpy() == 0)
+    else:
+        assert rel_err(dg.cpu().numpy()[:c], dg_ref) < (1e-4 if dtype == F32 else 1e-2)
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+def test_maxpool_and_gap(gpu, dtype):
+    rng = np.random.default_rng(7)
+    n, c, h, w = 2, 16, 11, 12
+    # many ties (post-ReLU zeros) to pin the first-max gradient rule
+    x = np.maximum(rng.standard_normal((n, c, h, w)), 0)
+    x = np.round(x * 4) / 4
+    y_ref, arg = ops.maxpool_fwd(x, (3, 3), (2, 2), (1, 1))
+    dy = rng.standard_normal(y_ref.shape)
+    if dtype == BF16:
+        dy = bf16_round(dy)
+    dx_ref = ops.maxpool_bwd(dy, arg, x.shape, (3, 3), (2, 2), (1, 1))
+    d = L.PoolDesc(dtype=dtype, n=n, h=h, w=w, c=pad8(c), r=3, s=3, stride_h=2, stride_w=2, pad_h=1, pad_w=1,
+                   type=L.RN_POOL_MAX, global_pool=0)
+    L.call("rn_pool_desc_init", C.byref(d))
+    xd = to_nhwc(x, dtype, gpu)
+    yd = torch.zeros((n, d.p, d.q, pad8(c)), dtype=tdt(dtype), device=gpu)
+    am = torch.zeros(yd.numel(), dtype=torch.uint8, device=gpu)
+    L.call("rn_pool_fwd", C.byref(d), p(xd), p(yd), p(am), stream())
+    dyd = to_nhwc(dy, dtype, gpu)
+    dxd = torch.zeros_like(xd)
+    L.call("rn_pool_bwd", C.byref(d), p(dyd), p(am), p(dxd), None, stream())
+    torch.cuda.synchronize()
+    assert rel_err(from_nhwc(yd, c), y_ref) == 0.0
+    assert rel_err(from_nhwc(dxd, c), dx_ref) < TOL[dtype]
+    # global average pool
+    g = L.PoolDesc(dtype=dtype, n=n, h=h, w=w, c=pad8(c), type=L.RN_POOL_AVG, global_pool=1)
+    L.call("rn_pool_desc_init", C.byref(g))
+    yg = torch.zeros((n, 1, 1, pad8(c)), dtype=tdt(dtype), device=gpu)
+    L.call("rn_pool_fwd", C.byref(g), p(xd), p(yg), None, stream())
+    dyg = rng.standard_normal((n, c, 1, 1))
+    dxg = torch.zeros_like(xd)
+    L.call("rn_pool_bwd", C.byref(g), p(to_nhwc(dyg, dtype, gpu)), None, p(dxg), None, stream())
+    torch.cuda.synchronize()
+    assert rel_err(from_nhwc(yg, c), ops.avgpool_global_fwd(x)) < TOL[dtype]
+    dyg_r = bf16_round(dyg) if dtype == BF16 else dyg
+    assert rel_err(from_nhwc(dxg, c), ops.avgpool_global_bwd(dyg_r, x.shape)) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+def test_softmax_output(gpu, dtype):
+    rng = np.random.default_rng(8)
+    b, ncls, ld = 37, 1000, 1000
+    z = rng.standard_normal((b, ncls)) * 3
+    lab = rng.integers(0, ncls, b).astype(np.float32)
+    lab[0] = np.argmax(z[0])
+    prob_ref = ops.softmax_output_fwd(z)
+    g_ref = ops.softmax_output_bwd(prob_ref, lab)
+    zd = torch.tensor(z, dtype=torch.float32, device=gpu)
+    ld_ = torch.tensor(lab, device=gpu)
+    prob = torch.zeros((b, ncls), device=gpu)
+    dl = torch.zeros((b, ld), dtype=tdt(dtype), device=gpu)
+    stats = torch.zeros(4, device=gpu)
+    L.call("rn_softmax_output", dtype, b, ncls, ld, p(zd), p(ld_), p(prob), p(dl), C.c_float(1.0), p(stats), stream())
+    torch.cuda.synchronize()
+    assert rel_err(prob.cpu().numpy(), prob_ref) < 1e-5
+    assert rel_err(dl.float().cpu().numpy(), g_ref) < (1e-5 if dtype == F32 else 1e-2)
+    st = stats.cpu().numpy()
+    assert abs(st[0] - ops.cross_entropy(prob_ref, lab)) < 1e-3 * b
+    top1 = (np.argmax(z, 1) == lab).sum()
+    top5 = sum(lab[i] in np.argsort(z[i])[-5:] for i in range(b))
+    assert st[1] == top1 and st[2] == top5
+
+
+def test_sgd_momentum(gpu):
+    rng = np.random.default_rng(9)
+    sizes = [7, 64, 1000, 3]
+    names = ["a_weight", "a_beta", "fc_weight", "fc_bias"]
+    offs = np.cumsum([0] + [((s + 3) // 4) * 4 for s in sizes])[:-1]
+    total = int(offs[-1] + sizes[-1] + 4)
+    w = rng.standard_normal(total).astype(np.float32)
+    g = rng.standard_normal(total).astype(np.float32)
+    m = rng.standard_normal(total).astype(np.float32) * 0.1
+    wd = np.array([ops.wd_mult_for(n) * 1e-4 for n in names], dtype=np.float32)
+    wr, mr = w.astype(np.float64).copy(), m.astype(np.float64).copy()
+    for o, s, d in zip(offs, sizes, wd):
+        ops.sgd_mom_update(wr[o:o + s], g[o:o + s].astype(np.float64), mr[o:o + s], 0.1, float(d), 0.9, 1 / 256.)
+    t = lambda a, dt=torch.float32: torch.tensor(a, dtype=dt, device=gpu)
+    wd_, gd, md = t(w), t(g), t(m)
+    L.call("rn_sgd_mom_update", len(sizes), p(t(offs, torch.int64)), p(t(sizes, torch.int64)), p(t(wd)), p(wd_),
+           p(gd), p(md), None, F32, C.c_float(0.1), None, C.c_float(0.9), C.c_float(1 / 256.), C.c_float(-1.0),
+           stream())
+    torch.cuda.synchronize()
+    for o, s in zip(offs, sizes):
+        assert rel_err(wd_.cpu().numpy()[o:o + s], wr[o:o + s]) < 1e-6
+        assert rel_err(md.cpu().numpy()[o:o + s], mr[o:o + s]) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+def test_quant_int8(gpu, dtype):
+    rng = np.random.default_rng(10)
+    n = 4096
+    w = rng.standard_normal(n)
+    if dtype == BF16:
+        w = bf16_round(w)
+    wq_ref, _ = ops.quant_int8_weight(w)
+    xd = torch.tensor(w, dtype=tdt(dtype), device=gpu)
+    out = torch.zeros_like(xd)
+    ws = torch.zeros(4096, device=gpu)
+    L.call("rn_quant_int8_fwd", dtype, n, p(xd), p(out), None, 1, 1, C.c_float(0.99), 1, 8, p(ws), stream())
+    torch.cuda.synchronize()
+    tol = 1e-6 if dtype == F32 else 1e-2
+    assert rel_err(out.float().cpu().numpy(), wq_ref) < tol
+    # activation: EMA state, clip and masked STE
+    x = rng.standard_normal(n) * 3
+    if dtype == BF16:
+        x = bf16_round(x)
+    mm = torch.tensor([2.0], device=gpu)
+    xq_ref, mm_ref = ops.quant_int8_act(x, 2.0, True, False)
+    xd = torch.tensor(x, dtype=tdt(dtype), device=gpu)
+    L.call("rn_quant_int8_fwd", dtype, n, p(xd), p(out), p(mm), 0, 1, C.c_float(0.99), 0, 8, p(ws), stream())
+    dy = rng.standard_normal(n)
+    dx = torch.zeros_like(xd)
+    L.call("rn_quant_int8_bwd", dtype, n, p(xd), p(torch.tensor(dy, dtype=tdt(dtype), device=gpu)), p(dx), p(mm), 0,
+           None, stream())
+    torch.cuda.synchronize()
+    assert abs(mm.item() - mm_ref) < 1e-5 * abs(mm_ref)
+    assert rel_err(out.float().cpu().numpy(), xq_ref) < tol
+    dyr = bf16_round(dy) if dtype == BF16 else dy
+    assert rel_err(dx.float().cpu().numpy(), ops.quant_int8_act_bwd(dyr, x, mm_ref)) < tol
