@@ -234,8 +234,12 @@ def init_params(graph, seed=2, dtype=np.float64):
     return args, aux
 
 
-def forward(graph, args, aux, data, label, is_train=True, quant_state=None, first_batch=True):
-    """Returns (prob, tape). Updates aux (moving stats) in place when is_train."""
+def forward(graph, args, aux, data, label, is_train=True, quant_state=None, first_batch=True, storage=None):
+    """Returns (prob, tape). Updates aux (moving stats) in place when is_train.
+
+    storage='bf16' emulates a bf16-storage runtime: conv/FC weights and every stored activation
+    are rounded to bf16 (logits stay fp32), arithmetic stays in the array dtype."""
+    rnd = ops.bf16_round if storage == "bf16" else (lambda a: a)
     env = {"data": data}
     tape = []
     qs = quant_state if quant_state is not None else {}
@@ -252,9 +256,10 @@ def forward(graph, args, aux, data, label, is_train=True, quant_state=None, firs
                 wq, _ = ops.quant_int8_weight(w)
                 rec.update(xraw=x, t=mm)
                 x, w = xq, wq
+            w = rnd(w)
             rec.update(x=x, w=w)
             if t == "conv":
-                y = ops.conv2d_fwd(x, w, op["stride"], op["pad"], op["groups"])
+                y = rnd(ops.conv2d_fwd(x, w, op["stride"], op["pad"], op["groups"]))
             else:
                 xf = x.reshape(x.shape[0], -1)
                 rec["x"] = xf
@@ -273,7 +278,7 @@ def forward(graph, args, aux, data, label, is_train=True, quant_state=None, firs
                 y = ops.bn_infer_fwd(x, args[nm + "_gamma"], args[nm + "_beta"], aux[nm + "_moving_mean"],
                                      aux[nm + "_moving_var"], op["eps"], op["fix_gamma"])
                 tape.append(dict(op=op))
-            env[op["y"]] = y
+            env[op["y"]] = rnd(y)
         elif t == "relu":
             y = ops.relu_fwd(env[op["x"]])
             env[op["y"]] = y
@@ -285,28 +290,30 @@ def forward(graph, args, aux, data, label, is_train=True, quant_state=None, firs
             tape.append(dict(op=op, arg=arg, shape=x.shape))
         elif t == "gap":
             x = env[op["x"]]
-            env[op["y"]] = ops.avgpool_global_fwd(x)
+            env[op["y"]] = rnd(ops.avgpool_global_fwd(x))
             tape.append(dict(op=op, shape=x.shape))
         elif t == "add":
-            env[op["y"]] = env[op["a"]] + env[op["b"]]
+            env[op["y"]] = rnd(env[op["a"]] + env[op["b"]])
             tape.append(dict(op=op))
         elif t == "softmax":
             prob = ops.softmax_output_fwd(env[op["x"]])
             env[op["y"]] = prob
             tape.append(dict(op=op, prob=prob))
-    return env["softmax"], dict(tape=tape, env=env, label=label)
+    return env["softmax"], dict(tape=tape, env=env, label=label, rnd=rnd)
 
 
 def backward(graph, args, fwd_state, grad_scale=1.0):
     """Returns grads {param name: array} for one forward tape."""
     tape = fwd_state["tape"]
     label = fwd_state["label"]
+    rnd = fwd_state.get("rnd", lambda a: a)
     grads = {}
     g = {}
 
     def acc(name, v):
+        v = rnd(v)
         if name in g:
-            g[name] = g[name] + v
+            g[name] = rnd(g[name] + v)
         else:
             g[name] = v
 
@@ -353,7 +360,7 @@ def backward(graph, args, fwd_state, grad_scale=1.0):
 
 
 def train_step(graph, args, aux, moms, data, label, lr, momentum=0.9, wd=1e-4, rescale_grad=None,
-               num_devices=1, quant_state=None, first_batch=True):
+               num_devices=1, quant_state=None, first_batch=True, storage=None):
     """One Solver iteration (core/solver.py:115-121): forward(is_train) + backward + SGD update.
 
     num_devices > 1 restates Module's even batch split: per-slice BN statistics, per-slice
@@ -368,7 +375,7 @@ def train_step(graph, args, aux, moms, data, label, lr, momentum=0.9, wd=1e-4, r
     for d in range(num_devices):
         aux_d = {k: v.copy() for k, v in aux.items()}
         prob, st = forward(graph, args, aux_d, data[d * sl:(d + 1) * sl], label[d * sl:(d + 1) * sl], True,
-                           quant_state, first_batch)
+                           quant_state, first_batch, storage)
         grads = backward(graph, args, st)
         for k, v in grads.items():
             gsum[k] = gsum[k] + v if k in gsum else v

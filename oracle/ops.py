@@ -20,6 +20,15 @@ MXNet semantics restated (the [MXNet 1.x, un-vendored] items of SURVEY.md sectio
 import numpy as np
 
 
+# ----------------------------------------------------------------------------- precision emulation
+def bf16_round(x):
+    """Round to the nearest bf16 (ties to even) and widen back -- emulates bf16 storage."""
+    x = np.asarray(x)
+    u = x.astype(np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) & 0xFFFF0000).astype(np.uint32)
+    return r.view(np.float32).astype(x.dtype)
+
+
 # ----------------------------------------------------------------------------- convolution
 def _windows(xp, r, s, sh, sw, p, q):
     """(N,C,Hp,Wp) padded input -> strided view (N,C,P,Q,R,S)."""

@@ -268,8 +268,10 @@ def test_sgd_momentum(gpu):
     for o, s, d in zip(offs, sizes, wd):
         ops.sgd_mom_update(wr[o:o + s], g[o:o + s].astype(np.float64), mr[o:o + s], 0.1, float(d), 0.9, 1 / 256.)
     t = lambda a, dt=torch.float32: torch.tensor(a, dtype=dt, device=gpu)
+    # keep every device table alive until the kernel has run (no temporaries behind raw pointers)
     wd_, gd, md = t(w), t(g), t(m)
-    L.call("rn_sgd_mom_update", len(sizes), p(t(offs, torch.int64)), p(t(sizes, torch.int64)), p(t(wd)), p(wd_),
+    offs_d, sizes_d, wds_d = t(offs, torch.int64), t(sizes, torch.int64), t(wd)
+    L.call("rn_sgd_mom_update", len(sizes), p(offs_d), p(sizes_d), p(wds_d), p(wd_),
            p(gd), p(md), None, F32, C.c_float(0.1), None, C.c_float(0.9), C.c_float(1 / 256.), C.c_float(-1.0),
            stream())
     torch.cuda.synchronize()

@@ -1,0 +1,110 @@
+"""CPU tests of the mx.sym IR, the graph builders, lowering (Plan) and a dry-run executor build."""
+import json
+
+import numpy as np
+import pytest
+
+import mxnet as mx
+from rn import graphs
+from rn.executor import Executor, Plan, PlanError
+
+
+def _nparams(sym, shape):
+    args = sym.list_arguments()
+    a, o, x = sym.infer_shape(data=shape, softmax_label=(shape[0],))
+    sizes = {n: int(np.prod(s)) for n, s in zip(args, a) if n not in ("data", "softmax_label")}
+    return len(sizes), sum(sizes.values()), o
+
+
+def test_param_counts_match_survey():
+    # SURVEY.md 8a rows A4-A6
+    assert _nparams(graphs.resnet50(), (2, 3, 224, 224))[:2] == (157, 25549486)
+    assert _nparams(graphs.resnext50_32x4d(), (2, 3, 224, 224))[:2] == (161, 25028904)
+    assert _nparams(graphs.resnet20_cifar(), (2, 3, 32, 32))[:2] == (65, 272474)
+    assert len(graphs.resnet50().list_auxiliary_states()) == 102
+
+
+def test_names_and_order_match_oracle():
+    from oracle import net as onet
+    sym = graphs.resnet50()
+    args = [n for n in sym.list_arguments() if n not in ("data", "softmax_label")]
+    assert args == list(onet.resnet50_imagenet().params)
+    sym = graphs.resnet20_cifar()
+    args = [n for n in sym.list_arguments() if n not in ("data", "softmax_label")]
+    assert args == list(onet.resnet20_cifar().params)
+
+
+def test_infer_shape_and_internals():
+    sym = graphs.resnet50()
+    internals = sym.get_internals()
+    _, outs, _ = internals.infer_shape(data=(2, 3, 224, 224), softmax_label=(2,))
+    shapes = dict(zip(internals.list_outputs(), outs))
+    assert shapes["conv0_output"] == (2, 64, 112, 112)
+    # auto-named like MXNet's NameManager (global counter): pooling<i>
+    assert any(k.startswith("pooling") and v == (2, 64, 56, 56) for k, v in shapes.items())
+    assert shapes["stage4_unit3_conv3_output"] == (2, 2048, 7, 7)
+    assert shapes["fc1_output"] == (2, 1000)
+
+
+def test_json_roundtrip():
+    sym = graphs.resnet20_cifar()
+    js = sym.tojson()
+    d = json.loads(js)
+    assert d["nodes"][d["heads"][0][0]]["op"] == "SoftmaxOutput"
+    sym2 = mx.sym.load_json(js)
+    assert sym2.list_arguments() == sym.list_arguments()
+    assert sym2.list_auxiliary_states() == sym.list_auxiliary_states()
+    a1 = sym.infer_shape(data=(4, 3, 32, 32), softmax_label=(4,))
+    a2 = sym2.infer_shape(data=(4, 3, 32, 32), softmax_label=(4,))
+    assert a1 == a2
+
+
+def test_auto_names_and_attrs():
+    x = mx.sym.Variable("data")
+    c = mx.sym.Convolution(data=x, num_filter=8, kernel=(3, 3), pad=(1, 1), no_bias=True, name="c1")
+    assert c.list_arguments() == ["data", "c1_weight"]
+    b = mx.sym.BatchNorm(data=c, fix_gamma=False, name="b1")
+    assert b.list_auxiliary_states() == ["b1_moving_mean", "b1_moving_var"]
+    s = c + b
+    s._set_attr(mirror_stage="True")
+    assert s.attr("mirror_stage") == "True"
+    q = mx.sym.contrib.Quantization_int8(data=x, name="q", is_weight=False)
+    assert q.list_auxiliary_states() == ["q_minmax"]
+
+
+def test_plan_fusion_and_flops():
+    p = Plan(graphs.resnet50(), [("data", (256, 3, 224, 224))], [("softmax_label", (256,))])
+    assert p.summary() == {"stem": 1, "bn": 50, "pool": 2, "conv": 52, "fc": 1, "softmax": 1}
+    # 16 residual adds are all fused into conv epilogues
+    assert sum(1 for op in p.ops if op.kind == "conv" and op.res is not None) == 16
+    # 6,220.6 GFLOP per 256-image step
+    assert abs(p.train_flops() / 1e9 - 6220.6) < 0.1
+    p20 = Plan(graphs.resnet20_cifar(), [("data", (128, 3, 32, 32))], [("softmax_label", (128,))])
+    assert abs(p20.train_flops() / 1e9 - 31.2) < 0.05
+
+
+def test_plan_rejects_unsupported():
+    with pytest.raises(PlanError):
+        Plan(graphs.resnext50_32x4d(), [("data", (2, 3, 224, 224))], [("softmax_label", (2,))])
+
+
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_executor_dry_run(dtype):
+    sym = graphs.resnet([3, 4, 6, 3], 4, [64, 256, 512, 1024, 2048], 16)
+    p = Plan(sym, [("data", (2, 3, 64, 64))], [("softmax_label", (2,))], dtype=dtype)
+    ex = Executor(p, "cpu")
+    names = [c[0] for c in ex._bwd]
+    assert names.count("rn_conv_bwd_filter") == 54 and names.count("rn_conv_bwd_data") == 53
+    assert names.count("rn_stem_shift_grad") == 1
+    # every parameter's gradient has a producing call, buckets cover the flat buffer in order
+    assert set(ex.param_done_at) == set(p.param_names)
+    b = ex.buckets()
+    assert b[0][0] == 0 and b[-1][1] == ex.nparam
+    assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
+    assert all(b[i][2] <= b[i + 1][2] for i in range(len(b) - 1))
+    # parameter I/O round trip (OIHW <-> KRSC)
+    w = np.random.default_rng(0).standard_normal((64, 256, 1, 1)).astype(np.float32)
+    ex.set_param("stage2_unit1_conv1_weight", np.random.default_rng(1).standard_normal((128, 256, 1, 1)))
+    w3 = np.random.default_rng(2).standard_normal((128, 128, 3, 3)).astype(np.float32)
+    ex.set_param("stage2_unit1_conv2_weight", w3)
+    np.testing.assert_array_equal(ex.get_param("stage2_unit1_conv2_weight"), w3)
