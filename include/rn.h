@@ -86,7 +86,7 @@ int rn_im2col_nchw(const rn_conv_desc* d, const float* x_nchw, const float* scal
 
 /* d(beta) of a BN feeding the stem conv, without the stem dgrad:
  * dbeta[c] += sum_{k,r,s} w[k,r,s,c] * sum_{n,p,q valid(r,s)} dy[n,p,q,k].
- * ws: float workspace of p*q*k_pad + k*r*s elements. */
+ * ws: float workspace of p*q*k_pad + p*s*k + k*r*s elements. */
 int rn_stem_shift_grad(const rn_conv_desc* d, const void* dy, const float* w_master, float* dbeta,
                        float* ws, rn_stream_t stream);
 

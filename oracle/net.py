@@ -234,11 +234,14 @@ def init_params(graph, seed=2, dtype=np.float64):
     return args, aux
 
 
-def forward(graph, args, aux, data, label, is_train=True, quant_state=None, first_batch=True, storage=None):
+def forward(graph, args, aux, data, label, is_train=True, quant_state=None, first_batch=True, storage=None,
+            relu_masks=None):
     """Returns (prob, tape). Updates aux (moving stats) in place when is_train.
 
     storage='bf16' emulates a bf16-storage runtime: conv/FC weights and every stored activation
-    are rounded to bf16 (logits stay fp32), arithmetic stays in the array dtype."""
+    are rounded to bf16 (logits stay fp32), arithmetic stays in the array dtype.
+    relu_masks {relu op name: bool array} replays given ReLU decisions (y = x * mask) instead of
+    x > 0 -- parity diagnostics use it to remove rounding-induced decision flips."""
     rnd = ops.bf16_round if storage == "bf16" else (lambda a: a)
     env = {"data": data}
     tape = []
@@ -280,9 +283,11 @@ def forward(graph, args, aux, data, label, is_train=True, quant_state=None, firs
                 tape.append(dict(op=op))
             env[op["y"]] = rnd(y)
         elif t == "relu":
-            y = ops.relu_fwd(env[op["x"]])
+            x = env[op["x"]]
+            mask = relu_masks[op["name"]] if (relu_masks is not None and op["name"] in relu_masks) else (x > 0)
+            y = x * mask
             env[op["y"]] = y
-            tape.append(dict(op=op, y=y))
+            tape.append(dict(op=op, y=y, mask=mask))
         elif t == "maxpool":
             x = env[op["x"]]
             y, arg = ops.maxpool_fwd(x, op["kernel"], op["stride"], op["pad"])
@@ -302,8 +307,9 @@ def forward(graph, args, aux, data, label, is_train=True, quant_state=None, firs
     return env["softmax"], dict(tape=tape, env=env, label=label, rnd=rnd)
 
 
-def backward(graph, args, fwd_state, grad_scale=1.0):
-    """Returns grads {param name: array} for one forward tape."""
+def backward(graph, args, fwd_state, grad_scale=1.0, keep=None):
+    """Returns grads {param name: array} for one forward tape. If `keep` is a dict, the full
+    gradient of every activation tensor is recorded into it (diagnostics)."""
     tape = fwd_state["tape"]
     label = fwd_state["label"]
     rnd = fwd_state.get("rnd", lambda a: a)
@@ -326,6 +332,8 @@ def backward(graph, args, fwd_state, grad_scale=1.0):
         dy = g.pop(op["y"], None)
         if dy is None:
             continue
+        if keep is not None:
+            keep[op["y"]] = dy
         if t == "conv":
             need_dx = op["x"] != "data"
             dx, dw = ops.conv2d_bwd(rec["x"], rec["w"], dy, op["stride"], op["pad"], op["groups"], need_dx=need_dx)
@@ -348,7 +356,7 @@ def backward(graph, args, fwd_state, grad_scale=1.0):
             if op["x"] != "data":
                 acc(op["x"], dx)
         elif t == "relu":
-            acc(op["x"], ops.relu_bwd(dy, rec["y"]))
+            acc(op["x"], dy * rec["mask"])
         elif t == "maxpool":
             acc(op["x"], ops.maxpool_bwd(dy, rec["arg"], rec["shape"], op["kernel"], op["stride"], op["pad"]))
         elif t == "gap":
@@ -360,7 +368,7 @@ def backward(graph, args, fwd_state, grad_scale=1.0):
 
 
 def train_step(graph, args, aux, moms, data, label, lr, momentum=0.9, wd=1e-4, rescale_grad=None,
-               num_devices=1, quant_state=None, first_batch=True, storage=None):
+               num_devices=1, quant_state=None, first_batch=True, storage=None, relu_masks=None):
     """One Solver iteration (core/solver.py:115-121): forward(is_train) + backward + SGD update.
 
     num_devices > 1 restates Module's even batch split: per-slice BN statistics, per-slice
@@ -375,7 +383,7 @@ def train_step(graph, args, aux, moms, data, label, lr, momentum=0.9, wd=1e-4, r
     for d in range(num_devices):
         aux_d = {k: v.copy() for k, v in aux.items()}
         prob, st = forward(graph, args, aux_d, data[d * sl:(d + 1) * sl], label[d * sl:(d + 1) * sl], True,
-                           quant_state, first_batch, storage)
+                           quant_state, first_batch, storage, relu_masks)
         grads = backward(graph, args, st)
         for k, v in grads.items():
             gsum[k] = gsum[k] + v if k in gsum else v

@@ -88,29 +88,40 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, 
   }
 }
 
-// finalize: one thread group per channel; 4 lanes per channel reduce the partials.
-template <typename T>
-__global__ void bn_fwd_finalize_kernel(const T* __restrict__ x, const float* __restrict__ part, int nrb,
-                                       int64_t m, int c, int c_real, float eps, float momentum,
-                                       int fix_gamma, const float* __restrict__ gamma,
-                                       const float* __restrict__ beta, float* moving_mean,
-                                       float* moving_var, float* save_mean, float* save_invstd,
-                                       float* scale, float* shift) {
-  const int ch = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int lane4 = threadIdx.x >> 6;  // 0..3
-  double s = 0.0, q = 0.0;
-  if (ch < c)
-    for (int b = lane4; b < nrb; b += 4) {
-      s += part[((int64_t)b * c + ch) * 2];
-      q += part[((int64_t)b * c + ch) * 2 + 1];
-    }
+// finalize: one block per channel; fp64 reduction of the per-row-block partials.
+__device__ __forceinline__ void block_sum2(double& s, double& q) {
   __shared__ double rs[256], rq[256];
   rs[threadIdx.x] = s;
   rq[threadIdx.x] = q;
   __syncthreads();
-  if (lane4 != 0 || ch >= c) return;
-  s = rs[threadIdx.x] + rs[threadIdx.x + 64] + rs[threadIdx.x + 128] + rs[threadIdx.x + 192];
-  q = rq[threadIdx.x] + rq[threadIdx.x + 64] + rq[threadIdx.x + 128] + rq[threadIdx.x + 192];
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      rs[threadIdx.x] += rs[threadIdx.x + o];
+      rq[threadIdx.x] += rq[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  s = rs[0];
+  q = rq[0];
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const T* __restrict__ x, const float* __restrict__ part,
+                                                              int nrb, int64_t m, int c, int c_real, float eps,
+                                                              float momentum, int fix_gamma,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ beta, float* moving_mean,
+                                                              float* moving_var, float* save_mean, float* save_invstd,
+                                                              float* scale, float* shift) {
+  const int ch = blockIdx.x;
+  double s = 0.0, q = 0.0;
+  for (int b = threadIdx.x; b < nrb; b += blockDim.x) {
+    const float2 v = reinterpret_cast<const float2*>(part)[(int64_t)b * c + ch];
+    s += v.x;
+    q += v.y;
+  }
+  block_sum2(s, q);
+  if (threadIdx.x != 0) return;
   if (ch >= c_real) {
     scale[ch] = 0.f;
     shift[ch] = 0.f;
@@ -150,24 +161,33 @@ __global__ void bn_infer_coef_kernel(int c, int c_real, float eps, int fix_gamma
   shift[ch] = beta[ch] - mm[ch] * g * invstd;
 }
 
+// 2D elementwise layout: thread (tc, tr) owns channel chunk blockIdx.x*ct+tc for rows
+// blockIdx.y*rows_per_block + tr (step rl) -> per-channel coefficients live in registers.
 template <typename T, bool RELU>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                        const float* __restrict__ scale,
-                                                       const float* __restrict__ shift, int64_t nchunk,
-                                                       int cpr) {
+                                                       const float* __restrict__ shift, int64_t m, int c, int ct,
+                                                       int64_t rows_per_block) {
   constexpr int CE = 16 / sizeof(T);
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nchunk;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int cb = (int)(i % cpr) * CE;
-    uint4 u = reinterpret_cast<const uint4*>(x)[i];
+  const int tc = threadIdx.x % ct, tr = threadIdx.x / ct, rl = blockDim.x / ct;
+  const int cbase = (blockIdx.x * ct + tc) * CE;
+  const int64_t r0 = blockIdx.y * rows_per_block;
+  const int64_t r1 = min(m, r0 + rows_per_block);
+  float sc[CE], sh[CE];
+#pragma unroll
+  for (int e = 0; e < CE; ++e) {
+    sc[e] = scale[cbase + e];
+    sh[e] = shift[cbase + e];
+  }
+  for (int64_t r = r0 + tr; r < r1; r += rl) {
     float f[CE];
-    chunk_to_f(u, f, (const T*)nullptr);
+    chunk_to_f(*reinterpret_cast<const uint4*>(x + r * c + cbase), f, (const T*)nullptr);
 #pragma unroll
     for (int e = 0; e < CE; ++e) {
-      float v = fmaf(f[e], scale[cb + e], shift[cb + e]);
+      const float v = fmaf(f[e], sc[e], sh[e]);
       f[e] = RELU ? fmaxf(v, 0.f) : v;
     }
-    reinterpret_cast<uint4*>(y)[i] = f_to_chunk(f, (const T*)nullptr);
+    *reinterpret_cast<uint4*>(y + r * c + cbase) = f_to_chunk(f, (const T*)nullptr);
   }
 }
 
@@ -221,27 +241,22 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
   }
 }
 
-// coef[c] = {A = g*invstd, mdz = sum dz / m, A2 = g*invstd^2*sum(dz*xhat)/m... , mean}
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int64_t m, int c,
-                                       int c_real, int fix_gamma, const float* __restrict__ gamma,
-                                       const float* __restrict__ save_mean,
-                                       const float* __restrict__ save_invstd, float* dgamma,
-                                       float* dbeta, float* __restrict__ coef) {
-  const int ch = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int lane4 = threadIdx.x >> 6;
+// coef[c] = {A = g*invstd, mean(dz), A2 = g*invstd^2*sum(dz*xhat)/m, mean}; block per channel.
+__global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int64_t m,
+                                                              int c, int c_real, int fix_gamma,
+                                                              const float* __restrict__ gamma,
+                                                              const float* __restrict__ save_mean,
+                                                              const float* __restrict__ save_invstd, float* dgamma,
+                                                              float* dbeta, float* __restrict__ coef) {
+  const int ch = blockIdx.x;
   double s = 0.0, q = 0.0;
-  if (ch < c)
-    for (int b = lane4; b < nrb; b += 4) {
-      s += part[((int64_t)b * c + ch) * 2];
-      q += part[((int64_t)b * c + ch) * 2 + 1];
-    }
-  __shared__ double rs[256], rq[256];
-  rs[threadIdx.x] = s;
-  rq[threadIdx.x] = q;
-  __syncthreads();
-  if (lane4 != 0 || ch >= c) return;
-  s = rs[threadIdx.x] + rs[threadIdx.x + 64] + rs[threadIdx.x + 128] + rs[threadIdx.x + 192];
-  q = rq[threadIdx.x] + rq[threadIdx.x + 64] + rq[threadIdx.x + 128] + rq[threadIdx.x + 192];
+  for (int b = threadIdx.x; b < nrb; b += blockDim.x) {
+    const float2 v = reinterpret_cast<const float2*>(part)[(int64_t)b * c + ch];
+    s += v.x;
+    q += v.y;
+  }
+  block_sum2(s, q);
+  if (threadIdx.x != 0) return;
   if (ch >= c_real) {
     coef[ch * 4 + 0] = 0.f;
     coef[ch * 4 + 1] = 0.f;
@@ -265,32 +280,67 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
                                                            T* __restrict__ dx, const T* __restrict__ add,
                                                            const float* __restrict__ coef,
                                                            const float* __restrict__ scale,
-                                                           const float* __restrict__ shift, int64_t nchunk,
-                                                           int cpr) {
+                                                           const float* __restrict__ shift, int64_t m, int c, int ct,
+                                                           int64_t rows_per_block) {
   constexpr int CE = 16 / sizeof(T);
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nchunk;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int cb = (int)(i % cpr) * CE;
+  const int tc = threadIdx.x % ct, tr = threadIdx.x / ct, rl = blockDim.x / ct;
+  const int cbase = (blockIdx.x * ct + tc) * CE;
+  const int64_t r0 = blockIdx.y * rows_per_block;
+  const int64_t r1 = min(m, r0 + rows_per_block);
+  float A[CE], mdz[CE], A2[CE], mu[CE], sc[CE], sh[CE];
+#pragma unroll
+  for (int e = 0; e < CE; ++e) {
+    const float4 cf = reinterpret_cast<const float4*>(coef)[cbase + e];
+    A[e] = cf.x;
+    mdz[e] = cf.y;
+    A2[e] = cf.z;
+    mu[e] = cf.w;
+    sc[e] = scale[cbase + e];
+    sh[e] = shift[cbase + e];
+  }
+  for (int64_t r = r0 + tr; r < r1; r += rl) {
+    const int64_t off = r * c + cbase;
     float fx[CE], fd[CE], fa[CE];
-    chunk_to_f(reinterpret_cast<const uint4*>(x)[i], fx, (const T*)nullptr);
-    chunk_to_f(reinterpret_cast<const uint4*>(dy)[i], fd, (const T*)nullptr);
-    if (add) chunk_to_f(reinterpret_cast<const uint4*>(add)[i], fa, (const T*)nullptr);
+    chunk_to_f(*reinterpret_cast<const uint4*>(x + off), fx, (const T*)nullptr);
+    chunk_to_f(*reinterpret_cast<const uint4*>(dy + off), fd, (const T*)nullptr);
+    if (add) chunk_to_f(*reinterpret_cast<const uint4*>(add + off), fa, (const T*)nullptr);
 #pragma unroll
     for (int e = 0; e < CE; ++e) {
-      const int ch = cb + e;
-      const float4 cf = reinterpret_cast<const float4*>(coef)[ch];
-      const float dz = RELU ? fd[e] * relu_mask(fx[e], scale[ch], shift[ch]) : fd[e];
-      float v = cf.x * (dz - cf.y) - cf.z * (fx[e] - cf.w);
+      const float dz = RELU ? fd[e] * relu_mask(fx[e], sc[e], sh[e]) : fd[e];
+      float v = A[e] * (dz - mdz[e]) - A2[e] * (fx[e] - mu[e]);
       if (add) v += fa[e];
       fd[e] = v;
     }
-    reinterpret_cast<uint4*>(dx)[i] = f_to_chunk(fd, (const T*)nullptr);
+    *reinterpret_cast<uint4*>(dx + off) = f_to_chunk(fd, (const T*)nullptr);
   }
 }
 
-int apply_grid(int64_t nchunk) {
-  int64_t g = (nchunk + 255) / 256;
-  return (int)std::min<int64_t>(std::max<int64_t>(g, 1), 256 * 16);
+// Elementwise (apply) geometry: same channel tiling as the reductions, more row blocks so
+// that ~8 blocks per CU stream with every thread touching >= 8 rows.
+template <typename T>
+Geo make_apply_geo(int64_t m, int c) {
+  Geo g = make_geo<T>(m, c);
+  int64_t want = std::max<int64_t>(1, 4096 / g.gx);
+  int64_t maxrb = std::max<int64_t>(1, m / (g.rl * 8));
+  g.nrb = (int)std::min(want, maxrb);
+  g.rows_per_block = ceil_div(m, g.nrb);
+  return g;
+}
+
+template <typename T, bool RELU>
+void launch_apply(const rn_bn_desc* d, const void* x, void* y, const float* scale, const float* shift,
+                  hipStream_t st) {
+  Geo a = make_apply_geo<T>(d->m, d->c);
+  hipLaunchKernelGGL((bn_apply_kernel<T, RELU>), dim3(a.gx, a.nrb), dim3(kThreads), 0, st, (const T*)x, (T*)y,
+                     scale, shift, d->m, d->c, a.ct, a.rows_per_block);
+}
+
+template <typename T, bool RELU>
+void launch_bwd_apply(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const void* add,
+                      const float* coef, const float* scale, const float* shift, hipStream_t st) {
+  Geo a = make_apply_geo<T>(d->m, d->c);
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RELU>), dim3(a.gx, a.nrb), dim3(kThreads), 0, st, (const T*)x,
+                     (const T*)dy, (T*)dx, (const T*)add, coef, scale, shift, d->m, d->c, a.ct, a.rows_per_block);
 }
 
 template <typename T>
@@ -301,18 +351,12 @@ int bn_fwd_train_t(const rn_bn_desc* d, const void* x, void* y, const float* gam
   float* part = reinterpret_cast<float*>(ws);
   hipLaunchKernelGGL(bn_stats_kernel<T>, dim3(g.gx, g.nrb), dim3(kThreads), 0, st, (const T*)x, d->m,
                      d->c, g.ct, g.rows_per_block, part);
-  hipLaunchKernelGGL(bn_fwd_finalize_kernel<T>, dim3((d->c + 63) / 64), dim3(256), 0, st, (const T*)x, part,
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel<T>, dim3(d->c), dim3(256), 0, st, (const T*)x, part,
                      g.nrb, d->m, d->c, d->c_real, d->eps, d->momentum, d->fix_gamma, gamma, beta, mm, mv,
                      smean, sinv, scale, shift);
   if (y) {
-    const int CE = 16 / sizeof(T);
-    const int64_t nchunk = d->m * d->c / CE;
-    if (d->relu)
-      hipLaunchKernelGGL((bn_apply_kernel<T, true>), dim3(apply_grid(nchunk)), dim3(256), 0, st, (const T*)x,
-                         (T*)y, scale, shift, nchunk, d->c / CE);
-    else
-      hipLaunchKernelGGL((bn_apply_kernel<T, false>), dim3(apply_grid(nchunk)), dim3(256), 0, st, (const T*)x,
-                         (T*)y, scale, shift, nchunk, d->c / CE);
+    if (d->relu) launch_apply<T, true>(d, x, y, scale, shift, st);
+    else launch_apply<T, false>(d, x, y, scale, shift, st);
   }
   return rn_check_launch("bn_fwd_train");
 }
@@ -320,14 +364,8 @@ int bn_fwd_train_t(const rn_bn_desc* d, const void* x, void* y, const float* gam
 template <typename T>
 int bn_apply_t(const rn_bn_desc* d, const void* x, void* y, const float* scale, const float* shift,
                hipStream_t st) {
-  const int CE = 16 / sizeof(T);
-  const int64_t nchunk = d->m * d->c / CE;
-  if (d->relu)
-    hipLaunchKernelGGL((bn_apply_kernel<T, true>), dim3(apply_grid(nchunk)), dim3(256), 0, st, (const T*)x,
-                       (T*)y, scale, shift, nchunk, d->c / CE);
-  else
-    hipLaunchKernelGGL((bn_apply_kernel<T, false>), dim3(apply_grid(nchunk)), dim3(256), 0, st, (const T*)x,
-                       (T*)y, scale, shift, nchunk, d->c / CE);
+  if (d->relu) launch_apply<T, true>(d, x, y, scale, shift, st);
+  else launch_apply<T, false>(d, x, y, scale, shift, st);
   return rn_check_launch("bn_apply");
 }
 
@@ -345,17 +383,11 @@ int bn_bwd_t(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const
   else
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(g.gx, g.nrb), dim3(kThreads), 0, st, (const T*)x,
                        (const T*)dy, d->m, d->c, g.ct, g.rows_per_block, smean, scale, shift, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((d->c + 63) / 64), dim3(256), 0, st, part, g.nrb, d->m, d->c,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(d->c), dim3(256), 0, st, part, g.nrb, d->m, d->c,
                      d->c_real, d->fix_gamma, gamma, smean, sinv, dgamma, dbeta, coef);
   if (dx) {
-    const int CE = 16 / sizeof(T);
-    const int64_t nchunk = d->m * d->c / CE;
-    if (d->relu)
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true>), dim3(apply_grid(nchunk)), dim3(256), 0, st, (const T*)x,
-                         (const T*)dy, (T*)dx, (const T*)add, coef, scale, shift, nchunk, d->c / CE);
-    else
-      hipLaunchKernelGGL((bn_bwd_apply_kernel<T, false>), dim3(apply_grid(nchunk)), dim3(256), 0, st, (const T*)x,
-                         (const T*)dy, (T*)dx, (const T*)add, coef, scale, shift, nchunk, d->c / CE);
+    if (d->relu) launch_bwd_apply<T, true>(d, x, dy, dx, add, coef, scale, shift, st);
+    else launch_bwd_apply<T, false>(d, x, dy, dx, add, coef, scale, shift, st);
   }
   return rn_check_launch("bn_bwd");
 }

@@ -84,7 +84,10 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
   constexpr int B_CH = BN / 32;
   constexpr int MI = BM / 32;          // 16x16 tiles per wave (rows)
   constexpr int NI = BN / 32;
-  __shared__ __attribute__((aligned(16))) uint4 smem[2 * (BM + BN) * 8];
+  // one LDS arena: double-buffered A/B stages in the K loop, the fp32 output tile after it
+  constexpr int kStageChunks = 2 * (BM + BN) * 8;
+  constexpr int kTileChunks = BM * (BN + 4) * 4 / 16;
+  __shared__ __attribute__((aligned(16))) uint4 smem[kStageChunks > kTileChunks ? kStageChunks : kTileChunks];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -120,23 +123,32 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
       a_wb[i] = 0;
     }
   }
-  int64_t b_off[B_CH];
+  int b_off[B_CH];  // 32-bit: weight matrices are far below 2^31 elements (host-checked)
   bool b_ok[B_CH];
 #pragma unroll
   for (int i = 0; i < B_CH; ++i) {
     const int col = n0 + (tid >> 3) + 32 * i;
     b_ok[i] = col < p.K;
-    b_off[i] = (int64_t)(b_ok[i] ? col : 0) * p.wrow;
+    b_off[i] = (b_ok[i] ? col : 0) * p.wrow;
   }
 
   const int ncb = (p.C + BKE - 1) / BKE;
   const int nstage = cl.nr * cl.ns * ncb;
 
-  uint4 ra[A_CH], rb[B_CH];
-  // stage iteration state
-  int st_tr = 0, st_ts = 0, st_cb = 0;
+  // register-staged loads: stage t+1 is loaded while stage t is computed, then written to
+  // the other LDS buffer (async-STAGE split: write after the MFMA phase).
+  uint4 ra0[A_CH], rb0[B_CH];
+  int st_tr = 0, st_ts = 0, st_cb = 0;  // next stage to load
 
-  auto load_stage = [&](int tr, int ts, int cb) {
+  auto load_stage = [&](uint4* ra, uint4* rb) {
+    const int tr = st_tr, ts = st_ts, cb = st_cb;
+    if (++st_cb == ncb) {
+      st_cb = 0;
+      if (++st_ts == cl.ns) {
+        st_ts = 0;
+        ++st_tr;
+      }
+    }
     const int r = cl.r0 + p.rstep * tr;
     const int s = cl.s0 + p.sstep * ts;
     const int hoff = cl.hoff0 + p.hinc * tr;
@@ -149,20 +161,20 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
       const int win = a_wb[i] + woff;
       const bool ok = cok && (unsigned)hin < (unsigned)p.H && (unsigned)win < (unsigned)p.W;
       if (ok) {
-        const int64_t off = ((int64_t)(a_pix[i] + hin * p.W + win)) * p.C + c;
+        const int off = (a_pix[i] + hin * p.W + win) * p.C + c;  // < 2^31 (host-checked)
         ra[i] = *reinterpret_cast<const uint4*>(xg + off);
       } else {
         ra[i] = make_uint4(0, 0, 0, 0);
       }
     }
-    const int64_t toff = (int64_t)(r * p.S + s) * p.C + c;
+    const int toff = (r * p.S + s) * p.C + c;
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       if (cok && b_ok[i]) rb[i] = *reinterpret_cast<const uint4*>(wg + b_off[i] + toff);
       else rb[i] = make_uint4(0, 0, 0, 0);
     }
   };
-  auto store_stage = [&](int buf) {
+  auto store_stage = [&](int buf, const uint4* ra, const uint4* rb) {
     uint4* As = smem + buf * (BM + BN) * 8;
     uint4* Bs = As + BM * 8;
 #pragma unroll
@@ -176,15 +188,6 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
       Bs[row * 8 + swz(row, ch)] = rb[i];
     }
   };
-  auto advance = [&]() {
-    if (++st_cb == ncb) {
-      st_cb = 0;
-      if (++st_ts == cl.ns) {
-        st_ts = 0;
-        ++st_tr;
-      }
-    }
-  };
 
   v4f acc[MI][NI];
 #pragma unroll
@@ -192,19 +195,8 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
-  if (nstage > 0) {
-    load_stage(st_tr, st_ts, st_cb);
-    advance();
-    store_stage(0);
-    __syncthreads();
-  }
-  for (int t = 0; t < nstage; ++t) {
-    const bool more = t + 1 < nstage;
-    if (more) {
-      load_stage(st_tr, st_ts, st_cb);
-      advance();
-    }
-    const uint4* As = smem + (t & 1) * (BM + BN) * 8;
+  auto compute = [&](int buf) {
+    const uint4* As = smem + buf * (BM + BN) * 8;
     const uint4* Bs = As + BM * 8;
 #pragma unroll
     for (int slab = 0; slab < 2; ++slab) {
@@ -225,35 +217,104 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
 #pragma unroll
         for (int j = 0; j < NI; ++j) mfma_slab<T>(acc[i][j], af[i], bfr[j]);
     }
-    if (more) store_stage((t + 1) & 1);
+  };
+
+  // ---- epilogue chunk assignment (decoded once; residual chunks prefetched in the last stage)
+  constexpr int OE = 16 / sizeof(OutT);  // output elements per 16-byte chunk
+  constexpr int CPR = BN / OE;           // chunks per tile row
+  constexpr int EPC = BM * CPR / 256;    // epilogue chunks per thread
+  constexpr int EPH = EPC >= 2 ? EPC / 2 : 1;  // processed in halves (register pressure)
+  const OutT* __restrict__ ag = reinterpret_cast<const OutT*>(p.add);
+  int64_t ep_off[EPH];
+  uint4 ep_add[EPH];
+  auto prefetch_add = [&](int half) {
+#pragma unroll
+    for (int k = 0; k < EPH; ++k) {
+      const int cidx = tid + 256 * (k + half * EPH);
+      const int row = cidx / CPR;
+      const int cc = cidx - row * CPR;
+      const int m = m0 + row;
+      const int col0 = n0 + cc * OE;
+      ep_off[k] = -1;
+      ep_add[k] = make_uint4(0, 0, 0, 0);
+      if (m < Mc && col0 < p.K) {
+        const int n = fdiv(m, cl.fdPQ);
+        const int rem = m - n * cl.Pc * cl.Qc;
+        const int ii = fdiv(rem, cl.fdQ);
+        const int jj = rem - ii * cl.Qc;
+        const int oh = cl.a + p.ostep_h * ii;
+        const int ow = cl.b + p.ostep_w * jj;
+        ep_off[k] = ((int64_t)(n * p.P + oh) * p.Q + ow) * p.ldo + col0;
+        if (ag && col0 + OE <= p.K) ep_add[k] = *reinterpret_cast<const uint4*>(ag + ep_off[k]);
+      }
+    }
+  };
+
+  if (nstage > 0) {
+    load_stage(ra0, rb0);
+    store_stage(0, ra0, rb0);
+    __syncthreads();
+  }
+  for (int t = 0; t < nstage; ++t) {
+    const bool more = t + 1 < nstage;
+    if (more) load_stage(ra0, rb0);
+    compute(t & 1);
+    if (more) store_stage((t + 1) & 1, ra0, rb0);
     __syncthreads();
   }
 
-  // ---- epilogue: (+bias) (+add) -> OutT
+  // ---- epilogue: stage the fp32 tile through LDS, then every thread writes whole 16-byte
+  // output chunks along a row (+bias, +prefetched add_src chunk).
+  constexpr int LDT = BN + 4;  // fp32 row stride of the staged tile (pad: 2-way -> conflict-free)
+  static_assert(BM * LDT * 4 <= (int)sizeof(smem), "epilogue tile does not fit the staging LDS");
+  static_assert(BM * CPR % 256 == 0, "epilogue chunks must divide over the block");
+  float* tile = reinterpret_cast<float*>(smem);
+  prefetch_add(0);  // residual loads fly while the accumulator tile is staged
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int row = wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + e;
+        const int col = wn * (BN / 2) + j * 16 + (lane & 15);
+        tile[row * LDT + col] = acc[i][j][e];
+      }
+  __syncthreads();
   OutT* __restrict__ yg = reinterpret_cast<OutT*>(p.y);
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
+  for (int half = 0; half < EPC / EPH; ++half) {
+  if (half > 0) prefetch_add(half);
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int m = m0 + wm * (BM / 2) + i * 16 + (lane >> 4) * 4 + e;
-      if (m >= Mc) continue;
-      const int n = fdiv(m, cl.fdPQ);
-      const int rem = m - n * cl.Pc * cl.Qc;
-      const int ii = fdiv(rem, cl.fdQ);
-      const int jj = rem - ii * cl.Qc;
-      const int oh = cl.a + p.ostep_h * ii;
-      const int ow = cl.b + p.ostep_w * jj;
-      const int64_t orow = ((int64_t)(n * p.P + oh) * p.Q + ow) * p.ldo;
+  for (int k = 0; k < EPH; ++k) {
+    if (ep_off[k] < 0) continue;
+    const int cidx = tid + 256 * (k + half * EPH);
+    const int row = cidx / CPR;
+    const int cc = cidx - row * CPR;
+    const int col0 = n0 + cc * OE;
+    float v[OE];
 #pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int col = n0 + wn * (BN / 2) + j * 16 + (lane & 15);
-        if (col >= p.K) continue;
-        float v = acc[i][j][e];
-        if (p.bias) v += p.bias[col];
-        if (p.add) v += load_out<OutT>(p.add, orow + col);
-        yg[orow + col] = from_f<OutT>(v);
+    for (int e = 0; e < OE; ++e) v[e] = tile[row * LDT + cc * OE + e];
+    if (p.bias) {
+#pragma unroll
+      for (int e = 0; e < OE; ++e) v[e] += (col0 + e < p.K) ? p.bias[col0 + e] : 0.f;
+    }
+    if (col0 + OE <= p.K) {  // full chunk: vector path
+      if (ag) {
+        float a[OE];
+        chunk_to_f(ep_add[k], a, (const OutT*)nullptr);
+#pragma unroll
+        for (int e = 0; e < OE; ++e) v[e] += a[e];
+      }
+      *reinterpret_cast<uint4*>(yg + ep_off[k]) = f_to_chunk(v, (const OutT*)nullptr);
+    } else {  // ragged last chunk (num_hidden % 8 != 0)
+      for (int e = 0; e < OE && col0 + e < p.K; ++e) {
+        float o = v[e];
+        if (ag) o += to_f(ag[ep_off[k] + e]);
+        yg[ep_off[k] + e] = from_f<OutT>(o);
       }
     }
+  }
   }
 }
 
@@ -496,34 +557,43 @@ __global__ void pack_crsk_kernel(const float* __restrict__ wm, T* __restrict__ o
   }
 }
 
+// thread per (row m, 16-byte output chunk): 8 (bf16) / 4 (f32) consecutive im2col columns
 template <typename T>
-__global__ void im2col_nchw_kernel(const float* __restrict__ x, const float* __restrict__ scale,
-                                   const float* __restrict__ shift, T* __restrict__ cols, int N,
-                                   int C, int H, int W, int P, int Q, int R, int S, int sh, int sw,
-                                   int ph, int pw, int kc) {
-  const int64_t M = (int64_t)N * P * Q;
+__global__ __launch_bounds__(256) void im2col_nchw_kernel(const float* __restrict__ x, const float* __restrict__ scale,
+                                                          const float* __restrict__ shift, T* __restrict__ cols, int N,
+                                                          int C, int H, int W, int P, int Q, int R, int S, int sh,
+                                                          int sw, int ph, int pw, int kc, FastDiv fdQ, FastDiv fdP,
+                                                          FastDiv fdCH) {
+  constexpr int CE = 16 / sizeof(T);
+  const int cpr = kc / CE;
+  const int64_t total = (int64_t)N * P * Q * cpr;
   const int kreal = R * S * C;
-  const int64_t total = M * kc;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const int col = (int)(i % kc);
-    const int64_t m = i / kc;
-    float v = 0.f;
-    if (col < kreal) {
-      const int c = col % C;
-      const int tap = col / C;
-      const int r = tap / S, s = tap % S;
-      const int q = (int)(m % Q);
-      const int64_t t2 = m / Q;
-      const int pp = (int)(t2 % P);
-      const int n = (int)(t2 / P);
-      const int h = pp * sh - ph + r, w = q * sw - pw + s;
-      if (h >= 0 && h < H && w >= 0 && w < W) {
-        v = x[(((int64_t)n * C + c) * H + h) * W + w];
-        if (scale) v = fmaf(v, scale[c], shift[c]);
+    const int m = (int)(i / cpr);
+    const int ck = (int)(i - (int64_t)m * cpr);
+    const int t2 = fdiv(m, fdQ);
+    const int q = m - t2 * Q;
+    const int n = fdiv(t2, fdP);
+    const int pp = t2 - n * P;
+    float v[CE];
+#pragma unroll
+    for (int e = 0; e < CE; ++e) {
+      const int col = ck * CE + e;
+      float val = 0.f;
+      if (col < kreal) {
+        const int tap = fdiv(col, fdCH);
+        const int c = col - tap * C;
+        const int r = tap / S, s = tap - (tap / S) * S;
+        const int h = pp * sh - ph + r, w = q * sw - pw + s;
+        if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
+          val = x[(((int64_t)n * C + c) * H + h) * W + w];
+          if (scale) val = fmaf(val, scale[c], shift[c]);
+        }
       }
+      v[e] = val;
     }
-    cols[i] = from_f<T>(v);
+    reinterpret_cast<uint4*>(cols)[i] = f_to_chunk(v, (const T*)nullptr);
   }
 }
 
@@ -539,10 +609,24 @@ __global__ void stem_sum_n_kernel(const T* __restrict__ dy, float* __restrict__ 
     ws[i] = acc;
   }
 }
-// G[k][r][s] = sum_{p in V(r), q in V(s)} S[p][q][k]
-__global__ void stem_tap_sum_kernel(const float* __restrict__ ws, float* __restrict__ g, int K,
-                                    int kpad, int R, int S, int H, int W, int P, int Q, int sh,
-                                    int sw, int ph, int pw) {
+// separable rectangle sums: Tq[p][s][k] = sum_{q in V(s)} S[p][q][k];
+// G[k][r][s] = sum_{p in V(r)} Tq[p][s][k]   (V = output positions whose tap lands in-bounds)
+__global__ void stem_colsum_kernel(const float* __restrict__ ws, float* __restrict__ tq, int K, int kpad, int S,
+                                   int W, int P, int Q, int sw, int pw) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= P * S * K) return;
+  const int k = idx % K;
+  const int s = (idx / K) % S;
+  const int pp = idx / (K * S);
+  float acc = 0.f;
+  for (int q = 0; q < Q; ++q) {
+    const int w = q * sw - pw + s;
+    if (w >= 0 && w < W) acc += ws[((int64_t)pp * Q + q) * kpad + k];
+  }
+  tq[idx] = acc;
+}
+__global__ void stem_tap_sum_kernel(const float* __restrict__ tq, float* __restrict__ g, int K, int R, int S, int H,
+                                    int P, int sh, int ph) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= K * R * S) return;
   const int k = idx / (R * S);
@@ -551,12 +635,7 @@ __global__ void stem_tap_sum_kernel(const float* __restrict__ ws, float* __restr
   float acc = 0.f;
   for (int pp = 0; pp < P; ++pp) {
     const int h = pp * sh - ph + r;
-    if (h < 0 || h >= H) continue;
-    for (int q = 0; q < Q; ++q) {
-      const int w = q * sw - pw + s;
-      if (w < 0 || w >= W) continue;
-      acc += ws[((int64_t)pp * Q + q) * kpad + k];
-    }
+    if (h >= 0 && h < H) acc += tq[((int64_t)pp * S + s) * K + k];
   }
   g[idx] = acc;
 }
@@ -633,6 +712,8 @@ IgemmArgs make_igemm_args(const rn_conv_desc* d, int mode) {
 
 template <typename T, typename OutT>
 int launch_igemm(const IgemmArgs& a, hipStream_t st) {
+  RN_CHECK_ARG((int64_t)a.N * a.H * a.W * a.C < (1ll << 31), "gathered tensor exceeds 2^31 elements");
+  RN_CHECK_ARG((int64_t)a.K * a.wrow < (1ll << 31), "weight matrix exceeds 2^31 elements");
   int maxMc = 0;
   for (int z = 0; z < a.ncls; ++z) maxMc = std::max(maxMc, a.N * a.cls[z].Pc * a.cls[z].Qc);
   if (maxMc == 0) return 0;
@@ -767,16 +848,19 @@ int rn_im2col_nchw(const rn_conv_desc* d, const float* x, const float* scale, co
   RN_CHECK_ARG(d && x && cols, "null argument");
   RN_CHECK_ARG(kc >= d->r * d->s * d->c_real && kc % 8 == 0, "bad kc");
   RN_CHECK_ARG((scale == nullptr) == (shift == nullptr), "scale/shift must both be set");
-  const int64_t total = (int64_t)d->n * d->p * d->q * kc;
   hipStream_t st = as_stream(stream);
-  if (d->dtype == RN_BF16)
+  const FastDiv fq = make_fastdiv(d->q), fp = make_fastdiv(d->p), fc = make_fastdiv(d->c_real);
+  if (d->dtype == RN_BF16) {
+    const int64_t total = (int64_t)d->n * d->p * d->q * (kc / 8);
     hipLaunchKernelGGL(im2col_nchw_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st, x,
                        scale, shift, (bf16_t*)cols, d->n, d->c_real, d->h, d->w, d->p, d->q, d->r,
-                       d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, kc);
-  else
+                       d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, kc, fq, fp, fc);
+  } else {
+    const int64_t total = (int64_t)d->n * d->p * d->q * (kc / 4);
     hipLaunchKernelGGL(im2col_nchw_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, x,
                        scale, shift, (float*)cols, d->n, d->c_real, d->h, d->w, d->p, d->q, d->r,
-                       d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, kc);
+                       d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, kc, fq, fp, fc);
+  }
   return rn_check_launch("im2col");
 }
 
@@ -792,11 +876,14 @@ int rn_stem_shift_grad(const rn_conv_desc* d, const void* dy, const float* wm, f
   else
     hipLaunchKernelGGL(stem_sum_n_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st,
                        (const float*)dy, ws, d->n, PQ, d->k_pad);
-  float* g = ws + total;
+  float* tq = ws + total;
+  const int ntq = d->p * d->s * d->k;
+  hipLaunchKernelGGL(stem_colsum_kernel, dim3((ntq + 255) / 256), dim3(256), 0, st, ws, tq, d->k, d->k_pad, d->s,
+                     d->w, d->p, d->q, d->stride_w, d->pad_w);
+  float* g = tq + ntq;
   const int nkt = d->k * d->r * d->s;
-  hipLaunchKernelGGL(stem_tap_sum_kernel, dim3((nkt + 63) / 64), dim3(64), 0, st, ws, g, d->k,
-                     d->k_pad, d->r, d->s, d->h, d->w, d->p, d->q, d->stride_h, d->stride_w,
-                     d->pad_h, d->pad_w);
+  hipLaunchKernelGGL(stem_tap_sum_kernel, dim3((nkt + 63) / 64), dim3(64), 0, st, tq, g, d->k, d->r, d->s, d->h,
+                     d->p, d->stride_h, d->pad_h);
   hipLaunchKernelGGL(stem_shift_reduce_kernel, dim3(d->c_real), dim3(256), 0, st, g, wm, dbeta,
                      d->k, d->r * d->s, d->c_real);
   return rn_check_launch("stem_shift_grad");

@@ -219,6 +219,7 @@ class Plan:
                     done.add(id(n))  # folded into the stem conv (bn_data)
                     continue
                 self._lower_bn(n, relu_node)
+                self.ops[-1].relu_name = relu_node.name if relu_node is not None else None
                 done.add(id(n))
                 if relu_node is not None:
                     self.alias[id(relu_node)] = id(n)
@@ -229,7 +230,7 @@ class Plan:
                     raise PlanError("Activation %s is not supported" % act)
                 x = self.tensor(n.inputs[0][0])
                 y = self._new_tensor(n, self.shape_of(n))
-                self.ops.append(PlanOp("relu", n.name, x=x, y=y))
+                self.ops.append(PlanOp("relu", n.name, x=x, y=y, relu_name=n.name))
                 done.add(id(n))
             elif op in ("_Plus", "elemwise_add", "ElementWiseSum"):
                 if len(n.inputs) != 2:
@@ -238,7 +239,8 @@ class Plan:
                 b = self.tensor(n.inputs[1][0])
                 relu_node = fused_add_relu.get(id(n))
                 y = self._new_tensor(n, self.shape_of(n))
-                self.ops.append(PlanOp("add", n.name, a=a, b=b, y=y, relu=relu_node is not None))
+                self.ops.append(PlanOp("add", n.name, a=a, b=b, y=y, relu=relu_node is not None,
+                                       relu_name=relu_node.name if relu_node is not None else None))
                 done.add(id(n))
                 if relu_node is not None:
                     self.alias[id(relu_node)] = id(n)
@@ -616,7 +618,7 @@ class Executor:
                 op.wk = self._zeros(y.c * op.kc, self.tdtype)
                 self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(d1), self._pp(op.weight),
                                              self._p(op.wk), None, sp))
-                stem_ws = max(stem_ws, y.h * y.w * y.cp + y.c * op.kernel[0] * op.kernel[1] + 64)
+                stem_ws = max(stem_ws, y.h * y.w * y.cp + y.h * op.kernel[1] * y.c + y.c * op.kernel[0] * op.kernel[1] + 64)
                 xnchw = self._p(self.act(x))
                 if op.bn:
                     b = op.bn

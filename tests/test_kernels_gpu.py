@@ -127,7 +127,7 @@ def test_stem_im2col_and_shift_grad(gpu, dtype):
     dw = torch.zeros(k * r * r * c, dtype=torch.float32, device=gpu)
     L.call("rn_conv_bwd_filter", C.byref(d1), p(cols), p(dyd), p(dw), stream())
     dbeta = torch.zeros(c, dtype=torch.float32, device=gpu)
-    ws = torch.zeros(P * Q * pad8(k) + k * r * r, dtype=torch.float32, device=gpu)
+    ws = torch.zeros(P * Q * pad8(k) + P * r * k + k * r * r, dtype=torch.float32, device=gpu)
     L.call("rn_stem_shift_grad", C.byref(dfull), p(dyd), p(master), p(dbeta), p(ws), stream())
     torch.cuda.synchronize()
     assert rel_err(from_nhwc(y, k), ref) < TOL[dtype]
@@ -174,7 +174,7 @@ def test_bn_relu(gpu, dtype, case):
     dyd = to_nhwc(dy, dtype, gpu)
     dxd = torch.zeros_like(xd)
     addd = to_nhwc(np.ones_like(x), dtype, gpu)
-    dg, db = torch.zeros(cp, device=gpu), torch.zeros(cp, device=gpu)
+    dg, db = torch.zeros(cp, dtype=torch.float32, device=gpu), torch.zeros(cp, dtype=torch.float32, device=gpu)
     L.call("rn_bn_bwd", C.byref(d), p(xd), p(dyd), p(dxd), p(addd), p(g_d), p(sm), p(si), p(sc), p(sh), p(dg), p(db),
            p(ws), stream())
     torch.cuda.synchronize()
@@ -239,10 +239,10 @@ def test_softmax_output(gpu, dtype):
     prob_ref = ops.softmax_output_fwd(z)
     g_ref = ops.softmax_output_bwd(prob_ref, lab)
     zd = torch.tensor(z, dtype=torch.float32, device=gpu)
-    ld_ = torch.tensor(lab, device=gpu)
-    prob = torch.zeros((b, ncls), device=gpu)
+    ld_ = torch.tensor(lab, dtype=torch.float32, device=gpu)
+    prob = torch.zeros((b, ncls), dtype=torch.float32, device=gpu)
     dl = torch.zeros((b, ld), dtype=tdt(dtype), device=gpu)
-    stats = torch.zeros(4, device=gpu)
+    stats = torch.zeros(4, dtype=torch.float32, device=gpu)
     L.call("rn_softmax_output", dtype, b, ncls, ld, p(zd), p(ld_), p(prob), p(dl), C.c_float(1.0), p(stats), stream())
     torch.cuda.synchronize()
     assert rel_err(prob.cpu().numpy(), prob_ref) < 1e-5
@@ -290,7 +290,7 @@ def test_quant_int8(gpu, dtype):
     wq_ref, _ = ops.quant_int8_weight(w)
     xd = torch.tensor(w, dtype=tdt(dtype), device=gpu)
     out = torch.zeros_like(xd)
-    ws = torch.zeros(4096, device=gpu)
+    ws = torch.zeros(4096, dtype=torch.float32, device=gpu)
     L.call("rn_quant_int8_fwd", dtype, n, p(xd), p(out), None, 1, 1, C.c_float(0.99), 1, 8, p(ws), stream())
     torch.cuda.synchronize()
     tol = 1e-6 if dtype == F32 else 1e-2
@@ -299,7 +299,7 @@ def test_quant_int8(gpu, dtype):
     x = rng.standard_normal(n) * 3
     if dtype == BF16:
         x = bf16_round(x)
-    mm = torch.tensor([2.0], device=gpu)
+    mm = torch.tensor([2.0], dtype=torch.float32, device=gpu)
     xq_ref, mm_ref = ops.quant_int8_act(x, 2.0, True, False)
     xd = torch.tensor(x, dtype=tdt(dtype), device=gpu)
     L.call("rn_quant_int8_fwd", dtype, n, p(xd), p(out), p(mm), 0, 1, C.c_float(0.99), 0, 8, p(ws), stream())

@@ -12,11 +12,9 @@ import torch.nn.functional as F
 from oracle import net as onet
 from oracle import ops
 
-torch.set_default_dtype(torch.float64)
-
-
 def T(a, grad=False):
-    return torch.tensor(np.asarray(a, dtype=np.float64), requires_grad=grad)
+    # explicit dtype: never touch torch's global default (GPU tests share the session)
+    return torch.tensor(np.asarray(a, dtype=np.float64), dtype=torch.float64, requires_grad=grad)
 
 
 @pytest.mark.parametrize("case", [(2, 6, 9, 7, 4, 3, 2, 1, 1), (1, 8, 8, 8, 16, 1, 1, 0, 1), (2, 8, 10, 10, 8, 3, 1, 1, 4),

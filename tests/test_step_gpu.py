@@ -4,21 +4,24 @@ Same initial parameters, same seeded synthetic batch (data/imagenet.py:15-18 res
 two Solver steps (forward(is_train) -> backward -> SGD update, core/solver.py:115-121).
 Tolerances (max |err| / max |ref| per tensor):
   ResNet-20 fp32: probs 1e-4, grads 2e-3, updated params 1e-5, moving stats 1e-4.
-  ResNet-50 fp32: probs 1e-4; every grad (Frobenius-relative), param and moving stat within 4x
-    the numpy oracle's own fp32-vs-fp64 error + 2e-3 (the small-spatial R50 is ill-conditioned:
-    train-mode BN backward over few elements cancels heavily and ReLU decisions flip, so an fp32
-    implementation is judged against what fp32 numpy achieves on the same inputs).
-  bf16 runtime path: per-kernel parity lives in test_kernels_gpu.py; whole-network, bf16 storage
-    makes tiny-config gradients noise-dominated even in the oracle's bf16-storage emulation, so the
-    check is the loss trajectory of 4 SGD steps on a fixed batch: ResNet-20 within 2% of the fp64
-    oracle at every step, ResNet-50 within 10% and decreasing.
+  ResNet-50 fp32: probs 1e-4, loss 1e-5. At this small spatial size a single ReLU decision
+    that flips under fp32 rounding (e.g. in stage4_unit3_bn2: 4x2x2 = 16 elements per channel)
+    moves every upstream gradient by ~1/sqrt(8192) = 1.1% -- numpy fp32 vs fp64 shows the same
+    chaos, and which elements flip depends on fp32 atomic summation order. So the oracle REPLAYS
+    the ReLU decisions the device made (oracle.net.forward relu_masks); then every gradient must
+    match the fp64 oracle to max(1e-4, 4x the error numpy fp32 makes on that tensor under the same
+    decisions) (Frobenius-relative; only cancellation-dominated BN-gamma grads use the second term).
+  ResNet-20 two steps: the same replay for step 1's decisions, step 2 compared on probs (1e-4).
+  bf16 runtime path: per-kernel parity lives in test_kernels_gpu.py. Whole-network, bf16 storage
+    makes tiny-config gradients noise-dominated (also in the oracle's bf16-storage emulation),
+    so the checks are: first-step loss within 2% of the fp64 oracle, and 4 SGD steps on a fixed
+    batch decrease the loss monotonically (ResNet-20 below 80% / ResNet-50 below 50% of the start).
 """
 import numpy as np
 import pytest
 
 from oracle import net as onet
-from step_util import (assert_conditioned, ce_loss, conditioned_errors, max_rel, module_step, oracle_state,
-                       oracle_step)
+from step_util import ce_loss, fro_rel, max_rel, module_step, oracle_state, oracle_step, replayed_parity
 
 pytestmark = pytest.mark.gpu
 
@@ -33,15 +36,23 @@ def _check(res, ref, tol_p=1e-4, tol_g=2e-3, tol_w=1e-5, tol_a=1e-4, step=0):
     assert worst[0] < tol_a, worst
 
 
+def _assert_replayed(errs):
+    bad = {n: v for n, v in errs.items() if v[0] > v[2]}
+    assert not bad, sorted(bad.items(), key=lambda kv: -kv[1][0])[:5]
+
+
 def test_resnet20_cifar_fp32_two_steps(gpu):
     from rn import graphs
     g = onet.resnet20_cifar()
     args, aux = oracle_state(g)
     data, label = onet.synthetic_batch(8, (3, 32, 32), 10)
-    ref = oracle_step(g, args, aux, data, label, steps=2)
     res = module_step(graphs.resnet20_cifar(), args, aux, data, label, "float32", steps=2)
-    _check(res, ref, step=0)
-    assert max_rel(res["prob"][1], ref["prob"][1]) < 1e-4
+    assert len(res["relu_masks"][0]) == 19
+    errs, ref = replayed_parity(res, g, args, aux, data, label)
+    _assert_replayed(errs)
+    assert max_rel(res["prob"][0], ref["prob"][0]) < 1e-4
+    ref2 = oracle_step(g, args, aux, data, label, steps=2)
+    assert max_rel(res["prob"][1], ref2["prob"][1]) < 1e-4
 
 
 def test_resnet50_fp32_small(gpu):
@@ -49,12 +60,19 @@ def test_resnet50_fp32_small(gpu):
     g = onet.resnet50_imagenet(num_classes=16)
     args, aux = oracle_state(g)
     data, label = onet.synthetic_batch(4, (3, 64, 64), 16)
-    ref = oracle_step(g, args, aux, data, label)
-    ref32 = oracle_step(g, args, aux, data, label, dtype=np.float32)
     res = module_step(graphs.resnet([3, 4, 6, 3], 4, [64, 256, 512, 1024, 2048], 16), args, aux, data, label,
                       "float32")
+    assert len(res["relu_masks"][0]) == 50
+    errs, ref = replayed_parity(res, g, args, aux, data, label)
     assert max_rel(res["prob"][0], ref["prob"][0]) < 1e-4
-    assert_conditioned(conditioned_errors(res, ref, ref32))
+    assert abs(ce_loss(res["prob"][0], label) - ce_loss(ref["prob"][0], label)) < 1e-5 * ce_loss(ref["prob"][0], label)
+    _assert_replayed(errs)
+    assert sum(1 for v in errs.values() if v[0] <= 1e-4) >= 150  # all but a few cancellation-dominated tensors
+    # updated params inherit the gradient bar (beta_1 = -lr*g/B for zero-initialised betas)
+    worst = max((fro_rel(res["args"][n], ref["args"][n]), n) for n in ref["args"])
+    assert worst[0] < 1e-4, worst
+    worst = max((max_rel(res["aux"][n], ref["aux"][n]), n) for n in ref["aux"])
+    assert worst[0] < 1e-5, worst
 
 
 def _loss_traj(g, symf, n, hw, ncls, steps, lr):
@@ -65,17 +83,20 @@ def _loss_traj(g, symf, n, hw, ncls, steps, lr):
     return [ce_loss(p, label) for p in res["prob"]], [ce_loss(p, label) for p in ref["prob"]]
 
 
+def _check_traj(gpu_l, ref_l, final_frac):
+    assert abs(gpu_l[0] - ref_l[0]) < 0.02 * ref_l[0], (gpu_l, ref_l)
+    assert all(b < a for a, b in zip(gpu_l, gpu_l[1:])), gpu_l
+    assert gpu_l[-1] < final_frac * gpu_l[0], gpu_l
+
+
 def test_resnet20_bf16_loss_trajectory(gpu):
     from rn import graphs
     gpu_l, ref_l = _loss_traj(onet.resnet20_cifar(), graphs.resnet20_cifar, 8, 32, 10, 4, 0.1)
-    for a, b in zip(gpu_l, ref_l):
-        assert abs(a - b) < 0.02 * b, (gpu_l, ref_l)
+    _check_traj(gpu_l, ref_l, 0.8)
 
 
 def test_resnet50_bf16_loss_trajectory(gpu):
     from rn import graphs
     gpu_l, ref_l = _loss_traj(onet.resnet50_imagenet(16),
                               lambda: graphs.resnet([3, 4, 6, 3], 4, [64, 256, 512, 1024, 2048], 16), 4, 64, 16, 4, 0.05)
-    for a, b in zip(gpu_l, ref_l):
-        assert abs(a - b) < 0.10 * b, (gpu_l, ref_l)
-    assert gpu_l[-1] < gpu_l[0], gpu_l
+    _check_traj(gpu_l, ref_l, 0.5)
