@@ -37,6 +37,35 @@ def conv_call_flops(name, args):
     return 2 * macs_fwd
 
 
+def conv_call_bytes(ex, name, args):
+    """Algorithmic HBM bytes of one conv call: every operand read once, every output written once."""
+    d = args[0]._obj
+    es = 2 if ex.dtype == 0 else 4
+    x = d.n * d.h * d.w * d.c * es
+    y = d.n * d.p * d.q * d.k_pad * es
+    w = d.k * d.r * d.s * d.c_real * es
+    if name == "rn_conv_fwd":
+        yb = d.n * d.p * d.q * d.k_pad * (4 if args[4] == 1 else es)
+        return x + w + yb + (y if args[5] is not None else 0)
+    if name == "rn_conv_bwd_data":
+        return y + w + x + (x if args[4] is not None else 0)
+    return x + y + 2 * d.k * d.r * d.s * d.c_real * 4  # wgrad: fp32 dW read-modify-write
+
+
+def pmc_traffic(family):
+    """HBM bytes per launch of `family` from the committed rocprofv3 PMC summary (tools/pmc_bench.sh +
+    tools/pmc_summary.py: FETCH_SIZE doubled per the gfx950 correction, plus WRITE_SIZE)."""
+    path = os.environ.get("RN_PMC_JSON", os.path.join(REPO, "profiles", "r01", "pmc_hbm_bytes_per_launch.json"))
+    try:
+        with open(path) as f:
+            rec = json.load(f).get(family)
+    except OSError:
+        return None, None
+    if not rec:
+        return None, None
+    return rec["hbm_bytes"], os.path.relpath(path, REPO)
+
+
 def family_of(ex, name, args):
     if name == "rn_conv_bwd_filter":
         return "wgrad_kernel<bf16,128,128>" if ex.dtype == 0 else "wgrad_kernel<f32,128,128>"
@@ -56,12 +85,14 @@ class FamilyTimer:
         self.torch, self.ex, self.family = torch, ex, family
         self.idx = []
         self.flops = 0
+        self.bytes = 0
         for lst_name in ("_fwd_train", "_bwd"):
             lst = getattr(ex, lst_name)
             for i, (name, fn, args) in enumerate(lst):
                 if family_of(ex, name, args) == family:
                     self.idx.append((lst_name, i))
                     self.flops += conv_call_flops(name, args)
+                    self.bytes += conv_call_bytes(ex, name, args)
         self.events = []
 
     def wrap(self):
@@ -221,6 +252,8 @@ def main():
         per_launch_flops = timer.flops / max(1, len(timer.idx))
         avg_ms = fam_ms / max(fam_n, 1)
         achieved = per_launch_flops / (avg_ms * 1e-3) / 1e12
+        traffic, traffic_src = pmc_traffic(dom)
+        alg_bytes = timer.bytes / max(1, len(timer.idx))
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "images/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
@@ -231,7 +264,10 @@ def main():
                 "seq_len": None, "parallelism": "dp%d" % world, "per_gpu_images_per_sec": round(value / world, 2)},
             "roofline": {"bound": "mfma", "kernel": dom, "launches_per_step": len(timer.idx),
                          "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+                         "traffic": round(traffic) if traffic else None, "traffic_unit": "HBM bytes/launch",
+                         "traffic_source": traffic_src, "algorithmic_bytes": round(alg_bytes),
+                         "flops_per_launch": round(per_launch_flops),
                          "avg_launch_ms": round(avg_ms, 4),
                          "step_tflops": round(flops_step / (ms_step * 1e-3) / 1e12, 2),
                          "step_frac": round(flops_step / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
