@@ -65,7 +65,7 @@ int rn_conv_fwd(const rn_conv_desc* d, const void* x, const void* w_krsc, void* 
 int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
                      const void* add_src, rn_stream_t stream);
 
-/* dw_krsc (fp32, KRSC with channel stride c_real... see rn_conv_weight_numel) += x^T * dy.
+/* dw_krsc (fp32, KRSC with channel stride c_real/groups, see rn_conv_weight_numel) += x^T * dy.
  * Accumulates with fp32 atomics: the caller zeroes dw once per step. */
 int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, float* dw,
                        rn_stream_t stream);
@@ -73,8 +73,16 @@ int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, flo
 /* Number of fp32 elements of the master weight (K x R x S x c_real/groups, KRSC). */
 int64_t rn_conv_weight_numel(const rn_conv_desc* d);
 
+#define RN_GROUP_BLOCK 64
+/* Elements of the compute copy written by rn_conv_weight_pack: which = 0 (w_krsc) or 1 (w_crsk). */
+int64_t rn_conv_pack_numel(const rn_conv_desc* d, int32_t which);
+
 /* From the fp32 KRSC master weight, write the compute copies: w_krsc (dtype, channel stride
- * c) and w_crsk (dtype, c rows, K stride k_pad). Either output may be NULL. */
+ * c) and w_crsk (dtype, c rows, K stride k_pad). Either output may be NULL.
+ * Grouped (groups > 1, symbol/resnext.py:23-25 num_group=32): the copies are block-diagonal
+ * over RN_GROUP_BLOCK-wide column blocks -- for output column j the reduction runs over the
+ * channels of the groups that j's 64-column block touches, zero outside j's own group
+ * (w_krsc: [k][r][s][cblk], w_crsk: [c][r][s][kblk]); sizes from rn_conv_pack_numel. */
 int rn_conv_weight_pack(const rn_conv_desc* d, const float* w_master, void* w_krsc, void* w_crsk,
                         rn_stream_t stream);
 
@@ -83,6 +91,21 @@ int rn_conv_weight_pack(const rn_conv_desc* d, const float* w_master, void* w_kr
  * kc = round_up(r*s*c_real, 32). conv0 then runs as a 1x1 conv over cols. */
 int rn_im2col_nchw(const rn_conv_desc* d, const float* x_nchw, const float* scale,
                    const float* shift, void* cols, int32_t kc, rn_stream_t stream);
+
+/* Quantized stem (symbol/resnet_int8.py:96-98, int8_api.py:133-136): conv0 reads
+ * Quantization_int8(bn_data(x)). Updates the activation minmax state (EMA of max|affine(x)|,
+ * when is_train) and writes the im2col matrix of the fake-quantized affine input.
+ * ws: >= 2 floats. */
+int rn_im2col_nchw_quant(const rn_conv_desc* d, const float* x_nchw, const float* scale,
+                         const float* shift, float* minmax, int32_t is_train, float ema_decay,
+                         int32_t first_batch, int32_t nbits, float* ws, void* cols, int32_t kc,
+                         rn_stream_t stream);
+/* The activation STE zeroes the gradient of clipped inputs (|affine(x)| >= minmax):
+ * dbeta[c] -= sum over clipped (n,c,h,w) of (conv0 data-gradient), with w_q the fp32 KRSC
+ * quantized weight conv0 ran with. Run after rn_stem_shift_grad. */
+int rn_stem_quant_clip_grad(const rn_conv_desc* d, const float* x_nchw, const float* scale,
+                            const float* shift, const float* minmax, const void* dy, const float* w_q,
+                            float* dbeta, rn_stream_t stream);
 
 /* d(beta) of a BN feeding the stem conv, without the stem dgrad:
  * dbeta[c] += sum_{k,r,s} w[k,r,s,c] * sum_{n,p,q valid(r,s)} dy[n,p,q,k].

@@ -235,13 +235,15 @@ def init_params(graph, seed=2, dtype=np.float64):
 
 
 def forward(graph, args, aux, data, label, is_train=True, quant_state=None, first_batch=True, storage=None,
-            relu_masks=None):
+            relu_masks=None, quant_values=None):
     """Returns (prob, tape). Updates aux (moving stats) in place when is_train.
 
     storage='bf16' emulates a bf16-storage runtime: conv/FC weights and every stored activation
     are rounded to bf16 (logits stay fp32), arithmetic stays in the array dtype.
     relu_masks {relu op name: bool array} replays given ReLU decisions (y = x * mask) instead of
-    x > 0 -- parity diagnostics use it to remove rounding-induced decision flips."""
+    x > 0 -- parity diagnostics use it to remove rounding-induced decision flips.
+    quant_values {'<conv>_data' / '<conv>_weight': array} likewise replays given int8 rounding
+    decisions (the fake-quantized tensors) while the quantizer state still updates."""
     rnd = ops.bf16_round if storage == "bf16" else (lambda a: a)
     env = {"data": data}
     tape = []
@@ -257,6 +259,9 @@ def forward(graph, args, aux, data, label, is_train=True, quant_state=None, firs
                 xq, mm = ops.quant_int8_act(x, qs.get(key, 0.0), is_train, first_batch or key not in qs)
                 qs[key] = mm
                 wq, _ = ops.quant_int8_weight(w)
+                if quant_values is not None:
+                    xq = quant_values.get(op["name"] + "_data", xq).reshape(xq.shape).astype(xq.dtype)
+                    wq = quant_values.get(op["name"] + "_weight", wq).reshape(wq.shape).astype(wq.dtype)
                 rec.update(xraw=x, t=mm)
                 x, w = xq, wq
             w = rnd(w)
@@ -368,7 +373,7 @@ def backward(graph, args, fwd_state, grad_scale=1.0, keep=None):
 
 
 def train_step(graph, args, aux, moms, data, label, lr, momentum=0.9, wd=1e-4, rescale_grad=None,
-               num_devices=1, quant_state=None, first_batch=True, storage=None, relu_masks=None):
+               num_devices=1, quant_state=None, first_batch=True, storage=None, relu_masks=None, quant_values=None):
     """One Solver iteration (core/solver.py:115-121): forward(is_train) + backward + SGD update.
 
     num_devices > 1 restates Module's even batch split: per-slice BN statistics, per-slice
@@ -383,7 +388,7 @@ def train_step(graph, args, aux, moms, data, label, lr, momentum=0.9, wd=1e-4, r
     for d in range(num_devices):
         aux_d = {k: v.copy() for k, v in aux.items()}
         prob, st = forward(graph, args, aux_d, data[d * sl:(d + 1) * sl], label[d * sl:(d + 1) * sl], True,
-                           quant_state, first_batch, storage, relu_masks)
+                           quant_state, first_batch, storage, relu_masks, quant_values)
         grads = backward(graph, args, st)
         for k, v in grads.items():
             gsum[k] = gsum[k] + v if k in gsum else v

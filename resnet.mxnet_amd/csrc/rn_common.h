@@ -97,3 +97,23 @@ __device__ __forceinline__ float wave_max(float v) {
 
 static inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 static inline hipStream_t as_stream(rn_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ------------------------------------------------------------------ int8 fake quantization
+// Shared by rn_misc.hip (Quantization_int8 on a tensor) and rn_conv.hip (the quantized stem).
+// State: weights t = max|w|; activations t = EMA of max|x| (initialised from the first batch),
+// symbol/clip_grad_quantization_int8.py:37-54 and quant_ops.py:17-31.
+__device__ __forceinline__ float quant_state_update(float curmax, float* minmax, int is_weight, int is_train,
+                                                   float decay, int first) {
+  if (is_weight) {
+    if (is_train && minmax) *minmax = curmax;
+    return curmax;
+  }
+  if (is_train) *minmax = first ? curmax : (*minmax) * decay + curmax * (1.f - decay);
+  return *minmax;
+}
+// round(clip(v, -t, t) / unit) * unit, unit = t / qmax; mx.nd.round is half away from zero (= roundf)
+__device__ __forceinline__ float quant_value(float v, float t, float qmax, int clip) {
+  const float unit = t / qmax;
+  if (clip) v = fminf(fmaxf(v, -t), t);
+  return unit > 0.f ? roundf(v / unit) * unit : 0.f;
+}

@@ -47,6 +47,8 @@ struct IgemmArgs {
   int hmul, wmul;      // row coordinate multiplier (stride fwd, 1 dgrad)
   int hinc, winc;      // gathered coordinate change per tap step (+1 fwd, -1 dgrad)
   int ostep_h, ostep_w;
+  int gcol, gred;      // grouped: output columns / reduction channels per group (dense: 2^30, 0)
+  int cblk;            // reduction channels per column block (dense: C)
   int ncls;
   IgemmCls cls[4];
 };
@@ -98,6 +100,8 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
   const int m0 = blockIdx.x * BM;
   if (m0 >= Mc) return;
   const int n0 = blockIdx.y * BN;
+  // grouped conv: the block's columns touch groups n0/gcol.., whose input channels start here
+  const int cbase = (n0 / p.gcol) * p.gred;
 
   const T* __restrict__ xg = reinterpret_cast<const T*>(p.x);
   const T* __restrict__ wg = reinterpret_cast<const T*>(p.w);
@@ -132,7 +136,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
     b_off[i] = (b_ok[i] ? col : 0) * p.wrow;
   }
 
-  const int ncb = (p.C + BKE - 1) / BKE;
+  const int ncb = (p.cblk + BKE - 1) / BKE;
   const int nstage = cl.nr * cl.ns * ncb;
 
   // register-staged loads: stage t+1 is loaded while stage t is computed, then written to
@@ -154,20 +158,20 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
     const int hoff = cl.hoff0 + p.hinc * tr;
     const int woff = cl.woff0 + p.winc * ts;
     const int c = cb * BKE + ch * CE;
-    const bool cok = c < p.C;
+    const bool cok = c < p.cblk && cbase + c < p.C;  // a grouped block may run past the last group
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int hin = a_hb[i] + hoff;
       const int win = a_wb[i] + woff;
       const bool ok = cok && (unsigned)hin < (unsigned)p.H && (unsigned)win < (unsigned)p.W;
       if (ok) {
-        const int off = (a_pix[i] + hin * p.W + win) * p.C + c;  // < 2^31 (host-checked)
+        const int off = (a_pix[i] + hin * p.W + win) * p.C + cbase + c;  // < 2^31 (host-checked)
         ra[i] = *reinterpret_cast<const uint4*>(xg + off);
       } else {
         ra[i] = make_uint4(0, 0, 0, 0);
       }
     }
-    const int toff = (r * p.S + s) * p.C + c;
+    const int toff = (r * p.S + s) * p.cblk + c;
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       if (cok && b_ok[i]) rb[i] = *reinterpret_cast<const uint4*>(wg + b_off[i] + toff);
@@ -329,7 +333,8 @@ struct WgradArgs {
   int ldw;
   int M;
   int m_per_split;
-  FastDiv fdQ, fdPQ, fdC, fdS;
+  int grouped, gk, gc, cblk;  // grouped: rows / channels per group, channels per row block
+  FastDiv fdQ, fdPQ, fdC, fdS;  // fdC divides by cblk (dense: C)
 };
 
 // 16-byte chunk swizzle of an LDS image whose rows are read 4-at-a-time by
@@ -359,6 +364,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   const int mbeg = blockIdx.z * p.m_per_split;
   const int mend = min(p.M, mbeg + p.m_per_split);
   if (mbeg >= mend) return;
+  const int cbase = p.grouped ? (k0 / p.gk) * p.gc : 0;
 
   const T* __restrict__ xg = reinterpret_cast<const T*>(p.x);
   const T* __restrict__ dyg = reinterpret_cast<const T*>(p.dy);
@@ -370,13 +376,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   // B assignment: fixed column chunk -> (tap r,s ; channel c)
   const int b_c = tid % B_CPR;
   const int bcol = n0 + b_c * CE;
-  const bool b_cok = bcol < p.ncol_load;
+  bool b_cok = bcol < p.ncol_load;
   int b_r = 0, b_s = 0, b_ch = 0;
   if (b_cok) {
     const int tap = fdiv(bcol, p.fdC);
-    b_ch = bcol - tap * p.C;
+    b_ch = cbase + bcol - tap * p.cblk;
     b_r = fdiv(tap, p.fdS);
     b_s = tap - b_r * p.S;
+    b_cok = b_ch < p.C;  // a grouped block may run past the last group
   }
   const int b_hoff = b_r - p.ph, b_woff = b_s - p.pw;
 
@@ -521,7 +528,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int col = n0 + wn * (BNC / 2) + j * 16 + (lane & 15);
-        if (col < p.ncol) atomicAdd(p.dw + (int64_t)k * p.ldw + col, acc[i][j][e]);
+        if (!p.grouped) {
+          if (col < p.ncol) atomicAdd(p.dw + (int64_t)k * p.ldw + col, acc[i][j][e]);
+        } else if (col < p.ncol_load) {  // keep the block-diagonal part: channel in k's group
+          const int tap = fdiv(col, p.fdC);
+          const int c = cbase + col - tap * p.cblk;
+          const int g = k / p.gk;
+          if (c / p.gc == g) atomicAdd(p.dw + (int64_t)k * p.ldw + tap * p.gc + (c - g * p.gc), acc[i][j][e]);
+        }
       }
     }
   }
@@ -557,13 +571,44 @@ __global__ void pack_crsk_kernel(const float* __restrict__ wm, T* __restrict__ o
   }
 }
 
+// Grouped compute copy, block-diagonal over RN_GROUP_BLOCK-column blocks (see rn.h):
+// out[col][tap][j], j < cblk: reduction index red = base(col's block) + j; nonzero only when
+// red belongs to col's group. fwd (transpose 0): col = k, red = c. dgrad (1): col = c, red = k.
+template <typename T>
+__global__ void pack_group_kernel(const float* __restrict__ wm, T* __restrict__ out, int ncols, int RS,
+                                  int cblk, int gcol, int gred, int cpg, int transpose) {
+  const int64_t total = (int64_t)ncols * RS * cblk;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int j = (int)(i % cblk);
+    const int64_t t = i / cblk;
+    const int tap = (int)(t % RS);
+    const int col = (int)(t / RS);
+    const int n0 = col / RN_GROUP_BLOCK * RN_GROUP_BLOCK;
+    const int red = (n0 / gcol) * gred + j;
+    const int g = col / gcol;
+    float v = 0.f;
+    if (red / gred == g) {
+      v = transpose ? wm[((int64_t)red * RS + tap) * cpg + (col - g * gcol)]
+                    : wm[((int64_t)col * RS + tap) * cpg + (red - g * gred)];
+    }
+    out[i] = from_f<T>(v);
+  }
+}
+
+// columns of one RN_GROUP_BLOCK block -> reduction channels it spans
+inline int group_blk(int gcol, int gred) {
+  return (gcol >= RN_GROUP_BLOCK ? 1 : RN_GROUP_BLOCK / gcol) * gred;
+}
+
 // thread per (row m, 16-byte output chunk): 8 (bf16) / 4 (f32) consecutive im2col columns
 template <typename T>
 __global__ __launch_bounds__(256) void im2col_nchw_kernel(const float* __restrict__ x, const float* __restrict__ scale,
                                                           const float* __restrict__ shift, T* __restrict__ cols, int N,
                                                           int C, int H, int W, int P, int Q, int R, int S, int sh,
                                                           int sw, int ph, int pw, int kc, FastDiv fdQ, FastDiv fdP,
-                                                          FastDiv fdCH) {
+                                                          FastDiv fdCH, const float* __restrict__ qthr, float qmax) {
+  const float qt = qthr ? *qthr : 0.f;
   constexpr int CE = 16 / sizeof(T);
   const int cpr = kc / CE;
   const int64_t total = (int64_t)N * P * Q * cpr;
@@ -589,11 +634,71 @@ __global__ __launch_bounds__(256) void im2col_nchw_kernel(const float* __restric
         if ((unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W) {
           val = x[(((int64_t)n * C + c) * H + h) * W + w];
           if (scale) val = fmaf(val, scale[c], shift[c]);
+          if (qthr) val = quant_value(val, qt, qmax, 1);  // conv0_data Quantization_int8
         }
       }
       v[e] = val;
     }
     reinterpret_cast<uint4*>(cols)[i] = f_to_chunk(v, (const T*)nullptr);
+  }
+}
+
+// ---- quantized stem (symbol/resnet_int8.py:96-98: conv0 reads Quantization_int8(bn_data(x)))
+// max |x*scale[c] + shift[c]| over the NCHW input
+__global__ void stem_affine_absmax_kernel(const float* __restrict__ x, const float* __restrict__ scale,
+                                          const float* __restrict__ shift, int64_t total, int C, int HW,
+                                          float* __restrict__ out) {
+  float m = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    float v = x[i];
+    if (scale) {
+      const int c = (int)((i / HW) % C);
+      v = fmaf(v, scale[c], shift[c]);
+    }
+    m = fmaxf(m, fabsf(v));
+  }
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(out), __float_as_uint(m));
+}
+__global__ void stem_quant_state_kernel(const float* __restrict__ curmax, float* minmax, int is_train, float decay,
+                                        int first, float* __restrict__ thr) {
+  *thr = quant_state_update(*curmax, minmax, 0, is_train, decay, first);
+}
+// The activation STE zeroes the gradient where |v| >= t (clip_grad_quantization_int8.py:56-67).
+// rn_stem_shift_grad sums the unmasked gradient; subtract the clipped elements' share:
+// dbeta[c] -= dx[n,c,h,w] at every clipped (n,c,h,w), dx = sum_{k,r,s} w[k,r,s,c] dy[n,p,q,k].
+template <typename T>
+__global__ void stem_clip_grad_kernel(const float* __restrict__ x, const float* __restrict__ scale,
+                                      const float* __restrict__ shift, const float* __restrict__ thr,
+                                      const T* __restrict__ dy, const float* __restrict__ wq,
+                                      float* __restrict__ dbeta, int N, int C, int H, int W, int P, int Q, int K,
+                                      int kpad, int R, int S, int sh, int sw, int ph, int pw) {
+  const float t = *thr;
+  const int64_t total = (int64_t)N * C * H * W;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int w = (int)(i % W);
+    const int h = (int)((i / W) % H);
+    const int c = (int)((i / ((int64_t)H * W)) % C);
+    const int n = (int)(i / ((int64_t)C * H * W));
+    float v = x[i];
+    if (scale) v = fmaf(v, scale[c], shift[c]);
+    if (v > -t && v < t) continue;
+    float g = 0.f;
+    for (int r = 0; r < R; ++r) {
+      const int hp = h + ph - r;
+      if (hp < 0 || hp % sh) continue;
+      const int pp = hp / sh;
+      if (pp >= P) continue;
+      for (int s = 0; s < S; ++s) {
+        const int wp = w + pw - s;
+        if (wp < 0 || wp % sw) continue;
+        const int qq = wp / sw;
+        if (qq >= Q) continue;
+        const T* dyp = dy + (((int64_t)n * P + pp) * Q + qq) * kpad;
+        for (int k = 0; k < K; ++k) g += wq[((int64_t)(k * R + r) * S + s) * C + c] * to_f(dyp[k]);
+      }
+    }
+    atomicAdd(dbeta + c, -g);
   }
 }
 
@@ -675,6 +780,12 @@ IgemmArgs make_igemm_args(const rn_conv_desc* d, int mode) {
     a.hmul = d->stride_h; a.wmul = d->stride_w;
     a.hinc = 1; a.winc = 1;
     a.ostep_h = 1; a.ostep_w = 1;
+    a.gcol = 1 << 30; a.gred = 0; a.cblk = a.C;
+    if (d->groups > 1) {
+      a.gcol = d->k / d->groups; a.gred = d->c / d->groups;
+      a.cblk = group_blk(a.gcol, a.gred);
+      a.wrow = d->r * d->s * a.cblk;
+    }
     a.ncls = 1;
     IgemmCls& c = a.cls[0];
     c.a = 0; c.b = 0; c.Pc = d->p; c.Qc = d->q; c.r0 = 0; c.s0 = 0; c.nr = d->r; c.ns = d->s;
@@ -688,6 +799,12 @@ IgemmArgs make_igemm_args(const rn_conv_desc* d, int mode) {
     a.hmul = 1; a.wmul = 1;
     a.hinc = -1; a.winc = -1;
     a.ostep_h = d->stride_h; a.ostep_w = d->stride_w;
+    a.gcol = 1 << 30; a.gred = 0; a.cblk = a.C;
+    if (d->groups > 1) {
+      a.gcol = d->c / d->groups; a.gred = d->k / d->groups;
+      a.cblk = group_blk(a.gcol, a.gred);
+      a.wrow = d->r * d->s * a.cblk;
+    }
     a.ncls = d->stride_h * d->stride_w;
     for (int z = 0; z < a.ncls; ++z) {
       IgemmCls& c = a.cls[z];
@@ -717,7 +834,7 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   int maxMc = 0;
   for (int z = 0; z < a.ncls; ++z) maxMc = std::max(maxMc, a.N * a.cls[z].Pc * a.cls[z].Qc);
   if (maxMc == 0) return 0;
-  if (a.K <= 64) {
+  if (a.K <= 64 || a.gred > 0) {  // grouped: the block width is RN_GROUP_BLOCK
     dim3 grid((unsigned)ceil_div(maxMc, 128), (unsigned)ceil_div(a.K, 64), a.ncls);
     hipLaunchKernelGGL((igemm_kernel<T, OutT, 128, 64>), grid, dim3(256), 0, st, a);
   } else {
@@ -738,9 +855,18 @@ int rn_conv_desc_init(rn_conv_desc* d) {
   RN_CHECK_ARG(d->r > 0 && d->s > 0 && d->stride_h > 0 && d->stride_w > 0, "bad kernel/stride");
   RN_CHECK_ARG(d->pad_h >= 0 && d->pad_w >= 0, "bad pad");
   if (d->groups <= 0) d->groups = 1;
-  RN_CHECK_ARG(d->groups == 1, "grouped convolution is not supported by this build");
   if (d->c_real <= 0) d->c_real = d->c;
   if (d->k_pad <= 0) d->k_pad = (d->k + 7) / 8 * 8;
+  if (d->groups > 1) {
+    const int g = d->groups;
+    RN_CHECK_ARG(d->c == d->c_real && d->k == d->k_pad, "grouped conv needs unpadded channels");
+    RN_CHECK_ARG(d->c % g == 0 && d->k % g == 0, "channels not divisible by num_group");
+    const int cpg = d->c / g, kpg = d->k / g;
+    auto fits = [](int v) { return RN_GROUP_BLOCK % v == 0 || v % RN_GROUP_BLOCK == 0; };
+    RN_CHECK_ARG(fits(cpg) && fits(kpg), "channels per group must divide or be a multiple of 64");
+    RN_CHECK_ARG(group_blk(kpg, cpg) % 8 == 0 && group_blk(cpg, kpg) % 8 == 0,
+                 "grouped block reduction must be a multiple of 8 channels");
+  }
   RN_CHECK_ARG(d->c % 8 == 0, "channel stride must be a multiple of 8");
   RN_CHECK_ARG(d->k_pad % 8 == 0 && d->k_pad >= d->k, "k_pad must be a multiple of 8 >= k");
   RN_CHECK_ARG(d->c_real <= d->c, "c_real > c");
@@ -755,6 +881,15 @@ int rn_conv_desc_init(rn_conv_desc* d) {
 
 int64_t rn_conv_weight_numel(const rn_conv_desc* d) {
   return (int64_t)d->k * d->r * d->s * (d->c_real / (d->groups > 0 ? d->groups : 1));
+}
+
+int64_t rn_conv_pack_numel(const rn_conv_desc* d, int32_t which) {
+  const int64_t RS = (int64_t)d->r * d->s;
+  if (d->groups > 1) {
+    const int cpg = d->c / d->groups, kpg = d->k / d->groups;
+    return which == 0 ? d->k * RS * group_blk(kpg, cpg) : d->c * RS * group_blk(cpg, kpg);
+  }
+  return which == 0 ? d->k * RS * d->c : d->c * RS * d->k_pad;
 }
 
 int rn_conv_fwd(const rn_conv_desc* d, const void* x, const void* w, void* y, int32_t y_dtype,
@@ -794,10 +929,20 @@ int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, flo
   a.ncol_load = d->r * d->s * d->c;
   a.ncol = d->r * d->s * d->c_real;
   a.ldw = a.ncol;
+  a.cblk = d->c;
+  const bool grouped = d->groups > 1;
+  if (grouped) {
+    a.grouped = 1;
+    a.gk = d->k / d->groups; a.gc = d->c / d->groups;
+    a.cblk = group_blk(a.gk, a.gc);
+    a.ncol_load = d->r * d->s * a.cblk;
+    a.ncol = d->r * d->s * a.gc;
+    a.ldw = a.ncol;
+  }
   a.M = d->n * d->p * d->q;
   a.fdQ = make_fastdiv(d->q); a.fdPQ = make_fastdiv(d->p * d->q);
-  a.fdC = make_fastdiv(d->c); a.fdS = make_fastdiv(d->s);
-  const int bmk = 128, bnc = 128;
+  a.fdC = make_fastdiv(a.cblk); a.fdS = make_fastdiv(d->s);
+  const int bmk = grouped ? RN_GROUP_BLOCK : 128, bnc = grouped ? RN_GROUP_BLOCK : 128;
   const int tiles = (int)(ceil_div(a.ncol_load, bnc) * ceil_div(a.K, bmk));
   const int bkm = d->dtype == RN_BF16 ? 64 : 32;
   const int64_t mstages = ceil_div(a.M, bkm);
@@ -810,10 +955,16 @@ int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, flo
   split = ceil_div(a.M, a.m_per_split);
   dim3 grid((unsigned)ceil_div(a.ncol_load, bnc), (unsigned)ceil_div(a.K, bmk), (unsigned)split);
   hipStream_t st = as_stream(stream);
-  if (d->dtype == RN_BF16)
+  if (grouped) {
+    if (d->dtype == RN_BF16)
+      hipLaunchKernelGGL((wgrad_kernel<bf16_t, RN_GROUP_BLOCK, RN_GROUP_BLOCK>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((wgrad_kernel<float, RN_GROUP_BLOCK, RN_GROUP_BLOCK>), grid, dim3(256), 0, st, a);
+  } else if (d->dtype == RN_BF16) {
     hipLaunchKernelGGL((wgrad_kernel<bf16_t, 128, 128>), grid, dim3(256), 0, st, a);
-  else
+  } else {
     hipLaunchKernelGGL((wgrad_kernel<float, 128, 128>), grid, dim3(256), 0, st, a);
+  }
   return rn_check_launch("wgrad");
 }
 
@@ -822,6 +973,24 @@ int rn_conv_weight_pack(const rn_conv_desc* d, const float* wm, void* w_krsc, vo
   RN_CHECK_ARG(d && wm, "null argument");
   hipStream_t st = as_stream(stream);
   const int RS = d->r * d->s;
+  if (d->groups > 1) {
+    const int cpg = d->c / d->groups, kpg = d->k / d->groups;
+    for (int which = 0; which < 2; ++which) {
+      void* out = which == 0 ? w_krsc : w_crsk;
+      if (!out) continue;
+      const int ncols = which == 0 ? d->k : d->c;
+      const int gcol = which == 0 ? kpg : cpg, gred = which == 0 ? cpg : kpg;
+      const int cblk = group_blk(gcol, gred);
+      const int64_t total = (int64_t)ncols * RS * cblk;
+      if (d->dtype == RN_BF16)
+        hipLaunchKernelGGL(pack_group_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st, wm, (bf16_t*)out,
+                           ncols, RS, cblk, gcol, gred, cpg, which);
+      else
+        hipLaunchKernelGGL(pack_group_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, wm, (float*)out,
+                           ncols, RS, cblk, gcol, gred, cpg, which);
+    }
+    return rn_check_launch("weight_pack");
+  }
   if (w_krsc) {
     const int64_t total = (int64_t)d->k * RS * d->c;
     if (d->dtype == RN_BF16)
@@ -843,8 +1012,11 @@ int rn_conv_weight_pack(const rn_conv_desc* d, const float* wm, void* w_krsc, vo
   return rn_check_launch("weight_pack");
 }
 
-int rn_im2col_nchw(const rn_conv_desc* d, const float* x, const float* scale, const float* shift,
-                   void* cols, int32_t kc, rn_stream_t stream) {
+}  // extern "C"
+
+namespace {
+int im2col_launch(const rn_conv_desc* d, const float* x, const float* scale, const float* shift, const float* qthr,
+                  float qmax, void* cols, int32_t kc, rn_stream_t stream) {
   RN_CHECK_ARG(d && x && cols, "null argument");
   RN_CHECK_ARG(kc >= d->r * d->s * d->c_real && kc % 8 == 0, "bad kc");
   RN_CHECK_ARG((scale == nullptr) == (shift == nullptr), "scale/shift must both be set");
@@ -854,14 +1026,59 @@ int rn_im2col_nchw(const rn_conv_desc* d, const float* x, const float* scale, co
     const int64_t total = (int64_t)d->n * d->p * d->q * (kc / 8);
     hipLaunchKernelGGL(im2col_nchw_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st, x,
                        scale, shift, (bf16_t*)cols, d->n, d->c_real, d->h, d->w, d->p, d->q, d->r,
-                       d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, kc, fq, fp, fc);
+                       d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, kc, fq, fp, fc, qthr, qmax);
   } else {
     const int64_t total = (int64_t)d->n * d->p * d->q * (kc / 4);
     hipLaunchKernelGGL(im2col_nchw_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, x,
                        scale, shift, (float*)cols, d->n, d->c_real, d->h, d->w, d->p, d->q, d->r,
-                       d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, kc, fq, fp, fc);
+                       d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, kc, fq, fp, fc, qthr, qmax);
   }
   return rn_check_launch("im2col");
+}
+}  // namespace
+
+extern "C" {
+
+int rn_im2col_nchw(const rn_conv_desc* d, const float* x, const float* scale, const float* shift,
+                   void* cols, int32_t kc, rn_stream_t stream) {
+  return im2col_launch(d, x, scale, shift, nullptr, 0.f, cols, kc, stream);
+}
+
+int rn_im2col_nchw_quant(const rn_conv_desc* d, const float* x, const float* scale, const float* shift,
+                         float* minmax, int32_t is_train, float ema_decay, int32_t first_batch, int32_t nbits,
+                         float* ws, void* cols, int32_t kc, rn_stream_t stream) {
+  RN_CHECK_ARG(d && x && minmax && ws, "null argument");
+  RN_CHECK_ARG(nbits >= 2 && nbits <= 16, "bad nbits");
+  hipStream_t st = as_stream(stream);
+  float* curmax = ws;
+  float* thr = ws + 1;
+  hipMemsetAsync(curmax, 0, sizeof(float), st);
+  if (is_train) {
+    const int64_t total = (int64_t)d->n * d->c_real * d->h * d->w;
+    hipLaunchKernelGGL(stem_affine_absmax_kernel, dim3(grid_for(total)), dim3(256), 0, st, x, scale, shift, total,
+                       d->c_real, d->h * d->w, curmax);
+  }
+  hipLaunchKernelGGL(stem_quant_state_kernel, dim3(1), dim3(1), 0, st, curmax, minmax, is_train, ema_decay,
+                     first_batch, thr);
+  if (rn_check_launch("im2col_quant_state")) return -1;
+  return im2col_launch(d, x, scale, shift, thr, (float)((1 << (nbits - 1)) - 1), cols, kc, stream);
+}
+
+int rn_stem_quant_clip_grad(const rn_conv_desc* d, const float* x, const float* scale, const float* shift,
+                            const float* minmax, const void* dy, const float* w_q, float* dbeta,
+                            rn_stream_t stream) {
+  RN_CHECK_ARG(d && x && minmax && dy && w_q && dbeta, "null argument");
+  hipStream_t st = as_stream(stream);
+  const int64_t total = (int64_t)d->n * d->c_real * d->h * d->w;
+  if (d->dtype == RN_BF16)
+    hipLaunchKernelGGL(stem_clip_grad_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st, x, scale, shift,
+                       minmax, (const bf16_t*)dy, w_q, dbeta, d->n, d->c_real, d->h, d->w, d->p, d->q, d->k, d->k_pad,
+                       d->r, d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w);
+  else
+    hipLaunchKernelGGL(stem_clip_grad_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, x, scale, shift,
+                       minmax, (const float*)dy, w_q, dbeta, d->n, d->c_real, d->h, d->w, d->p, d->q, d->k, d->k_pad,
+                       d->r, d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w);
+  return rn_check_launch("stem_quant_clip_grad");
 }
 
 int rn_stem_shift_grad(const rn_conv_desc* d, const void* dy, const float* wm, float* dbeta,

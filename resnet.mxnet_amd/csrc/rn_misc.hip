@@ -289,31 +289,14 @@ __global__ void absmax_kernel(int64_t n, const T* __restrict__ x, float* __restr
 }
 __global__ void quant_state_kernel(const float* __restrict__ curmax, float* minmax, int is_weight, int is_train,
                                    float decay, int first, float* __restrict__ thr) {
-  float t;
-  if (is_weight) {
-    t = *curmax;
-    if (is_train && minmax) *minmax = t;
-  } else {
-    if (is_train) {
-      const float nv = first ? *curmax : (*minmax) * decay + (*curmax) * (1.f - decay);
-      *minmax = nv;
-    }
-    t = *minmax;
-  }
-  *thr = t;
+  *thr = quant_state_update(*curmax, minmax, is_weight, is_train, decay, first);
 }
 template <typename T>
 __global__ void quant_apply_kernel(int64_t n, const T* __restrict__ x, T* __restrict__ out,
                                    const float* __restrict__ thr, float qmax, int clip) {
   const float t = *thr;
-  const float unit = t / qmax;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float v = to_f(x[i]);
-    if (clip) v = fminf(fmaxf(v, -t), t);
-    // mx.nd.round: half away from zero
-    const float qv = unit > 0.f ? roundf(v / unit) * unit : 0.f;
-    out[i] = from_f<T>(qv);
-  }
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = from_f<T>(quant_value(to_f(x[i]), t, qmax, clip));
 }
 template <typename T>
 __global__ void quant_bwd_kernel(int64_t n, const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx,

@@ -100,6 +100,7 @@ class Plan:
         self.tensors = {}
         self.alias = {}
         self.ops = []
+        self.qweight = {}  # id(weight Quantization_int8 node) -> quant info
         self._lower()
 
     # --- shapes of every node output
@@ -152,6 +153,28 @@ class Plan:
         while node.op in ("identity", "Cast", "Flatten"):
             node = node.inputs[0][0]
         return node
+
+    @staticmethod
+    def _is_quant(node):
+        return node is not None and node.op == "_contrib_Quantization_int8"
+
+    def _quant_info(self, n):
+        """Quantization_int8 attrs (int8_api.py:133-136; semantics clip_grad_quantization_int8.py)."""
+        if _parse(n.attrs.get("quant_mode", "minmax")) != "minmax":
+            raise PlanError("%s: quant_mode other than 'minmax' not supported" % n.name)
+        if int(_parse(n.attrs.get("delay_quant", 0))):
+            raise PlanError("%s: delay_quant > 0 not supported" % n.name)
+        if _parse(n.attrs.get("is_weight_perchannel", False)):
+            raise PlanError("%s: per-channel weight quantization not supported" % n.name)
+        return dict(name=n.name, minmax=n.inputs[1][0].name, ema=float(_parse(n.attrs.get("ema_decay", 0.99))),
+                    nbits=int(_parse(n.attrs.get("nbits", 8))),
+                    is_weight=bool(_parse(n.attrs.get("is_weight", False))))
+
+    def _stem_quant(self, node, cons):
+        """A data Quantization_int8 whose only consumer is the stem conv (folded into its im2col)."""
+        cl = cons.get(id(node), [])
+        return self._is_quant(node) and len(cl) == 1 and cl[0] is not None and cl[0].op == "Convolution" and \
+            self._is_stem(cl[0])
 
     # --- lowering
     def _lower(self):
@@ -214,7 +237,8 @@ class Plan:
                         _parse(cl[0].attrs.get("act_type")) == "relu":
                     relu_node = cl[0]
                 src = self._var_input(n.inputs[0][0])
-                stem_consumers = [c for c in cl if c is not None and c.op == "Convolution" and self._is_stem(c)]
+                stem_consumers = [c for c in cl if c is not None and
+                                  ((c.op == "Convolution" and self._is_stem(c)) or self._stem_quant(c, cons))]
                 if src.op == "null" and src.name in data_vars and stem_consumers and len(cl) == 1:
                     done.add(id(n))  # folded into the stem conv (bn_data)
                     continue
@@ -224,6 +248,21 @@ class Plan:
                 if relu_node is not None:
                     self.alias[id(relu_node)] = id(n)
                     done.add(id(relu_node))
+            elif op == "_contrib_Quantization_int8":
+                q = self._quant_info(n)
+                src = n.inputs[0][0]
+                if q["is_weight"]:
+                    if src.op != "null":
+                        raise PlanError("%s: weight quantization of a computed tensor" % n.name)
+                    q["param"] = src.name
+                    self.qweight[id(n)] = q
+                elif not self._stem_quant(n, cons):  # (the stem's is folded into its im2col)
+                    x = self.tensor(src)
+                    if x.kind != "act":
+                        raise PlanError("%s: data quantization of a non-activation tensor" % n.name)
+                    y = self._new_tensor(n, x.shape)
+                    self.ops.append(PlanOp("quant", n.name, x=x, y=y, q=q))
+                done.add(id(n))
             elif op == "Activation":
                 act = _parse(n.attrs.get("act_type"))
                 if act != "relu":
@@ -271,9 +310,15 @@ class Plan:
 
     def _param_node(self, node, idx):
         p = node.inputs[idx][0]
+        if self._is_quant(p) and id(p) in self.qweight:
+            return self.qweight[id(p)]["param"]
         if p.op != "null":
             raise PlanError("%s: computed weights are not supported" % node.name)
         return p.name
+
+    def _weight_quant(self, node, idx=1):
+        p = node.inputs[idx][0]
+        return self.qweight.get(id(p)) if self._is_quant(p) else None
 
     def _conv_attrs(self, n):
         k = _tup(n.attrs["kernel"])
@@ -287,8 +332,6 @@ class Plan:
 
     def _lower_conv(self, n, cons, fused):
         k, st, pd, g = self._conv_attrs(n)
-        if g != 1:
-            raise PlanError("%s: grouped convolution (num_group=%d) is not supported yet" % (n.name, g))
         xshape = self.shape_of(n.inputs[0][0])
         yshape = self.shape_of(n)
         wname = self._param_node(n, 1)
@@ -296,7 +339,13 @@ class Plan:
             raise PlanError("%s: convolution bias not supported" % n.name)
         y = self._new_tensor(n, yshape)
         if self._is_stem(n):
+            if g != 1:
+                raise PlanError("%s: grouped stem convolution not supported" % n.name)
             src = self._var_input(n.inputs[0][0])
+            squant = None
+            if self._is_quant(src):
+                squant = self._quant_info(src)
+                src = self._var_input(src.inputs[0][0])
             bn = None
             if src.op == "BatchNorm":
                 bn = src
@@ -308,7 +357,7 @@ class Plan:
             kc = _pad8(k[0] * k[1] * xshape[1])
             kc = (kc + 31) // 32 * 32
             op = PlanOp("stem", n.name, x=self.tensors[id(src)], y=y, weight=wname, kernel=k, stride=st, pad=pd,
-                        kc=kc, bn=None)
+                        kc=kc, bn=None, quant=squant, qweight=self._weight_quant(n))
             if bn is not None:
                 op.bn = dict(name=bn.name, gamma=self._param_node(bn, 1), beta=self._param_node(bn, 2),
                              mean=bn.inputs[3][0].name, var=bn.inputs[4][0].name,
@@ -323,7 +372,10 @@ class Plan:
         res = None
         if fused is not None:
             res = self.tensor(fused[1])
-        self.ops.append(PlanOp("conv", n.name, x=x, y=y, weight=wname, kernel=k, stride=st, pad=pd, res=res))
+        if g != 1 and (xshape[1] % 8 or yshape[1] % 8):
+            raise PlanError("%s: grouped convolution needs channel counts that are multiples of 8" % n.name)
+        self.ops.append(PlanOp("conv", n.name, x=x, y=y, weight=wname, kernel=k, stride=st, pad=pd, res=res,
+                               groups=g, qweight=self._weight_quant(n)))
 
     def _lower_bn(self, n, relu_node):
         x = self.tensor(n.inputs[0][0])
@@ -359,7 +411,8 @@ class Plan:
         no_bias = bool(_parse(n.attrs.get("no_bias", False)))
         y = self._new_tensor(n, (x.n, nh), F32, kind="logits")
         self.ops.append(PlanOp("fc", n.name, x=x, y=y, weight=self._param_node(n, 1),
-                               bias=None if no_bias else self._param_node(n, 2), nh=nh))
+                               bias=None if no_bias else self._param_node(n, 2), nh=nh,
+                               qweight=self._weight_quant(n)))
 
     def summary(self):
         kinds = {}
@@ -373,7 +426,7 @@ class Plan:
         for op in self.ops:
             if op.kind in ("conv", "stem"):
                 y = op.y
-                cin = op.x.shape[1]
+                cin = op.x.shape[1] // getattr(op, "groups", 1)
                 macs = y.n * y.h * y.w * y.c * cin * op.kernel[0] * op.kernel[1]
                 total += 2 * macs * (2 if op.kind == "stem" else 3)
             elif op.kind == "fc":
@@ -441,6 +494,8 @@ class Executor:
         self._acts = {}
         self._grads = {}
         self._fwd_train, self._fwd_infer, self._bwd = [], [], []
+        # Quantization_int8: activation EMA states initialise from the first training batch
+        self._qfirst = L.C.c_int32(1)
         self._build_params()
         self._alloc_acts()
         self._build_forward()
@@ -577,9 +632,10 @@ class Executor:
     def _sp(self):
         return L.C.c_void_p(0 if self.stream is None else self.stream.cuda_stream)
 
-    def _conv_desc(self, n, h, w, c, c_real, k, kernel, stride, pad):
+    def _conv_desc(self, n, h, w, c, c_real, k, kernel, stride, pad, groups=1):
         d = L.ConvDesc(dtype=self.dtype, n=n, h=h, w=w, c=c, c_real=c_real, k=k, k_pad=_pad8(k), r=kernel[0],
-                       s=kernel[1], stride_h=stride[0], stride_w=stride[1], pad_h=pad[0], pad_w=pad[1], groups=1)
+                       s=kernel[1], stride_h=stride[0], stride_w=stride[1], pad_h=pad[0], pad_w=pad[1],
+                       groups=groups)
         L.check(self.lib.rn_conv_desc_init(L.C.byref(d)), "rn_conv_desc_init")
         return d
 
@@ -606,8 +662,12 @@ class Executor:
                 op.bn_desc = d
         self.ws = self._zeros(ws_bytes // 4 + 16, self.torch.float32)
         wsp = self._p(self.ws)
+        self.qws = self._zeros(4096, self.torch.float32)
+        qwsp = self._p(self.qws)
         for op in plan.ops:
             F, I = [], []  # train-mode, infer-mode call lists
+            op.wsrc = self._weight_source(op, qwsp, sp) if getattr(op, "qweight", None) else \
+                (self._pp(op.weight) if getattr(op, "weight", None) else None)
             if op.kind == "stem":
                 x, y = op.x, op.y
                 d1 = self._conv_desc(x.n, y.h, y.w, op.kc, op.kernel[0] * op.kernel[1] * x.c, y.c, (1, 1), (1, 1),
@@ -616,7 +676,7 @@ class Executor:
                 op.d1, op.dfull = d1, dfull
                 op.cols = self._zeros(x.n * y.h * y.w * op.kc, self.tdtype)
                 op.wk = self._zeros(y.c * op.kc, self.tdtype)
-                self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(d1), self._pp(op.weight),
+                self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(d1), op.wsrc,
                                              self._p(op.wk), None, sp))
                 stem_ws = max(stem_ws, y.h * y.w * y.cp + y.h * op.kernel[1] * y.c + y.c * op.kernel[0] * op.kernel[1] + 64)
                 xnchw = self._p(self.act(x))
@@ -639,24 +699,29 @@ class Executor:
                     I.append(self._call("rn_bn_fwd_infer", L.C.byref(op.bn_desc), self._p(op.nhwc8),
                                         self._p(op.nhwc8), self._pp(b["gamma"]), self._pp(b["beta"]),
                                         self._ap(b["mean"]), self._ap(b["var"]), sc, sh, sp))
+                else:
+                    sc = sh = None
+                if op.quant:
+                    q = op.quant
+                    for lst, tr in ((F, 1), (I, 0)):
+                        lst.append(self._call("rn_im2col_nchw_quant", L.C.byref(dfull), xnchw, sc, sh,
+                                              self._ap(q["minmax"]), tr, q["ema"], self._qfirst, q["nbits"], qwsp,
+                                              self._p(op.cols), op.kc, sp))
+                else:
                     for lst in (F, I):
                         lst.append(self._call("rn_im2col_nchw", L.C.byref(dfull), xnchw, sc, sh, self._p(op.cols),
                                               op.kc, sp))
-                else:
-                    for lst in (F, I):
-                        lst.append(self._call("rn_im2col_nchw", L.C.byref(dfull), xnchw, None, None,
-                                              self._p(op.cols), op.kc, sp))
                 for lst in (F, I):
                     lst.append(self._call("rn_conv_fwd", L.C.byref(d1), self._p(op.cols), self._p(op.wk),
                                           self._p(self.act(y)), self.dtype, None, None, sp))
             elif op.kind == "conv":
                 x, y = op.x, op.y
-                d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad)
+                d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad, op.groups)
                 assert (d.p, d.q) == (y.h, y.w), (op.name, d.p, d.q, y.h, y.w)
                 op.desc = d
-                op.wk = self._zeros(y.c * op.kernel[0] * op.kernel[1] * x.cp, self.tdtype)
-                op.wc = self._zeros(x.cp * op.kernel[0] * op.kernel[1] * y.cp, self.tdtype)
-                self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(d), self._pp(op.weight), self._p(op.wk),
+                op.wk = self._zeros(self.lib.rn_conv_pack_numel(L.C.byref(d), 0), self.tdtype)
+                op.wc = self._zeros(self.lib.rn_conv_pack_numel(L.C.byref(d), 1), self.tdtype)
+                self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(d), op.wsrc, self._p(op.wk),
                                              self._p(op.wc), sp))
                 res = self._p(self.act(op.res)) if op.res is not None else None
                 c = self._call("rn_conv_fwd", L.C.byref(d), self._p(self.act(x)), self._p(op.wk),
@@ -683,6 +748,12 @@ class Executor:
                                self._p(self.act(op.y)), 1, sp)
                 F.append(c)
                 I.append(c)
+            elif op.kind == "quant":
+                q = op.q
+                for lst, tr in ((F, 1), (I, 0)):
+                    lst.append(self._call("rn_quant_int8_fwd", self.dtype, op.x.numel, self._p(self.act(op.x)),
+                                          self._p(self.act(op.y)), self._ap(q["minmax"]), 0, tr, q["ema"],
+                                          self._qfirst, q["nbits"], qwsp, sp))
             elif op.kind == "add":
                 c = self._call("rn_eltwise_add", op.y.numel, self.dtype, self._p(self.act(op.a)),
                                self._p(self.act(op.b)), self._p(self.act(op.y)), int(op.relu), sp)
@@ -709,7 +780,7 @@ class Executor:
                 op.desc = d
                 op.wk = self._zeros(op.nh * x.cp, self.tdtype)
                 op.wc = self._zeros(x.cp * _pad8(op.nh), self.tdtype)
-                self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(d), self._pp(op.weight), self._p(op.wk),
+                self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(d), op.wsrc, self._p(op.wk),
                                              self._p(op.wc), sp))
                 bias = self._pp(op.bias) if op.bias else None
                 c = self._call("rn_conv_fwd", L.C.byref(d), self._p(self.act(x)), self._p(op.wk),
@@ -729,6 +800,17 @@ class Executor:
             self._fwd_train.extend(F)
             self._fwd_infer.extend(I)
         self.stem_ws = self._zeros(stem_ws, self.torch.float32)
+
+    def _weight_source(self, op, qwsp, sp):
+        """Quantization_int8 on a weight (int8_api.py:131-132): the compute copies are packed from a
+        fake-quantized fp32 copy of the master, refreshed with every repack; the STE passes the
+        gradient to the master unchanged."""
+        q = op.qweight
+        n = int(np.prod(self.plan.param_shape(op.weight)))
+        op.qw = self._zeros(n, self.torch.float32)
+        self.packs.append(self._call("rn_quant_int8_fwd", F32, n, self._pp(op.weight), self._p(op.qw),
+                                     self._ap(q["minmax"]), 1, 1, q["ema"], 0, q["nbits"], qwsp, sp))
+        return self._p(op.qw)
 
     # ------------------------------------------------------------------ backward
     def _build_backward(self):
@@ -774,8 +856,12 @@ class Executor:
                 self.param_done_at[op.weight] = len(self._bwd)
                 if op.bn:
                     self._bwd.append(self._call("rn_stem_shift_grad", L.C.byref(op.dfull), self._p(dy),
-                                                self._pp(op.weight), self._gp(op.bn["beta"]), self._p(self.stem_ws),
-                                                sp))
+                                                op.wsrc, self._gp(op.bn["beta"]), self._p(self.stem_ws), sp))
+                    if op.quant:
+                        _, _, sc, sh = op.bn_ptrs
+                        self._bwd.append(self._call("rn_stem_quant_clip_grad", L.C.byref(op.dfull),
+                                                    self._p(self.act(op.x)), sc, sh, self._ap(op.quant["minmax"]),
+                                                    self._p(dy), op.wsrc, self._gp(op.bn["beta"]), sp))
                     self.param_done_at[op.bn["beta"]] = len(self._bwd)
                     self.param_done_at[op.bn["gamma"]] = len(self._bwd)
             elif op.kind == "bn":
@@ -786,6 +872,12 @@ class Executor:
                                             op.sh, self._gp(op.gamma), self._gp(op.beta), wsp, sp))
                 self.param_done_at[op.gamma] = len(self._bwd)
                 self.param_done_at[op.beta] = len(self._bwd)
+            elif op.kind == "quant":
+                if op.x.needs_grad:
+                    out, add = gs.contribute(op.x)
+                    self._bwd.append(self._call("rn_quant_int8_bwd", self.dtype, op.x.numel, self._p(self.act(op.x)),
+                                                self._p(dy), self._p(out), self._ap(op.q["minmax"]), 0, self._p(add),
+                                                sp))
             elif op.kind == "relu":
                 if op.x.needs_grad:
                     out, add = gs.contribute(op.x)
@@ -836,6 +928,8 @@ class Executor:
 
     def forward(self, is_train=True):
         self._run(self._fwd_train if is_train else self._fwd_infer)
+        if is_train:
+            self._qfirst.value = 0
 
     def backward(self, hooks=None):
         self.grad.zero_()

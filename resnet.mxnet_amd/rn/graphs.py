@@ -6,7 +6,9 @@ the reference function it mirrors, so checkpoints and parity fixtures are interc
   resnet(...)          <-> symbol/resnet.py:77-121   (ResNet-v2, pre-activation bottleneck/basic)
   resnet_cifar10(...)  <-> symbol/resnet.py:123-148  (post-activation basic units)
   resnext(...)         <-> symbol/resnext.py:72-103  (grouped 3x3, BN on the shortcut)
-tests/test_dropin.py checks that equivalence against the reference files when they exist.
+  resnet_int8(...)     <-> symbol/resnet_int8.py:69-131 + int8_api.py:120-171 (fake-quant QAT)
+The equivalence is checked against parameter counts and names restated from the reference
+(tests/test_symbol_plan.py) -- the reference files themselves are never imported.
 """
 import mxnet as mx
 
@@ -137,6 +139,89 @@ def resnext(units, num_stage, filter_list, num_classes, data_type="float32", num
     if data_type == "float16":
         fc1 = mx.sym.Cast(data=fc1, dtype="float32")
     return mx.sym.SoftmaxOutput(data=fc1, name="softmax")
+
+
+# ----------------------------------------------------------------------------- int8 (QAT) graph
+def quant_conv(name, data, num_filter, kernel, stride, pad=(0, 0), no_bias=True, num_group=1, in_channels=None,
+               quant_mode="minmax", delay_quant=0, ema_decay=0.99, workspace=512):
+    """int8_api.py:120-150 quant_conv_cxx: Quantization_int8 on the weight ('<name>_weight') and on
+    the data ('<name>_data') feeding a plain Convolution."""
+    weight = mx.sym.Variable(name=name + "_weight", shape=(num_filter, in_channels // num_group) + tuple(kernel),
+                             dtype="float32")
+    weight_q = mx.sym.contrib.Quantization_int8(data=weight, name=name + "_weight", quant_mode=quant_mode,
+                                                is_weight=True, is_weight_perchannel=False, ema_decay=ema_decay,
+                                                delay_quant=delay_quant, grad_mode="ste", workspace=workspace)
+    data_q = mx.sym.contrib.Quantization_int8(data=data, name=name + "_data", quant_mode=quant_mode, is_weight=False,
+                                              is_weight_perchannel=False, ema_decay=ema_decay,
+                                              delay_quant=delay_quant, grad_mode="ste", workspace=workspace)
+    kw = dict(name=name, data=data_q, num_filter=num_filter, kernel=kernel, stride=stride, pad=pad, no_bias=no_bias,
+              weight=weight_q)
+    if num_group != 1:
+        kw["num_group"] = num_group
+    return mx.sym.Convolution(**kw)
+
+
+def quant_fc(name, data, num_hidden, in_channels, quant_mode="minmax", delay_quant=0, ema_decay=0.99,
+             workspace=512):
+    """int8_api.py:152-171 quant_fc_cxx."""
+    weight = mx.sym.Variable(name=name + "_weight", shape=(num_hidden, in_channels), dtype="float32")
+    fc_q = mx.sym.contrib.Quantization_int8(data=weight, name=name + "_weight", is_weight=True, ema_decay=ema_decay,
+                                            delay_quant=delay_quant, quant_mode=quant_mode,
+                                            is_weight_perchannel=False, grad_mode="ste", workspace=workspace)
+    data_q = mx.sym.contrib.Quantization_int8(data=data, name=name + "_data", is_weight=False, ema_decay=ema_decay,
+                                              delay_quant=delay_quant, quant_mode=quant_mode,
+                                              is_weight_perchannel=False, grad_mode="ste", workspace=workspace)
+    return mx.sym.FullyConnected(data=data_q, num_hidden=num_hidden, name=name, weight=fc_q)
+
+
+def _int8_unit(x, cin, nf, stride, dim_match, name, bottle_neck, mom, qkw):
+    """resnet_int8.py:12-66 residual_unit_int8 (pre-activation, every conv quantized)."""
+    a1 = _relu(_bn(x, name + "_bn1", mom=mom), name + "_relu1")
+    if bottle_neck:
+        specs = [(nf // 4, (1, 1), (1, 1), (0, 0)), (nf // 4, (3, 3), stride, (1, 1)), (nf, (1, 1), (1, 1), (0, 0))]
+    else:
+        specs = [(nf, (3, 3), stride, (1, 1)), (nf, (3, 3), (1, 1), (1, 1))]
+    h, c = a1, cin
+    for i, (f, k, s, p) in enumerate(specs):
+        if i > 0:
+            h = _relu(_bn(h, "%s_bn%d" % (name, i + 1), mom=mom), "%s_relu%d" % (name, i + 1))
+        h = quant_conv("%s_conv%d" % (name, i + 1), h, f, k, s, p, in_channels=c, **qkw)
+        c = f
+    sc = x if dim_match else quant_conv(name + "_sc", a1, nf, (1, 1), stride, in_channels=cin, **qkw)
+    return h + sc
+
+
+def resnet_int8(units, num_stage, filter_list, num_classes, data_type="float32", bottle_neck=True, bn_mom=0.9,
+                workspace=512, memonger=False, grad_scale=1.0, dataset_type="imagenet", quant_mode="minmax",
+                delay_quant=0, ema_decay=0.99):
+    """symbol/resnet_int8.py:69-131 (the C5 config graph; BN stays separate)."""
+    assert len(units) == num_stage
+    qkw = dict(quant_mode=quant_mode, delay_quant=delay_quant, ema_decay=ema_decay, workspace=workspace)
+    data = mx.sym.Variable(name="data")
+    data = mx.sym.identity(data=data, name="id")
+    data = _bn(data, "bn_data", fix_gamma=True, eps=2e-5, mom=bn_mom)
+    if dataset_type == "imagenet":
+        body = quant_conv("conv0", data, filter_list[0], (7, 7), (2, 2), (3, 3), in_channels=3, **qkw)
+        body = _relu(_bn(body, "bn0", mom=bn_mom), "relu0")
+        body = mx.sym.Pooling(data=body, kernel=(3, 3), stride=(2, 2), pad=(1, 1), pool_type="max")
+    else:
+        body = quant_conv("conv0", data, filter_list[0], (3, 3), (1, 1), (1, 1), in_channels=3, **qkw)
+    c = filter_list[0]
+    for i in range(num_stage):
+        st = (1, 1) if i == 0 else (2, 2)
+        body = _int8_unit(body, c, filter_list[i + 1], st, False, "stage%d_unit1" % (i + 1), bottle_neck, bn_mom, qkw)
+        c = filter_list[i + 1]
+        for j in range(units[i] - 1):
+            body = _int8_unit(body, c, c, (1, 1), True, "stage%d_unit%d" % (i + 1, j + 2), bottle_neck, bn_mom, qkw)
+    body = _relu(_bn(body, "bn1", mom=bn_mom), "relu1")
+    pool1 = mx.sym.Pooling(data=body, global_pool=True, kernel=(7, 7), pool_type="avg", name="pool1")
+    flat = mx.sym.Flatten(data=pool1)
+    fc1 = quant_fc("fc1", flat, num_classes, c, **qkw)
+    return mx.sym.SoftmaxOutput(data=fc1, name="softmax")
+
+
+def resnet50_int8(num_classes=1000):
+    return resnet_int8([3, 4, 6, 3], 4, [64, 256, 512, 1024, 2048], num_classes, "float32", True)
 
 
 def resnet50(num_classes=1000):

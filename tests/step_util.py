@@ -15,16 +15,18 @@ def module_step(sym, args, aux, data, label, precision, lr=0.1, wd=1e-4, momentu
     mod = mx.mod.Module(sym, context=ctx or [mx.gpu(0)], precision=precision)
     mod.bind(data_shapes=[("data", data.shape)], label_shapes=[("softmax_label", label.shape)], for_training=True)
     mod.init_params(arg_params={k: v.astype(np.float32) for k, v in args.items()},
-                    aux_params={k: v.astype(np.float32) for k, v in aux.items()})
+                    aux_params={k: v.astype(np.float32) for k, v in aux.items()},
+                    allow_missing=True)  # Quantization_int8 minmax states start at 0 (initializer)
     mod.init_optimizer(kvstore="device", optimizer="sgd",
                        optimizer_params={"learning_rate": lr, "wd": wd, "momentum": momentum})
-    out = {"prob": [], "grads": [], "relu_masks": []}
+    out = {"prob": [], "grads": [], "relu_masks": [], "quant_values": []}
     batch = mx.io.DataBatch(data=[mx.nd.array(data)], label=[mx.nd.array(label)])
     ex = mod.executor
     for _ in range(steps):
         mod.forward(batch, is_train=True)
         out["prob"].append(mod.get_outputs()[0].asnumpy().copy())
         out["relu_masks"].append(gpu_relu_masks(ex))
+        out["quant_values"].append(gpu_quant_values(ex))
         mod.backward()
         out["grads"].append({n: ex.get_param(n, grad=True) for n in ex.plan.param_names})
         mod.update()
@@ -50,14 +52,47 @@ def gpu_relu_masks(ex):
     return masks
 
 
-def replayed_parity(res, g, args, aux, data, label, steps=1, base_tol=1e-4, factor=4.0):
+def gpu_quant_values(ex):
+    """The fake-quantized tensors the device computed (Quantization_int8 outputs), keyed like
+    oracle.net.forward's quant_values: '<conv>_data' (NCHW) and '<conv>_weight' (OIHW)."""
+    vals = {}
+    for op in ex.plan.ops:
+        q = getattr(op, "qweight", None)
+        if q is not None:
+            k, c, r, s_ = ex.param_shape[op.weight] if len(ex.param_shape[op.weight]) == 4 else \
+                ex.param_shape[op.weight] + (1, 1)
+            vals[q["name"]] = op.qw.cpu().numpy().reshape(k, r, s_, c).transpose(0, 3, 1, 2)
+        if op.kind == "quant":
+            t = op.y
+            a = ex.act(t).float().cpu().numpy().reshape(t.n, t.h, t.w, t.cp)[..., :t.c].transpose(0, 3, 1, 2)
+            vals[op.q["name"]] = a
+        elif op.kind == "stem" and op.quant:
+            # rebuild the quantized stem input from its im2col matrix
+            x, y = op.x, op.y
+            r, s_ = op.kernel
+            (sh, sw), (ph, pw) = op.stride, op.pad
+            cols = op.cols.float().cpu().numpy().reshape(x.n, y.h, y.w, op.kc)
+            xq = np.zeros((x.n, x.c, x.h, x.w), np.float32)
+            for rr in range(r):
+                for ss in range(s_):
+                    hs = np.arange(y.h) * sh - ph + rr
+                    ws = np.arange(y.w) * sw - pw + ss
+                    hv, wv = (hs >= 0) & (hs < x.h), (ws >= 0) & (ws < x.w)
+                    blk = cols[:, hv][:, :, wv][..., (rr * s_ + ss) * x.c:(rr * s_ + ss + 1) * x.c]
+                    xq[:, :, hs[hv][:, None], ws[wv][None, :]] = blk.transpose(0, 3, 1, 2)
+            vals[op.quant["name"]] = xq
+    return vals
+
+
+def replayed_parity(res, g, args, aux, data, label, steps=1, base_tol=1e-4, factor=4.0, quant_values=None):
     """Oracle fp64 and fp32 runs replaying the device's ReLU decisions; returns per-grad-tensor
     (gpu_err, numpy_fp32_err, tol) Frobenius-relative errors and the fp64 reference. Tensors whose
     reference cancels heavily (e.g. BN gamma grads: sum dz*xhat) get factor x the error numpy fp32
     itself makes on them."""
     masks = res["relu_masks"][0]
-    ref = oracle_step(g, args, aux, data, label, relu_masks=masks, steps=steps)
-    r32 = oracle_step(g, args, aux, data, label, relu_masks=masks, steps=steps, dtype=np.float32)
+    ref = oracle_step(g, args, aux, data, label, relu_masks=masks, steps=steps, quant_values=quant_values)
+    r32 = oracle_step(g, args, aux, data, label, relu_masks=masks, steps=steps, dtype=np.float32,
+                      quant_values=quant_values)
     out = {}
     for n in ref["grads"][0]:
         e = fro_rel(res["grads"][0][n], ref["grads"][0][n])
@@ -67,20 +102,22 @@ def replayed_parity(res, g, args, aux, data, label, steps=1, base_tol=1e-4, fact
 
 
 def oracle_step(graph, args, aux, data, label, lr=0.1, wd=1e-4, momentum=0.9, steps=1, dtype=np.float64,
-                storage=None, relu_masks=None):
+                storage=None, relu_masks=None, quant_values=None):
     args = {k: v.astype(dtype) for k, v in args.items()}
     aux = {k: v.astype(dtype) for k, v in aux.items()}
     data = data.astype(dtype)
     moms = {k: np.zeros_like(v) for k, v in args.items()}
     probs, grads = [], []
     cur_aux = {k: v.copy() for k, v in aux.items()}
-    for _ in range(steps):
+    qstate = {}
+    for i in range(steps):
         prob, g, auxes = onet.train_step(graph, args, cur_aux, moms, data, label, lr, momentum, wd, storage=storage,
-                                         relu_masks=relu_masks)
+                                         relu_masks=relu_masks, quant_values=quant_values, quant_state=qstate,
+                                         first_batch=i == 0)
         cur_aux = auxes[0]
         probs.append(prob)
         grads.append(g)
-    return {"prob": probs, "grads": grads, "args": args, "aux": cur_aux}
+    return {"prob": probs, "grads": grads, "args": args, "aux": cur_aux, "quant_state": qstate}
 
 
 def fro_rel(a, b):

@@ -312,3 +312,109 @@ def test_quant_int8(gpu, dtype):
     assert rel_err(out.float().cpu().numpy(), xq_ref) < tol
     dyr = bf16_round(dy) if dtype == BF16 else dy
     assert rel_err(dx.float().cpu().numpy(), ops.quant_int8_act_bwd(dyr, x, mm_ref)) < tol
+
+
+GCONV_CASES = [
+    # n, c, h, w, k, r, stride, pad, groups -- ResNeXt-50 32x4d conv2 shapes at small spatial size
+    (2, 128, 9, 9, 128, 3, 1, 1, 32),   # 4 channels per group
+    (2, 256, 10, 10, 256, 3, 2, 1, 32),  # 8 per group, stride 2 (dgrad parity classes)
+    (2, 512, 6, 6, 512, 3, 1, 1, 32),   # 16 per group
+    (1, 1024, 5, 5, 1024, 3, 2, 1, 32),  # 32 per group
+    (2, 128, 6, 6, 256, 1, 1, 0, 2),    # 64 -> 128 per group (block inside one group)
+]
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("case", GCONV_CASES)
+def test_grouped_conv(gpu, dtype, case):
+    """Grouped convolution (symbol/resnext.py:23-25) fwd / dgrad / wgrad vs the oracle."""
+    n, c, h, w, k, r, st, pd, g = case
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal((n, c, h, w))
+    wt = rng.standard_normal((k, c // g, r, r)) / np.sqrt(c // g * r * r)
+    P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+    dy = rng.standard_normal((n, k, P, Q))
+    if dtype == BF16:
+        x, wt, dy = bf16_round(x), bf16_round(wt), bf16_round(dy)
+    y_ref = ops.conv2d_fwd(x, wt, (st, st), (pd, pd), g)
+    dx_ref, dw_ref = ops.conv2d_bwd(x, wt, dy, (st, st), (pd, pd), g)
+    d = L.ConvDesc(dtype=dtype, n=n, h=h, w=w, c=c, c_real=c, k=k, k_pad=k, r=r, s=r, stride_h=st, stride_w=st,
+                   pad_h=pd, pad_w=pd, groups=g)
+    L.call("rn_conv_desc_init", C.byref(d))
+    lib = L.load()
+    wk = torch.zeros(lib.rn_conv_pack_numel(C.byref(d), 0), dtype=tdt(dtype), device=gpu)
+    wc = torch.zeros(lib.rn_conv_pack_numel(C.byref(d), 1), dtype=tdt(dtype), device=gpu)
+    master = _master_krsc(wt, gpu)
+    assert master.numel() == lib.rn_conv_weight_numel(C.byref(d))
+    L.call("rn_conv_weight_pack", C.byref(d), p(master), p(wk), p(wc), stream())
+    xd, dyd = to_nhwc(x, dtype, gpu), to_nhwc(dy, dtype, gpu)
+    y = torch.zeros((n, P, Q, k), dtype=tdt(dtype), device=gpu)
+    L.call("rn_conv_fwd", C.byref(d), p(xd), p(wk), p(y), dtype, None, None, stream())
+    dx = torch.zeros((n, h, w, c), dtype=tdt(dtype), device=gpu)
+    L.call("rn_conv_bwd_data", C.byref(d), p(dyd), p(wc), p(dx), None, stream())
+    dw = torch.zeros(master.numel(), dtype=torch.float32, device=gpu)
+    L.call("rn_conv_bwd_filter", C.byref(d), p(xd), p(dyd), p(dw), stream())
+    torch.cuda.synchronize()
+    assert rel_err(from_nhwc(y, k), y_ref) < TOL[dtype]
+    assert rel_err(from_nhwc(dx, c), dx_ref) < TOL[dtype]
+    dw_h = dw.cpu().numpy().reshape(k, r, r, c // g).transpose(0, 3, 1, 2)
+    assert rel_err(dw_h, dw_ref) < (TOL[dtype] if dtype == F32 else 5e-3)
+
+
+def _im2col_ref(xq, r, st, pd, kc):
+    n, c, h, w = xq.shape
+    P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+    xp = np.pad(xq, ((0, 0), (0, 0), (pd, pd), (pd, pd)))
+    cols = np.zeros((n, P, Q, kc))
+    for rr in range(r):
+        for ss in range(r):
+            patch = xp[:, :, rr:rr + st * P:st, ss:ss + st * Q:st]  # n, c, P, Q
+            base = (rr * r + ss) * c
+            cols[..., base:base + c] = patch.transpose(0, 2, 3, 1)
+    return cols.reshape(n * P * Q, kc)
+
+
+def test_stem_quant(gpu):
+    """conv0 of resnet_int8 (symbol/resnet_int8.py:96-98): Quantization_int8(bn_data(x)) folded into
+    the stem im2col, and the STE-masked bn_data beta gradient (clip_grad_quantization_int8.py)."""
+    n, c, h, w, k, r, st, pd, kc = 2, 3, 20, 18, 16, 7, 2, 3, 160
+    rng = np.random.default_rng(12)
+    x1 = rng.uniform(-1, 1, (n, c, h, w)).astype(np.float32)
+    x2 = (x1 * 1.5).astype(np.float32)
+    scale = np.array([1.5, 0.5, 2.0], dtype=np.float32)
+    shift = np.array([0.1, -0.2, 0.3], dtype=np.float32)
+    aff = lambda x: x * scale[None, :, None, None] + shift[None, :, None, None]
+    t1 = np.abs(aff(x1)).max()
+    t2 = np.float32(t1 * np.float32(0.99) + np.abs(aff(x2)).max() * np.float32(0.01))
+    xq_ref, _ = ops.quant_int8_act(aff(x2).astype(np.float64), float(t2), False, False)
+    mask = (aff(x2) > -t2) & (aff(x2) < t2)
+    assert (~mask).sum() > 10  # the EMA threshold clips part of the second batch
+    wq = ops.quant_int8_weight(rng.standard_normal((k, c, r, r)) * 0.1)[0]
+    P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+    dy = rng.standard_normal((n, k, P, Q))
+    dx_ref, _ = ops.conv2d_bwd(xq_ref, wq, dy, (st, st), (pd, pd))
+    dbeta_ref = (dx_ref * mask).sum(axis=(0, 2, 3))
+
+    dfull = conv_desc(F32, n, 8, h, w, k, r, r, st, pd, c_real=c)
+    sc = torch.tensor(scale, device=gpu)
+    sh = torch.tensor(shift, device=gpu)
+    minmax = torch.zeros(1, dtype=torch.float32, device=gpu)
+    ws = torch.zeros(16, dtype=torch.float32, device=gpu)
+    cols = torch.zeros(n * P * Q * kc, dtype=torch.float32, device=gpu)
+    for x, first in ((x1, 1), (x2, 0)):
+        xd = torch.from_numpy(x).to(gpu)
+        L.call("rn_im2col_nchw_quant", C.byref(dfull), p(xd), p(sc), p(sh), p(minmax), 1, C.c_float(0.99), first, 8,
+               p(ws), p(cols), kc, stream())
+    torch.cuda.synchronize()
+    assert abs(minmax.item() - float(t2)) <= 1e-6 * float(t2)
+    got = cols.cpu().numpy().reshape(n * P * Q, kc)
+    assert rel_err(got, _im2col_ref(xq_ref, r, st, pd, kc)) < 1e-6
+    master = _master_krsc(wq, gpu)
+    dyd = to_nhwc(dy, F32, gpu)
+    dbeta = torch.zeros(c, dtype=torch.float32, device=gpu)
+    sws = torch.zeros(P * Q * pad8(k) + P * r * k + k * r * r, dtype=torch.float32, device=gpu)
+    L.call("rn_stem_shift_grad", C.byref(dfull), p(dyd), p(master), p(dbeta), p(sws), stream())
+    L.call("rn_stem_quant_clip_grad", C.byref(dfull), p(xd), p(sc), p(sh), p(minmax), p(dyd), p(master), p(dbeta),
+           stream())
+    torch.cuda.synchronize()
+    assert rel_err(dbeta.cpu().numpy(), dbeta_ref) < 1e-4

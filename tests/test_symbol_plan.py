@@ -83,9 +83,22 @@ def test_plan_fusion_and_flops():
     assert abs(p20.train_flops() / 1e9 - 31.2) < 0.05
 
 
+def test_plan_resnext_grouped():
+    p = Plan(graphs.resnext50_32x4d(), [("data", (256, 3, 224, 224))], [("softmax_label", (256,))])
+    assert sum(1 for op in p.ops if op.kind == "conv" and op.groups == 32) == 16
+    # 6,437.6 GFLOP per 256-image step
+    assert abs(p.train_flops() / 1e9 - 6437.6) < 0.1
+    ex = Executor(Plan(graphs.resnext50_32x4d(), [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")
+    names = [c[0] for c in ex._bwd]
+    assert names.count("rn_conv_bwd_filter") == 54  # 53 conv + fc1
+
+
 def test_plan_rejects_unsupported():
+    x = mx.sym.Variable("data")
+    c = mx.sym.Convolution(data=x, num_filter=8, kernel=(3, 3), dilate=(2, 2), no_bias=True, name="c")
+    sym = mx.sym.SoftmaxOutput(data=mx.sym.FullyConnected(data=c, num_hidden=4, name="fc"), name="softmax")
     with pytest.raises(PlanError):
-        Plan(graphs.resnext50_32x4d(), [("data", (2, 3, 224, 224))], [("softmax_label", (2,))])
+        Plan(sym, [("data", (2, 8, 16, 16))], [("softmax_label", (2,))])
 
 
 @pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
@@ -108,3 +121,21 @@ def test_executor_dry_run(dtype):
     w3 = np.random.default_rng(2).standard_normal((128, 128, 3, 3)).astype(np.float32)
     ex.set_param("stage2_unit1_conv2_weight", w3)
     np.testing.assert_array_equal(ex.get_param("stage2_unit1_conv2_weight"), w3)
+
+
+def test_plan_int8_quantization():
+    """resnet_int8 (symbol/resnet_int8.py): 108 Quantization_int8 nodes -> 54 weight
+    quantizations folded into the weight packs, 53 activation quant ops, 1 folded into the stem."""
+    sym = graphs.resnet50_int8()
+    aux = sym.list_auxiliary_states()
+    assert len(aux) == 210 and sum(a.endswith("_minmax") for a in aux) == 108
+    p = Plan(sym, [("data", (256, 3, 224, 224))], [("softmax_label", (256,))])
+    assert p.summary() == {"stem": 1, "bn": 50, "pool": 2, "quant": 53, "conv": 52, "fc": 1, "softmax": 1}
+    assert sum(1 for op in p.ops if getattr(op, "qweight", None)) == 54
+    assert [op for op in p.ops if op.kind == "stem"][0].quant["minmax"] == "conv0_data_minmax"
+    assert abs(p.train_flops() / 1e9 - 6220.6) < 0.1
+    ex = Executor(Plan(graphs.resnet_int8([1, 1, 1, 1], 4, [64, 256, 512, 1024, 2048], 16),
+                       [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")
+    names = [c[0] for c in ex._bwd]
+    assert names.count("rn_quant_int8_bwd") == 17 and names.count("rn_stem_quant_clip_grad") == 1
+    assert [c[0] for c in ex.packs].count("rn_quant_int8_fwd") == 18
