@@ -44,7 +44,7 @@ def conv_call_bytes(ex, name, args):
     x = d.n * d.h * d.w * d.c * es
     y = d.n * d.p * d.q * d.k_pad * es
     w = d.k * d.r * d.s * d.c_real * es
-    if name == "rn_conv_fwd":
+    if name in ("rn_conv_fwd", "rn_conv_fwd_bnstats"):
         yb = d.n * d.p * d.q * d.k_pad * (4 if args[4] == 1 else es)
         return x + w + yb + (y if args[5] is not None else 0)
     if name == "rn_conv_bwd_data":
@@ -69,10 +69,10 @@ def pmc_traffic(family):
 def family_of(ex, name, args):
     if name == "rn_conv_bwd_filter":
         return "wgrad_kernel<bf16,128,128>" if ex.dtype == 0 else "wgrad_kernel<f32,128,128>"
-    if name in ("rn_conv_fwd", "rn_conv_bwd_data"):
+    if name in ("rn_conv_fwd", "rn_conv_fwd_bnstats", "rn_conv_bwd_data"):
         d = args[0]._obj
-        ncol = d.k if name == "rn_conv_fwd" else d.c
-        out_f32 = name == "rn_conv_fwd" and args[4] == 1 and ex.dtype == 0
+        ncol = d.c if name == "rn_conv_bwd_data" else d.k
+        out_f32 = name != "rn_conv_bwd_data" and args[4] == 1 and ex.dtype == 0
         tile = "128x64" if ncol <= 64 else "128x128"
         return "igemm_kernel<bf16,%s,%s>" % ("f32" if out_f32 else "bf16", tile)
     return None

@@ -60,6 +60,13 @@ int rn_conv_desc_init(rn_conv_desc* d);
 int rn_conv_fwd(const rn_conv_desc* d, const void* x, const void* w_krsc, void* y, int32_t y_dtype,
                 const void* add_src, const float* bias, rn_stream_t stream);
 
+/* rn_conv_fwd that also emits the BatchNorm statistics of y for a following BatchNorm in
+ * training mode (saves the statistics pass over y): part = float[rn_conv_bnstats_blocks(d)][3][k_pad]
+ * per-block partials (S1, S2, pivot), consumed by rn_bn_fwd_train_part with rows_blk = 128. */
+int rn_conv_fwd_bnstats(const rn_conv_desc* d, const void* x, const void* w_krsc, void* y, int32_t y_dtype,
+                        const void* add_src, const float* bias, float* part, rn_stream_t stream);
+int64_t rn_conv_bnstats_blocks(const rn_conv_desc* d);
+
 /* dx = conv_transpose(dy, w) (+ add_src). w_crsk is the CRSK re-layout made by
  * rn_conv_weight_pack (row count c, K stride k_pad). */
 int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
@@ -139,6 +146,13 @@ int rn_bn_fwd_train(const rn_bn_desc* d, const void* x, void* y, const float* ga
                     float* save_invstd, float* scale, float* shift, void* ws, rn_stream_t stream);
 
 /* Inference forward with moving statistics (use_global_stats / is_train=False). */
+/* rn_bn_fwd_train with the batch statistics already reduced per row block by the producer
+ * (rn_conv_fwd_bnstats): fp64 merge of part[nblk][3][ld] -> coefficients, moving stats, then
+ * y = bn(x) (+relu) when y != NULL. ws: rn_bn_workspace_bytes(d) (rows_blk = 128). */
+int rn_bn_fwd_train_part(const rn_bn_desc* d, const float* part, int64_t nblk, int32_t rows_blk, int32_t ld,
+                         const void* x, void* y, const float* gamma, const float* beta, float* moving_mean,
+                         float* moving_var, float* save_mean, float* save_invstd, float* scale, float* shift,
+                         void* ws, rn_stream_t stream);
 int rn_bn_fwd_infer(const rn_bn_desc* d, const void* x, void* y, const float* gamma,
                     const float* beta, const float* moving_mean, const float* moving_var,
                     float* scale, float* shift, rn_stream_t stream);

@@ -145,6 +145,92 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_kernel(const T* __restric
   }
 }
 
+// finalize from per-row-block partials written by a producing kernel's epilogue (the conv
+// epilogue of rn_conv_fwd_bnstats): part[b][0|1|2][ld] = S1 = sum(v - p_b), S2 = sum((v - p_b)^2)
+// and the pivot p_b, over the block's n_b rows. Shifting a partial to another pivot q is exact:
+//   S1' = S1 + n d,  S2' = S2 + 2 d S1 + n d^2,  d = p_b - q.
+// Pass 1 (grid c/64 x groups of 64 row blocks, reads coalesced across channels) merges each group
+// onto its first pivot in fp64; pass 2 merges the groups per channel and finalizes.
+constexpr int kPartGroup = 64;
+__global__ __launch_bounds__(256) void bn_part_merge_kernel(const float* __restrict__ part, int nblk, int64_t m,
+                                                            int rows_blk, int ld, int c,
+                                                            double* __restrict__ part2) {
+  const int ch = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int sub = threadIdx.x >> 6;
+  const int b0 = blockIdx.y * kPartGroup;
+  const int b1 = min(nblk, b0 + kPartGroup);
+  __shared__ double red[3][4][64];
+  double s1 = 0.0, s2 = 0.0, n = 0.0, q = 0.0;
+  if (ch < c) {
+    q = part[(int64_t)b0 * 3 * ld + 2 * ld + ch];
+    for (int b = b0 + sub; b < b1; b += 4) {
+      const float* pb = part + (int64_t)b * 3 * ld + ch;
+      const double nb = (double)min<int64_t>(rows_blk, m - (int64_t)b * rows_blk);
+      const double d = (double)pb[2 * ld] - q;
+      const double a = pb[0];
+      s1 += a + nb * d;
+      s2 += (double)pb[ld] + 2.0 * d * a + nb * d * d;
+      n += nb;
+    }
+  }
+  red[0][sub][threadIdx.x & 63] = s1;
+  red[1][sub][threadIdx.x & 63] = s2;
+  red[2][sub][threadIdx.x & 63] = n;
+  __syncthreads();
+  if (sub == 0 && ch < c) {
+    for (int t = 1; t < 4; ++t) {
+      s1 += red[0][t][threadIdx.x];
+      s2 += red[1][t][threadIdx.x];
+      n += red[2][t][threadIdx.x];
+    }
+    double* dst = part2 + (int64_t)blockIdx.y * 4 * c + ch;
+    dst[0] = s1;
+    dst[c] = s2;
+    dst[2 * c] = n;
+    dst[3 * c] = q;
+  }
+}
+
+__global__ __launch_bounds__(64) void bn_fwd_finalize_part_kernel(const double* __restrict__ part2, int ngrp,
+                                                                  int64_t m, int c, int c_real, float eps,
+                                                                  float momentum, int fix_gamma,
+                                                                  const float* __restrict__ gamma,
+                                                                  const float* __restrict__ beta,
+                                                                  float* moving_mean, float* moving_var,
+                                                                  float* save_mean, float* save_invstd,
+                                                                  float* scale, float* shift) {
+  const int ch = blockIdx.x * 64 + threadIdx.x;
+  if (ch >= c) return;
+  if (ch >= c_real) {
+    scale[ch] = 0.f;
+    shift[ch] = 0.f;
+    return;
+  }
+  const double q = part2[3 * c + ch];  // group 0's pivot
+  double s1 = 0.0, s2 = 0.0;
+  for (int gi = 0; gi < ngrp; ++gi) {
+    const double* pg = part2 + (int64_t)gi * 4 * c + ch;
+    const double d = pg[3 * c] - q, a = pg[0], nb = pg[2 * c];
+    s1 += a + nb * d;
+    s2 += pg[c] + 2.0 * d * a + nb * d * d;
+  }
+  const double md = s1 / (double)m;
+  const double mean = q + md;
+  double var = s2 / (double)m - md * md;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = fix_gamma ? 1.f : gamma[ch];
+  const float sc = g * invstd;
+  scale[ch] = sc;
+  shift[ch] = beta[ch] - (float)mean * sc;
+  save_mean[ch] = (float)mean;
+  save_invstd[ch] = invstd;
+  if (moving_mean) {
+    moving_mean[ch] = moving_mean[ch] * momentum + (float)mean * (1.f - momentum);
+    moving_var[ch] = moving_var[ch] * momentum + (float)var * (1.f - momentum);
+  }
+}
+
 __global__ void bn_infer_coef_kernel(int c, int c_real, float eps, int fix_gamma, const float* gamma,
                                      const float* beta, const float* mm, const float* mv, float* scale,
                                      float* shift) {
@@ -398,7 +484,9 @@ extern "C" {
 
 int64_t rn_bn_workspace_bytes(const rn_bn_desc* d) {
   Geo g = d->dtype == RN_BF16 ? make_geo<bf16_t>(d->m, d->c) : make_geo<float>(d->m, d->c);
-  return ((int64_t)g.nrb * d->c * 2 + (int64_t)d->c * 4) * (int64_t)sizeof(float) + 64;
+  const int64_t stats = ((int64_t)g.nrb * d->c * 2 + (int64_t)d->c * 4) * (int64_t)sizeof(float) + 64;
+  const int64_t merge = ceil_div(ceil_div(d->m, 128), kPartGroup) * 4 * d->c * (int64_t)sizeof(double) + 64;
+  return std::max(stats, merge);  // rn_bn_fwd_train_part: 128-row producer blocks
 }
 
 static int check_bn(const rn_bn_desc* d) {
@@ -422,6 +510,32 @@ int rn_bn_fwd_train(const rn_bn_desc* d, const void* x, void* y, const float* ga
                                   shift, ws, st);
   return bn_fwd_train_t<float>(d, x, y, gamma, beta, moving_mean, moving_var, save_mean, save_invstd, scale,
                                shift, ws, st);
+}
+
+int rn_bn_fwd_train_part(const rn_bn_desc* d, const float* part, int64_t nblk, int32_t rows_blk, int32_t ld,
+                         const void* x, void* y, const float* gamma, const float* beta, float* moving_mean,
+                         float* moving_var, float* save_mean, float* save_invstd, float* scale, float* shift,
+                         void* ws, rn_stream_t stream) {
+  if (check_bn(d)) return -1;
+  RN_CHECK_ARG(part && nblk > 0 && rows_blk > 0 && ld >= d->c, "bad partials");
+  RN_CHECK_ARG((int64_t)nblk * rows_blk >= d->m, "partials do not cover the rows");
+  RN_CHECK_ARG(beta && save_mean && save_invstd && scale && shift, "null argument");
+  RN_CHECK_ARG(d->fix_gamma || gamma, "gamma required unless fix_gamma");
+  RN_CHECK_ARG((moving_mean == nullptr) == (moving_var == nullptr), "moving stats must both be set");
+  RN_CHECK_ARG(ws != nullptr, "null workspace");
+  hipStream_t st = as_stream(stream);
+  const int ngrp = (int)ceil_div(nblk, kPartGroup);
+  double* part2 = reinterpret_cast<double*>(ws);
+  hipLaunchKernelGGL(bn_part_merge_kernel, dim3((d->c + 63) / 64, ngrp), dim3(256), 0, st, part, (int)nblk, d->m,
+                     rows_blk, ld, d->c, part2);
+  hipLaunchKernelGGL(bn_fwd_finalize_part_kernel, dim3((d->c + 63) / 64), dim3(64), 0, st, part2, ngrp, d->m, d->c,
+                     d->c_real, d->eps, d->momentum, d->fix_gamma, gamma, beta, moving_mean, moving_var, save_mean,
+                     save_invstd, scale, shift);
+  if (rn_check_launch("bn_fwd_finalize_part")) return -1;
+  if (!y) return 0;
+  RN_CHECK_ARG(x != nullptr, "null x");
+  if (d->dtype == RN_BF16) return bn_apply_t<bf16_t>(d, x, y, scale, shift, st);
+  return bn_apply_t<float>(d, x, y, scale, shift, st);
 }
 
 int rn_bn_fwd_infer(const rn_bn_desc* d, const void* x, void* y, const float* gamma, const float* beta,

@@ -49,11 +49,21 @@ struct IgemmArgs {
   int ostep_h, ostep_w;
   int gcol, gred;      // grouped: output columns / reduction channels per group (dense: 2^30, 0)
   int cblk;            // reduction channels per column block (dense: C)
+  float* stats;        // fwd only, nullable: per-block BatchNorm partials [m tiles][3][ldo]
+  int ntn;             // n tiles (grid = m tiles * ntn)
   int ncls;
   IgemmCls cls[4];
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ (row & 7); }
+
+// XCD-aware block order: the dispatcher deals consecutive workgroup ids round-robin over the 8
+// XCDs (each with a private L2). Bijective remap so that every XCD walks a contiguous range of
+// logical tiles: neighbouring tiles (which share operand panels) then share an L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
 
 template <typename T>
 __device__ __forceinline__ void mfma_slab(v4f& acc, const uint4& a, const uint4& b);
@@ -78,6 +88,42 @@ __device__ __forceinline__ float load_out(const void* p, int64_t i) {
   return to_f(reinterpret_cast<const OutT*>(p)[i]);
 }
 
+// BatchNorm statistics of the block's output rows, from the staged (stored-precision) fp32 tile:
+// per column, pivot p = row 0's value, S1 = sum(v - p), S2 = sum((v - p)^2) over the block's
+// valid rows -> part[blk][0|1|2][col] (merged exactly in fp64 by rn_bn_fwd_train_part).
+template <int BM, int BN, int LDT>
+__device__ __forceinline__ void bn_stats_epilogue(float* tile, float* __restrict__ part, int ld, int m0, int n0,
+                                                  int Mc, int mtile) {
+  constexpr int TPC = 256 / BN;  // threads per column
+  const int tid = threadIdx.x;
+  const int col = tid % BN, sub = tid / BN;
+  const int nv = min(BM, Mc - m0);
+  __syncthreads();
+  const float piv = tile[col];
+  float s1 = 0.f, s2 = 0.f;
+  for (int r = sub; r < nv; r += TPC) {
+    const float d = tile[r * LDT + col] - piv;
+    s1 += d;
+    s2 = fmaf(d, d, s2);
+  }
+  __syncthreads();
+  tile[(2 * sub) * LDT + col] = s1;
+  tile[(2 * sub + 1) * LDT + col] = s2;
+  __syncthreads();
+  if (sub == 0 && n0 + col < ld) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int t = 0; t < TPC; ++t) {
+      a += tile[(2 * t) * LDT + col];
+      b += tile[(2 * t + 1) * LDT + col];
+    }
+    float* dst = part + (int64_t)mtile * 3 * ld + n0 + col;
+    dst[0] = a;
+    dst[ld] = b;
+    dst[2 * ld] = piv;
+  }
+}
+
 template <typename T, typename OutT, int BM, int BN>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
   constexpr int CE = 16 / sizeof(T);   // elements per chunk
@@ -97,9 +143,13 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
   const int wm = wid >> 1, wn = wid & 1;
   const IgemmCls& cl = p.cls[blockIdx.z];
   const int Mc = p.N * cl.Pc * cl.Qc;
-  const int m0 = blockIdx.x * BM;
+  // 1-D grid over (m tile, n tile), n fastest: the n tiles reading one gathered A panel are
+  // consecutive logical blocks and, after the remap, run on one XCD
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mtile = lid / p.ntn;
+  const int m0 = mtile * BM;
   if (m0 >= Mc) return;
-  const int n0 = blockIdx.y * BN;
+  const int n0 = (lid - mtile * p.ntn) * BN;
   // grouped conv: the block's columns touch groups n0/gcol.., whose input channels start here
   const int cbase = (n0 / p.gcol) * p.gred;
 
@@ -310,7 +360,13 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
 #pragma unroll
         for (int e = 0; e < OE; ++e) v[e] += a[e];
       }
-      *reinterpret_cast<uint4*>(yg + ep_off[k]) = f_to_chunk(v, (const OutT*)nullptr);
+      const uint4 out = f_to_chunk(v, (const OutT*)nullptr);
+      *reinterpret_cast<uint4*>(yg + ep_off[k]) = out;
+      if (p.stats) {  // keep the stored (rounded) values for the BatchNorm statistics below
+        chunk_to_f(out, v, (const OutT*)nullptr);
+#pragma unroll
+        for (int e = 0; e < OE; ++e) tile[row * LDT + cc * OE + e] = v[e];
+      }
     } else {  // ragged last chunk (num_hidden % 8 != 0)
       for (int e = 0; e < OE && col0 + e < p.K; ++e) {
         float o = v[e];
@@ -320,6 +376,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
     }
   }
   }
+  if (p.stats) bn_stats_epilogue<BM, BN, LDT>(tile, p.stats, p.ldo, m0, n0, Mc, mtile);
 }
 
 // ------------------------------------------------------------------------------ wgrad
@@ -334,6 +391,7 @@ struct WgradArgs {
   int M;
   int m_per_split;
   int grouped, gk, gc, cblk;  // grouped: rows / channels per group, channels per row block
+  int nct, nkt;               // column tiles, k tiles (grid = splits * nkt * nct)
   FastDiv fdQ, fdPQ, fdC, fdS;  // fdC divides by cblk (dense: C)
 };
 
@@ -359,9 +417,16 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
-  const int n0 = blockIdx.x * BNC;  // dw column tile
-  const int k0 = blockIdx.y * BMK;  // dw row tile (output channels)
-  const int mbeg = blockIdx.z * p.m_per_split;
+  // 1-D grid over (m split, k tile, column tile), column fastest, XCD-remapped: the tiles of one
+  // m range (which re-read the same dy rows and x pixels) share an L2
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_split = p.nct * p.nkt;
+  const int zs = lid / per_split;
+  const int rem = lid - zs * per_split;
+  const int kt = rem / p.nct;
+  const int n0 = (rem - kt * p.nct) * BNC;  // dw column tile
+  const int k0 = kt * BMK;                  // dw row tile (output channels)
+  const int mbeg = zs * p.m_per_split;
   const int mend = min(p.M, mbeg + p.m_per_split);
   if (mbeg >= mend) return;
   const int cbase = p.grouped ? (k0 / p.gk) * p.gc : 0;
@@ -834,12 +899,15 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   int maxMc = 0;
   for (int z = 0; z < a.ncls; ++z) maxMc = std::max(maxMc, a.N * a.cls[z].Pc * a.cls[z].Qc);
   if (maxMc == 0) return 0;
+  IgemmArgs b = a;
   if (a.K <= 64 || a.gred > 0) {  // grouped: the block width is RN_GROUP_BLOCK
-    dim3 grid((unsigned)ceil_div(maxMc, 128), (unsigned)ceil_div(a.K, 64), a.ncls);
-    hipLaunchKernelGGL((igemm_kernel<T, OutT, 128, 64>), grid, dim3(256), 0, st, a);
+    b.ntn = (int)ceil_div(a.K, 64);
+    dim3 grid((unsigned)(ceil_div(maxMc, 128) * b.ntn), 1, a.ncls);
+    hipLaunchKernelGGL((igemm_kernel<T, OutT, 128, 64>), grid, dim3(256), 0, st, b);
   } else {
-    dim3 grid((unsigned)ceil_div(maxMc, 128), (unsigned)ceil_div(a.K, 128), a.ncls);
-    hipLaunchKernelGGL((igemm_kernel<T, OutT, 128, 128>), grid, dim3(256), 0, st, a);
+    b.ntn = (int)ceil_div(a.K, 128);
+    dim3 grid((unsigned)(ceil_div(maxMc, 128) * b.ntn), 1, a.ncls);
+    hipLaunchKernelGGL((igemm_kernel<T, OutT, 128, 128>), grid, dim3(256), 0, st, b);
   }
   return rn_check_launch("igemm");
 }
@@ -892,11 +960,12 @@ int64_t rn_conv_pack_numel(const rn_conv_desc* d, int32_t which) {
   return which == 0 ? d->k * RS * d->c : d->c * RS * d->k_pad;
 }
 
-int rn_conv_fwd(const rn_conv_desc* d, const void* x, const void* w, void* y, int32_t y_dtype,
-                const void* add_src, const float* bias, rn_stream_t stream) {
+int rn_conv_fwd_bnstats(const rn_conv_desc* d, const void* x, const void* w, void* y, int32_t y_dtype,
+                        const void* add_src, const float* bias, float* part, rn_stream_t stream) {
   RN_CHECK_ARG(d && x && w && y, "null argument");
   IgemmArgs a = make_igemm_args(d, 0);
-  a.x = x; a.w = w; a.y = y; a.add = add_src; a.bias = bias;
+  a.x = x; a.w = w; a.y = y; a.add = add_src; a.bias = bias; a.stats = part;
+  RN_CHECK_ARG(!part || d->k % 8 == 0, "BatchNorm statistics need whole 8-channel chunks");
   hipStream_t st = as_stream(stream);
   if (d->dtype == RN_BF16) {
     if (y_dtype == RN_BF16) return launch_igemm<bf16_t, bf16_t>(a, st);
@@ -905,6 +974,13 @@ int rn_conv_fwd(const rn_conv_desc* d, const void* x, const void* w, void* y, in
   RN_CHECK_ARG(y_dtype == RN_F32, "f32 compute requires f32 output");
   return launch_igemm<float, float>(a, st);
 }
+
+int rn_conv_fwd(const rn_conv_desc* d, const void* x, const void* w, void* y, int32_t y_dtype,
+                const void* add_src, const float* bias, rn_stream_t stream) {
+  return rn_conv_fwd_bnstats(d, x, w, y, y_dtype, add_src, bias, nullptr, stream);
+}
+
+int64_t rn_conv_bnstats_blocks(const rn_conv_desc* d) { return ceil_div((int64_t)d->n * d->p * d->q, 128); }
 
 int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
                      const void* add_src, rn_stream_t stream) {
@@ -953,7 +1029,9 @@ int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, flo
   int64_t stages_per = ceil_div(mstages, split);
   a.m_per_split = (int)(stages_per * bkm);
   split = ceil_div(a.M, a.m_per_split);
-  dim3 grid((unsigned)ceil_div(a.ncol_load, bnc), (unsigned)ceil_div(a.K, bmk), (unsigned)split);
+  a.nct = (int)ceil_div(a.ncol_load, bnc);
+  a.nkt = (int)ceil_div(a.K, bmk);
+  dim3 grid((unsigned)(a.nct * a.nkt * split));
   hipStream_t st = as_stream(stream);
   if (grouped) {
     if (d->dtype == RN_BF16)

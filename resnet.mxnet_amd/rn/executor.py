@@ -15,6 +15,7 @@ fp32 master buffer (conv / FC weights in KRSC), ordered in reverse forward order
 gradient buckets complete front-to-back during backward (RCCL bucketing, rn/dist.py).
 """
 import math
+import os
 
 import numpy as np
 
@@ -648,6 +649,20 @@ class Executor:
         self.packs = []   # weight pack calls (after every update)
         self.bn_state = {}
         stem_ws = 64
+        # BatchNorm statistics straight from the producing conv's epilogue (no separate stats pass)
+        producer = {}
+        for op in plan.ops:
+            op.bnstats = False
+            op.part_src = None
+            if op.kind in ("conv", "stem"):
+                producer[id(op.y)] = op
+        if os.environ.get("RN_BN_EPILOGUE_STATS", "0") == "1":  # measured slower end-to-end
+            for op in plan.ops:
+                if op.kind == "bn" and not op.use_global_stats:
+                    src = producer.get(id(op.x))
+                    if src is not None and src.y.c % 8 == 0 and src.y.cp == op.x.cp:
+                        src.bnstats = True
+                        op.part_src = src
         for op in plan.ops:
             if op.kind == "bn":
                 d = L.BNDesc(dtype=self.dtype, m=op.x.rows, c=op.x.cp, c_real=op.x.c, eps=op.eps,
@@ -711,9 +726,9 @@ class Executor:
                     for lst in (F, I):
                         lst.append(self._call("rn_im2col_nchw", L.C.byref(dfull), xnchw, sc, sh, self._p(op.cols),
                                               op.kc, sp))
-                for lst in (F, I):
-                    lst.append(self._call("rn_conv_fwd", L.C.byref(d1), self._p(op.cols), self._p(op.wk),
-                                          self._p(self.act(y)), self.dtype, None, None, sp))
+                I.append(self._call("rn_conv_fwd", L.C.byref(d1), self._p(op.cols), self._p(op.wk),
+                                    self._p(self.act(y)), self.dtype, None, None, sp))
+                F.append(self._conv_fwd_call(op, d1, self._p(op.cols), None, sp))
             elif op.kind == "conv":
                 x, y = op.x, op.y
                 d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad, op.groups)
@@ -724,10 +739,9 @@ class Executor:
                 self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(d), op.wsrc, self._p(op.wk),
                                              self._p(op.wc), sp))
                 res = self._p(self.act(op.res)) if op.res is not None else None
-                c = self._call("rn_conv_fwd", L.C.byref(d), self._p(self.act(x)), self._p(op.wk),
-                               self._p(self.act(y)), self.dtype, res, None, sp)
-                F.append(c)
-                I.append(c)
+                I.append(self._call("rn_conv_fwd", L.C.byref(d), self._p(self.act(x)), self._p(op.wk),
+                                    self._p(self.act(y)), self.dtype, res, None, sp))
+                F.append(self._conv_fwd_call(op, d, self._p(self.act(x)), res, sp))
             elif op.kind == "bn":
                 x, y = op.x, op.y
                 c = x.cp
@@ -738,6 +752,12 @@ class Executor:
                                    gamma, self._pp(op.beta), self._ap(op.mean), self._ap(op.var), op.sc, op.sh, sp)
                 if op.use_global_stats:
                     F.append(infer)
+                elif op.part_src is not None:
+                    s_ = op.part_src
+                    F.append(self._call("rn_bn_fwd_train_part", L.C.byref(op.desc), self._p(s_.part), s_.part_blocks,
+                                        128, s_.y.cp, self._p(self.act(x)), self._p(self.act(y)), gamma,
+                                        self._pp(op.beta), self._ap(op.mean), self._ap(op.var), op.sm, op.si, op.sc,
+                                        op.sh, wsp, sp))
                 else:
                     F.append(self._call("rn_bn_fwd_train", L.C.byref(op.desc), self._p(self.act(x)),
                                         self._p(self.act(y)), gamma, self._pp(op.beta), self._ap(op.mean),
@@ -800,6 +820,16 @@ class Executor:
             self._fwd_train.extend(F)
             self._fwd_infer.extend(I)
         self.stem_ws = self._zeros(stem_ws, self.torch.float32)
+
+    def _conv_fwd_call(self, op, d, xptr, res, sp):
+        """Training-mode conv forward; emits the next BatchNorm's statistics when one consumes y."""
+        y = self._p(self.act(op.y))
+        if not op.bnstats:
+            return self._call("rn_conv_fwd", L.C.byref(d), xptr, self._p(op.wk), y, self.dtype, res, None, sp)
+        op.part_blocks = int(self.lib.rn_conv_bnstats_blocks(L.C.byref(d)))
+        op.part = self._zeros(op.part_blocks * 3 * op.y.cp, self.torch.float32)
+        return self._call("rn_conv_fwd_bnstats", L.C.byref(d), xptr, self._p(op.wk), y, self.dtype, res, None,
+                          self._p(op.part), sp)
 
     def _weight_source(self, op, qwsp, sp):
         """Quantization_int8 on a weight (int8_api.py:131-132): the compute copies are packed from a

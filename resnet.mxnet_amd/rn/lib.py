@@ -38,6 +38,8 @@ class PoolDesc(C.Structure):
 SIGNATURES = {
     "rn_conv_desc_init": (_i32, [_P]),
     "rn_conv_fwd": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P]),
+    "rn_conv_fwd_bnstats": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P]),
+    "rn_conv_bnstats_blocks": (_i64, [_P]),
     "rn_conv_bwd_data": (_i32, [_P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_filter": (_i32, [_P, _P, _P, _P, _P]),
     "rn_conv_weight_numel": (_i64, [_P]),
@@ -49,6 +51,7 @@ SIGNATURES = {
     "rn_stem_shift_grad": (_i32, [_P, _P, _P, _P, _P, _P]),
     "rn_bn_workspace_bytes": (_i64, [_P]),
     "rn_bn_fwd_train": (_i32, [_P] * 13),
+    "rn_bn_fwd_train_part": (_i32, [_P, _P, _i64, _i32, _i32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rn_bn_fwd_infer": (_i32, [_P] * 10),
     "rn_bn_apply": (_i32, [_P] * 6),
     "rn_bn_bwd": (_i32, [_P] * 14),

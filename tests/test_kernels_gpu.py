@@ -418,3 +418,47 @@ def test_stem_quant(gpu):
            stream())
     torch.cuda.synchronize()
     assert rel_err(dbeta.cpu().numpy(), dbeta_ref) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("case", [(3, 32, 13, 11, 48, 3, 2, 1), (2, 64, 14, 14, 256, 1, 1, 0), (2, 16, 9, 9, 64, 1, 1, 0)])
+def test_conv_bnstats_epilogue(gpu, dtype, case):
+    """BatchNorm statistics emitted by the conv epilogue (rn_conv_fwd_bnstats, with the fused
+    residual add) and merged by rn_bn_fwd_train_part == a BatchNorm over the stored conv output."""
+    n, c, h, w, k, r, st, pd = case
+    x, wt = _conv_data(case, 13)
+    if dtype == BF16:
+        x, wt = bf16_round(x), bf16_round(wt)
+    P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+    res = np.random.default_rng(14).standard_normal((n, k, P, Q)) + 3.0  # offset mean: exercises the pivots
+    if dtype == BF16:
+        res = bf16_round(res)
+    d = conv_desc(dtype, n, c, h, w, k, r, r, st, pd)
+    xd = to_nhwc(x, dtype, gpu)
+    wk = torch.zeros(k * r * r * d.c, dtype=tdt(dtype), device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), p(wk), None, stream())
+    y = torch.zeros((n, P, Q, d.k_pad), dtype=tdt(dtype), device=gpu)
+    lib = L.load()
+    nblk = lib.rn_conv_bnstats_blocks(C.byref(d))
+    part = torch.zeros(nblk * 3 * d.k_pad, dtype=torch.float32, device=gpu)
+    L.call("rn_conv_fwd_bnstats", C.byref(d), p(xd), p(wk), p(y), dtype, p(to_nhwc(res, dtype, gpu)), None, p(part),
+           stream())
+    torch.cuda.synchronize()
+    conv_out = from_nhwc(y, k)  # the stored (rounded) values the statistics must describe
+    gamma = np.random.default_rng(15).uniform(0.5, 1.5, k)
+    beta = np.random.default_rng(16).standard_normal(k) * 0.1
+    y_ref, cache = ops.bn_train_fwd(conv_out, gamma, beta, 1e-5, False)
+    mm_ref, mv_ref = ops.bn_moving_update(np.zeros(k), np.ones(k), cache[3], cache[4], 0.9)
+    bd = L.BNDesc(dtype=dtype, m=n * P * Q, c=d.k_pad, c_real=k, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1)
+    f = lambda a: torch.tensor(np.pad(a, (0, d.k_pad - k)), dtype=torch.float32, device=gpu)
+    g_d, b_d, mm, mv = f(gamma), f(beta), f(np.zeros(k)), f(np.ones(k))
+    sm, si, sc, sh = [torch.zeros(d.k_pad, dtype=torch.float32, device=gpu) for _ in range(4)]
+    yb = torch.zeros_like(y)
+    ws = torch.zeros(lib.rn_bn_workspace_bytes(C.byref(bd)) // 4 + 16, dtype=torch.float32, device=gpu)
+    L.call("rn_bn_fwd_train_part", C.byref(bd), p(part), nblk, 128, d.k_pad, p(y), p(yb), p(g_d), p(b_d), p(mm), p(mv),
+           p(sm), p(si), p(sc), p(sh), p(ws), stream())
+    torch.cuda.synchronize()
+    assert rel_err(sm.cpu().numpy()[:k], cache[3]) < 1e-6
+    assert rel_err(mv.cpu().numpy()[:k], mv_ref) < 1e-5
+    assert rel_err(mm.cpu().numpy()[:k], mm_ref) < 1e-5
+    assert rel_err(from_nhwc(yb, k), ops.relu_fwd(y_ref)) < TOL[dtype]
