@@ -117,3 +117,7 @@ __device__ __forceinline__ float quant_value(float v, float t, float qmax, int c
   if (clip) v = fminf(fmaxf(v, -t), t);
   return unit > 0.f ? roundf(v / unit) * unit : 0.f;
 }
+
+// ------------------------------------------------------------------ tuning knobs (rn_set_tuning)
+enum { RN_TUNE_WGRAD_DMA = 0, RN_TUNE_IGEMM_DMA = 1, RN_TUNE_COUNT = 8 };
+extern int g_tune[RN_TUNE_COUNT];

@@ -313,9 +313,17 @@ __global__ void quant_bwd_kernel(int64_t n, const T* __restrict__ x, const T* __
 
 }  // namespace
 
+int g_tune[RN_TUNE_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0};
+
 extern "C" {
 
 const char* rn_last_error(void) { return g_last_error.c_str(); }
+
+int rn_set_tuning(int32_t key, int32_t value) {
+  RN_CHECK_ARG(key >= 0 && key < RN_TUNE_COUNT, "bad tuning key");
+  g_tune[key] = value;
+  return 0;
+}
 int32_t rn_version(void) { return 100; }
 int32_t rn_device_cu_count(void) {
   int dev = 0;

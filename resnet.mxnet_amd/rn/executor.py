@@ -491,7 +491,11 @@ class Executor:
         self.lib = L.load()
         # device='cpu' builds the full call plan without launching anything (CPU dry-run tests)
         self.dry_run = self.device.type == "cpu"
-        self.stream = None if self.dry_run else torch.cuda.current_stream(self.device)
+        # every bound call shares ONE c_void_p stream argument, re-pointed at torch's current stream
+        # whenever a call list runs: the plan then follows the caller's stream -- torch ops, RCCL
+        # ordering and HIP-graph capture (torch.cuda.graph) all see the same stream
+        self._spv = L.C.c_void_p(0)
+        self._sync_stream()
         self._acts = {}
         self._grads = {}
         self._fwd_train, self._fwd_infer, self._bwd = [], [], []
@@ -631,7 +635,15 @@ class Executor:
             self._bwd.append(item)
 
     def _sp(self):
-        return L.C.c_void_p(0 if self.stream is None else self.stream.cuda_stream)
+        return self._spv
+
+    @property
+    def stream(self):
+        return None if self.dry_run else self.torch.cuda.current_stream(self.device)
+
+    def _sync_stream(self):
+        if not self.dry_run:
+            self._spv.value = self.torch.cuda.current_stream(self.device).cuda_stream
 
     def _conv_desc(self, n, h, w, c, c_real, k, kernel, stride, pad, groups=1):
         d = L.ConvDesc(dtype=self.dtype, n=n, h=h, w=w, c=c, c_real=c_real, k=k, k_pad=_pad8(k), r=kernel[0],
@@ -957,11 +969,13 @@ class Executor:
                     self.act(tt).copy_(lsrc.reshape(-1).to(torch.float32), non_blocking=True)
 
     def forward(self, is_train=True):
+        self._sync_stream()
         self._run(self._fwd_train if is_train else self._fwd_infer)
         if is_train:
             self._qfirst.value = 0
 
     def backward(self, hooks=None):
+        self._sync_stream()
         self.grad.zero_()
         if not hooks:
             self._run(self._bwd)
@@ -977,9 +991,11 @@ class Executor:
                 h()
 
     def repack_weights(self):
+        self._sync_stream()
         self._run(self.wpack_calls)
 
     def sgd_update(self, lr, wd, momentum, rescale_grad, clip=-1.0):
+        self._sync_stream()
         if self._wd_value != wd:
             self.opt_wds.copy_(self.torch.from_numpy(self.wd_mult * np.float32(wd)))
             self._wd_value = wd

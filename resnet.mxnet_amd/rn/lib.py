@@ -67,6 +67,7 @@ SIGNATURES = {
     "rn_relu_bwd": (_i32, [_i64, _i32, _P, _P, _P, _P, _P]),
     "rn_quant_int8_fwd": (_i32, [_i32, _i64, _P, _P, _P, _i32, _i32, _f32, _i32, _i32, _P, _P]),
     "rn_quant_int8_bwd": (_i32, [_i32, _i64, _P, _P, _P, _P, _i32, _P, _P]),
+    "rn_set_tuning": (_i32, [_i32, _i32]),
     "rn_last_error": (C.c_char_p, []),
     "rn_version": (_i32, []),
     "rn_device_cu_count": (_i32, []),
@@ -95,6 +96,10 @@ def load(auto_build=True):
         fn.restype = res
         fn.argtypes = args
     _lib = lib
+    # RN_TUNE="key=value,..." selects kernel variants (rn_set_tuning; A/B measurements)
+    for kv in filter(None, os.environ.get("RN_TUNE", "").split(",")):
+        k, v = kv.split("=")
+        check(lib.rn_set_tuning(int(k), int(v)), "rn_set_tuning")
     return lib
 
 

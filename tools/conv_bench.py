@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="fwd,dgrad,wgrad")
     ap.add_argument("--filter", default="")
+    ap.add_argument("--cold", action="store_true", help="evict L2/MALL (write 512 MB) before every timed call")
     a = ap.parse_args()
     import torch
     from rn import graphs
@@ -39,6 +40,7 @@ def main():
             shapes[key] = [op.name, 0]
         shapes[key][1] += 1
     dev = torch.device("cuda:0")
+    flush = torch.empty(128 << 20, dtype=torch.float32, device=dev) if a.cold else None
     st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     modes = a.only.split(",")
     tot = {m: 0.0 for m in modes}
@@ -73,13 +75,26 @@ def main():
             fn = calls[m]
             for _ in range(3):
                 L.check(fn(), m)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(a.iters):
-                fn()
-            e1.record()
-            torch.cuda.synchronize()
-            ms = e0.elapsed_time(e1) / a.iters
+            if flush is None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    fn()
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / a.iters
+            else:
+                evs = []
+                for _ in range(a.iters):
+                    flush.fill_(1.0)
+                    dw.zero_()
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    fn()
+                    e1.record()
+                    evs.append((e0, e1))
+                torch.cuda.synchronize()
+                ms = sum(x.elapsed_time(y) for x, y in evs) / a.iters
             tot[m] += ms * cnt
             row += "%8.1fus %6.0fT" % (ms * 1e3, flops / ms / 1e9)
         flops_tot += flops * cnt
