@@ -1018,7 +1018,10 @@ int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, flo
   a.M = d->n * d->p * d->q;
   a.fdQ = make_fastdiv(d->q); a.fdPQ = make_fastdiv(d->p * d->q);
   a.fdC = make_fastdiv(a.cblk); a.fdS = make_fastdiv(d->s);
-  const int bmk = grouped ? RN_GROUP_BLOCK : 128, bnc = grouped ? RN_GROUP_BLOCK : 128;
+  // 64-wide tiles where K or the column count is <= 64 (stage-1 layers): a 128 tile would spend
+  // half (or three quarters) of its MFMAs on zero rows / columns
+  const int bmk = (grouped || a.K <= 64) ? 64 : 128;
+  const int bnc = (grouped || a.ncol_load <= 64) ? 64 : 128;
   const int tiles = (int)(ceil_div(a.ncol_load, bnc) * ceil_div(a.K, bmk));
   const int bkm = d->dtype == RN_BF16 ? 64 : 32;
   const int64_t mstages = ceil_div(a.M, bkm);
@@ -1039,9 +1042,15 @@ int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, flo
     else
       hipLaunchKernelGGL((wgrad_kernel<float, RN_GROUP_BLOCK, RN_GROUP_BLOCK>), grid, dim3(256), 0, st, a);
   } else if (d->dtype == RN_BF16) {
-    hipLaunchKernelGGL((wgrad_kernel<bf16_t, 128, 128>), grid, dim3(256), 0, st, a);
+    if (bmk == 64 && bnc == 64) hipLaunchKernelGGL((wgrad_kernel<bf16_t, 64, 64>), grid, dim3(256), 0, st, a);
+    else if (bmk == 64) hipLaunchKernelGGL((wgrad_kernel<bf16_t, 64, 128>), grid, dim3(256), 0, st, a);
+    else if (bnc == 64) hipLaunchKernelGGL((wgrad_kernel<bf16_t, 128, 64>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_kernel<bf16_t, 128, 128>), grid, dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL((wgrad_kernel<float, 128, 128>), grid, dim3(256), 0, st, a);
+    if (bmk == 64 && bnc == 64) hipLaunchKernelGGL((wgrad_kernel<float, 64, 64>), grid, dim3(256), 0, st, a);
+    else if (bmk == 64) hipLaunchKernelGGL((wgrad_kernel<float, 64, 128>), grid, dim3(256), 0, st, a);
+    else if (bnc == 64) hipLaunchKernelGGL((wgrad_kernel<float, 128, 64>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_kernel<float, 128, 128>), grid, dim3(256), 0, st, a);
   }
   return rn_check_launch("wgrad");
 }
