@@ -146,6 +146,15 @@ int rn_bn_fwd_train(const rn_bn_desc* d, const void* x, void* y, const float* ga
                     float* save_invstd, float* scale, float* shift, void* ws, rn_stream_t stream);
 
 /* Inference forward with moving statistics (use_global_stats / is_train=False). */
+/* Stem input: conv0 reads bn_data(data) (symbol/resnet.py:90-93, fix_gamma BatchNorm over the
+ * NCHW fp32 batch). Writes the NHWC-8 compute copy out[n*h*w][8] (d->dtype; channels >= c are 0)
+ * of the normalised input. mode 0: batch statistics (training; moving stats updated, save_* and
+ * scale/shift written); 1: moving statistics (inference / use_global_stats); 2: no BatchNorm.
+ * d: dtype, m = n*h*w, c = 8, c_real = c, eps, momentum, fix_gamma. ws: 2*c*256 floats. */
+int rn_stem_prepare(const rn_bn_desc* d, const float* x_nchw, int32_t n, int32_t c, int32_t h, int32_t w, void* out,
+                    int32_t mode, const float* gamma, const float* beta, float* moving_mean, float* moving_var,
+                    float* save_mean, float* save_invstd, float* scale, float* shift, void* ws, rn_stream_t stream);
+
 /* rn_bn_fwd_train with the batch statistics already reduced per row block by the producer
  * (rn_conv_fwd_bnstats): fp64 merge of part[nblk][3][ld] -> coefficients, moving stats, then
  * y = bn(x) (+relu) when y != NULL. ws: rn_bn_workspace_bytes(d) (rows_blk = 128). */

@@ -231,6 +231,87 @@ __global__ __launch_bounds__(64) void bn_fwd_finalize_part_kernel(const double* 
   }
 }
 
+// ---- stem input (bn_data over the NCHW fp32 `data`, symbol/resnet.py:90): statistics straight from
+// the NCHW planes, then one pass writing the normalised NHWC-8 compute copy for conv0.
+// part[b][c][2]: shifted sums over images [b*ipb, (b+1)*ipb) of channel c, pivot x[0][c][0][0].
+__global__ __launch_bounds__(256) void stem_stats_kernel(const float* __restrict__ x, int n, int c, int hw, int ipb,
+                                                         float* __restrict__ part) {
+  const int ch = blockIdx.x;
+  const int b = blockIdx.y;
+  const float piv = x[(int64_t)ch * hw];
+  float s = 0.f, q = 0.f;
+  for (int img = b * ipb; img < min(n, (b + 1) * ipb); ++img) {
+    const float4* pl = reinterpret_cast<const float4*>(x + ((int64_t)img * c + ch) * hw);
+    for (int i = threadIdx.x; i < hw / 4; i += blockDim.x) {
+      const float4 v = pl[i];
+      const float d0 = v.x - piv, d1 = v.y - piv, d2 = v.z - piv, d3 = v.w - piv;
+      s += (d0 + d1) + (d2 + d3);
+      q = fmaf(d0, d0, fmaf(d1, d1, fmaf(d2, d2, fmaf(d3, d3, q))));
+    }
+  }
+  double sd = s, qd = q;
+  block_sum2(sd, qd);
+  if (threadIdx.x == 0) {
+    part[((int64_t)b * c + ch) * 2] = (float)sd;
+    part[((int64_t)b * c + ch) * 2 + 1] = (float)qd;
+  }
+}
+
+__global__ __launch_bounds__(256) void stem_finalize_kernel(const float* __restrict__ x, const float* __restrict__ part,
+                                                            int nb, int64_t m, int c, int hw, float eps,
+                                                            float momentum, int fix_gamma, const float* gamma,
+                                                            const float* beta, float* moving_mean, float* moving_var,
+                                                            float* save_mean, float* save_invstd, float* scale,
+                                                            float* shift) {
+  const int ch = blockIdx.x;
+  double s = 0.0, q = 0.0;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) {
+    s += part[((int64_t)b * c + ch) * 2];
+    q += part[((int64_t)b * c + ch) * 2 + 1];
+  }
+  block_sum2(s, q);
+  if (threadIdx.x != 0) return;
+  const double md = s / (double)m;
+  const double mean = (double)x[(int64_t)ch * hw] + md;
+  double var = q / (double)m - md * md;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = fix_gamma ? 1.f : gamma[ch];
+  scale[ch] = g * invstd;
+  shift[ch] = beta[ch] - (float)mean * g * invstd;
+  save_mean[ch] = (float)mean;
+  save_invstd[ch] = invstd;
+  if (moving_mean) {
+    moving_mean[ch] = moving_mean[ch] * momentum + (float)mean * (1.f - momentum);
+    moving_var[ch] = moving_var[ch] * momentum + (float)var * (1.f - momentum);
+  }
+}
+
+// thread per pixel: NCHW fp32 (c <= 8 channels) -> one 8-channel NHWC chunk, affine applied
+template <typename T>
+__global__ __launch_bounds__(256) void stem_to_nhwc8_kernel(const float* __restrict__ x, int64_t npix, int c, int hw,
+                                                            const float* __restrict__ scale,
+                                                            const float* __restrict__ shift, T* __restrict__ out) {
+  constexpr int CE = 16 / sizeof(T);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < npix; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t img = i / hw;
+    const int64_t pix = i - img * hw;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float f = 0.f;
+      if (e < c) {
+        f = x[(img * c + e) * hw + pix];
+        if (scale) f = fmaf(f, scale[e], shift[e]);
+      }
+      v[e] = f;
+    }
+#pragma unroll
+    for (int h = 0; h < 8 / CE; ++h)
+      reinterpret_cast<uint4*>(out + i * 8)[h] = f_to_chunk(v + h * CE, (const T*)nullptr);
+  }
+}
+
 __global__ void bn_infer_coef_kernel(int c, int c_real, float eps, int fix_gamma, const float* gamma,
                                      const float* beta, const float* mm, const float* mv, float* scale,
                                      float* shift) {
@@ -536,6 +617,42 @@ int rn_bn_fwd_train_part(const rn_bn_desc* d, const float* part, int64_t nblk, i
   RN_CHECK_ARG(x != nullptr, "null x");
   if (d->dtype == RN_BF16) return bn_apply_t<bf16_t>(d, x, y, scale, shift, st);
   return bn_apply_t<float>(d, x, y, scale, shift, st);
+}
+
+int rn_stem_prepare(const rn_bn_desc* d, const float* x, int32_t n, int32_t c, int32_t h, int32_t w, void* out,
+                    int32_t mode, const float* gamma, const float* beta, float* moving_mean, float* moving_var,
+                    float* save_mean, float* save_invstd, float* scale, float* shift, void* ws, rn_stream_t stream) {
+  RN_CHECK_ARG(d && x && out && c >= 1 && c <= 8 && n > 0 && h > 0 && w > 0, "bad arguments");
+  RN_CHECK_ARG(d->c == 8 && d->c_real == c && d->m == (int64_t)n * h * w, "desc must describe the NHWC-8 copy");
+  RN_CHECK_ARG(mode == 2 || (beta && scale && shift), "affine outputs required");
+  const int hw = h * w;
+  RN_CHECK_ARG(hw % 4 == 0, "h*w must be a multiple of 4");
+  hipStream_t st = as_stream(stream);
+  if (mode == 0) {
+    RN_CHECK_ARG(ws && save_mean && save_invstd && (d->fix_gamma || gamma), "null argument");
+    const int nb = std::min(n, 256);
+    const int ipb = (n + nb - 1) / nb;
+    const int nbe = (n + ipb - 1) / ipb;
+    float* part = reinterpret_cast<float*>(ws);
+    hipLaunchKernelGGL(stem_stats_kernel, dim3(c, nbe), dim3(256), 0, st, x, n, c, hw, ipb, part);
+    hipLaunchKernelGGL(stem_finalize_kernel, dim3(c), dim3(256), 0, st, x, part, nbe, d->m, c, hw, d->eps, d->momentum,
+                       d->fix_gamma, gamma, beta, moving_mean, moving_var, save_mean, save_invstd, scale, shift);
+  } else if (mode == 1) {
+    RN_CHECK_ARG(moving_mean && moving_var && (d->fix_gamma || gamma), "null argument");
+    hipLaunchKernelGGL(bn_infer_coef_kernel, dim3(1), dim3(64), 0, st, c, c, d->eps, d->fix_gamma, gamma, beta,
+                       moving_mean, moving_var, scale, shift);
+  }
+  const float* sc = mode == 2 ? nullptr : scale;
+  const float* sh = mode == 2 ? nullptr : shift;
+  const int64_t npix = (int64_t)n * hw;
+  const int grid = (int)std::min<int64_t>((npix + 255) / 256, 65536);
+  if (d->dtype == RN_BF16)
+    hipLaunchKernelGGL(stem_to_nhwc8_kernel<bf16_t>, dim3(grid), dim3(256), 0, st, x, npix, c, hw, sc, sh,
+                       (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(stem_to_nhwc8_kernel<float>, dim3(grid), dim3(256), 0, st, x, npix, c, hw, sc, sh,
+                       (float*)out);
+  return rn_check_launch("stem_prepare");
 }
 
 int rn_bn_fwd_infer(const rn_bn_desc* d, const void* x, void* y, const float* gamma, const float* beta,

@@ -51,6 +51,8 @@ struct IgemmArgs {
   int cblk;            // reduction channels per column block (dense: C)
   float* stats;        // fwd only, nullable: per-block BatchNorm partials [m tiles][3][ldo]
   int ntn;             // n tiles (grid = m tiles * ntn)
+  int smallc, lgc, rs; // fwd over C < one stage (the stem's 8 channels): k = tap*C + c flattened
+  FastDiv fdS;
   int ncls;
   IgemmCls cls[4];
 };
@@ -187,7 +189,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
   }
 
   const int ncb = (p.cblk + BKE - 1) / BKE;
-  const int nstage = cl.nr * cl.ns * ncb;
+  const int nstage = p.smallc ? (p.rs * p.C + BKE - 1) / BKE : cl.nr * cl.ns * ncb;
 
   // register-staged loads: stage t+1 is loaded while stage t is computed, then written to
   // the other LDS buffer (async-STAGE split: write after the MFMA phase).
@@ -195,20 +197,35 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
   int st_tr = 0, st_ts = 0, st_cb = 0;  // next stage to load
 
   auto load_stage = [&](uint4* ra, uint4* rb) {
-    const int tr = st_tr, ts = st_ts, cb = st_cb;
-    if (++st_cb == ncb) {
-      st_cb = 0;
-      if (++st_ts == cl.ns) {
-        st_ts = 0;
-        ++st_tr;
+    int hoff, woff, c, toff;
+    bool cok;
+    if (p.smallc) {
+      // several taps per stage: this thread's chunk is k = tap*C + c of the flattened reduction
+      const int k0 = st_cb * BKE + ch * CE;
+      ++st_cb;
+      const int tap = k0 >> p.lgc;
+      c = k0 & (p.C - 1);
+      hoff = (int)fdiv((uint32_t)tap, p.fdS);
+      woff = tap - hoff * p.S;
+      cok = tap < p.rs;
+      toff = k0;
+    } else {
+      const int tr = st_tr, ts = st_ts, cb = st_cb;
+      if (++st_cb == ncb) {
+        st_cb = 0;
+        if (++st_ts == cl.ns) {
+          st_ts = 0;
+          ++st_tr;
+        }
       }
+      const int r = cl.r0 + p.rstep * tr;
+      const int s = cl.s0 + p.sstep * ts;
+      hoff = cl.hoff0 + p.hinc * tr;
+      woff = cl.woff0 + p.winc * ts;
+      c = cb * BKE + ch * CE;
+      cok = c < p.cblk && cbase + c < p.C;  // a grouped block may run past the last group
+      toff = (r * p.S + s) * p.cblk + c;
     }
-    const int r = cl.r0 + p.rstep * tr;
-    const int s = cl.s0 + p.sstep * ts;
-    const int hoff = cl.hoff0 + p.hinc * tr;
-    const int woff = cl.woff0 + p.winc * ts;
-    const int c = cb * BKE + ch * CE;
-    const bool cok = c < p.cblk && cbase + c < p.C;  // a grouped block may run past the last group
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int hin = a_hb[i] + hoff;
@@ -221,7 +238,6 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
         ra[i] = make_uint4(0, 0, 0, 0);
       }
     }
-    const int toff = (r * p.S + s) * p.cblk + c;
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       if (cok && b_ok[i]) rb[i] = *reinterpret_cast<const uint4*>(wg + b_off[i] + toff);
@@ -391,6 +407,7 @@ struct WgradArgs {
   int M;
   int m_per_split;
   int grouped, gk, gc, cblk;  // grouped: rows / channels per group, channels per row block
+  int creal;                  // logical input channels (< C: padded stride, dw keeps c < creal)
   int nct, nkt;               // column tiles, k tiles (grid = splits * nkt * nct)
   FastDiv fdQ, fdPQ, fdC, fdS;  // fdC divides by cblk (dense: C)
 };
@@ -593,8 +610,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int col = n0 + wn * (BNC / 2) + j * 16 + (lane & 15);
-        if (!p.grouped) {
+        if (!p.grouped && p.creal == p.C) {
           if (col < p.ncol) atomicAdd(p.dw + (int64_t)k * p.ldw + col, acc[i][j][e]);
+        } else if (!p.grouped) {  // padded channels (the stem's 3 of 8): keep c < c_real
+          if (col < p.ncol_load) {
+            const int tap = fdiv(col, p.fdC);
+            const int c = col - tap * p.C;
+            if (c < p.creal) atomicAdd(p.dw + (int64_t)k * p.ldw + tap * p.creal + c, acc[i][j][e]);
+          }
         } else if (col < p.ncol_load) {  // keep the block-diagonal part: channel in k's group
           const int tap = fdiv(col, p.fdC);
           const int c = cbase + col - tap * p.cblk;
@@ -851,6 +874,13 @@ IgemmArgs make_igemm_args(const rn_conv_desc* d, int mode) {
       a.cblk = group_blk(a.gcol, a.gred);
       a.wrow = d->r * d->s * a.cblk;
     }
+    const int stage_elems = d->dtype == RN_BF16 ? 64 : 32;
+    if (d->groups == 1 && d->c < stage_elems && (d->c & (d->c - 1)) == 0 && d->r * d->s > 1) {
+      a.smallc = 1;
+      a.lgc = __builtin_ctz(d->c);
+      a.rs = d->r * d->s;
+      a.fdS = make_fastdiv(d->s);
+    }
     a.ncls = 1;
     IgemmCls& c = a.cls[0];
     c.a = 0; c.b = 0; c.Pc = d->p; c.Qc = d->q; c.r0 = 0; c.s0 = 0; c.nr = d->r; c.ns = d->s;
@@ -995,8 +1025,7 @@ int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, 
 int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, float* dw,
                        rn_stream_t stream) {
   RN_CHECK_ARG(d && x && dy && dw, "null argument");
-  RN_CHECK_ARG(d->r * d->s == 1 || d->c == d->c_real,
-               "wgrad of a padded-channel input needs the im2col (1x1) formulation");
+
   WgradArgs a{};
   a.x = x; a.dy = dy; a.dw = dw;
   a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.P = d->p; a.Q = d->q; a.K = d->k;
@@ -1006,6 +1035,7 @@ int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, flo
   a.ncol = d->r * d->s * d->c_real;
   a.ldw = a.ncol;
   a.cblk = d->c;
+  a.creal = d->c_real;
   const bool grouped = d->groups > 1;
   if (grouped) {
     a.grouped = 1;

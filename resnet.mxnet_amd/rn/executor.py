@@ -681,12 +681,12 @@ class Executor:
                              momentum=op.momentum, fix_gamma=int(op.fix_gamma), relu=int(op.relu))
                 ws_bytes = max(ws_bytes, self.lib.rn_bn_workspace_bytes(L.C.byref(d)))
                 op.desc = d
-            elif op.kind == "stem" and op.bn:
+            elif op.kind == "stem":
                 x = op.x
-                d = L.BNDesc(dtype=F32, m=x.n * x.h * x.w, c=8, c_real=x.c, eps=op.bn["eps"],
-                             momentum=op.bn["momentum"], fix_gamma=1, relu=0)
-                ws_bytes = max(ws_bytes, self.lib.rn_bn_workspace_bytes(L.C.byref(d)))
-                op.bn_desc = d
+                b = op.bn or {}
+                op.bn_desc = L.BNDesc(dtype=self.dtype, m=x.n * x.h * x.w, c=8, c_real=x.c, eps=b.get("eps", 1e-5),
+                                      momentum=b.get("momentum", 0.9), fix_gamma=1, relu=0)
+                ws_bytes = max(ws_bytes, 2 * 8 * 256 * 4 + 64)
         self.ws = self._zeros(ws_bytes // 4 + 16, self.torch.float32)
         wsp = self._p(self.ws)
         self.qws = self._zeros(4096, self.torch.float32)
@@ -696,51 +696,42 @@ class Executor:
             op.wsrc = self._weight_source(op, qwsp, sp) if getattr(op, "qweight", None) else \
                 (self._pp(op.weight) if getattr(op, "weight", None) else None)
             if op.kind == "stem":
+                # conv0 over the 3-channel input: bn_data statistics straight from the NCHW batch, one
+                # pass writing the normalised NHWC-8 copy, then the implicit GEMM in its small-C mode
+                # (k = tap*8 + c flattened; symbol/resnet.py:90-93)
                 x, y = op.x, op.y
-                d1 = self._conv_desc(x.n, y.h, y.w, op.kc, op.kernel[0] * op.kernel[1] * x.c, y.c, (1, 1), (1, 1),
-                                     (0, 0))
                 dfull = self._conv_desc(x.n, x.h, x.w, 8, x.c, y.c, op.kernel, op.stride, op.pad)
-                op.d1, op.dfull = d1, dfull
-                op.cols = self._zeros(x.n * y.h * y.w * op.kc, self.tdtype)
-                op.wk = self._zeros(y.c * op.kc, self.tdtype)
-                self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(d1), op.wsrc,
-                                             self._p(op.wk), None, sp))
+                assert (dfull.p, dfull.q) == (y.h, y.w), (op.name, dfull.p, dfull.q, y.h, y.w)
+                op.dfull = op.desc = dfull
+                op.x8 = self._zeros(x.n * x.h * x.w * 8, self.tdtype)
+                op.wk = self._zeros(y.c * op.kernel[0] * op.kernel[1] * 8, self.tdtype)
+                self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(dfull), op.wsrc, self._p(op.wk), None,
+                                             sp))
                 stem_ws = max(stem_ws, y.h * y.w * y.cp + y.h * op.kernel[1] * y.c + y.c * op.kernel[0] * op.kernel[1] + 64)
                 xnchw = self._p(self.act(x))
-                if op.bn:
-                    b = op.bn
-                    op.nhwc8 = self._zeros(x.n * x.h * x.w * 8, self.torch.float32)
-                    op.bnbuf = self._zeros(4 * 8, self.torch.float32)
-                    sm, si, sc, sh = [L.C.c_void_p(op.bnbuf.data_ptr() + 32 * i) for i in range(4)]
-                    op.bn_ptrs = (sm, si, sc, sh)
-                    F.append(self._call("rn_nchw_to_nhwc", x.n, x.c, x.h, x.w, 8, xnchw, self._p(op.nhwc8), F32, sp))
-                    if b["use_global_stats"]:
-                        F.append(self._call("rn_bn_fwd_infer", L.C.byref(op.bn_desc), self._p(op.nhwc8),
-                                            self._p(op.nhwc8), self._pp(b["gamma"]), self._pp(b["beta"]),
-                                            self._ap(b["mean"]), self._ap(b["var"]), sc, sh, sp))
-                    else:
-                        F.append(self._call("rn_bn_fwd_train", L.C.byref(op.bn_desc), self._p(op.nhwc8), None,
-                                            self._pp(b["gamma"]), self._pp(b["beta"]), self._ap(b["mean"]),
-                                            self._ap(b["var"]), sm, si, sc, sh, wsp, sp))
-                    I.append(self._call("rn_nchw_to_nhwc", x.n, x.c, x.h, x.w, 8, xnchw, self._p(op.nhwc8), F32, sp))
-                    I.append(self._call("rn_bn_fwd_infer", L.C.byref(op.bn_desc), self._p(op.nhwc8),
-                                        self._p(op.nhwc8), self._pp(b["gamma"]), self._pp(b["beta"]),
-                                        self._ap(b["mean"]), self._ap(b["var"]), sc, sh, sp))
+                op.bnbuf = self._zeros(4 * 8, self.torch.float32)
+                sm, si, sc, sh = [L.C.c_void_p(op.bnbuf.data_ptr() + 32 * i) for i in range(4)]
+                op.bn_ptrs = (sm, si, sc, sh)
+                b = op.bn
+                if b:
+                    bnargs = (self._pp(b["gamma"]), self._pp(b["beta"]), self._ap(b["mean"]), self._ap(b["var"]))
+                    mode_f = 1 if b["use_global_stats"] else 0
+                    mode_i = 1
                 else:
-                    sc = sh = None
+                    bnargs = (None, None, None, None)
+                    mode_f = mode_i = 2
+                for lst, mode in ((F, mode_f), (I, mode_i)):
+                    lst.append(self._call("rn_stem_prepare", L.C.byref(op.bn_desc), xnchw, x.n, x.c, x.h, x.w,
+                                          self._p(op.x8), mode, *bnargs, sm, si, sc, sh, wsp, sp))
                 if op.quant:
                     q = op.quant
                     for lst, tr in ((F, 1), (I, 0)):
-                        lst.append(self._call("rn_im2col_nchw_quant", L.C.byref(dfull), xnchw, sc, sh,
-                                              self._ap(q["minmax"]), tr, q["ema"], self._qfirst, q["nbits"], qwsp,
-                                              self._p(op.cols), op.kc, sp))
-                else:
-                    for lst in (F, I):
-                        lst.append(self._call("rn_im2col_nchw", L.C.byref(dfull), xnchw, sc, sh, self._p(op.cols),
-                                              op.kc, sp))
-                I.append(self._call("rn_conv_fwd", L.C.byref(d1), self._p(op.cols), self._p(op.wk),
+                        lst.append(self._call("rn_quant_int8_fwd", self.dtype, x.n * x.h * x.w * 8, self._p(op.x8),
+                                              self._p(op.x8), self._ap(q["minmax"]), 0, tr, q["ema"], self._qfirst,
+                                              q["nbits"], qwsp, sp))
+                I.append(self._call("rn_conv_fwd", L.C.byref(dfull), self._p(op.x8), self._p(op.wk),
                                     self._p(self.act(y)), self.dtype, None, None, sp))
-                F.append(self._conv_fwd_call(op, d1, self._p(op.cols), None, sp))
+                F.append(self._conv_fwd_call(op, dfull, self._p(op.x8), None, sp))
             elif op.kind == "conv":
                 x, y = op.x, op.y
                 d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad, op.groups)
@@ -893,7 +884,7 @@ class Executor:
                 if op.res is not None and op.res.needs_grad:
                     gs.alias(op.res, dy)
             elif op.kind == "stem":
-                self._bwd.append(self._call("rn_conv_bwd_filter", L.C.byref(op.d1), self._p(op.cols), self._p(dy),
+                self._bwd.append(self._call("rn_conv_bwd_filter", L.C.byref(op.dfull), self._p(op.x8), self._p(dy),
                                             self._gp(op.weight), sp))
                 self.param_done_at[op.weight] = len(self._bwd)
                 if op.bn:

@@ -67,19 +67,9 @@ def gpu_quant_values(ex):
             a = ex.act(t).float().cpu().numpy().reshape(t.n, t.h, t.w, t.cp)[..., :t.c].transpose(0, 3, 1, 2)
             vals[op.q["name"]] = a
         elif op.kind == "stem" and op.quant:
-            # rebuild the quantized stem input from its im2col matrix
-            x, y = op.x, op.y
-            r, s_ = op.kernel
-            (sh, sw), (ph, pw) = op.stride, op.pad
-            cols = op.cols.float().cpu().numpy().reshape(x.n, y.h, y.w, op.kc)
-            xq = np.zeros((x.n, x.c, x.h, x.w), np.float32)
-            for rr in range(r):
-                for ss in range(s_):
-                    hs = np.arange(y.h) * sh - ph + rr
-                    ws = np.arange(y.w) * sw - pw + ss
-                    hv, wv = (hs >= 0) & (hs < x.h), (ws >= 0) & (ws < x.w)
-                    blk = cols[:, hv][:, :, wv][..., (rr * s_ + ss) * x.c:(rr * s_ + ss + 1) * x.c]
-                    xq[:, :, hs[hv][:, None], ws[wv][None, :]] = blk.transpose(0, 3, 1, 2)
+            # the quantized stem input is the NHWC-8 compute copy conv0 reads
+            x = op.x
+            xq = op.x8.float().cpu().numpy().reshape(x.n, x.h, x.w, 8)[..., :x.c].transpose(0, 3, 1, 2)
             vals[op.quant["name"]] = xq
     return vals
 

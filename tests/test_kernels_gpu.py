@@ -462,3 +462,58 @@ def test_conv_bnstats_epilogue(gpu, dtype, case):
     assert rel_err(mv.cpu().numpy()[:k], mv_ref) < 1e-5
     assert rel_err(mm.cpu().numpy()[:k], mm_ref) < 1e-5
     assert rel_err(from_nhwc(yb, k), ops.relu_fwd(y_ref)) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_stem_prepare_and_smallc_conv(gpu, dtype, mode):
+    """conv0 path: bn_data (train / moving stats / none) over the NCHW batch -> NHWC-8 copy
+    (rn_stem_prepare), conv0 fwd in the implicit GEMM's small-C mode, conv0 wgrad over the padded
+    channels (symbol/resnet.py:90-93)."""
+    n, c, h, w, k, r, st, pd = 2, 3, 20, 16, 64, 7, 2, 3
+    rng = np.random.default_rng(17)
+    x = rng.uniform(-1, 1, (n, c, h, w)).astype(np.float32) * 2 + 0.5
+    gamma, beta = np.ones(c), rng.standard_normal(c) * 0.1
+    mm0, mv0 = rng.standard_normal(c) * 0.1, rng.uniform(0.5, 1.5, c)
+    if mode == 0:
+        xa, cache = ops.bn_train_fwd(x.astype(np.float64), gamma, beta, 2e-5, True)
+        mm_ref, mv_ref = ops.bn_moving_update(mm0, mv0, cache[3], cache[4], 0.9)
+    elif mode == 1:
+        xa = ops.bn_infer_fwd(x.astype(np.float64), gamma, beta, mm0, mv0, 2e-5, True)
+    else:
+        xa = x.astype(np.float64)
+    bd = L.BNDesc(dtype=dtype, m=n * h * w, c=8, c_real=c, eps=2e-5, momentum=0.9, fix_gamma=1, relu=0)
+    f = lambda a: torch.tensor(np.asarray(a, np.float32), device=gpu)
+    g_d, b_d, mm, mv = f(gamma), f(beta), f(mm0), f(mv0)
+    sm, si, sc, sh = [torch.zeros(8, dtype=torch.float32, device=gpu) for _ in range(4)]
+    ws = torch.zeros(4096 + 64, dtype=torch.float32, device=gpu)
+    x8 = torch.zeros(n * h * w * 8, dtype=tdt(dtype), device=gpu)
+    L.call("rn_stem_prepare", C.byref(bd), p(f(x)), n, c, h, w, p(x8), mode, p(g_d), p(b_d), p(mm), p(mv), p(sm),
+           p(si), p(sc), p(sh), p(ws), stream())
+    torch.cuda.synchronize()
+    got = x8.float().cpu().numpy().reshape(n, h, w, 8)
+    assert np.all(got[..., c:] == 0)
+    assert rel_err(got[..., :c].transpose(0, 3, 1, 2), xa) < (1e-5 if dtype == F32 else 8e-3)
+    if mode == 0:
+        assert rel_err(mm.cpu().numpy(), mm_ref) < 1e-5 and rel_err(mv.cpu().numpy(), mv_ref) < 1e-5
+    # conv0 on the NHWC-8 copy (small-C implicit GEMM) + wgrad over padded channels
+    xq = got[..., :c].transpose(0, 3, 1, 2).astype(np.float64)  # what the conv reads
+    wt = rng.standard_normal((k, c, r, r)) * 0.1
+    if dtype == BF16:
+        wt = bf16_round(wt)
+    d = conv_desc(dtype, n, 8, h, w, k, r, r, st, pd, c_real=c)
+    wk = torch.zeros(k * r * r * 8, dtype=tdt(dtype), device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), p(wk), None, stream())
+    y = torch.zeros((n, d.p, d.q, d.k_pad), dtype=tdt(dtype), device=gpu)
+    L.call("rn_conv_fwd", C.byref(d), p(x8), p(wk), p(y), dtype, None, None, stream())
+    dy = rng.standard_normal((n, k, d.p, d.q))
+    if dtype == BF16:
+        dy = bf16_round(dy)
+    dw = torch.zeros(k * r * r * c, dtype=torch.float32, device=gpu)
+    L.call("rn_conv_bwd_filter", C.byref(d), p(x8), p(to_nhwc(dy, dtype, gpu)), p(dw), stream())
+    torch.cuda.synchronize()
+    y_ref = ops.conv2d_fwd(xq, wt, (st, st), (pd, pd))
+    _, dw_ref = ops.conv2d_bwd(xq, wt, dy, (st, st), (pd, pd))
+    assert rel_err(from_nhwc(y, k), y_ref) < TOL[dtype]
+    assert rel_err(dw.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2), dw_ref) < \
+        (TOL[dtype] if dtype == F32 else 5e-3)
