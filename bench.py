@@ -177,6 +177,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=8)
     ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--host-input", action="store_true",
+                    help="feed the pinned host batch through Module.forward every step (PCIe-inclusive "
+                         "rate, the solver's own loop; not the headline value)")
     ap.add_argument("--graph", default="auto", choices=["auto", "0", "1"],
                     help="replay the captured step as one HIP graph (auto: on for a single GPU)")
     a = ap.parse_args()
@@ -215,8 +218,11 @@ def main():
     mod.forward(batch, is_train=True)  # H2D once: inputs resident from here on
     torch.cuda.synchronize()
 
+    pinned = mx.io.DataBatch(data=[mx.nd.array(data, ctx=mx.Context("cpu_pinned", 0))],
+                             label=[mx.nd.array(label, ctx=mx.Context("cpu_pinned", 0))])
+
     def step():
-        mod.forward(None, is_train=True)
+        mod.forward(pinned if a.host_input else None, is_train=True)
         mod.backward()
         mod.update()
 
@@ -226,7 +232,7 @@ def main():
     fams = calibrate_families(torch, ex, mod)
     dom = max(fams, key=lambda f: fams[f][0])
     timer = FamilyTimer(torch, ex, dom)
-    use_graph = a.graph == "1" or (a.graph == "auto" and world == 1)
+    use_graph = a.graph == "1" or (a.graph == "auto" and world == 1 and not a.host_input)
     graph = None
     if use_graph:
         # the whole training step (forward, backward, SGD, weight repack) as ONE HIP graph:
@@ -297,6 +303,8 @@ def main():
                          "families_ms_per_step": {f: round(v[0], 3) for f, v in fams.items()}},
             "outputs_finite": finite,
             "hip_graph": bool(use_graph),
+            "inputs": "pinned host batch copied every step (PCIe-inclusive)" if a.host_input else
+                      "resident in HBM",
         }
         if world == 1 and not a.no_cpu_baseline:
             try:

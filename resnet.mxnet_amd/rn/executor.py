@@ -607,6 +607,14 @@ class Executor:
     def _alloc_acts(self):
         for t in self.plan.tensors.values():
             self.act(t)
+        # input pipeline (data/imagenet.py SyntheticDataIter hands pinned host batches): two device
+        # buffers; the stem reads whichever _in_ptr points at
+        t = self.plan.data_tensor
+        self._in_bufs = [self.act(t), None]
+        self._in_free = [None, None]
+        self._in_idx = 0
+        self._in_ptr = L.C.c_void_p(self._in_bufs[0].data_ptr())
+        self._copy_stream = None
         self.stats = self._zeros(4, self.torch.float32)
 
     # ------------------------------------------------------------------ helpers
@@ -708,7 +716,7 @@ class Executor:
                 self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(dfull), op.wsrc, self._p(op.wk), None,
                                              sp))
                 stem_ws = max(stem_ws, y.h * y.w * y.cp + y.h * op.kernel[1] * y.c + y.c * op.kernel[0] * op.kernel[1] + 64)
-                xnchw = self._p(self.act(x))
+                xnchw = self._in_ptr  # the current input buffer (double-buffered H2D pipeline)
                 op.bnbuf = self._zeros(4 * 8, self.torch.float32)
                 sm, si, sc, sh = [L.C.c_void_p(op.bnbuf.data_ptr() + 32 * i) for i in range(4)]
                 op.bn_ptrs = (sm, si, sc, sh)
@@ -893,7 +901,7 @@ class Executor:
                     if op.quant:
                         _, _, sc, sh = op.bn_ptrs
                         self._bwd.append(self._call("rn_stem_quant_clip_grad", L.C.byref(op.dfull),
-                                                    self._p(self.act(op.x)), sc, sh, self._ap(op.quant["minmax"]),
+                                                    self._in_ptr, sc, sh, self._ap(op.quant["minmax"]),
                                                     self._p(dy), op.wsrc, self._gp(op.bn["beta"]), sp))
                     self.param_done_at[op.bn["beta"]] = len(self._bwd)
                     self.param_done_at[op.bn["gamma"]] = len(self._bwd)
@@ -945,13 +953,36 @@ class Executor:
                 raise L.RNError("%s: %s" % (name, self.lib.rn_last_error().decode()))
 
     def set_input(self, data_np, label_np=None):
-        """H2D copy of one batch (host numpy / torch) into the data/label buffers."""
+        """H2D copy of one batch (host numpy / torch) into the data/label buffers.
+
+        A pinned host batch (mx.nd.array(..., ctx=cpu_pinned), data/imagenet.py:17-18) is copied
+        asynchronously on a separate copy stream into the buffer the previous step is NOT using;
+        the compute stream waits only for that copy. Because the host enqueues a whole step ahead of
+        the GPU, step t+1's PCIe transfer overlaps step t's backward."""
         torch = self.torch
         t = self.plan.data_tensor
-        dst = self.act(t)
         src = torch.as_tensor(np.ascontiguousarray(data_np, dtype=np.float32)) if isinstance(data_np, np.ndarray) \
             else data_np
-        dst.copy_(src.reshape(-1).to(torch.float32), non_blocking=True)
+        src = src.reshape(-1)
+        if src.dtype != torch.float32:
+            src = src.to(torch.float32)
+        if not self.dry_run and src.device.type == "cpu" and src.is_pinned():
+            i = self._in_idx ^ 1
+            if self._in_bufs[i] is None:
+                self._in_bufs[i] = self._zeros(t.numel, torch.float32)
+                self._copy_stream = torch.cuda.Stream(self.device)
+            cs = self._copy_stream
+            if self._in_free[i] is not None:
+                cs.wait_event(self._in_free[i])  # the step that last read this buffer has finished
+            with torch.cuda.stream(cs):
+                self._in_bufs[i].copy_(src, non_blocking=True)
+                done = torch.cuda.Event()
+                done.record(cs)
+            torch.cuda.current_stream(self.device).wait_event(done)
+            self._in_idx = i
+            self._in_ptr.value = self._in_bufs[i].data_ptr()
+        else:
+            self._in_bufs[self._in_idx].copy_(src, non_blocking=True)
         if label_np is not None:
             for tt in self.plan.tensors.values():
                 if tt.kind == "label":
@@ -959,17 +990,25 @@ class Executor:
                         if isinstance(label_np, np.ndarray) else label_np
                     self.act(tt).copy_(lsrc.reshape(-1).to(torch.float32), non_blocking=True)
 
+    def _mark_input_read(self):
+        if not self.dry_run and self._in_bufs[1] is not None:
+            ev = self.torch.cuda.Event()
+            ev.record(self.torch.cuda.current_stream(self.device))
+            self._in_free[self._in_idx] = ev
+
     def forward(self, is_train=True):
         self._sync_stream()
         self._run(self._fwd_train if is_train else self._fwd_infer)
         if is_train:
             self._qfirst.value = 0
+        self._mark_input_read()
 
     def backward(self, hooks=None):
         self._sync_stream()
         self.grad.zero_()
         if not hooks:
             self._run(self._bwd)
+            self._mark_input_read()
             return
         # hooks: {bwd index -> callable}, e.g. RCCL bucket all-reduce launches
         calls = self._bwd
@@ -980,6 +1019,7 @@ class Executor:
             h = hooks.get(i + 1)
             if h is not None:
                 h()
+        self._mark_input_read()
 
     def repack_weights(self):
         self._sync_stream()
