@@ -165,6 +165,26 @@ def cpu_baseline(batch=8, steps=2, image=224):
                       "after 1 warm-up (%.1f s)" % (batch, image, image, steps, dt)}
 
 
+def cpu_baseline_c1(batch=128, steps=3):
+    """BASELINE.json configs[0]: ResNet-20 CIFAR-10 32x32, batch 128 -- the reference's own CPU case --
+    as the numpy fp32 oracle step on the host cores."""
+    import numpy as np
+    from oracle import net as onet
+    g = onet.resnet20_cifar()
+    args, aux = onet.init_params(g, dtype=np.float32)
+    moms = {k: np.zeros_like(v) for k, v in args.items()}
+    data, label = onet.synthetic_batch(batch, (3, 32, 32), 10, dtype=np.float32)
+    onet.train_step(g, args, aux, moms, data, label, 0.1)
+    t0 = time.time()
+    for _ in range(steps):
+        onet.train_step(g, args, aux, moms, data, label, 0.1)
+    dt = time.time() - t0
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    return {"value": round(batch * steps / dt, 3), "unit": "images/sec", "cores": cores, "kind": "port",
+            "sample": "numpy fp32 oracle ResNet-20 CIFAR-10 train step, batch %d at 32x32, %d timed steps (%.1f s)"
+                      % (batch, steps, dt)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -309,6 +329,7 @@ def main():
         if world == 1 and not a.no_cpu_baseline:
             try:
                 out["cpu_baseline"] = cpu_baseline(a.cpu_batch, a.cpu_steps)
+                out["cpu_baseline_c1"] = cpu_baseline_c1()
             except Exception as e:  # baseline must not hide the GPU number
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)

@@ -1055,8 +1055,12 @@ int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, flo
   const int tiles = (int)(ceil_div(a.ncol_load, bnc) * ceil_div(a.K, bmk));
   const int bkm = d->dtype == RN_BF16 ? 64 : 32;
   const int64_t mstages = ceil_div(a.M, bkm);
-  // split M so that the grid covers ~4 blocks per CU, with >= 8 stages per block
-  int64_t want = std::max<int64_t>(1, (4 * 256 + tiles - 1) / tiles);
+  // split M so that the whole grid is ONE round of resident blocks (floor: a partly filled second
+  // round of long blocks is the worst tail), with >= 8 stages per block. Resident blocks per CU
+  // of each tile variant (VGPR / LDS bound): 128x128 -> 2, 64x128 / 128x64 -> 3, 64x64 -> 5.
+  int per_cu = (bmk == 128 && bnc == 128) ? 2 : (bmk == 64 && bnc == 64) ? 5 : 3;
+  if (g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU] > 0) per_cu = g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU];
+  int64_t want = std::max<int64_t>(1, (int64_t)per_cu * 256 / tiles);
   int64_t maxsplit = std::max<int64_t>(1, mstages / 8);
   int64_t split = std::min(want, maxsplit);
   int64_t stages_per = ceil_div(mstages, split);
