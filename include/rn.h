@@ -67,6 +67,14 @@ int rn_conv_fwd_bnstats(const rn_conv_desc* d, const void* x, const void* w_krsc
                         const void* add_src, const float* bias, float* part, rn_stream_t stream);
 int64_t rn_conv_bnstats_blocks(const rn_conv_desc* d);
 
+/* rn_conv_fwd whose input is the PRE-BatchNorm tensor of a BatchNorm+ReLU (pre-activation
+ * units, symbol/resnet.py:17-31): the kernel stages max(x*in_scale[c] + in_shift[c], 0) (the
+ * coefficients rn_bn_fwd_train / rn_bn_fwd_infer computed), so the BN+ReLU output is never
+ * written. in_scale/in_shift nullable (plain conv); part: as rn_conv_fwd_bnstats, nullable. */
+int rn_conv_fwd_x(const rn_conv_desc* d, const void* x, const void* w_krsc, void* y, int32_t y_dtype,
+                  const void* add_src, const float* bias, const float* in_scale, const float* in_shift,
+                  float* part, rn_stream_t stream);
+
 /* dx = conv_transpose(dy, w) (+ add_src). w_crsk is the CRSK re-layout made by
  * rn_conv_weight_pack (row count c, K stride k_pad). */
 int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
@@ -76,6 +84,10 @@ int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, 
  * Accumulates with fp32 atomics: the caller zeroes dw once per step. */
 int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, float* dw,
                        rn_stream_t stream);
+
+/* rn_conv_bwd_filter over the same BN+ReLU-on-load input as rn_conv_fwd_x. */
+int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, float* dw, const float* in_scale,
+                         const float* in_shift, rn_stream_t stream);
 
 /* Number of fp32 elements of the master weight (K x R x S x c_real/groups, KRSC). */
 int64_t rn_conv_weight_numel(const rn_conv_desc* d);

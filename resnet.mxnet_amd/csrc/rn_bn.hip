@@ -659,11 +659,13 @@ int rn_bn_fwd_infer(const rn_bn_desc* d, const void* x, void* y, const float* ga
                     const float* moving_mean, const float* moving_var, float* scale, float* shift,
                     rn_stream_t stream) {
   if (check_bn(d)) return -1;
-  RN_CHECK_ARG(x && y && beta && moving_mean && moving_var && scale && shift, "null argument");
+  RN_CHECK_ARG(beta && moving_mean && moving_var && scale && shift, "null argument");
   RN_CHECK_ARG(d->fix_gamma || gamma, "gamma required unless fix_gamma");
   hipStream_t st = as_stream(stream);
   hipLaunchKernelGGL(bn_infer_coef_kernel, dim3((d->c + 255) / 256), dim3(256), 0, st, d->c, d->c_real, d->eps,
                      d->fix_gamma, gamma, beta, moving_mean, moving_var, scale, shift);
+  if (!y) return rn_check_launch("bn_fwd_infer");  // coefficients only (consumer applies them)
+  RN_CHECK_ARG(x != nullptr, "null x");
   if (d->dtype == RN_BF16) return bn_apply_t<bf16_t>(d, x, y, scale, shift, st);
   return bn_apply_t<float>(d, x, y, scale, shift, st);
 }

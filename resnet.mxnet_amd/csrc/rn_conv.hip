@@ -50,6 +50,8 @@ struct IgemmArgs {
   int gcol, gred;      // grouped: output columns / reduction channels per group (dense: 2^30, 0)
   int cblk;            // reduction channels per column block (dense: C)
   float* stats;        // fwd only, nullable: per-block BatchNorm partials [m tiles][3][ldo]
+  const float* in_sc;  // fwd only, nullable: BN+ReLU applied to the gathered input while staging
+  const float* in_sh;
   int ntn;             // n tiles (grid = m tiles * ntn)
   int smallc, lgc, rs; // fwd over C < one stage (the stem's 8 channels): k = tap*C + c flattened
   FastDiv fdS;
@@ -58,6 +60,25 @@ struct IgemmArgs {
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ (row & 7); }
+
+// BatchNorm-apply + ReLU of the consumer's input, applied while staging (the BN+ReLU output of
+// pre-activation units feeding 1x1 convs is never written to HBM): v = max(x*sc[c] + sh[c], 0)
+// over one 16-byte chunk of channels c..c+CE-1.
+template <typename T>
+__device__ __forceinline__ uint4 bnrelu_chunk(const uint4& u, const float* __restrict__ sc,
+                                              const float* __restrict__ sh, int c) {
+  constexpr int CE = 16 / sizeof(T);
+  float f[CE], a[CE], b[CE];
+  chunk_to_f(u, f, (const T*)nullptr);
+#pragma unroll
+  for (int e = 0; e < CE; e += 4) {  // 16-byte coefficient loads (channel chunks are 16-B aligned)
+    *reinterpret_cast<float4*>(a + e) = *reinterpret_cast<const float4*>(sc + c + e);
+    *reinterpret_cast<float4*>(b + e) = *reinterpret_cast<const float4*>(sh + c + e);
+  }
+#pragma unroll
+  for (int e = 0; e < CE; ++e) f[e] = fmaxf(fmaf(f[e], a[e], b[e]), 0.f);
+  return f_to_chunk(f, (const T*)nullptr);
+}
 
 // XCD-aware block order: the dispatcher deals consecutive workgroup ids round-robin over the 8
 // XCDs (each with a private L2). Bijective remap so that every XCD walks a contiguous range of
@@ -234,6 +255,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
       if (ok) {
         const int off = (a_pix[i] + hin * p.W + win) * p.C + cbase + c;  // < 2^31 (host-checked)
         ra[i] = *reinterpret_cast<const uint4*>(xg + off);
+        if (p.in_sc) ra[i] = bnrelu_chunk<T>(ra[i], p.in_sc, p.in_sh, c);
       } else {
         ra[i] = make_uint4(0, 0, 0, 0);
       }
@@ -409,6 +431,8 @@ struct WgradArgs {
   int grouped, gk, gc, cblk;  // grouped: rows / channels per group, channels per row block
   int creal;                  // logical input channels (< C: padded stride, dw keeps c < creal)
   int nct, nkt;               // column tiles, k tiles (grid = splits * nkt * nct)
+  const float* in_sc;         // nullable: BN+ReLU applied to the gathered x while staging
+  const float* in_sh;
   FastDiv fdQ, fdPQ, fdC, fdS;  // fdC divides by cblk (dense: C)
 };
 
@@ -416,7 +440,7 @@ struct WgradArgs {
 // ds_read_b64_tr_b16 (rows 8g+4h+q): keeps the 8 rows of a 32-lane half on distinct slots.
 __device__ __forceinline__ int swz_tr(int row) { return 2 * ((row & 3) | (((row >> 3) & 1) << 2)); }
 
-template <typename T, int BMK, int BNC>
+template <typename T, int BMK, int BNC, bool XF = false>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   constexpr int CE = 16 / sizeof(T);
   constexpr int BKM = 128 / sizeof(T);        // m rows per stage
@@ -468,6 +492,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
     b_cok = b_ch < p.C;  // a grouped block may run past the last group
   }
   const int b_hoff = b_r - p.ph, b_woff = b_s - p.pw;
+  // BN+ReLU input transform: this thread's column chunk (channels b_ch..) is fixed for the kernel
+  float tsc[XF ? CE : 1], tsh[XF ? CE : 1];
+  if constexpr (XF) {
+#pragma unroll
+    for (int e = 0; e < CE; ++e) {
+      tsc[e] = b_cok ? p.in_sc[b_ch + e] : 0.f;
+      tsh[e] = b_cok ? p.in_sh[b_ch + e] : 0.f;
+    }
+  }
 
   uint4 ra[A_CH], rb[B_CH];
   auto load_stage = [&](int mb) {
@@ -490,9 +523,17 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
         const int qq = rem - pp * p.Q;
         const int hin = pp * p.sh + b_hoff;
         const int win = qq * p.sw + b_woff;
-        if ((unsigned)hin < (unsigned)p.H && (unsigned)win < (unsigned)p.W)
+        if ((unsigned)hin < (unsigned)p.H && (unsigned)win < (unsigned)p.W) {
           v = *reinterpret_cast<const uint4*>(
               xg + ((int64_t)(n * p.H + hin) * p.W + win) * p.C + b_ch);
+          if constexpr (XF) {
+            float f[CE];
+            chunk_to_f(v, f, (const T*)nullptr);
+#pragma unroll
+            for (int e = 0; e < CE; ++e) f[e] = fmaxf(fmaf(f[e], tsc[e], tsh[e]), 0.f);
+            v = f_to_chunk(f, (const T*)nullptr);
+          }
+        }
       }
       rb[i] = v;
     }
@@ -847,6 +888,14 @@ __global__ void stem_shift_reduce_kernel(const float* __restrict__ g, const floa
   if (threadIdx.x == 0) dbeta[c] += red[0];
 }
 
+template <typename T, bool XF>
+void launch_wgrad_tiles(int bmk, int bnc, dim3 grid, hipStream_t st, const WgradArgs& a) {
+  if (bmk == 64 && bnc == 64) hipLaunchKernelGGL((wgrad_kernel<T, 64, 64, XF>), grid, dim3(256), 0, st, a);
+  else if (bmk == 64) hipLaunchKernelGGL((wgrad_kernel<T, 64, 128, XF>), grid, dim3(256), 0, st, a);
+  else if (bnc == 64) hipLaunchKernelGGL((wgrad_kernel<T, 128, 64, XF>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((wgrad_kernel<T, 128, 128, XF>), grid, dim3(256), 0, st, a);
+}
+
 int grid_for(int64_t total, int block = 256) {
   int64_t g = (total + block - 1) / block;
   if (g > 8192) g = 8192;
@@ -990,11 +1039,15 @@ int64_t rn_conv_pack_numel(const rn_conv_desc* d, int32_t which) {
   return which == 0 ? d->k * RS * d->c : d->c * RS * d->k_pad;
 }
 
-int rn_conv_fwd_bnstats(const rn_conv_desc* d, const void* x, const void* w, void* y, int32_t y_dtype,
-                        const void* add_src, const float* bias, float* part, rn_stream_t stream) {
+int rn_conv_fwd_x(const rn_conv_desc* d, const void* x, const void* w, void* y, int32_t y_dtype,
+                  const void* add_src, const float* bias, const float* in_scale, const float* in_shift,
+                  float* part, rn_stream_t stream) {
   RN_CHECK_ARG(d && x && w && y, "null argument");
+  RN_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "in_scale / in_shift must both be set");
+  RN_CHECK_ARG(!in_scale || d->groups == 1, "input transform on a grouped conv");
   IgemmArgs a = make_igemm_args(d, 0);
   a.x = x; a.w = w; a.y = y; a.add = add_src; a.bias = bias; a.stats = part;
+  a.in_sc = in_scale; a.in_sh = in_shift;
   RN_CHECK_ARG(!part || d->k % 8 == 0, "BatchNorm statistics need whole 8-channel chunks");
   hipStream_t st = as_stream(stream);
   if (d->dtype == RN_BF16) {
@@ -1007,7 +1060,12 @@ int rn_conv_fwd_bnstats(const rn_conv_desc* d, const void* x, const void* w, voi
 
 int rn_conv_fwd(const rn_conv_desc* d, const void* x, const void* w, void* y, int32_t y_dtype,
                 const void* add_src, const float* bias, rn_stream_t stream) {
-  return rn_conv_fwd_bnstats(d, x, w, y, y_dtype, add_src, bias, nullptr, stream);
+  return rn_conv_fwd_x(d, x, w, y, y_dtype, add_src, bias, nullptr, nullptr, nullptr, stream);
+}
+
+int rn_conv_fwd_bnstats(const rn_conv_desc* d, const void* x, const void* w, void* y, int32_t y_dtype,
+                        const void* add_src, const float* bias, float* part, rn_stream_t stream) {
+  return rn_conv_fwd_x(d, x, w, y, y_dtype, add_src, bias, nullptr, nullptr, part, stream);
 }
 
 int64_t rn_conv_bnstats_blocks(const rn_conv_desc* d) { return ceil_div((int64_t)d->n * d->p * d->q, 128); }
@@ -1022,12 +1080,15 @@ int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, 
   return launch_igemm<float, float>(a, st);
 }
 
-int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, float* dw,
-                       rn_stream_t stream) {
+int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, float* dw, const float* in_scale,
+                         const float* in_shift, rn_stream_t stream) {
   RN_CHECK_ARG(d && x && dy && dw, "null argument");
+  RN_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "in_scale / in_shift must both be set");
+  RN_CHECK_ARG(!in_scale || d->groups == 1, "input transform on a grouped conv");
 
   WgradArgs a{};
   a.x = x; a.dy = dy; a.dw = dw;
+  a.in_sc = in_scale; a.in_sh = in_shift;
   a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.P = d->p; a.Q = d->q; a.K = d->k;
   a.ldy = d->k_pad; a.R = d->r; a.S = d->s; a.sh = d->stride_h; a.sw = d->stride_w;
   a.ph = d->pad_h; a.pw = d->pad_w;
@@ -1058,7 +1119,7 @@ int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, flo
   // split M so that the whole grid is ONE round of resident blocks (floor: a partly filled second
   // round of long blocks is the worst tail), with >= 8 stages per block. Resident blocks per CU
   // of each tile variant (VGPR / LDS bound): 128x128 -> 2, 64x128 / 128x64 -> 3, 64x64 -> 5.
-  int per_cu = (bmk == 128 && bnc == 128) ? 2 : (bmk == 64 && bnc == 64) ? 5 : 3;
+  int per_cu = (bmk == 128 && bnc == 128) ? 2 : (bmk == 64 && bnc == 64) ? (in_scale ? 4 : 5) : 3;
   if (g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU] > 0) per_cu = g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU];
   int64_t want = std::max<int64_t>(1, (int64_t)per_cu * 256 / tiles);
   int64_t maxsplit = std::max<int64_t>(1, mstages / 8);
@@ -1076,17 +1137,17 @@ int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, flo
     else
       hipLaunchKernelGGL((wgrad_kernel<float, RN_GROUP_BLOCK, RN_GROUP_BLOCK>), grid, dim3(256), 0, st, a);
   } else if (d->dtype == RN_BF16) {
-    if (bmk == 64 && bnc == 64) hipLaunchKernelGGL((wgrad_kernel<bf16_t, 64, 64>), grid, dim3(256), 0, st, a);
-    else if (bmk == 64) hipLaunchKernelGGL((wgrad_kernel<bf16_t, 64, 128>), grid, dim3(256), 0, st, a);
-    else if (bnc == 64) hipLaunchKernelGGL((wgrad_kernel<bf16_t, 128, 64>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((wgrad_kernel<bf16_t, 128, 128>), grid, dim3(256), 0, st, a);
+    if (in_scale) launch_wgrad_tiles<bf16_t, true>(bmk, bnc, grid, st, a);
+    else launch_wgrad_tiles<bf16_t, false>(bmk, bnc, grid, st, a);
   } else {
-    if (bmk == 64 && bnc == 64) hipLaunchKernelGGL((wgrad_kernel<float, 64, 64>), grid, dim3(256), 0, st, a);
-    else if (bmk == 64) hipLaunchKernelGGL((wgrad_kernel<float, 64, 128>), grid, dim3(256), 0, st, a);
-    else if (bnc == 64) hipLaunchKernelGGL((wgrad_kernel<float, 128, 64>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((wgrad_kernel<float, 128, 128>), grid, dim3(256), 0, st, a);
+    if (in_scale) launch_wgrad_tiles<float, true>(bmk, bnc, grid, st, a);
+    else launch_wgrad_tiles<float, false>(bmk, bnc, grid, st, a);
   }
   return rn_check_launch("wgrad");
+}
+
+int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, float* dw, rn_stream_t stream) {
+  return rn_conv_bwd_filter_x(d, x, dy, dw, nullptr, nullptr, stream);
 }
 
 int rn_conv_weight_pack(const rn_conv_desc* d, const float* wm, void* w_krsc, void* w_crsk,

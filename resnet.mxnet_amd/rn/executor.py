@@ -303,6 +303,38 @@ class Plan:
             else:
                 raise PlanError("operator %s (%s) is not supported by the MI355X runtime" % (op, n.name))
         self.outputs = [self.tensor(n) for n, _ in self.symbol._outputs]
+        self._fuse_bn_apply()
+
+    def _fuse_bn_apply(self):
+        """BatchNorm+ReLU whose output feeds ONLY 1x1 convolutions (act1 -> conv1 / sc, act3 -> conv3
+        of the pre-activation units, symbol/resnet.py:17-31): the convs stage max(x*sc+sh, 0) from
+        the BN input while loading (rn_conv_fwd_x / rn_conv_bwd_filter_x) and the BN+ReLU output is
+        never written or read back."""
+        for op in self.ops:
+            op.xf = None
+            if op.kind == "bn":
+                op.apply_fused = False
+        if os.environ.get("RN_BN_APPLY_FUSION", "0") != "1":  # opt-in: measured slower (DESIGN.md)
+            return
+        refs = {}
+        for op in self.ops:
+            for key in ("x", "res", "a", "b"):
+                t = getattr(op, key, None)
+                if isinstance(t, TensorSpec):
+                    refs.setdefault(id(t), []).append((op, key))
+        out_ids = {id(t) for t in self.outputs}
+        for bn in self.ops:
+            if bn.kind != "bn" or not bn.relu or id(bn.y) in out_ids:
+                continue
+            users = refs.get(id(bn.y), [])
+            ok = users and all(u.kind == "conv" and key == "x" and tuple(u.kernel) == (1, 1) and u.groups == 1 and
+                               not getattr(u, "qweight", None) for u, key in users)
+            if not ok:
+                continue
+            bn.apply_fused = True
+            bn.y.virtual = True
+            for u, _ in users:
+                u.xf = bn
 
     def _is_stem(self, conv_node):
         src = conv_node.inputs[0][0]
@@ -606,7 +638,8 @@ class Executor:
 
     def _alloc_acts(self):
         for t in self.plan.tensors.values():
-            self.act(t)
+            if not getattr(t, "virtual", False):  # a fused BN+ReLU output is never materialised
+                self.act(t)
         # input pipeline (data/imagenet.py SyntheticDataIter hands pinned host batches): two device
         # buffers; the stem reads whichever _in_ptr points at
         t = self.plan.data_tensor
@@ -750,28 +783,29 @@ class Executor:
                 self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(d), op.wsrc, self._p(op.wk),
                                              self._p(op.wc), sp))
                 res = self._p(self.act(op.res)) if op.res is not None else None
-                I.append(self._call("rn_conv_fwd", L.C.byref(d), self._p(self.act(x)), self._p(op.wk),
-                                    self._p(self.act(y)), self.dtype, res, None, sp))
-                F.append(self._conv_fwd_call(op, d, self._p(self.act(x)), res, sp))
+                xin = self._p(self.act(op.xf.x)) if op.xf is not None else self._p(self.act(x))
+                I.append(self._conv_fwd_call(op, d, xin, res, sp, stats=False))
+                F.append(self._conv_fwd_call(op, d, xin, res, sp))
             elif op.kind == "bn":
                 x, y = op.x, op.y
                 c = x.cp
                 op.buf = self._zeros(4 * c, self.torch.float32)
                 op.sm, op.si, op.sc, op.sh = [L.C.c_void_p(op.buf.data_ptr() + 4 * c * i) for i in range(4)]
                 gamma = self._pp(op.gamma)
-                infer = self._call("rn_bn_fwd_infer", L.C.byref(op.desc), self._p(self.act(x)), self._p(self.act(y)),
+                yptr = None if op.apply_fused else self._p(self.act(y))  # fused: coefficients only
+                infer = self._call("rn_bn_fwd_infer", L.C.byref(op.desc), self._p(self.act(x)), yptr,
                                    gamma, self._pp(op.beta), self._ap(op.mean), self._ap(op.var), op.sc, op.sh, sp)
                 if op.use_global_stats:
                     F.append(infer)
                 elif op.part_src is not None:
                     s_ = op.part_src
                     F.append(self._call("rn_bn_fwd_train_part", L.C.byref(op.desc), self._p(s_.part), s_.part_blocks,
-                                        128, s_.y.cp, self._p(self.act(x)), self._p(self.act(y)), gamma,
+                                        128, s_.y.cp, self._p(self.act(x)), yptr, gamma,
                                         self._pp(op.beta), self._ap(op.mean), self._ap(op.var), op.sm, op.si, op.sc,
                                         op.sh, wsp, sp))
                 else:
                     F.append(self._call("rn_bn_fwd_train", L.C.byref(op.desc), self._p(self.act(x)),
-                                        self._p(self.act(y)), gamma, self._pp(op.beta), self._ap(op.mean),
+                                        yptr, gamma, self._pp(op.beta), self._ap(op.mean),
                                         self._ap(op.var), op.sm, op.si, op.sc, op.sh, wsp, sp))
                 I.append(infer)
             elif op.kind == "relu":
@@ -832,15 +866,22 @@ class Executor:
             self._fwd_infer.extend(I)
         self.stem_ws = self._zeros(stem_ws, self.torch.float32)
 
-    def _conv_fwd_call(self, op, d, xptr, res, sp):
-        """Training-mode conv forward; emits the next BatchNorm's statistics when one consumes y."""
+    def _conv_fwd_call(self, op, d, xptr, res, sp, stats=True):
+        """Conv forward; emits the next BatchNorm's statistics when one consumes y (training), and
+        applies the producing BatchNorm+ReLU on load when that BN is fused (op.xf)."""
         y = self._p(self.act(op.y))
-        if not op.bnstats:
+        xf = getattr(op, "xf", None)
+        sc, sh = (xf.sc, xf.sh) if xf is not None else (None, None)
+        part = None
+        if stats and op.bnstats:
+            if getattr(op, "part", None) is None:
+                op.part_blocks = int(self.lib.rn_conv_bnstats_blocks(L.C.byref(d)))
+                op.part = self._zeros(op.part_blocks * 3 * op.y.cp, self.torch.float32)
+            part = self._p(op.part)
+        if sc is None and part is None:
             return self._call("rn_conv_fwd", L.C.byref(d), xptr, self._p(op.wk), y, self.dtype, res, None, sp)
-        op.part_blocks = int(self.lib.rn_conv_bnstats_blocks(L.C.byref(d)))
-        op.part = self._zeros(op.part_blocks * 3 * op.y.cp, self.torch.float32)
-        return self._call("rn_conv_fwd_bnstats", L.C.byref(d), xptr, self._p(op.wk), y, self.dtype, res, None,
-                          self._p(op.part), sp)
+        return self._call("rn_conv_fwd_x", L.C.byref(d), xptr, self._p(op.wk), y, self.dtype, res, None, sc, sh,
+                          part, sp)
 
     def _weight_source(self, op, qwsp, sp):
         """Quantization_int8 on a weight (int8_api.py:131-132): the compute copies are packed from a
@@ -882,8 +923,12 @@ class Executor:
                                                 self._p(out), self._p(add), sp))
             elif op.kind == "conv":
                 x = op.x
-                self._bwd.append(self._call("rn_conv_bwd_filter", L.C.byref(op.desc), self._p(self.act(x)),
-                                            self._p(dy), self._gp(op.weight), sp))
+                if op.xf is not None:  # input = BN+ReLU(bn input), applied on load
+                    self._bwd.append(self._call("rn_conv_bwd_filter_x", L.C.byref(op.desc), self._p(self.act(op.xf.x)),
+                                                self._p(dy), self._gp(op.weight), op.xf.sc, op.xf.sh, sp))
+                else:
+                    self._bwd.append(self._call("rn_conv_bwd_filter", L.C.byref(op.desc), self._p(self.act(x)),
+                                                self._p(dy), self._gp(op.weight), sp))
                 self.param_done_at[op.weight] = len(self._bwd)
                 if x.needs_grad:
                     out, add = gs.contribute(x)

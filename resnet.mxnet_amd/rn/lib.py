@@ -40,6 +40,8 @@ SIGNATURES = {
     "rn_conv_fwd": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P]),
     "rn_conv_fwd_bnstats": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P]),
     "rn_conv_bnstats_blocks": (_i64, [_P]),
+    "rn_conv_fwd_x": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P, _P, _P]),
+    "rn_conv_bwd_filter_x": (_i32, [_P, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_data": (_i32, [_P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_filter": (_i32, [_P, _P, _P, _P, _P]),
     "rn_conv_weight_numel": (_i64, [_P]),

@@ -47,7 +47,16 @@ def gpu_relu_masks(ex):
         if not name:
             continue
         t = op.y
-        a = ex.act(t).float().cpu().numpy().reshape(t.n, t.h, t.w, t.cp)[..., :t.c].transpose(0, 3, 1, 2)
+        if op.kind == "bn" and getattr(op, "apply_fused", False):
+            # BN+ReLU applied on load by its 1x1 consumers: the decision is fmaf(x, sc, sh) > 0 (exact
+            # in fp64 for fp32 operands, same sign as the device's fused multiply-add)
+            x = op.x
+            xv = ex.act(x).float().cpu().numpy().reshape(x.n, x.h, x.w, x.cp).astype(np.float64)
+            buf = op.buf.cpu().numpy().astype(np.float64)
+            sc, sh = buf[2 * x.cp:3 * x.cp], buf[3 * x.cp:4 * x.cp]
+            a = (xv * sc + sh)[..., :t.c].transpose(0, 3, 1, 2)
+        else:
+            a = ex.act(t).float().cpu().numpy().reshape(t.n, t.h, t.w, t.cp)[..., :t.c].transpose(0, 3, 1, 2)
         masks[name] = a > 0
     return masks
 

@@ -517,3 +517,40 @@ def test_stem_prepare_and_smallc_conv(gpu, dtype, mode):
     assert rel_err(from_nhwc(y, k), y_ref) < TOL[dtype]
     assert rel_err(dw.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2), dw_ref) < \
         (TOL[dtype] if dtype == F32 else 5e-3)
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("case", [(2, 64, 14, 14, 256, 1, 1, 0), (2, 256, 7, 9, 64, 1, 2, 0), (3, 48, 5, 5, 1000, 1, 1, 0)])
+def test_conv_bnrelu_on_load(gpu, dtype, case):
+    """rn_conv_fwd_x / rn_conv_bwd_filter_x: the conv reads the PRE-BatchNorm tensor and stages
+    max(x*sc + sh, 0) (the BN+ReLU of pre-activation units, symbol/resnet.py:17-31)."""
+    n, c, h, w, k, r, st, pd = case
+    x, wt = _conv_data(case, 18)
+    rng = np.random.default_rng(19)
+    sc = rng.uniform(0.5, 1.5, c)
+    sh = rng.standard_normal(c) * 0.5
+    if dtype == BF16:
+        x, wt = bf16_round(x), bf16_round(wt)
+    xa = np.maximum(x * sc[None, :, None, None] + sh[None, :, None, None], 0)
+    if dtype == BF16:
+        xa = bf16_round(xa)  # the staged operand is rounded to the compute dtype
+    y_ref = ops.conv2d_fwd(xa, wt, (st, st), (pd, pd))
+    P, Q = y_ref.shape[2:]
+    dy = rng.standard_normal((n, k, P, Q))
+    if dtype == BF16:
+        dy = bf16_round(dy)
+    _, dw_ref = ops.conv2d_bwd(xa, wt, dy, (st, st), (pd, pd))
+    d = conv_desc(dtype, n, c, h, w, k, r, r, st, pd)
+    f = lambda a: torch.tensor(np.pad(a, (0, d.c - c)), dtype=torch.float32, device=gpu)
+    scd, shd = f(sc), f(sh)
+    xd = to_nhwc(x, dtype, gpu)
+    wk = torch.zeros(k * r * r * d.c, dtype=tdt(dtype), device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), p(wk), None, stream())
+    y = torch.zeros((n, P, Q, d.k_pad), dtype=tdt(dtype), device=gpu)
+    L.call("rn_conv_fwd_x", C.byref(d), p(xd), p(wk), p(y), dtype, None, None, p(scd), p(shd), None, stream())
+    dw = torch.zeros(k * r * r * c, dtype=torch.float32, device=gpu)
+    L.call("rn_conv_bwd_filter_x", C.byref(d), p(xd), p(to_nhwc(dy, dtype, gpu)), p(dw), p(scd), p(shd), stream())
+    torch.cuda.synchronize()
+    assert rel_err(from_nhwc(y, k), y_ref) < TOL[dtype]
+    assert rel_err(dw.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2), dw_ref) < \
+        (TOL[dtype] if dtype == F32 else 5e-3)

@@ -90,7 +90,7 @@ def test_plan_resnext_grouped():
     assert abs(p.train_flops() / 1e9 - 6437.6) < 0.1
     ex = Executor(Plan(graphs.resnext50_32x4d(), [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")
     names = [c[0] for c in ex._bwd]
-    assert names.count("rn_conv_bwd_filter") == 54  # 53 conv + fc1
+    assert sum(n.startswith("rn_conv_bwd_filter") for n in names) == 54  # 53 conv + fc1
 
 
 def test_plan_rejects_unsupported():
@@ -107,7 +107,7 @@ def test_executor_dry_run(dtype):
     p = Plan(sym, [("data", (2, 3, 64, 64))], [("softmax_label", (2,))], dtype=dtype)
     ex = Executor(p, "cpu")
     names = [c[0] for c in ex._bwd]
-    assert names.count("rn_conv_bwd_filter") == 54 and names.count("rn_conv_bwd_data") == 53
+    assert sum(n.startswith("rn_conv_bwd_filter") for n in names) == 54 and names.count("rn_conv_bwd_data") == 53
     assert names.count("rn_stem_shift_grad") == 1
     # every parameter's gradient has a producing call, buckets cover the flat buffer in order
     assert set(ex.param_done_at) == set(p.param_names)
@@ -139,3 +139,16 @@ def test_plan_int8_quantization():
     names = [c[0] for c in ex._bwd]
     assert names.count("rn_quant_int8_bwd") == 17 and names.count("rn_stem_quant_clip_grad") == 1
     assert [c[0] for c in ex.packs].count("rn_quant_int8_fwd") == 18
+
+
+def test_plan_bn_apply_fusion_opt_in(monkeypatch):
+    """RN_BN_APPLY_FUSION=1: BN+ReLU outputs read only by 1x1 convs are applied on load."""
+    monkeypatch.setenv("RN_BN_APPLY_FUSION", "1")
+    p = Plan(graphs.resnet50(), [("data", (2, 3, 224, 224))], [("softmax_label", (2,))])
+    fused = [op for op in p.ops if op.kind == "bn" and op.apply_fused]
+    # bn1 of every unit (-> conv1, and sc in unit 1) and bn3 (-> conv3); not bn2 (3x3) / bn0 / bn1 final
+    assert len(fused) == 32
+    assert all(getattr(op, "xf", None) is not None for op in p.ops if op.kind == "conv" and op.kernel == (1, 1))
+    monkeypatch.setenv("RN_BN_APPLY_FUSION", "0")
+    p = Plan(graphs.resnet50(), [("data", (2, 3, 224, 224))], [("softmax_label", (2,))])
+    assert not any(op.apply_fused for op in p.ops if op.kind == "bn")
