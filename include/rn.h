@@ -272,7 +272,9 @@ int rn_quant_int8_bwd(int32_t dtype, int64_t n, const void* x, const void* dy, v
  * ------------------------------------------------------------------------------------- */
 const char* rn_last_error(void);
 /* Kernel-variant switches (A/B measurements): 0 = wgrad LDS-DMA staging (default off),
- * 1 = reserved, 2 = wgrad split-M target blocks per CU (default 4). Process-global. */
+ * 1 = igemm LDS-DMA staging (default off: measured slower), 2 = wgrad split-M target blocks per CU
+ * (default: occupancy), 3 = diagnostic only:
+ * igemm A operand from one L1-resident chunk (wrong results; isolates memory latency). */
 int rn_set_tuning(int32_t key, int32_t value);
 int32_t rn_version(void);
 /* Number of compute units of the current device (for split heuristics / reporting). */

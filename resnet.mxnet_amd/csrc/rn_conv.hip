@@ -54,12 +54,22 @@ struct IgemmArgs {
   const float* in_sh;
   int ntn;             // n tiles (grid = m tiles * ntn)
   int smallc, lgc, rs; // fwd over C < one stage (the stem's 8 channels): k = tap*C + c flattened
+  int diag_l1;         // diagnostic (rn_set_tuning 3): every A row reads the same L1-resident chunk
+  int x_bytes, w_bytes;  // LDS-DMA buffer descriptors
   FastDiv fdS;
   int ncls;
   IgemmCls cls[4];
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ (row & 7); }
+
+// LDS-DMA (buffer_load ... lds) of one 16-byte chunk per lane: the LDS destination is the
+// wave-uniform base + 16 * lane; an out-of-range voffset reads zeros (halo / ragged edges).
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, const void* lds_wave_base, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (__attribute__((address_space(3))) void*)lds_wave_base, 16, voff,
+                                           0, 0, 0);
+}
+constexpr uint32_t kOob = 0xFFFFFFF0u;
 
 // BatchNorm-apply + ReLU of the consumer's input, applied while staging (the BN+ReLU output of
 // pre-activation units feeding 1x1 convs is never written to HBM): v = max(x*sc[c] + sh[c], 0)
@@ -147,7 +157,7 @@ __device__ __forceinline__ void bn_stats_epilogue(float* tile, float* __restrict
   }
 }
 
-template <typename T, typename OutT, int BM, int BN>
+template <typename T, typename OutT, int BM, int BN, bool DMA = false>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
   constexpr int CE = 16 / sizeof(T);   // elements per chunk
   constexpr int BKE = 128 / sizeof(T); // reduction elements per stage
@@ -200,6 +210,32 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
       a_wb[i] = 0;
     }
   }
+  // LDS-DMA staging writes each wave's 1 KiB lane-linearly (lane l -> row 8w + l/8 (+32 i), slot
+  // l&7), so a lane fetches the source chunk the XOR read-swizzle expects in that slot; the XOR
+  // term (row & 7) is the same for all of a thread's rows.
+  const int lch = DMA ? (ch ^ ((tid >> 3) & 7)) : ch;
+  // DMA fast path: per row, the gathered offset of tap (0,0) and a bitmask of the class's taps that
+  // land inside the image, so a stage costs one shift/and/add/select per row
+  int a_row[DMA ? A_CH : 1];
+  uint64_t a_mask[DMA ? A_CH : 1];
+  if constexpr (DMA) {
+    if (!p.smallc) {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        uint64_t msk = 0;
+        for (int tr = 0; tr < cl.nr; ++tr) {
+          const int hin = a_hb[i] + cl.hoff0 + p.hinc * tr;
+          if ((unsigned)hin >= (unsigned)p.H) continue;
+          for (int ts = 0; ts < cl.ns; ++ts) {
+            const int win = a_wb[i] + cl.woff0 + p.winc * ts;
+            if ((unsigned)win < (unsigned)p.W) msk |= 1ull << (tr * cl.ns + ts);
+          }
+        }
+        a_mask[i] = msk;
+        a_row[i] = msk ? (a_pix[i] + (a_hb[i] + cl.hoff0) * p.W + a_wb[i] + cl.woff0) * p.C + cbase + lch * CE : 0;
+      }
+    }
+  }
   int b_off[B_CH];  // 32-bit: weight matrices are far below 2^31 elements (host-checked)
   bool b_ok[B_CH];
 #pragma unroll
@@ -216,13 +252,17 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
   // the other LDS buffer (async-STAGE split: write after the MFMA phase).
   uint4 ra0[A_CH], rb0[B_CH];
   int st_tr = 0, st_ts = 0, st_cb = 0;  // next stage to load
+  int st_buf = 0;                       // LDS buffer the next DMA stage lands in
+  const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.w_bytes, 0x00020000);
 
   auto load_stage = [&](uint4* ra, uint4* rb) {
     int hoff, woff, c, toff;
+    int dtr = 0, dts = 0, dcb = 0;  // stage's tap / channel-block (DMA fast path)
     bool cok;
     if (p.smallc) {
       // several taps per stage: this thread's chunk is k = tap*C + c of the flattened reduction
-      const int k0 = st_cb * BKE + ch * CE;
+      const int k0 = st_cb * BKE + lch * CE;
       ++st_cb;
       const int tap = k0 >> p.lgc;
       c = k0 & (p.C - 1);
@@ -232,6 +272,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
       toff = k0;
     } else {
       const int tr = st_tr, ts = st_ts, cb = st_cb;
+      dtr = tr; dts = ts; dcb = cb;
       if (++st_cb == ncb) {
         st_cb = 0;
         if (++st_ts == cl.ns) {
@@ -243,9 +284,43 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
       const int s = cl.s0 + p.sstep * ts;
       hoff = cl.hoff0 + p.hinc * tr;
       woff = cl.woff0 + p.winc * ts;
-      c = cb * BKE + ch * CE;
+      c = cb * BKE + lch * CE;
       cok = c < p.cblk && cbase + c < p.C;  // a grouped block may run past the last group
       toff = (r * p.S + s) * p.cblk + c;
+    }
+    if constexpr (DMA) {
+      const int buf = st_buf;
+      st_buf ^= 1;
+      const uint4* As = smem + buf * (BM + BN) * 8;
+      const uint4* Bs = As + BM * 8;
+      const int wrow = (tid >> 6) * 8;  // first row of this wave's 1 KiB piece
+      if (!p.smallc) {
+        // uniform per stage: tap index inside the class and its offset from tap (0,0)
+        const int tapi = dtr * cl.ns + dts;
+        const int toffa = ((hoff - cl.hoff0) * p.W + (woff - cl.woff0)) * p.C + dcb * BKE;
+#pragma unroll
+        for (int i = 0; i < A_CH; ++i) {
+          const bool ok = cok && ((a_mask[i] >> tapi) & 1ull);
+          const uint32_t off = ok ? (uint32_t)((a_row[i] + toffa) * (int)sizeof(T)) : kOob;
+          dma16(rs_x, As + (wrow + 32 * i) * 8, off);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < A_CH; ++i) {
+          const int hin = a_hb[i] + hoff;
+          const int win = a_wb[i] + woff;
+          const bool ok = cok && (unsigned)hin < (unsigned)p.H && (unsigned)win < (unsigned)p.W;
+          const uint32_t off =
+              ok ? (uint32_t)(((a_pix[i] + hin * p.W + win) * p.C + cbase + c) * (int)sizeof(T)) : kOob;
+          dma16(rs_x, As + (wrow + 32 * i) * 8, off);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        const uint32_t off = (cok && b_ok[i]) ? (uint32_t)((b_off[i] + toff) * (int)sizeof(T)) : kOob;
+        dma16(rs_w, Bs + (wrow + 32 * i) * 8, off);
+      }
+      return;
     }
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
@@ -253,7 +328,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
       const int win = a_wb[i] + woff;
       const bool ok = cok && (unsigned)hin < (unsigned)p.H && (unsigned)win < (unsigned)p.W;
       if (ok) {
-        const int off = (a_pix[i] + hin * p.W + win) * p.C + cbase + c;  // < 2^31 (host-checked)
+        const int off = p.diag_l1 ? (c & 63) : (a_pix[i] + hin * p.W + win) * p.C + cbase + c;  // < 2^31
         ra[i] = *reinterpret_cast<const uint4*>(xg + off);
         if (p.in_sc) ra[i] = bnrelu_chunk<T>(ra[i], p.in_sc, p.in_sh, c);
       } else {
@@ -342,17 +417,33 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
     }
   };
 
-  if (nstage > 0) {
-    load_stage(ra0, rb0);
-    store_stage(0, ra0, rb0);
-    __syncthreads();
-  }
-  for (int t = 0; t < nstage; ++t) {
-    const bool more = t + 1 < nstage;
-    if (more) load_stage(ra0, rb0);
-    compute(t & 1);
-    if (more) store_stage((t + 1) & 1, ra0, rb0);
-    __syncthreads();
+  if constexpr (DMA) {
+    // LDS-DMA: no staging registers and no ds_write pass (the VGPR->LDS store path is the slowest
+    // LDS path); stage t+1 is in flight while stage t is computed
+    if (nstage > 0) {
+      load_stage(ra0, rb0);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+    }
+    for (int t = 0; t < nstage; ++t) {
+      if (t + 1 < nstage) load_stage(ra0, rb0);
+      compute(t & 1);
+      __builtin_amdgcn_s_waitcnt(0);
+      __syncthreads();
+    }
+  } else {
+    if (nstage > 0) {
+      load_stage(ra0, rb0);
+      store_stage(0, ra0, rb0);
+      __syncthreads();
+    }
+    for (int t = 0; t < nstage; ++t) {
+      const bool more = t + 1 < nstage;
+      if (more) load_stage(ra0, rb0);
+      compute(t & 1);
+      if (more) store_stage((t + 1) & 1, ra0, rb0);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: stage the fp32 tile through LDS, then every thread writes whole 16-byte
@@ -979,14 +1070,27 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   for (int z = 0; z < a.ncls; ++z) maxMc = std::max(maxMc, a.N * a.cls[z].Pc * a.cls[z].Qc);
   if (maxMc == 0) return 0;
   IgemmArgs b = a;
+  b.diag_l1 = g_tune[RN_TUNE_DIAG_IGEMM_L1];
+  const int64_t xb = (int64_t)a.N * a.H * a.W * a.C * (int64_t)sizeof(T);
+  const int64_t wb = (int64_t)a.K * a.wrow * (int64_t)sizeof(T);
+  b.x_bytes = (int)std::min<int64_t>(xb, INT32_MAX);
+  b.w_bytes = (int)std::min<int64_t>(wb, INT32_MAX);
+  // LDS-DMA staging (opt-in, rn_set_tuning 1) unless the input transform needs a register pass or an operand is
+  // too large for 32-bit buffer offsets
+  int max_taps = 0;
+  for (int z = 0; z < a.ncls; ++z) max_taps = std::max(max_taps, a.cls[z].nr * a.cls[z].ns);
+  const bool dma = g_tune[RN_TUNE_IGEMM_DMA] > 0 && !a.in_sc && !b.diag_l1 && xb < INT32_MAX && wb < INT32_MAX &&
+                   max_taps <= 64;
   if (a.K <= 64 || a.gred > 0) {  // grouped: the block width is RN_GROUP_BLOCK
     b.ntn = (int)ceil_div(a.K, 64);
     dim3 grid((unsigned)(ceil_div(maxMc, 128) * b.ntn), 1, a.ncls);
-    hipLaunchKernelGGL((igemm_kernel<T, OutT, 128, 64>), grid, dim3(256), 0, st, b);
+    if (dma) hipLaunchKernelGGL((igemm_kernel<T, OutT, 128, 64, true>), grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((igemm_kernel<T, OutT, 128, 64, false>), grid, dim3(256), 0, st, b);
   } else {
     b.ntn = (int)ceil_div(a.K, 128);
     dim3 grid((unsigned)(ceil_div(maxMc, 128) * b.ntn), 1, a.ncls);
-    hipLaunchKernelGGL((igemm_kernel<T, OutT, 128, 128>), grid, dim3(256), 0, st, b);
+    if (dma) hipLaunchKernelGGL((igemm_kernel<T, OutT, 128, 128, true>), grid, dim3(256), 0, st, b);
+    else hipLaunchKernelGGL((igemm_kernel<T, OutT, 128, 128, false>), grid, dim3(256), 0, st, b);
   }
   return rn_check_launch("igemm");
 }
