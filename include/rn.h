@@ -67,6 +67,16 @@ int rn_conv_fwd_bnstats(const rn_conv_desc* d, const void* x, const void* w_krsc
                         const void* add_src, const float* bias, float* part, rn_stream_t stream);
 int64_t rn_conv_bnstats_blocks(const rn_conv_desc* d);
 
+/* rn_conv_bwd_data that also reduces the BatchNorm+ReLU backward of the BN whose output gradient
+ * this call completes (dx here = d(bn output), bn_x = the BN input, bn_mean / bn_scale / bn_shift =
+ * its saved mean and the scale/shift of its forward): part[rn_conv_bnred_blocks(d)][c][2] receives
+ * per-output-block (sum dz, sum dz*(x - mean)), dz = dx * [bn_x*scale + shift > 0] (relu != 0);
+ * rn_bn_bwd_part then finishes the BN backward without its own reduction pass over x and dy. */
+int rn_conv_bwd_data_bnred(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx, const void* add_src,
+                           const void* bn_x, const float* bn_mean, const float* bn_scale, const float* bn_shift,
+                           int32_t relu, float* part, rn_stream_t stream);
+int64_t rn_conv_bnred_blocks(const rn_conv_desc* d);
+
 /* rn_conv_fwd whose input is the PRE-BatchNorm tensor of a BatchNorm+ReLU (pre-activation
  * units, symbol/resnet.py:17-31): the kernel stages max(x*in_scale[c] + in_shift[c], 0) (the
  * coefficients rn_bn_fwd_train / rn_bn_fwd_infer computed), so the BN+ReLU output is never
@@ -174,6 +184,12 @@ int rn_bn_fwd_train_part(const rn_bn_desc* d, const float* part, int64_t nblk, i
                          const void* x, void* y, const float* gamma, const float* beta, float* moving_mean,
                          float* moving_var, float* save_mean, float* save_invstd, float* scale, float* shift,
                          void* ws, rn_stream_t stream);
+/* rn_bn_bwd with the reduction already done by the producer of dy (rn_conv_bwd_data_bnred):
+ * finalize over part[nrb][c][2], then dx = BN-backward(dy) (+ add_src). ws: >= 4*c floats + 16 B. */
+int rn_bn_bwd_part(const rn_bn_desc* d, const float* part, int64_t nrb, const void* x, const void* dy, void* dx,
+                   const void* add_src, const float* gamma, const float* save_mean, const float* save_invstd,
+                   const float* scale, const float* shift, float* dgamma, float* dbeta, void* ws,
+                   rn_stream_t stream);
 int rn_bn_fwd_infer(const rn_bn_desc* d, const void* x, void* y, const float* gamma,
                     const float* beta, const float* moving_mean, const float* moving_var,
                     float* scale, float* shift, rn_stream_t stream);

@@ -655,6 +655,29 @@ int rn_stem_prepare(const rn_bn_desc* d, const float* x, int32_t n, int32_t c, i
   return rn_check_launch("stem_prepare");
 }
 
+int rn_bn_bwd_part(const rn_bn_desc* d, const float* part, int64_t nrb, const void* x, const void* dy, void* dx,
+                   const void* add_src, const float* gamma, const float* save_mean, const float* save_invstd,
+                   const float* scale, const float* shift, float* dgamma, float* dbeta, void* ws,
+                   rn_stream_t stream) {
+  if (check_bn(d)) return -1;
+  RN_CHECK_ARG(part && nrb > 0 && x && dy && save_mean && save_invstd && scale && shift && ws, "null argument");
+  RN_CHECK_ARG(d->fix_gamma || gamma, "gamma required unless fix_gamma");
+  hipStream_t st = as_stream(stream);
+  float* coef = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 15) & ~uintptr_t(15));
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(d->c), dim3(256), 0, st, part, (int)nrb, d->m, d->c, d->c_real,
+                     d->fix_gamma, gamma, save_mean, save_invstd, dgamma, dbeta, coef);
+  if (dx) {
+    if (d->dtype == RN_BF16) {
+      if (d->relu) launch_bwd_apply<bf16_t, true>(d, x, dy, dx, add_src, coef, scale, shift, st);
+      else launch_bwd_apply<bf16_t, false>(d, x, dy, dx, add_src, coef, scale, shift, st);
+    } else {
+      if (d->relu) launch_bwd_apply<float, true>(d, x, dy, dx, add_src, coef, scale, shift, st);
+      else launch_bwd_apply<float, false>(d, x, dy, dx, add_src, coef, scale, shift, st);
+    }
+  }
+  return rn_check_launch("bn_bwd_part");
+}
+
 int rn_bn_fwd_infer(const rn_bn_desc* d, const void* x, void* y, const float* gamma, const float* beta,
                     const float* moving_mean, const float* moving_var, float* scale, float* shift,
                     rn_stream_t stream) {

@@ -56,6 +56,12 @@ struct IgemmArgs {
   int smallc, lgc, rs; // fwd over C < one stage (the stem's 8 channels): k = tap*C + c flattened
   int diag_l1;         // diagnostic (rn_set_tuning 3): every A row reads the same L1-resident chunk
   int x_bytes, w_bytes;  // LDS-DMA buffer descriptors
+  // dgrad only, nullable: the BatchNorm-backward reduction of the gradient this conv completes
+  // (sum dz, sum dz*(x - mean), dz = dy * relu'(bn(x))) per output block -> bnred[blk][ldo][2]
+  float* bnred;
+  const void* bn_x;
+  const float *bn_mean, *bn_sc, *bn_sh;
+  int bn_relu, mt_max;
   FastDiv fdS;
   int ncls;
   IgemmCls cls[4];
@@ -181,8 +187,17 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   const int mtile = lid / p.ntn;
   const int m0 = mtile * BM;
-  if (m0 >= Mc) return;
   const int n0 = (lid - mtile * p.ntn) * BN;
+  if (m0 >= Mc) {  // (a dgrad parity class with fewer rows): empty BN-reduction partials
+    if (p.bnred)
+      for (int col = threadIdx.x; col < BN; col += 256)
+        if (n0 + col < p.ldo) {
+          float* dst = p.bnred + ((int64_t)(blockIdx.z * p.mt_max + mtile) * p.ldo + n0 + col) * 2;
+          dst[0] = 0.f;
+          dst[1] = 0.f;
+        }
+    return;
+  }
   // grouped conv: the block's columns touch groups n0/gcol.., whose input channels start here
   const int cbase = (n0 / p.gcol) * p.gred;
 
@@ -394,6 +409,8 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
   const OutT* __restrict__ ag = reinterpret_cast<const OutT*>(p.add);
   int64_t ep_off[EPH];
   uint4 ep_add[EPH];
+  uint4 ep_x[EPH];
+  const T* __restrict__ bxg = reinterpret_cast<const T*>(p.bn_x);
   auto prefetch_add = [&](int half) {
 #pragma unroll
     for (int k = 0; k < EPH; ++k) {
@@ -413,6 +430,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
         const int ow = cl.b + p.ostep_w * jj;
         ep_off[k] = ((int64_t)(n * p.P + oh) * p.Q + ow) * p.ldo + col0;
         if (ag && col0 + OE <= p.K) ep_add[k] = *reinterpret_cast<const uint4*>(ag + ep_off[k]);
+        if (p.bnred) ep_x[k] = *reinterpret_cast<const uint4*>(bxg + ep_off[k]);
       }
     }
   };
@@ -465,6 +483,19 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
       }
   __syncthreads();
   OutT* __restrict__ yg = reinterpret_cast<OutT*>(p.y);
+  // BN-backward reduction: this thread's column chunk is fixed (256 % CPR == 0)
+  float r_mu[OE], r_sc[OE], r_sh[OE], r1[OE], r2[OE];
+  if (p.bnred) {
+    const int c0 = n0 + (tid % CPR) * OE;
+#pragma unroll
+    for (int e = 0; e < OE; ++e) {
+      const bool okc = c0 + e < p.K;
+      r_mu[e] = okc ? p.bn_mean[c0 + e] : 0.f;
+      r_sc[e] = okc ? p.bn_sc[c0 + e] : 0.f;
+      r_sh[e] = okc ? p.bn_sh[c0 + e] : 0.f;
+      r1[e] = r2[e] = 0.f;
+    }
+  }
 #pragma unroll
   for (int half = 0; half < EPC / EPH; ++half) {
   if (half > 0) prefetch_add(half);
@@ -491,6 +522,17 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
       }
       const uint4 out = f_to_chunk(v, (const OutT*)nullptr);
       *reinterpret_cast<uint4*>(yg + ep_off[k]) = out;
+      if (p.bnred) {  // on the stored (rounded) gradient, as a separate BN-backward pass would read it
+        float g[OE], xv[OE];
+        chunk_to_f(out, g, (const OutT*)nullptr);
+        chunk_to_f(ep_x[k], xv, (const T*)nullptr);
+#pragma unroll
+        for (int e = 0; e < OE; ++e) {
+          const float dz = (!p.bn_relu || fmaf(xv[e], r_sc[e], r_sh[e]) > 0.f) ? g[e] : 0.f;
+          r1[e] += dz;
+          r2[e] = fmaf(dz, xv[e] - r_mu[e], r2[e]);
+        }
+      }
       if (p.stats) {  // keep the stored (rounded) values for the BatchNorm statistics below
         chunk_to_f(out, v, (const OutT*)nullptr);
 #pragma unroll
@@ -506,6 +548,39 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
   }
   }
   if (p.stats) bn_stats_epilogue<BM, BN, LDT>(tile, p.stats, p.ldo, m0, n0, Mc, mtile);
+  if (p.bnred) {
+    // rows -> one partial per column: lanes sharing the column chunk (stride CPR) first, then waves
+#pragma unroll
+    for (int off = CPR; off < 64; off <<= 1)
+#pragma unroll
+      for (int e = 0; e < OE; ++e) {
+        r1[e] += __shfl_xor(r1[e], off, 64);
+        r2[e] += __shfl_xor(r2[e], off, 64);
+      }
+    __syncthreads();  // the staged tile is no longer read
+    float* red = tile;  // [wave][CPR][OE][2]
+    if (lane < CPR) {
+#pragma unroll
+      for (int e = 0; e < OE; ++e) {
+        red[((wid * CPR + lane) * OE + e) * 2] = r1[e];
+        red[((wid * CPR + lane) * OE + e) * 2 + 1] = r2[e];
+      }
+    }
+    __syncthreads();
+    if (tid < CPR * OE) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        a += red[((w * CPR) * OE + tid) * 2];
+        b += red[((w * CPR) * OE + tid) * 2 + 1];
+      }
+      if (n0 + tid < p.ldo) {
+        float* dst = p.bnred + ((int64_t)(blockIdx.z * p.mt_max + mtile) * p.ldo + n0 + tid) * 2;
+        dst[0] = a;
+        dst[1] = b;
+      }
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------ wgrad
@@ -1174,14 +1249,35 @@ int rn_conv_fwd_bnstats(const rn_conv_desc* d, const void* x, const void* w, voi
 
 int64_t rn_conv_bnstats_blocks(const rn_conv_desc* d) { return ceil_div((int64_t)d->n * d->p * d->q, 128); }
 
-int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
-                     const void* add_src, rn_stream_t stream) {
+int64_t rn_conv_bnred_blocks(const rn_conv_desc* d) {
+  IgemmArgs a = make_igemm_args(d, 1);
+  int maxMc = 0;
+  for (int z = 0; z < a.ncls; ++z) maxMc = std::max(maxMc, a.N * a.cls[z].Pc * a.cls[z].Qc);
+  return (int64_t)a.ncls * ceil_div(maxMc, 128);
+}
+
+int rn_conv_bwd_data_bnred(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx, const void* add_src,
+                           const void* bn_x, const float* bn_mean, const float* bn_scale, const float* bn_shift,
+                           int32_t relu, float* part, rn_stream_t stream) {
   RN_CHECK_ARG(d && dy && w_crsk && dx, "null argument");
   IgemmArgs a = make_igemm_args(d, 1);
   a.x = dy; a.w = w_crsk; a.y = dx; a.add = add_src; a.bias = nullptr;
+  if (part) {
+    RN_CHECK_ARG(bn_x && bn_mean && bn_scale && bn_shift, "BN reduction needs x, mean, scale, shift");
+    RN_CHECK_ARG(d->c % 8 == 0 && d->c == d->c_real, "BN reduction needs whole 8-channel chunks");
+    int maxMc = 0;
+    for (int z = 0; z < a.ncls; ++z) maxMc = std::max(maxMc, a.N * a.cls[z].Pc * a.cls[z].Qc);
+    a.bnred = part; a.bn_x = bn_x; a.bn_mean = bn_mean; a.bn_sc = bn_scale; a.bn_sh = bn_shift;
+    a.bn_relu = relu; a.mt_max = (int)ceil_div(maxMc, 128);
+  }
   hipStream_t st = as_stream(stream);
   if (d->dtype == RN_BF16) return launch_igemm<bf16_t, bf16_t>(a, st);
   return launch_igemm<float, float>(a, st);
+}
+
+int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx, const void* add_src,
+                     rn_stream_t stream) {
+  return rn_conv_bwd_data_bnred(d, dy, w_crsk, dx, add_src, nullptr, nullptr, nullptr, nullptr, 0, nullptr, stream);
 }
 
 int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, float* dw, const float* in_scale,

@@ -486,12 +486,14 @@ class _GradState:
                 return pend[0]
             buf = self.ex.grad_buf(t)
             self.ex._emit_bwd(("add", t.numel, pend[0], pend[1], buf))
+            self.ex._gw[key] = ("other",)
             pend = pend[2:]
             self.has_value.add(key)
         else:
             buf = self.ex.grad_buf(t)
         for p in pend:
             self.ex._emit_bwd(("add", t.numel, buf, p, buf))
+            self.ex._gw[key] = ("other",)
         return buf
 
     def contribute(self, t):
@@ -901,6 +903,8 @@ class Executor:
         gs = _GradState(self)
         wsp = self._p(self.ws)
         self.param_done_at = {}  # param -> index in self._bwd after which its grad is final
+        self._gw = {}  # id(tensor) -> last writer of its gradient buffer: ("dgrad", call index, conv op)
+        bwd_fusion = os.environ.get("RN_BN_BWD_FUSION", "0") == "1"  # opt-in: measured slower
         for op in reversed(plan.ops):
             if op.kind == "softmax":
                 gs.has_value.add(id(op.x))  # dlogits written by the forward softmax call
@@ -934,6 +938,7 @@ class Executor:
                     out, add = gs.contribute(x)
                     self._bwd.append(self._call("rn_conv_bwd_data", L.C.byref(op.desc), self._p(dy), self._p(op.wc),
                                                 self._p(out), self._p(add), sp))
+                    self._gw[id(x)] = ("dgrad", len(self._bwd) - 1, op, dy, out, add)
                 if op.res is not None and op.res.needs_grad:
                     gs.alias(op.res, dy)
             elif op.kind == "stem":
@@ -953,9 +958,25 @@ class Executor:
             elif op.kind == "bn":
                 x = op.x
                 out, add = (gs.contribute(x) if x.needs_grad else (None, None))
-                self._bwd.append(self._call("rn_bn_bwd", L.C.byref(op.desc), self._p(self.act(x)), self._p(dy),
-                                            self._p(out), self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc,
-                                            op.sh, self._gp(op.gamma), self._gp(op.beta), wsp, sp))
+                w = self._gw.get(id(op.y))
+                if bwd_fusion and w and w[0] == "dgrad" and dy is self._grads.get(id(op.y)) and \
+                        op.y.c % 8 == 0 and op.y.c == op.y.cp:
+                    # the conv dgrad that completes this BN's output gradient also reduces its backward
+                    # (sum dz, sum dz*(x - mean)); the BN then needs only finalize + apply
+                    _, ci, cop, cdy, cout, cadd = w
+                    op.bnred_blocks = int(self.lib.rn_conv_bnred_blocks(L.C.byref(cop.desc)))
+                    op.bnred = self._zeros(op.bnred_blocks * op.y.cp * 2, self.torch.float32)
+                    self._bwd[ci] = self._call("rn_conv_bwd_data_bnred", L.C.byref(cop.desc), self._p(cdy),
+                                               self._p(cop.wc), self._p(cout), self._p(cadd), self._p(self.act(x)),
+                                               op.sm, op.sc, op.sh, int(op.relu), self._p(op.bnred), sp)
+                    self._bwd.append(self._call("rn_bn_bwd_part", L.C.byref(op.desc), self._p(op.bnred),
+                                                op.bnred_blocks, self._p(self.act(x)), self._p(dy), self._p(out),
+                                                self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc, op.sh,
+                                                self._gp(op.gamma), self._gp(op.beta), wsp, sp))
+                else:
+                    self._bwd.append(self._call("rn_bn_bwd", L.C.byref(op.desc), self._p(self.act(x)), self._p(dy),
+                                                self._p(out), self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc,
+                                                op.sh, self._gp(op.gamma), self._gp(op.beta), wsp, sp))
                 self.param_done_at[op.gamma] = len(self._bwd)
                 self.param_done_at[op.beta] = len(self._bwd)
             elif op.kind == "quant":

@@ -42,6 +42,9 @@ SIGNATURES = {
     "rn_conv_bnstats_blocks": (_i64, [_P]),
     "rn_conv_fwd_x": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_filter_x": (_i32, [_P, _P, _P, _P, _P, _P, _P]),
+    "rn_conv_bwd_data_bnred": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P, _P]),
+    "rn_conv_bnred_blocks": (_i64, [_P]),
+    "rn_bn_bwd_part": (_i32, [_P, _P, _i64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_data": (_i32, [_P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_filter": (_i32, [_P, _P, _P, _P, _P]),
     "rn_conv_weight_numel": (_i64, [_P]),

@@ -554,3 +554,58 @@ def test_conv_bnrelu_on_load(gpu, dtype, case):
     assert rel_err(from_nhwc(y, k), y_ref) < TOL[dtype]
     assert rel_err(dw.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2), dw_ref) < \
         (TOL[dtype] if dtype == F32 else 5e-3)
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("case", [(2, 64, 14, 14, 128, 3, 1, 1), (2, 128, 14, 14, 256, 1, 2, 0),
+                                  (3, 32, 13, 11, 48, 3, 2, 1)])
+def test_dgrad_bn_backward_fusion(gpu, dtype, case):
+    """rn_conv_bwd_data_bnred + rn_bn_bwd_part == conv dgrad followed by the BatchNorm+ReLU backward
+    of the BN that produced the conv's input (pre-activation units)."""
+    n, c, h, w, k, r, st, pd = case
+    rng = np.random.default_rng(20)
+    xb = rng.standard_normal((n, c, h, w)) * 1.5 + 0.3            # BN input
+    gamma, beta = rng.uniform(0.5, 1.5, c), rng.standard_normal(c) * 0.2
+    if dtype == BF16:
+        xb = bf16_round(xb)
+    a_ref, cache = ops.bn_train_fwd(xb, gamma, beta, 1e-5, False)
+    act = ops.relu_fwd(a_ref)                                      # conv input
+    wt = rng.standard_normal((k, c, r, r)) / np.sqrt(c * r * r)
+    P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+    dy = rng.standard_normal((n, k, P, Q))
+    prev = rng.standard_normal((n, c, h, w)) * 0.5                # an earlier contribution (add_src)
+    if dtype == BF16:
+        wt, dy, prev = bf16_round(wt), bf16_round(dy), bf16_round(prev)
+    dact_ref, _ = ops.conv2d_bwd(act, wt, dy, (st, st), (pd, pd))
+    dact_ref = dact_ref + prev
+    dact_in = bf16_round(dact_ref) if dtype == BF16 else dact_ref  # the stored gradient the BN reads
+    dz = ops.relu_bwd(dact_in, act)
+    dx_ref, dg_ref, db_ref = ops.bn_train_bwd(dz, cache, False)
+
+    d = conv_desc(dtype, n, c, h, w, k, r, r, st, pd)
+    wc = torch.zeros(d.c * r * r * d.k_pad, dtype=tdt(dtype), device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), None, p(wc), stream())
+    bd = L.BNDesc(dtype=dtype, m=n * h * w, c=d.c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1)
+    f = lambda a: torch.tensor(np.pad(np.asarray(a, np.float64), (0, d.c - c)), dtype=torch.float32, device=gpu)
+    g_d, b_d, mm, mv = f(gamma), f(beta), f(np.zeros(c)), f(np.ones(c))
+    sm, si, sc, sh = [torch.zeros(d.c, dtype=torch.float32, device=gpu) for _ in range(4)]
+    lib = L.load()
+    ws = torch.zeros(lib.rn_bn_workspace_bytes(C.byref(bd)) // 4 + 16, dtype=torch.float32, device=gpu)
+    xbd = to_nhwc(xb, dtype, gpu)
+    L.call("rn_bn_fwd_train", C.byref(bd), p(xbd), None, p(g_d), p(b_d), p(mm), p(mv), p(sm), p(si), p(sc), p(sh),
+           p(ws), stream())
+    dact = to_nhwc(prev, dtype, gpu)                               # accumulated in place (add_src = out)
+    nrb = lib.rn_conv_bnred_blocks(C.byref(d))
+    part = torch.full((nrb * d.c * 2,), float("nan"), dtype=torch.float32, device=gpu)  # every slot written
+    L.call("rn_conv_bwd_data_bnred", C.byref(d), p(to_nhwc(dy, dtype, gpu)), p(wc), p(dact), p(dact), p(xbd), p(sm),
+           p(sc), p(sh), 1, p(part), stream())
+    dx = torch.zeros_like(xbd)
+    dg, db = torch.zeros(d.c, dtype=torch.float32, device=gpu), torch.zeros(d.c, dtype=torch.float32, device=gpu)
+    L.call("rn_bn_bwd_part", C.byref(bd), p(part), nrb, p(xbd), p(dact), p(dx), None, p(g_d), p(sm), p(si), p(sc),
+           p(sh), p(dg), p(db), p(ws), stream())
+    torch.cuda.synchronize()
+    assert rel_err(from_nhwc(dact, c), dact_ref) < TOL[dtype]
+    assert not torch.isnan(part).any()
+    assert rel_err(db.cpu().numpy()[:c], db_ref) < (1e-4 if dtype == F32 else 2e-2)
+    assert rel_err(dg.cpu().numpy()[:c], dg_ref) < (1e-4 if dtype == F32 else 2e-2)
+    assert rel_err(from_nhwc(dx, c), dx_ref) < (TOL[dtype] * 5 if dtype == F32 else 3e-2)
