@@ -72,11 +72,34 @@ def family_of(ex, name, args):
         return "wgrad_kernel<bf16,128,128>" if ex.dtype == 0 else "wgrad_kernel<f32,128,128>"
     if name in ("rn_conv_fwd", "rn_conv_fwd_bnstats", "rn_conv_bwd_data"):
         d = args[0]._obj
-        ncol = d.c if name == "rn_conv_bwd_data" else d.k
-        out_f32 = name != "rn_conv_bwd_data" and args[4] == 1 and ex.dtype == 0
+        dgrad = name == "rn_conv_bwd_data"
+        ncol = d.c if dgrad else d.k
+        out_f32 = not dgrad and args[4] == 1 and ex.dtype == 0
+        big = big_tile(d, dgrad) if (ex.dtype == 0 and not out_f32 and name != "rn_conv_fwd_bnstats" and
+                                     (dgrad or args[6] is None)) else None
+        if big:
+            return "igemm_big_kernel<256x%d>" % big
         tile = "128x64" if ncol <= 64 else "128x128"
         return "igemm_kernel<bf16,%s,%s>" % ("f32" if out_f32 else "bf16", tile)
     return None
+
+
+def big_tile(d, dgrad):
+    """Mirror of launch_igemm's 256-row tile choice (rn_conv.hip; RN_TUNE key 4 at its default):
+    the tile's column count, or None for the 128-row kernel."""
+    ncol = d.c if dgrad else d.k
+    smallc = not dgrad and d.c < 64 and (d.c & (d.c - 1)) == 0 and d.r * d.s > 1
+    if d.groups != 1 or smallc or ncol < 128:
+        return None
+    if dgrad:
+        rows = 0
+        for a in range(d.stride_h):
+            for b in range(d.stride_w):
+                pc, qc = -(-(d.h - a) // d.stride_h), -(-(d.w - b) // d.stride_w)
+                rows += -(-(d.n * pc * qc) // 256)
+    else:
+        rows = -(-(d.n * d.p * d.q) // 256)
+    return 256 if ncol >= 256 and rows * -(-ncol // 256) >= 192 else 128
 
 
 class FamilyTimer:

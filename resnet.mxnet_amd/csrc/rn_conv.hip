@@ -583,6 +583,239 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
   }
 }
 
+// ------------------------------------------------------------------------------ igemm, 256-row tiles
+// The same implicit GEMM (fwd and dgrad classes, bf16 in / bf16 out, optional residual add) on a
+// 256 x BN tile run by 8 waves (2 along M x 4 along N, each 128 x BN/4): twice the MFMA work per
+// staged byte of the 128 x 128 kernel, one workgroup per CU. Both operands are staged by LDS-DMA
+// (buffer_load ... lds, 16 B per lane; padding / halo rows read zeros through an out-of-range
+// offset) issued from inline asm, so hipcc does not drain them before every ds_read: NBUF K-tile
+// buffers, NBUF-1 K-tiles in flight, one counted vmcnt + barrier per 64-deep K-tile. The epilogue
+// stages each wave's accumulators through LDS in two 64-row halves and writes 16-byte row chunks.
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ v4i make_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  v4i r;
+  r.x = (int)(uint32_t)a;
+  r.y = (int)((uint32_t)(a >> 32) & 0xFFFFu);  // stride 0
+  r.z = (int)bytes;
+  r.w = 0x00020000;
+  return r;
+}
+
+// one 16-byte LDS-DMA per lane into the wave-uniform LDS byte address lds (+16 * lane); M0 is
+// compiler-reserved, so it is saved and restored inside the statement
+__device__ __forceinline__ void dma16_asm(const v4i& rsrc, uint32_t lds, uint32_t voff) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(lds), "s"(rsrc)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+template <int BN, int NBUF>
+__global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
+  constexpr int BM = 256, CE = 8, BKE = 64;
+  constexpr int AR = BM / 64, BR = BN / 64;  // DMA rounds per K-tile (64 rows each)
+  constexpr int LPT = AR + BR;               // DMA instructions per thread per K-tile
+  constexpr int WN = BN / 4;                 // wave tile columns
+  constexpr int MI = 8, NI = WN / 16;        // 16x16 accumulators per wave
+  constexpr int kStage = (BM + BN) * 8;      // 16-byte chunks per K-tile
+  constexpr int EP_LD = WN + 4;              // staged fp32 row stride
+  constexpr int EP_WAVE = 64 * EP_LD;        // floats per wave per epilogue half
+  constexpr int kEpChunks = 8 * EP_WAVE / 4;
+  __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * kStage > kEpChunks ? NBUF * kStage : kEpChunks];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const IgemmCls& cl = p.cls[blockIdx.z];
+  const int Mc = p.N * cl.Pc * cl.Qc;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mtile = lid / p.ntn;
+  const int m0 = mtile * BM;
+  const int n0 = (lid - mtile * p.ntn) * BN;
+  if (m0 >= Mc) return;
+
+  // DMA lane -> (row 8*wid + lane/8 (+64 i), LDS slot lane&7); it fetches the source chunk that the
+  // XOR read-swizzle expects in that slot
+  const int lch = (lane & 7) ^ ((lane >> 3) & 7);
+  int a_row[AR], a_h[AR], a_w[AR];  // row offset of tap (0,0); its gathered coordinates
+#pragma unroll
+  for (int i = 0; i < AR; ++i) {
+    const int m = m0 + 64 * i + (tid >> 3);
+    if (m < Mc) {
+      const int n = fdiv(m, cl.fdPQ);
+      const int rem = m - n * cl.Pc * cl.Qc;
+      const int ii = fdiv(rem, cl.fdQ);
+      const int jj = rem - ii * cl.Qc;
+      a_h[i] = ii * p.hmul + cl.hb0 + cl.hoff0;
+      a_w[i] = jj * p.wmul + cl.wb0 + cl.woff0;
+      a_row[i] = ((n * p.H + a_h[i]) * p.W + a_w[i]) * p.C + lch * CE;  // may point before the image: masked
+    } else {
+      a_h[i] = -(1 << 28);  // never inside the image
+      a_w[i] = 0;
+      a_row[i] = 0;
+    }
+  }
+  int b_off[BR];
+  bool b_ok[BR];
+#pragma unroll
+  for (int i = 0; i < BR; ++i) {
+    const int col = n0 + 64 * i + (tid >> 3);
+    b_ok[i] = col < p.K;
+    b_off[i] = (b_ok[i] ? col : 0) * p.wrow + lch * CE;
+  }
+  const v4i rs_x = make_rsrc(p.x, (uint32_t)p.x_bytes);
+  const v4i rs_w = make_rsrc(p.w, (uint32_t)p.w_bytes);
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);  // this wave's 8 rows
+
+  const int ncb = (p.cblk + BKE - 1) / BKE;
+  const int nstage = cl.nr * cl.ns * ncb;
+  int st_tr = 0, st_ts = 0, st_cb = 0;
+  auto issue = [&](int buf) __attribute__((always_inline)) {
+    const int tr = st_tr, ts = st_ts, cb = st_cb;
+    if (++st_cb == ncb) {
+      st_cb = 0;
+      if (++st_ts == cl.ns) {
+        st_ts = 0;
+        ++st_tr;
+      }
+    }
+    const int c = cb * BKE + lch * CE;
+    const bool cok = c < p.cblk;
+    const int dh = p.hinc * tr, dw = p.winc * ts;
+    const int toffa = (dh * p.W + dw) * p.C + cb * BKE;
+    const int toffb = ((cl.r0 + p.rstep * tr) * p.S + cl.s0 + p.sstep * ts) * p.cblk + cb * BKE;
+    const uint32_t la = lds0 + buf * (kStage * 16);
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const bool ok = cok && (unsigned)(a_h[i] + dh) < (unsigned)p.H && (unsigned)(a_w[i] + dw) < (unsigned)p.W;
+      dma16_asm(rs_x, la + i * 8192, ok ? (uint32_t)((a_row[i] + toffa) * 2) : kOob);
+    }
+#pragma unroll
+    for (int i = 0; i < BR; ++i)
+      dma16_asm(rs_w, la + BM * 128 + i * 8192, (cok && b_ok[i]) ? (uint32_t)((b_off[i] + toffb) * 2) : kOob);
+  };
+
+  v4f acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const uint4* As = smem + buf * kStage;
+    const uint4* Bs = As + BM * 8;
+#pragma unroll
+    for (int slab = 0; slab < 2; ++slab) {
+      uint4 af[MI], bfr[NI];
+      const int kc = slab * 4 + (lane >> 4);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int row = wn * WN + j * 16 + (lane & 15);
+        bfr[j] = Bs[row * 8 + swz(row, kc)];
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int row = wm * 128 + i * 16 + (lane & 15);
+        af[i] = As[row * 8 + swz(row, kc)];
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) mfma_slab<bf16_t>(acc[i][j], af[i], bfr[j]);
+    }
+  };
+
+#pragma unroll
+  for (int s = 0; s < NBUF - 1; ++s)
+    if (s < nstage) issue(s);
+  for (int t = 0; t < nstage; ++t) {
+    // K-tile t has landed for this thread once at most the later K-tiles' DMAs are outstanding
+    if (NBUF == 3 && t + 1 < nstage) wait_vmcnt<LPT>();
+    else wait_vmcnt<0>();
+    __syncthreads();  // ... for every thread; and every wave is done reading the buffer refilled next
+    if (t + NBUF - 1 < nstage) issue((t + NBUF - 1) % NBUF);
+    compute(t % NBUF);
+  }
+  __syncthreads();  // the epilogue reuses the staging buffers
+
+  // ---- epilogue: per wave, 64 accumulator rows at a time through LDS, then 16-byte row chunks
+  constexpr int CPR = WN / 8;  // 16-byte output chunks per wave row
+  float* ep = reinterpret_cast<float*>(smem) + wid * EP_WAVE;
+  const bf16_t* __restrict__ ag = reinterpret_cast<const bf16_t*>(p.add);
+  bf16_t* __restrict__ yg = reinterpret_cast<bf16_t*>(p.y);
+  const int cc = lane % CPR;
+  const int col0 = n0 + wn * WN + cc * 8;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    int64_t off[CPR];  // this lane's rows: lane / CPR + (64 / CPR) k
+    uint4 addv[CPR];
+#pragma unroll
+    for (int k = 0; k < CPR; ++k) {
+      const int r = lane / CPR + (64 / CPR) * k;
+      const int m = m0 + wm * 128 + h * 64 + r;
+      off[k] = -1;
+      addv[k] = make_uint4(0, 0, 0, 0);
+      if (m < Mc && col0 < p.K) {
+        const int n = fdiv(m, cl.fdPQ);
+        const int rem = m - n * cl.Pc * cl.Qc;
+        const int ii = fdiv(rem, cl.fdQ);
+        const int jj = rem - ii * cl.Qc;
+        off[k] = ((int64_t)(n * p.P + cl.a + p.ostep_h * ii) * p.Q + cl.b + p.ostep_w * jj) * p.ldo + col0;
+        if (ag && col0 + 8 <= p.K) addv[k] = *reinterpret_cast<const uint4*>(ag + off[k]);
+      }
+    }
+    if (h > 0) __syncthreads();  // the first half's staged rows have been read
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) ep[(i * 16 + (lane >> 4) * 4 + e) * EP_LD + j * 16 + (lane & 15)] = acc[h * 4 + i][j][e];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CPR; ++k) {
+      if (off[k] < 0) continue;
+      const int r = lane / CPR + (64 / CPR) * k;
+      float v[8];
+      *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(ep + r * EP_LD + cc * 8);
+      *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(ep + r * EP_LD + cc * 8 + 4);
+      if (col0 + 8 <= p.K) {
+        if (ag) {
+          float a[8];
+          chunk_to_f(addv[k], a, (const bf16_t*)nullptr);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += a[e];
+        }
+        *reinterpret_cast<uint4*>(yg + off[k]) = f_to_chunk(v, (const bf16_t*)nullptr);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (col0 + e < p.K) {
+            float o = v[e];
+            if (ag) o += to_f(ag[off[k] + e]);
+            yg[off[k] + e] = from_f<bf16_t>(o);
+          }
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------ wgrad
 struct WgradArgs {
   const void* x;   // NHWC gathered (B operand)
@@ -1156,6 +1389,27 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   for (int z = 0; z < a.ncls; ++z) max_taps = std::max(max_taps, a.cls[z].nr * a.cls[z].ns);
   const bool dma = g_tune[RN_TUNE_IGEMM_DMA] > 0 && !a.in_sc && !b.diag_l1 && xb < INT32_MAX && wb < INT32_MAX &&
                    max_taps <= 64;
+  // 256-row tiles (rn_set_tuning 4: 0 auto, 1 off, 2 force 256x256, 3 force 256x128). Auto, from
+  // per-layer measurements over ResNet-50 (tools/conv_bench.py): 256x256 when the output has >= 256
+  // columns and the grid still has >= 192 tiles (one workgroup per CU; fewer leave too many CUs
+  // idle), else 256x128 when it has >= 128 columns, else the 128-row kernel.
+  const int big = g_tune[RN_TUNE_IGEMM_BIG];
+  if constexpr (std::is_same<T, bf16_t>::value && std::is_same<OutT, bf16_t>::value) {
+    const bool eligible = big != 1 && !a.in_sc && !a.stats && !a.bnred && !a.smallc && a.gred == 0 && !b.diag_l1 &&
+                          !a.bias && xb < INT32_MAX && wb < INT32_MAX && max_taps <= 32 && a.K >= 128;
+    if (eligible) {
+      int64_t rows = 0;  // 256-row tiles over all parity classes
+      for (int z = 0; z < a.ncls; ++z) rows += ceil_div((int64_t)a.N * a.cls[z].Pc * a.cls[z].Qc, 256);
+      int bn = (a.K >= 256 && rows * ceil_div(a.K, 256) >= 192) ? 256 : 128;
+      if (big == 2) bn = 256;
+      if (big == 3) bn = 128;
+      b.ntn = (int)ceil_div(a.K, bn);
+      dim3 grid((unsigned)(ceil_div(maxMc, 256) * b.ntn), 1, a.ncls);
+      if (bn == 256) hipLaunchKernelGGL((igemm_big_kernel<256, 2>), grid, dim3(512), 0, st, b);
+      else hipLaunchKernelGGL((igemm_big_kernel<128, 3>), grid, dim3(512), 0, st, b);
+      return rn_check_launch("igemm_big");
+    }
+  }
   if (a.K <= 64 || a.gred > 0) {  // grouped: the block width is RN_GROUP_BLOCK
     b.ntn = (int)ceil_div(a.K, 64);
     dim3 grid((unsigned)(ceil_div(maxMc, 128) * b.ntn), 1, a.ncls);

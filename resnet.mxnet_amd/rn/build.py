@@ -19,7 +19,8 @@ LIB_PATH = os.path.join(PKG_DIR, "librn.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
-            "-Wno-unused-result", "-munsafe-fp-atomics"]
+            "-Wno-unused-result", "-munsafe-fp-atomics",
+            "-mllvm", "-disable-promote-alloca-to-lds"]  # keep per-thread arrays out of the staging LDS
 
 
 def _sources():

@@ -609,3 +609,45 @@ def test_dgrad_bn_backward_fusion(gpu, dtype, case):
     assert rel_err(db.cpu().numpy()[:c], db_ref) < (1e-4 if dtype == F32 else 2e-2)
     assert rel_err(dg.cpu().numpy()[:c], dg_ref) < (1e-4 if dtype == F32 else 2e-2)
     assert rel_err(from_nhwc(dx, c), dx_ref) < (TOL[dtype] * 5 if dtype == F32 else 3e-2)
+
+
+BIG_CASES = [
+    # n, c, h, w, k, r, stride, pad: 256-row tiles (fwd when k >= 128, dgrad when c >= 128)
+    (2, 128, 14, 14, 256, 3, 1, 1),
+    (3, 256, 9, 11, 136, 3, 2, 1),     # ragged column tile, stride-2 dgrad classes
+    (2, 160, 13, 13, 384, 1, 2, 0),    # reduction 160: last 64-deep K-tile partly out of range
+    (1, 512, 7, 7, 512, 3, 1, 1),      # fewer rows than one tile
+    (4, 128, 28, 28, 128, 3, 1, 1),    # several row tiles
+]
+
+
+@pytest.mark.parametrize("mode", [2, 3])
+@pytest.mark.parametrize("case", BIG_CASES)
+def test_conv_big_tiles(gpu, mode, case):
+    """igemm_big_kernel (rn_set_tuning 4: 2 = 256x256, 3 = 256x128) for fwd + residual and dgrad."""
+    n, c, h, w, k, r, st, pd = case
+    x, wt = _conv_data(case, 5)
+    x, wt = bf16_round(x), bf16_round(wt)
+    P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+    rng = np.random.default_rng(6)
+    res = bf16_round(rng.standard_normal((n, k, P, Q)))
+    dy = bf16_round(rng.standard_normal((n, k, P, Q)))
+    ref = ops.conv2d_fwd(x, wt, (st, st), (pd, pd)) + res
+    dx_ref, _ = ops.conv2d_bwd(x, wt, dy, (st, st), (pd, pd))
+    d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd)
+    wk = torch.zeros(k * r * r * d.c, dtype=torch.bfloat16, device=gpu)
+    wc = torch.zeros(d.c * r * r * d.k_pad, dtype=torch.bfloat16, device=gpu)
+    wm = _master_krsc(wt, gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(wm), p(wk), p(wc), stream())
+    y = torch.zeros((n, P, Q, d.k_pad), dtype=torch.bfloat16, device=gpu)
+    dx = torch.zeros((n, h, w, d.c), dtype=torch.bfloat16, device=gpu)
+    xd, rd, dyd = to_nhwc(x, BF16, gpu), to_nhwc(res, BF16, gpu), to_nhwc(dy, BF16, gpu)  # alive across the calls
+    L.call("rn_set_tuning", 4, mode)
+    try:
+        L.call("rn_conv_fwd", C.byref(d), p(xd), p(wk), p(y), BF16, p(rd), None, stream())
+        L.call("rn_conv_bwd_data", C.byref(d), p(dyd), p(wc), p(dx), None, stream())
+        torch.cuda.synchronize()
+    finally:
+        L.call("rn_set_tuning", 4, 0)
+    assert rel_err(from_nhwc(y, k), ref) < TOL[BF16]
+    assert rel_err(from_nhwc(dx, c), dx_ref) < TOL[BF16]

@@ -10,6 +10,9 @@ import csv, json, re, sys, collections
 
 
 def family(name):
+    m = re.search(r"igemm_big_kernel<(\d+),", name)
+    if m:
+        return "igemm_big_kernel<256x%s>" % m.group(1)
     m = re.search(r"(igemm_kernel|wgrad_kernel)<([^>]*)>", name)
     if m:
         args = [a.strip() for a in m.group(2).split(",")]
