@@ -595,10 +595,10 @@ typedef int v4i __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ v4i make_rsrc(const void* base, uint32_t bytes) {
   const uint64_t a = (uint64_t)base;
-  v4i r;
-  r.x = (int)(uint32_t)a;
-  r.y = (int)((uint32_t)(a >> 32) & 0xFFFFu);  // stride 0
-  r.z = (int)bytes;
+  v4i r;  // readfirstlane: provably wave-uniform, so the asm "s" operand gets SGPRs
+  r.x = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r.y = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xFFFFu));  // stride 0
+  r.z = __builtin_amdgcn_readfirstlane((int)bytes);
   r.w = 0x00020000;
   return r;
 }
@@ -607,6 +607,7 @@ __device__ __forceinline__ v4i make_rsrc(const void* base, uint32_t bytes) {
 // compiler-reserved, so it is saved and restored inside the statement
 __device__ __forceinline__ void dma16_asm(const v4i& rsrc, uint32_t lds, uint32_t voff) {
   uint32_t keep;
+  lds = __builtin_amdgcn_readfirstlane(lds);  // free when already scalar; M0 is written by an SALU move
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %2\n\t"
@@ -615,6 +616,24 @@ __device__ __forceinline__ void dma16_asm(const v4i& rsrc, uint32_t lds, uint32_
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(voff), "s"(lds), "s"(rsrc)
+      : "memory");
+}
+
+// the same through global_load_lds_dwordx4 with a per-lane 64-bit source address (no buffer
+// descriptor in SGPRs); masked lanes read a zero chunk
+__device__ __attribute__((aligned(16))) const uint4 g_zero_chunk = {0u, 0u, 0u, 0u};
+
+__device__ __forceinline__ void dma16_global(const void* src, uint32_t lds) {
+  uint32_t keep;
+  lds = __builtin_amdgcn_readfirstlane(lds);
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
       : "memory");
 }
 
@@ -1067,6 +1086,164 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
       }
     }
   }
+}
+
+// ------------------------------------------------------------------------------ wgrad, big tiles
+// dW[k0..+BMK][n0..+256] += dy^T * gather(x) over one M range, 8 waves (2 along k x 4 along the
+// columns), bf16, dense, unpadded channels. Both operands are staged by inline-asm LDS-DMA into
+// [64 m][row] images whose 16-byte chunks are XOR-swizzled (swz_tr) by choosing each lane's SOURCE
+// chunk, and read with ds_read_b64_tr_b16 as in wgrad_kernel. NBUF buffers, NBUF-1 M-tiles in flight.
+template <int BMK, int NBUF>
+__global__ __launch_bounds__(512, 1) void wgrad_big_kernel(WgradArgs p) {
+  constexpr int BNC = 256, CE = 8, BKM = 64;
+  constexpr int A_CPR = BMK / 8, B_CPR = BNC / 8;      // 16-byte chunks per LDS row
+  constexpr int A_RPI = 64 / A_CPR, B_RPI = 64 / B_CPR;  // rows per 1 KiB DMA instruction
+  constexpr int AR = BKM / A_RPI / 8, BR = BKM / B_RPI / 8;  // DMA instructions per wave per M-tile
+  constexpr int LPT = AR + BR;
+  constexpr int MI = BMK / 32, NI = 4;
+  constexpr int A_SZ = BKM * A_CPR, B_SZ = BKM * B_CPR;  // chunks
+  constexpr int kStage = A_SZ + B_SZ;
+  __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * kStage];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 2, wn = wid & 3;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int per_split = p.nct * p.nkt;
+  const int zs = lid / per_split;
+  const int rem0 = lid - zs * per_split;
+  const int kt = rem0 / p.nct;
+  const int n0 = (rem0 - kt * p.nct) * BNC;
+  const int k0 = kt * BMK;
+  const int mbeg = zs * p.m_per_split;
+  const int mend = min(p.M, mbeg + p.m_per_split);
+  if (mbeg >= mend) return;
+
+  // per-lane DMA rows (fixed within an M-tile) and source chunks
+  int a_row[AR], a_col[AR];
+#pragma unroll
+  for (int j = 0; j < AR; ++j) {
+    a_row[j] = (wid * AR + j) * A_RPI + lane / A_CPR;
+    const int slot = lane % A_CPR;
+    const int k = k0 + 8 * (slot ^ (swz_tr(a_row[j]) & (A_CPR - 1)));
+    a_col[j] = k < p.ldy ? k : -1;
+  }
+  int b_row[BR], b_h[BR], b_w[BR], b_ch[BR];
+#pragma unroll
+  for (int j = 0; j < BR; ++j) {
+    b_row[j] = (wid * BR + j) * B_RPI + lane / B_CPR;
+    const int slot = lane % B_CPR;
+    const int col = n0 + 8 * (slot ^ (swz_tr(b_row[j]) & (B_CPR - 1)));
+    if (col < p.ncol_load) {
+      const int tap = fdiv(col, p.fdC);
+      b_ch[j] = col - tap * p.C;
+      const int r = fdiv(tap, p.fdS);
+      b_h[j] = r - p.ph;
+      b_w[j] = tap - r * p.S - p.pw;
+    } else {
+      b_ch[j] = -1;
+      b_h[j] = b_w[j] = 0;
+    }
+  }
+  const char* __restrict__ dyb = reinterpret_cast<const char*>(p.dy);
+  const char* __restrict__ xb = reinterpret_cast<const char*>(p.x);
+  const char* zb = reinterpret_cast<const char*>(&g_zero_chunk);
+  const uint32_t lds_a = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * AR * 1024);  // this wave's pieces
+  const uint32_t lds_b = __builtin_amdgcn_readfirstlane(lds_addr(smem) + A_SZ * 16 + wid * BR * 1024);
+
+  // branch-free (selects only), 32-bit byte offsets (both tensors < 4 GiB, host-checked), so the
+  // compiler can interleave it with the MFMAs of the slab it is placed between
+  auto issue = [&](int mb, int buf) __attribute__((always_inline)) {
+    const uint32_t la = buf * (kStage * 16);
+#pragma unroll
+    for (int j = 0; j < AR; ++j) {
+      const int m = mb + a_row[j];
+      const bool ok = a_col[j] >= 0 && m < mend;
+      const uint32_t off = (uint32_t)(m * p.ldy + a_col[j]) * 2u;
+      dma16_global(ok ? (const void*)(dyb + off) : (const void*)zb, lds_a + la + j * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < BR; ++j) {
+      const int m = mb + b_row[j];
+      const int n = fdiv(m, p.fdPQ);
+      const int rem = m - n * p.P * p.Q;
+      const int pp = fdiv(rem, p.fdQ);
+      const int qq = rem - pp * p.Q;
+      const int hin = pp * p.sh + b_h[j];
+      const int win = qq * p.sw + b_w[j];
+      const bool ok = b_ch[j] >= 0 && m < mend && (unsigned)hin < (unsigned)p.H && (unsigned)win < (unsigned)p.W;
+      const uint32_t off = (uint32_t)(((n * p.H + hin) * p.W + win) * p.C + b_ch[j]) * 2u;
+      dma16_global(ok ? (const void*)(xb + off) : (const void*)zb, lds_b + la + j * 1024);
+    }
+  };
+
+  v4f acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int buf, int slab) __attribute__((always_inline)) {
+    const char* Ab = reinterpret_cast<const char*>(smem + buf * kStage);
+    const char* Bb = Ab + A_SZ * 16;
+    const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+    {
+      v8s af[MI], bfv[NI];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = slab * 32 + 8 * g + 4 * h + q;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int col = wn * 64 + j * 16 + 4 * pp;
+          const int byte = row * (B_CPR * 16) + ((((col * 2) >> 4) ^ (swz_tr(row) & (B_CPR - 1))) << 4) + ((col * 2) & 15);
+          v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(Bb + byte));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bfv[j][4 * h + e] = v[e];
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int col = wm * (BMK / 2) + i * 16 + 4 * pp;
+          const int byte = row * (A_CPR * 16) + ((((col * 2) >> 4) ^ (swz_tr(row) & (A_CPR - 1))) << 4) + ((col * 2) & 15);
+          v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(Ab + byte));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) af[i][4 * h + e] = v[e];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  const int nstage = (mend - mbeg + BKM - 1) / BKM;
+#pragma unroll
+  for (int s = 0; s < NBUF - 1; ++s) issue(mbeg + s * BKM, s);
+  for (int t = 0; t < nstage; ++t) {
+    if (NBUF == 3) wait_vmcnt<LPT>();  // the later M-tile's DMAs (real or past the range) may stay in flight
+    else wait_vmcnt<0>();
+    __syncthreads();
+    compute(t % NBUF, 0);
+    // unconditional (past the range every lane reads the zero chunk into a buffer nobody reads):
+    // no branch, so the address arithmetic can interleave with slab 0's MFMAs
+    issue(mbeg + (t + NBUF - 1) * BKM, (t + NBUF - 1) % NBUF);
+    compute(t % NBUF, 1);
+  }
+  wait_vmcnt<0>();
+
+  // D[row = k][col] -> fp32 atomic add into dw (dense, unpadded: ldw = ncol)
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = k0 + wm * (BMK / 2) + i * 16 + (lane >> 4) * 4 + e;
+      if (k >= p.K) continue;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = n0 + wn * 64 + j * 16 + (lane & 15);
+        if (col < p.ncol) atomicAdd(p.dw + (int64_t)k * p.ldw + col, acc[i][j][e]);
+      }
+    }
 }
 
 // ------------------------------------------------------------------------------ helpers
@@ -1563,6 +1740,29 @@ int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, f
   a.M = d->n * d->p * d->q;
   a.fdQ = make_fastdiv(d->q); a.fdPQ = make_fastdiv(d->p * d->q);
   a.fdC = make_fastdiv(a.cblk); a.fdS = make_fastdiv(d->s);
+  hipStream_t st = as_stream(stream);
+  // 256-column, 8-wave LDS-DMA tiles (rn_set_tuning 5: 1 = on, default off) for dense bf16 layers
+  // with >= 128 output channels and >= 256 columns; the M range is split so that the grid is one
+  // round of one workgroup per CU, with >= 4 M-tiles per workgroup. Measured slower than the
+  // 128-tile kernel on every ResNet-50 layer: with the M split, the fp32 atomic epilogue issues
+  // (workgroups x tile area) adds, 4x more per workgroup at 256x256, and that dominates the
+  // small-M layers (stage 3-4).
+  if (d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c && a.K >= 128 && a.ncol_load >= 256 &&
+      g_tune[RN_TUNE_WGRAD_BIG] == 1 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX &&
+      (int64_t)a.M * a.ldy < INT32_MAX) {
+    const int bmk = a.K >= 256 ? 256 : 128;
+    a.nct = (int)ceil_div(a.ncol_load, 256);
+    a.nkt = (int)ceil_div(a.K, bmk);
+    const int64_t tiles = (int64_t)a.nct * a.nkt;
+    const int64_t mtiles = ceil_div(a.M, 64);
+    int64_t split = std::min<int64_t>(std::max<int64_t>(1, 256 / tiles), std::max<int64_t>(1, mtiles / 4));
+    a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
+    split = ceil_div(a.M, a.m_per_split);
+    dim3 grid((unsigned)(tiles * split));
+    if (bmk == 256) hipLaunchKernelGGL((wgrad_big_kernel<256, 2>), grid, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_big_kernel<128, 3>), grid, dim3(512), 0, st, a);
+    return rn_check_launch("wgrad_big");
+  }
   // 64-wide tiles where K or the column count is <= 64 (stage-1 layers): a 128 tile would spend
   // half (or three quarters) of its MFMAs on zero rows / columns
   const int bmk = (grouped || a.K <= 64) ? 64 : 128;
@@ -1584,7 +1784,6 @@ int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, f
   a.nct = (int)ceil_div(a.ncol_load, bnc);
   a.nkt = (int)ceil_div(a.K, bmk);
   dim3 grid((unsigned)(a.nct * a.nkt * split));
-  hipStream_t st = as_stream(stream);
   if (grouped) {
     if (d->dtype == RN_BF16)
       hipLaunchKernelGGL((wgrad_kernel<bf16_t, RN_GROUP_BLOCK, RN_GROUP_BLOCK>), grid, dim3(256), 0, st, a);

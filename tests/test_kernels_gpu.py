@@ -618,13 +618,15 @@ BIG_CASES = [
     (2, 160, 13, 13, 384, 1, 2, 0),    # reduction 160: last 64-deep K-tile partly out of range
     (1, 512, 7, 7, 512, 3, 1, 1),      # fewer rows than one tile
     (4, 128, 28, 28, 128, 3, 1, 1),    # several row tiles
+    (8, 256, 16, 16, 512, 1, 2, 0),    # wgrad: M split over several workgroups
 ]
 
 
 @pytest.mark.parametrize("mode", [2, 3])
 @pytest.mark.parametrize("case", BIG_CASES)
 def test_conv_big_tiles(gpu, mode, case):
-    """igemm_big_kernel (rn_set_tuning 4: 2 = 256x256, 3 = 256x128) for fwd + residual and dgrad."""
+    """igemm_big_kernel (rn_set_tuning 4: 2 = 256x256, 3 = 256x128) for fwd + residual and dgrad;
+    wgrad_big_kernel (rn_set_tuning 5 = 1; >= 128 output channels, >= 256 columns) for the weight gradient."""
     n, c, h, w, k, r, st, pd = case
     x, wt = _conv_data(case, 5)
     x, wt = bf16_round(x), bf16_round(wt)
@@ -633,7 +635,7 @@ def test_conv_big_tiles(gpu, mode, case):
     res = bf16_round(rng.standard_normal((n, k, P, Q)))
     dy = bf16_round(rng.standard_normal((n, k, P, Q)))
     ref = ops.conv2d_fwd(x, wt, (st, st), (pd, pd)) + res
-    dx_ref, _ = ops.conv2d_bwd(x, wt, dy, (st, st), (pd, pd))
+    dx_ref, dw_ref = ops.conv2d_bwd(x, wt, dy, (st, st), (pd, pd))
     d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd)
     wk = torch.zeros(k * r * r * d.c, dtype=torch.bfloat16, device=gpu)
     wc = torch.zeros(d.c * r * r * d.k_pad, dtype=torch.bfloat16, device=gpu)
@@ -641,13 +643,19 @@ def test_conv_big_tiles(gpu, mode, case):
     L.call("rn_conv_weight_pack", C.byref(d), p(wm), p(wk), p(wc), stream())
     y = torch.zeros((n, P, Q, d.k_pad), dtype=torch.bfloat16, device=gpu)
     dx = torch.zeros((n, h, w, d.c), dtype=torch.bfloat16, device=gpu)
+    dw = torch.zeros(k * r * r * c, dtype=torch.float32, device=gpu)
     xd, rd, dyd = to_nhwc(x, BF16, gpu), to_nhwc(res, BF16, gpu), to_nhwc(dy, BF16, gpu)  # alive across the calls
     L.call("rn_set_tuning", 4, mode)
+    L.call("rn_set_tuning", 5, 1)
     try:
         L.call("rn_conv_fwd", C.byref(d), p(xd), p(wk), p(y), BF16, p(rd), None, stream())
         L.call("rn_conv_bwd_data", C.byref(d), p(dyd), p(wc), p(dx), None, stream())
+        L.call("rn_conv_bwd_filter", C.byref(d), p(xd), p(dyd), p(dw), stream())  # wgrad_big_kernel when eligible
         torch.cuda.synchronize()
     finally:
         L.call("rn_set_tuning", 4, 0)
+        L.call("rn_set_tuning", 5, 0)
     assert rel_err(from_nhwc(y, k), ref) < TOL[BF16]
     assert rel_err(from_nhwc(dx, c), dx_ref) < TOL[BF16]
+    dw_h = dw.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2)
+    assert rel_err(dw_h, dw_ref) < 5e-3
