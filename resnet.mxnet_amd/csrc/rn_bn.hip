@@ -191,28 +191,40 @@ __global__ __launch_bounds__(256) void bn_part_merge_kernel(const float* __restr
   }
 }
 
-__global__ __launch_bounds__(64) void bn_fwd_finalize_part_kernel(const double* __restrict__ part2, int ngrp,
-                                                                  int64_t m, int c, int c_real, float eps,
-                                                                  float momentum, int fix_gamma,
-                                                                  const float* __restrict__ gamma,
-                                                                  const float* __restrict__ beta,
-                                                                  float* moving_mean, float* moving_var,
-                                                                  float* save_mean, float* save_invstd,
-                                                                  float* scale, float* shift) {
-  const int ch = blockIdx.x * 64 + threadIdx.x;
-  if (ch >= c) return;
+__global__ __launch_bounds__(256) void bn_fwd_finalize_part_kernel(const double* __restrict__ part2, int ngrp,
+                                                                   int64_t m, int c, int c_real, float eps,
+                                                                   float momentum, int fix_gamma,
+                                                                   const float* __restrict__ gamma,
+                                                                   const float* __restrict__ beta,
+                                                                   float* moving_mean, float* moving_var,
+                                                                   float* save_mean, float* save_invstd,
+                                                                   float* scale, float* shift) {
+  // 4 threads per channel walk the groups (latency-bound loop: more of them in flight), then an LDS sum
+  const int ch = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int sub = threadIdx.x >> 6;
+  __shared__ double red[2][4][64];
+  double s1 = 0.0, s2 = 0.0, q = 0.0;
+  if (ch < c) {
+    q = part2[3 * c + ch];  // group 0's pivot
+    for (int gi = sub; gi < ngrp; gi += 4) {
+      const double* pg = part2 + (int64_t)gi * 4 * c + ch;
+      const double d = pg[3 * c] - q, a = pg[0], nb = pg[2 * c];
+      s1 += a + nb * d;
+      s2 += pg[c] + 2.0 * d * a + nb * d * d;
+    }
+  }
+  red[0][sub][threadIdx.x & 63] = s1;
+  red[1][sub][threadIdx.x & 63] = s2;
+  __syncthreads();
+  if (sub != 0 || ch >= c) return;
+  for (int t = 1; t < 4; ++t) {
+    s1 += red[0][t][threadIdx.x];
+    s2 += red[1][t][threadIdx.x];
+  }
   if (ch >= c_real) {
     scale[ch] = 0.f;
     shift[ch] = 0.f;
     return;
-  }
-  const double q = part2[3 * c + ch];  // group 0's pivot
-  double s1 = 0.0, s2 = 0.0;
-  for (int gi = 0; gi < ngrp; ++gi) {
-    const double* pg = part2 + (int64_t)gi * 4 * c + ch;
-    const double d = pg[3 * c] - q, a = pg[0], nb = pg[2 * c];
-    s1 += a + nb * d;
-    s2 += pg[c] + 2.0 * d * a + nb * d * d;
   }
   const double md = s1 / (double)m;
   const double mean = q + md;
@@ -609,7 +621,7 @@ int rn_bn_fwd_train_part(const rn_bn_desc* d, const float* part, int64_t nblk, i
   double* part2 = reinterpret_cast<double*>(ws);
   hipLaunchKernelGGL(bn_part_merge_kernel, dim3((d->c + 63) / 64, ngrp), dim3(256), 0, st, part, (int)nblk, d->m,
                      rows_blk, ld, d->c, part2);
-  hipLaunchKernelGGL(bn_fwd_finalize_part_kernel, dim3((d->c + 63) / 64), dim3(64), 0, st, part2, ngrp, d->m, d->c,
+  hipLaunchKernelGGL(bn_fwd_finalize_part_kernel, dim3((d->c + 63) / 64), dim3(256), 0, st, part2, ngrp, d->m, d->c,
                      d->c_real, d->eps, d->momentum, d->fix_gamma, gamma, beta, moving_mean, moving_var, save_mean,
                      save_invstd, scale, shift);
   if (rn_check_launch("bn_fwd_finalize_part")) return -1;

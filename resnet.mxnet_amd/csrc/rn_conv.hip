@@ -55,6 +55,7 @@ struct IgemmArgs {
   int ntn;             // n tiles (grid = m tiles * ntn)
   int smallc, lgc, rs; // fwd over C < one stage (the stem's 8 channels): k = tap*C + c flattened
   int diag_l1;         // diagnostic (rn_set_tuning 3): every A row reads the same L1-resident chunk
+  int sched;           // igemm_big_kernel schedule experiments (rn_set_tuning 7, bit mask)
   int x_bytes, w_bytes;  // LDS-DMA buffer descriptors
   // dgrad only, nullable: the BatchNorm-backward reduction of the gradient this conv completes
   // (sum dz, sum dz*(x - mean), dz = dy * relu'(bn(x))) per output block -> bnred[blk][ldo][2]
@@ -646,7 +647,10 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
-template <int BN, int NBUF>
+// EPI: 0 plain; 1 (fwd) BatchNorm statistics of the stored output per 128-row half (one wave row):
+// part[2*mtile + wm][S1 | S2 | pivot][ldo], as igemm_kernel's bn_stats_epilogue; 2 (dgrad) the
+// BatchNorm-backward reduction of the stored gradient: bnred[class][2*mtile + wm][ldo][2].
+template <int BN, int NBUF, int EPI = 0>
 __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
   constexpr int BM = 256, CE = 8, BKE = 64;
   constexpr int AR = BM / 64, BR = BN / 64;  // DMA rounds per K-tile (64 rows each)
@@ -667,7 +671,18 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
   const int mtile = lid / p.ntn;
   const int m0 = mtile * BM;
   const int n0 = (lid - mtile * p.ntn) * BN;
-  if (m0 >= Mc) return;
+  if (m0 >= Mc) {  // (a dgrad parity class with fewer rows): empty BN-reduction partials
+    if constexpr (EPI == 2)
+      for (int e = tid; e < 2 * BN; e += 512) {
+        const int hh = e / BN, col = n0 + e % BN;
+        if (col < p.ldo && 2 * mtile + hh < p.mt_max) {
+          float* dst = p.bnred + ((int64_t)(blockIdx.z * p.mt_max + 2 * mtile + hh) * p.ldo + col) * 2;
+          dst[0] = 0.f;
+          dst[1] = 0.f;
+        }
+      }
+    return;
+  }
 
   // DMA lane -> (row 8*wid + lane/8 (+64 i), LDS slot lane&7); it fetches the source chunk that the
   // XOR read-swizzle expects in that slot
@@ -704,9 +719,17 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
 
   const int ncb = (p.cblk + BKE - 1) / BKE;
   const int nstage = cl.nr * cl.ns * ncb;
-  int st_tr = 0, st_ts = 0, st_cb = 0;
-  auto issue = [&](int buf) __attribute__((always_inline)) {
+  int st_tr = 0, st_ts = 0, st_cb = 0, st_n = 0;
+  // one K-tile's DMAs: prep() fixes the tile's uniform offsets, piece(k) issues DMA k (A rounds
+  // first, then B). A tile past the range issues zero-fill DMAs (kOob) into a buffer nobody reads,
+  // so the main loop has no branch around them.
+  int d_toffa = 0, d_toffb = 0, d_dh = 0, d_dw = 0;
+  bool d_cok = false;
+  uint32_t d_la = 0;
+  const uint32_t dmask = (p.sched & 2) ? 0xFFF0u : 0xFFFFFFFFu;  // diagnostic: L2-resident sources
+  auto prep = [&](int buf) __attribute__((always_inline)) {
     const int tr = st_tr, ts = st_ts, cb = st_cb;
+    const bool live = st_n++ < nstage;
     if (++st_cb == ncb) {
       st_cb = 0;
       if (++st_ts == cl.ns) {
@@ -714,20 +737,27 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
         ++st_tr;
       }
     }
-    const int c = cb * BKE + lch * CE;
-    const bool cok = c < p.cblk;
-    const int dh = p.hinc * tr, dw = p.winc * ts;
-    const int toffa = (dh * p.W + dw) * p.C + cb * BKE;
-    const int toffb = ((cl.r0 + p.rstep * tr) * p.S + cl.s0 + p.sstep * ts) * p.cblk + cb * BKE;
-    const uint32_t la = lds0 + buf * (kStage * 16);
-#pragma unroll
-    for (int i = 0; i < AR; ++i) {
-      const bool ok = cok && (unsigned)(a_h[i] + dh) < (unsigned)p.H && (unsigned)(a_w[i] + dw) < (unsigned)p.W;
-      dma16_asm(rs_x, la + i * 8192, ok ? (uint32_t)((a_row[i] + toffa) * 2) : kOob);
+    d_cok = live && cb * BKE + lch * CE < p.cblk;
+    d_dh = p.hinc * tr;
+    d_dw = p.winc * ts;
+    d_toffa = (d_dh * p.W + d_dw) * p.C + cb * BKE;
+    d_toffb = ((cl.r0 + p.rstep * tr) * p.S + cl.s0 + p.sstep * ts) * p.cblk + cb * BKE;
+    d_la = lds0 + buf * (kStage * 16);
+  };
+  auto piece = [&](int k) __attribute__((always_inline)) {
+    if (k < AR) {
+      const bool ok = d_cok && (unsigned)(a_h[k] + d_dh) < (unsigned)p.H && (unsigned)(a_w[k] + d_dw) < (unsigned)p.W;
+      dma16_asm(rs_x, d_la + k * 8192, ok ? ((uint32_t)((a_row[k] + d_toffa) * 2) & dmask) : kOob);
+    } else {
+      const int i = k - AR;
+      dma16_asm(rs_w, d_la + BM * 128 + i * 8192,
+                (d_cok && b_ok[i]) ? ((uint32_t)((b_off[i] + d_toffb) * 2) & dmask) : kOob);
     }
+  };
+  auto issue = [&](int buf) __attribute__((always_inline)) {
+    prep(buf);
 #pragma unroll
-    for (int i = 0; i < BR; ++i)
-      dma16_asm(rs_w, la + BM * 128 + i * 8192, (cok && b_ok[i]) ? (uint32_t)((b_off[i] + toffb) * 2) : kOob);
+    for (int k = 0; k < LPT; ++k) piece(k);
   };
 
   v4f acc[MI][NI];
@@ -736,6 +766,8 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
 
+  // the MFMAs of K-tile `buf`, with the next K-tile's DMAs between the first MFMA groups
+  // (inline asm is a scheduling boundary: each DMA's address arithmetic overlaps the MFMAs around it)
   auto compute = [&](int buf) __attribute__((always_inline)) {
     const uint4* As = smem + buf * kStage;
     const uint4* Bs = As + BM * 8;
@@ -754,23 +786,32 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
         af[i] = As[row * 8 + swz(row, kc)];
       }
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
+      for (int i = 0; i < MI; ++i) {
 #pragma unroll
         for (int j = 0; j < NI; ++j) mfma_slab<bf16_t>(acc[i][j], af[i], bfr[j]);
+        // 256x256 (2 buffers): the DMAs early (slab 0) so they have the longest to land; 256x128
+        // (3 buffers, one more K-tile in flight): spread over both slabs. Measured per layer.
+        const int step = slab * MI + i;
+        if (NBUF == 2 ? step < LPT : ((step & 1) && (step >> 1) < LPT)) piece(NBUF == 2 ? step : step >> 1);
+      }
     }
   };
 
 #pragma unroll
-  for (int s = 0; s < NBUF - 1; ++s)
-    if (s < nstage) issue(s);
+  for (int s = 0; s < NBUF - 1; ++s) issue(s);
   for (int t = 0; t < nstage; ++t) {
     // K-tile t has landed for this thread once at most the later K-tiles' DMAs are outstanding
-    if (NBUF == 3 && t + 1 < nstage) wait_vmcnt<LPT>();
-    else wait_vmcnt<0>();
-    __syncthreads();  // ... for every thread; and every wave is done reading the buffer refilled next
-    if (t + NBUF - 1 < nstage) issue((t + NBUF - 1) % NBUF);
+    if (!(p.sched & 4)) {  // (diagnostic bit 4: no wait, no barrier -- wrong results)
+      if (NBUF == 3) wait_vmcnt<LPT>();
+      else wait_vmcnt<0>();
+      __syncthreads();  // ... for every thread; and every wave is done reading the buffer refilled next
+    }
+    prep((t + NBUF - 1) % NBUF);
+    if (p.sched & 1) __builtin_amdgcn_s_setprio(1);
     compute(t % NBUF);
+    if (p.sched & 1) __builtin_amdgcn_s_setprio(0);
   }
+  wait_vmcnt<0>();  // the zero-fill DMAs past the range land before the epilogue reuses the buffers
   __syncthreads();  // the epilogue reuses the staging buffers
 
   // ---- epilogue: per wave, 64 accumulator rows at a time through LDS, then 16-byte row chunks
@@ -780,16 +821,34 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
   bf16_t* __restrict__ yg = reinterpret_cast<bf16_t*>(p.y);
   const int cc = lane % CPR;
   const int col0 = n0 + wn * WN + cc * 8;
+  const bool half_ok = m0 + wm * 128 < Mc;  // this wave row holds at least one output row
+  // BatchNorm partials of this lane's 8 columns (EPI 1: S1, S2 about the pivot; EPI 2: sum dz,
+  // sum dz * (x - mean)), over its rows; the lanes sharing a column chunk are summed at the end
+  constexpr int NS = EPI ? 8 : 1;
+  float s1[NS], s2[NS], piv[NS], r_mu[NS], r_sc[NS], r_sh[NS];
+#pragma unroll
+  for (int e = 0; e < NS; ++e) {
+    s1[e] = s2[e] = piv[e] = r_mu[e] = r_sc[e] = r_sh[e] = 0.f;
+    if constexpr (EPI == 2) {
+      const bool okc = col0 + e < p.K;
+      r_mu[e] = okc ? p.bn_mean[col0 + e] : 0.f;
+      r_sc[e] = okc ? p.bn_sc[col0 + e] : 0.f;
+      r_sh[e] = okc ? p.bn_sh[col0 + e] : 0.f;
+    }
+  }
+  const bf16_t* __restrict__ bxg = reinterpret_cast<const bf16_t*>(p.bn_x);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     int64_t off[CPR];  // this lane's rows: lane / CPR + (64 / CPR) k
     uint4 addv[CPR];
+    uint4 xpre[EPI == 2 ? CPR : 1];  // BN input at the same positions (EPI 2), loaded with the residual
 #pragma unroll
     for (int k = 0; k < CPR; ++k) {
       const int r = lane / CPR + (64 / CPR) * k;
       const int m = m0 + wm * 128 + h * 64 + r;
       off[k] = -1;
       addv[k] = make_uint4(0, 0, 0, 0);
+      if constexpr (EPI == 2) xpre[k] = make_uint4(0, 0, 0, 0);
       if (m < Mc && col0 < p.K) {
         const int n = fdiv(m, cl.fdPQ);
         const int rem = m - n * cl.Pc * cl.Qc;
@@ -797,6 +856,8 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
         const int jj = rem - ii * cl.Qc;
         off[k] = ((int64_t)(n * p.P + cl.a + p.ostep_h * ii) * p.Q + cl.b + p.ostep_w * jj) * p.ldo + col0;
         if (ag && col0 + 8 <= p.K) addv[k] = *reinterpret_cast<const uint4*>(ag + off[k]);
+        if constexpr (EPI == 2)
+          if (col0 + 8 <= p.K) xpre[k] = *reinterpret_cast<const uint4*>(bxg + off[k]);
       }
     }
     if (h > 0) __syncthreads();  // the first half's staged rows have been read
@@ -807,6 +868,12 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) ep[(i * 16 + (lane >> 4) * 4 + e) * EP_LD + j * 16 + (lane & 15)] = acc[h * 4 + i][j][e];
     __syncthreads();
+    if constexpr (EPI == 1) {
+      if (h == 0) {  // pivot: the wave row's first (rounded) conv value of each column
+#pragma unroll
+        for (int e = 0; e < 8; ++e) piv[e] = to_f(from_f<bf16_t>(ep[cc * 8 + e]));
+      }
+    }
 #pragma unroll
     for (int k = 0; k < CPR; ++k) {
       if (off[k] < 0) continue;
@@ -821,7 +888,29 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += a[e];
         }
-        *reinterpret_cast<uint4*>(yg + off[k]) = f_to_chunk(v, (const bf16_t*)nullptr);
+        const uint4 out = f_to_chunk(v, (const bf16_t*)nullptr);
+        *reinterpret_cast<uint4*>(yg + off[k]) = out;
+        if constexpr (EPI != 0) {  // on the stored (rounded) values, as a separate pass would read them
+          float g[8];
+          chunk_to_f(out, g, (const bf16_t*)nullptr);
+          if constexpr (EPI == 1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float d = g[e] - piv[e];
+              s1[e] += d;
+              s2[e] = fmaf(d, d, s2[e]);
+            }
+          } else {
+            float xv[8];
+            chunk_to_f(xpre[EPI == 2 ? k : 0], xv, (const bf16_t*)nullptr);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float dz = (!p.bn_relu || fmaf(xv[e], r_sc[e], r_sh[e]) > 0.f) ? g[e] : 0.f;
+              s1[e] += dz;
+              s2[e] = fmaf(dz, xv[e] - r_mu[e], s2[e]);
+            }
+          }
+        }
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e)
@@ -830,6 +919,37 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
             if (ag) o += to_f(ag[off[k] + e]);
             yg[off[k] + e] = from_f<bf16_t>(o);
           }
+      }
+    }
+  }
+  if constexpr (EPI != 0) {
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += __shfl_xor(s1[e], o, 64);
+        s2[e] += __shfl_xor(s2[e], o, 64);
+      }
+    if (lane < CPR) {
+      const int c0 = n0 + wn * WN + lane * 8;
+      const int blk = 2 * mtile + wm;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int col = c0 + e;
+        if (col >= p.ldo) continue;
+        const bool okc = col < p.K;
+        if constexpr (EPI == 1) {
+          if (half_ok) {
+            float* dst = p.stats + (int64_t)blk * 3 * p.ldo + col;
+            dst[0] = okc ? s1[e] : 0.f;
+            dst[p.ldo] = okc ? s2[e] : 0.f;
+            dst[2 * p.ldo] = piv[e];
+          }
+        } else if (blk < p.mt_max) {  // (a half past the class's rows may lie past its partial slots)
+          float* dst = p.bnred + ((int64_t)(blockIdx.z * p.mt_max + blk) * p.ldo + col) * 2;
+          dst[0] = (half_ok && okc) ? s1[e] : 0.f;
+          dst[1] = (half_ok && okc) ? s2[e] : 0.f;
+        }
       }
     }
   }
@@ -849,6 +969,7 @@ struct WgradArgs {
   int grouped, gk, gc, cblk;  // grouped: rows / channels per group, channels per row block
   int creal;                  // logical input channels (< C: padded stride, dw keeps c < creal)
   int nct, nkt;               // column tiles, k tiles (grid = splits * nkt * nct)
+  int diag_noepi;             // diagnostic (rn_set_tuning 6): skip the dW epilogue (wrong results)
   const float* in_sc;         // nullable: BN+ReLU applied to the gathered x while staging
   const float* in_sh;
   FastDiv fdQ, fdPQ, fdC, fdS;  // fdC divides by cblk (dense: C)
@@ -1060,6 +1181,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   }
 
   // epilogue: D[row = k][col] -> atomic add into dw
+  if (p.diag_noepi) {  // keep the accumulators live without touching memory
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (s == 12345.678f) p.dw[0] = s;
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
 #pragma unroll
@@ -1556,6 +1686,7 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   if (maxMc == 0) return 0;
   IgemmArgs b = a;
   b.diag_l1 = g_tune[RN_TUNE_DIAG_IGEMM_L1];
+  b.sched = g_tune[RN_TUNE_IGEMM_SCHED];
   const int64_t xb = (int64_t)a.N * a.H * a.W * a.C * (int64_t)sizeof(T);
   const int64_t wb = (int64_t)a.K * a.wrow * (int64_t)sizeof(T);
   b.x_bytes = (int)std::min<int64_t>(xb, INT32_MAX);
@@ -1572,7 +1703,7 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   // idle), else 256x128 when it has >= 128 columns, else the 128-row kernel.
   const int big = g_tune[RN_TUNE_IGEMM_BIG];
   if constexpr (std::is_same<T, bf16_t>::value && std::is_same<OutT, bf16_t>::value) {
-    const bool eligible = big != 1 && !a.in_sc && !a.stats && !a.bnred && !a.smallc && a.gred == 0 && !b.diag_l1 &&
+    const bool eligible = big != 1 && !a.in_sc && !a.smallc && a.gred == 0 && !b.diag_l1 &&
                           !a.bias && xb < INT32_MAX && wb < INT32_MAX && max_taps <= 32 && a.K >= 128;
     if (eligible) {
       int64_t rows = 0;  // 256-row tiles over all parity classes
@@ -1582,8 +1713,17 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
       if (big == 3) bn = 128;
       b.ntn = (int)ceil_div(a.K, bn);
       dim3 grid((unsigned)(ceil_div(maxMc, 256) * b.ntn), 1, a.ncls);
-      if (bn == 256) hipLaunchKernelGGL((igemm_big_kernel<256, 2>), grid, dim3(512), 0, st, b);
-      else hipLaunchKernelGGL((igemm_big_kernel<128, 3>), grid, dim3(512), 0, st, b);
+      const int epi = a.stats ? 1 : a.bnred ? 2 : 0;
+#define RN_BIG(BNV, NB)                                                                                       \
+  if (epi == 0) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 0>), grid, dim3(512), 0, st, b);              \
+  else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 1>), grid, dim3(512), 0, st, b);         \
+  else hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 2>), grid, dim3(512), 0, st, b);
+      if (bn == 256) {
+        RN_BIG(256, 2)
+      } else {
+        RN_BIG(128, 3)
+      }
+#undef RN_BIG
       return rn_check_launch("igemm_big");
     }
   }
@@ -1738,6 +1878,7 @@ int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, f
     a.ldw = a.ncol;
   }
   a.M = d->n * d->p * d->q;
+  a.diag_noepi = g_tune[RN_TUNE_DIAG_WGRAD_NOEPI];
   a.fdQ = make_fastdiv(d->q); a.fdPQ = make_fastdiv(d->p * d->q);
   a.fdC = make_fastdiv(a.cblk); a.fdS = make_fastdiv(d->s);
   hipStream_t st = as_stream(stream);

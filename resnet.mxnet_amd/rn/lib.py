@@ -96,6 +96,11 @@ def load(auto_build=True):
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"librn.so not found at {LIB_PATH}: build it with "
                            "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+    # PyTorch-ROCm ships its own libamdhip64 (soname libamdhip64.so.7, DT_NEEDED "libamdhip64.so"):
+    # load it first so that librn's libamdhip64.so.7 resolves to that same runtime. Loading librn
+    # first pulls /opt/rocm's copy, torch then loads a second runtime, and librn's launches see no
+    # device ("no ROCm-capable device is detected"). Importing torch does not initialise the GPU.
+    import torch  # noqa: F401
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

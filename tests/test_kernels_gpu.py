@@ -420,9 +420,18 @@ def test_stem_quant(gpu):
     assert rel_err(dbeta.cpu().numpy(), dbeta_ref) < 1e-4
 
 
+@pytest.fixture(params=[0, 2], ids=["auto", "big256"])
+def big_tiles(request):
+    """rn_set_tuning 4 (igemm 256-row tiles): automatic choice, or 256x256 forced where eligible."""
+    L.call("rn_set_tuning", 4, request.param)
+    yield request.param
+    L.call("rn_set_tuning", 4, 0)
+
+
 @pytest.mark.parametrize("dtype", [F32, BF16])
-@pytest.mark.parametrize("case", [(3, 32, 13, 11, 48, 3, 2, 1), (2, 64, 14, 14, 256, 1, 1, 0), (2, 16, 9, 9, 64, 1, 1, 0)])
-def test_conv_bnstats_epilogue(gpu, dtype, case):
+@pytest.mark.parametrize("case", [(3, 32, 13, 11, 48, 3, 2, 1), (2, 64, 14, 14, 256, 1, 1, 0), (2, 16, 9, 9, 64, 1, 1, 0),
+                                  (3, 128, 20, 20, 256, 3, 1, 1)])
+def test_conv_bnstats_epilogue(gpu, dtype, case, big_tiles):
     """BatchNorm statistics emitted by the conv epilogue (rn_conv_fwd_bnstats, with the fused
     residual add) and merged by rn_bn_fwd_train_part == a BatchNorm over the stored conv output."""
     n, c, h, w, k, r, st, pd = case
@@ -441,8 +450,8 @@ def test_conv_bnstats_epilogue(gpu, dtype, case):
     lib = L.load()
     nblk = lib.rn_conv_bnstats_blocks(C.byref(d))
     part = torch.zeros(nblk * 3 * d.k_pad, dtype=torch.float32, device=gpu)
-    L.call("rn_conv_fwd_bnstats", C.byref(d), p(xd), p(wk), p(y), dtype, p(to_nhwc(res, dtype, gpu)), None, p(part),
-           stream())
+    rd = to_nhwc(res, dtype, gpu)
+    L.call("rn_conv_fwd_bnstats", C.byref(d), p(xd), p(wk), p(y), dtype, p(rd), None, p(part), stream())
     torch.cuda.synchronize()
     conv_out = from_nhwc(y, k)  # the stored (rounded) values the statistics must describe
     gamma = np.random.default_rng(15).uniform(0.5, 1.5, k)
@@ -558,8 +567,8 @@ def test_conv_bnrelu_on_load(gpu, dtype, case):
 
 @pytest.mark.parametrize("dtype", [F32, BF16])
 @pytest.mark.parametrize("case", [(2, 64, 14, 14, 128, 3, 1, 1), (2, 128, 14, 14, 256, 1, 2, 0),
-                                  (3, 32, 13, 11, 48, 3, 2, 1)])
-def test_dgrad_bn_backward_fusion(gpu, dtype, case):
+                                  (3, 32, 13, 11, 48, 3, 2, 1), (3, 256, 20, 20, 128, 3, 2, 1)])
+def test_dgrad_bn_backward_fusion(gpu, dtype, case, big_tiles):
     """rn_conv_bwd_data_bnred + rn_bn_bwd_part == conv dgrad followed by the BatchNorm+ReLU backward
     of the BN that produced the conv's input (pre-activation units)."""
     n, c, h, w, k, r, st, pd = case
@@ -597,8 +606,9 @@ def test_dgrad_bn_backward_fusion(gpu, dtype, case):
     dact = to_nhwc(prev, dtype, gpu)                               # accumulated in place (add_src = out)
     nrb = lib.rn_conv_bnred_blocks(C.byref(d))
     part = torch.full((nrb * d.c * 2,), float("nan"), dtype=torch.float32, device=gpu)  # every slot written
-    L.call("rn_conv_bwd_data_bnred", C.byref(d), p(to_nhwc(dy, dtype, gpu)), p(wc), p(dact), p(dact), p(xbd), p(sm),
-           p(sc), p(sh), 1, p(part), stream())
+    dyd = to_nhwc(dy, dtype, gpu)
+    L.call("rn_conv_bwd_data_bnred", C.byref(d), p(dyd), p(wc), p(dact), p(dact), p(xbd), p(sm), p(sc), p(sh), 1,
+           p(part), stream())
     dx = torch.zeros_like(xbd)
     dg, db = torch.zeros(d.c, dtype=torch.float32, device=gpu), torch.zeros(d.c, dtype=torch.float32, device=gpu)
     L.call("rn_bn_bwd_part", C.byref(bd), p(part), nrb, p(xbd), p(dact), p(dx), None, p(g_d), p(sm), p(si), p(sc),

@@ -86,8 +86,8 @@ def _loss_traj(g, symf, n, hw, ncls, steps, lr):
 
 def _check_traj(gpu_l, ref_l, final_frac):
     assert abs(gpu_l[0] - ref_l[0]) < 0.02 * ref_l[0], (gpu_l, ref_l)
-    # monotone until the fixed batch is memorised (loss at fp32 noise level)
-    assert all(b < a or b < 1e-3 for a, b in zip(gpu_l, gpu_l[1:])), gpu_l
+    # monotone until the fixed batch is memorised (below 1e-2 bf16 rounding moves it either way)
+    assert all(b < a or b < 1e-2 for a, b in zip(gpu_l, gpu_l[1:])), gpu_l
     assert gpu_l[-1] < final_frac * gpu_l[0], gpu_l
 
 
