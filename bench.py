@@ -45,11 +45,12 @@ def conv_call_bytes(ex, name, args):
     x = d.n * d.h * d.w * d.c * es
     y = d.n * d.p * d.q * d.k_pad * es
     w = d.k * d.r * d.s * d.c_real * es
-    if name in ("rn_conv_fwd", "rn_conv_fwd_bnstats"):
+    if name in ("rn_conv_fwd", "rn_conv_fwd_bnstats", "rn_conv_fwd_x"):
         yb = d.n * d.p * d.q * d.k_pad * (4 if args[4] == 1 else es)
         return x + w + yb + (y if args[5] is not None else 0)
-    if name == "rn_conv_bwd_data":
-        return y + w + x + (x if args[4] is not None else 0)
+    if name in ("rn_conv_bwd_data", "rn_conv_bwd_data_bnred"):
+        bnx = x if name == "rn_conv_bwd_data_bnred" else 0  # the fused BN-backward reduction reads the BN input
+        return y + w + x + (x if args[4] is not None else 0) + bnx
     return x + y + 2 * d.k * d.r * d.s * d.c_real * 4  # wgrad: fp32 dW read-modify-write
 
 
@@ -67,39 +68,26 @@ def pmc_traffic(family):
     return rec["hbm_bytes"], os.path.relpath(path, REPO)
 
 
+FWD_CALLS = ("rn_conv_fwd", "rn_conv_fwd_bnstats", "rn_conv_fwd_x")
+DGRAD_CALLS = ("rn_conv_bwd_data", "rn_conv_bwd_data_bnred")
+
+
 def family_of(ex, name, args):
     if name == "rn_conv_bwd_filter":
-        return "wgrad_kernel<bf16,128,128>" if ex.dtype == 0 else "wgrad_kernel<f32,128,128>"
-    if name in ("rn_conv_fwd", "rn_conv_fwd_bnstats", "rn_conv_bwd_data"):
+        return "wgrad_kernel<bf16,*>" if ex.dtype == 0 else "wgrad_kernel<f32,*>"
+    if name in FWD_CALLS + DGRAD_CALLS:
         d = args[0]._obj
-        dgrad = name == "rn_conv_bwd_data"
+        dgrad = name in DGRAD_CALLS
         ncol = d.c if dgrad else d.k
         out_f32 = not dgrad and args[4] == 1 and ex.dtype == 0
-        big = big_tile(d, dgrad) if (ex.dtype == 0 and not out_f32 and name != "rn_conv_fwd_bnstats" and
-                                     (dgrad or args[6] is None)) else None
+        plain = dgrad or (args[6] is None and (name != "rn_conv_fwd_x" or args[7] is None))
+        # the library's own choice (rn_conv_tile), so the family always matches the kernel that runs
+        big = ex.lib.rn_conv_tile(args[0], 1 if dgrad else 0) if (ex.dtype == 0 and not out_f32 and plain) else 0
         if big:
             return "igemm_big_kernel<256x%d>" % big
         tile = "128x64" if ncol <= 64 else "128x128"
         return "igemm_kernel<bf16,%s,%s>" % ("f32" if out_f32 else "bf16", tile)
     return None
-
-
-def big_tile(d, dgrad):
-    """Mirror of launch_igemm's 256-row tile choice (rn_conv.hip; RN_TUNE key 4 at its default):
-    the tile's column count, or None for the 128-row kernel."""
-    ncol = d.c if dgrad else d.k
-    smallc = not dgrad and d.c < 64 and (d.c & (d.c - 1)) == 0 and d.r * d.s > 1
-    if d.groups != 1 or smallc or ncol < 128:
-        return None
-    if dgrad:
-        rows = 0
-        for a in range(d.stride_h):
-            for b in range(d.stride_w):
-                pc, qc = -(-(d.h - a) // d.stride_h), -(-(d.w - b) // d.stride_w)
-                rows += -(-(d.n * pc * qc) // 256)
-    else:
-        rows = -(-(d.n * d.p * d.q) // 256)
-    return 256 if ncol >= 256 and rows * -(-ncol // 256) >= 192 else 128
 
 
 class FamilyTimer:

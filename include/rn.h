@@ -66,6 +66,10 @@ int rn_conv_fwd(const rn_conv_desc* d, const void* x, const void* w_krsc, void* 
 int rn_conv_fwd_bnstats(const rn_conv_desc* d, const void* x, const void* w_krsc, void* y, int32_t y_dtype,
                         const void* add_src, const float* bias, float* part, rn_stream_t stream);
 int64_t rn_conv_bnstats_blocks(const rn_conv_desc* d);
+/* Kernel variant the bf16 forward (mode 0, plain: no bias / input transform) or data-gradient
+ * (mode 1) of `d` runs: the column count of its 256-row tile (256 or 128), or 0 for the 128-row
+ * kernel. Lets a caller enable the BatchNorm epilogue fusions only where they pay. */
+int32_t rn_conv_tile(const rn_conv_desc* d, int32_t mode);
 
 /* rn_conv_bwd_data that also reduces the BatchNorm+ReLU backward of the BN whose output gradient
  * this call completes (dx here = d(bn output), bn_x = the BN input, bn_mean / bn_scale / bn_shift =

@@ -1677,6 +1677,25 @@ IgemmArgs make_igemm_args(const rn_conv_desc* d, int mode) {
   return a;
 }
 
+// Columns of the 256-row tile launch_igemm runs for these arguments (bf16 in and out), 0 for the
+// 128-row kernel. rn_set_tuning 4: 0 auto, 1 off, 2 force 256x256, 3 force 256x128. Auto, from
+// per-layer measurements over ResNet-50 (tools/conv_bench.py): 256x256 when the output has >= 256
+// columns and the grid still has >= 192 tiles (one workgroup per CU; fewer leave too many CUs
+// idle), else 256x128 when it has >= 128 columns, else the 128-row kernel.
+int big_tile_cols(const IgemmArgs& a, int64_t xb, int64_t wb) {
+  const int big = g_tune[RN_TUNE_IGEMM_BIG];
+  int max_taps = 0;
+  for (int z = 0; z < a.ncls; ++z) max_taps = std::max(max_taps, a.cls[z].nr * a.cls[z].ns);
+  const bool eligible = big != 1 && !a.in_sc && !a.smallc && a.gred == 0 && !g_tune[RN_TUNE_DIAG_IGEMM_L1] &&
+                        !a.bias && xb < INT32_MAX && wb < INT32_MAX && max_taps <= 32 && a.K >= 128;
+  if (!eligible) return 0;
+  if (big == 2) return 256;
+  if (big == 3) return 128;
+  int64_t rows = 0;  // 256-row tiles over all parity classes
+  for (int z = 0; z < a.ncls; ++z) rows += ceil_div((int64_t)a.N * a.cls[z].Pc * a.cls[z].Qc, 256);
+  return (a.K >= 256 && rows * ceil_div(a.K, 256) >= 192) ? 256 : 128;
+}
+
 template <typename T, typename OutT>
 int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   RN_CHECK_ARG((int64_t)a.N * a.H * a.W * a.C < (1ll << 31), "gathered tensor exceeds 2^31 elements");
@@ -1697,20 +1716,9 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   for (int z = 0; z < a.ncls; ++z) max_taps = std::max(max_taps, a.cls[z].nr * a.cls[z].ns);
   const bool dma = g_tune[RN_TUNE_IGEMM_DMA] > 0 && !a.in_sc && !b.diag_l1 && xb < INT32_MAX && wb < INT32_MAX &&
                    max_taps <= 64;
-  // 256-row tiles (rn_set_tuning 4: 0 auto, 1 off, 2 force 256x256, 3 force 256x128). Auto, from
-  // per-layer measurements over ResNet-50 (tools/conv_bench.py): 256x256 when the output has >= 256
-  // columns and the grid still has >= 192 tiles (one workgroup per CU; fewer leave too many CUs
-  // idle), else 256x128 when it has >= 128 columns, else the 128-row kernel.
-  const int big = g_tune[RN_TUNE_IGEMM_BIG];
   if constexpr (std::is_same<T, bf16_t>::value && std::is_same<OutT, bf16_t>::value) {
-    const bool eligible = big != 1 && !a.in_sc && !a.smallc && a.gred == 0 && !b.diag_l1 &&
-                          !a.bias && xb < INT32_MAX && wb < INT32_MAX && max_taps <= 32 && a.K >= 128;
-    if (eligible) {
-      int64_t rows = 0;  // 256-row tiles over all parity classes
-      for (int z = 0; z < a.ncls; ++z) rows += ceil_div((int64_t)a.N * a.cls[z].Pc * a.cls[z].Qc, 256);
-      int bn = (a.K >= 256 && rows * ceil_div(a.K, 256) >= 192) ? 256 : 128;
-      if (big == 2) bn = 256;
-      if (big == 3) bn = 128;
+    const int bn = big_tile_cols(a, xb, wb);
+    if (bn) {
       b.ntn = (int)ceil_div(a.K, bn);
       dim3 grid((unsigned)(ceil_div(maxMc, 256) * b.ntn), 1, a.ncls);
       const int epi = a.stats ? 1 : a.bnred ? 2 : 0;
@@ -1816,6 +1824,13 @@ int rn_conv_fwd(const rn_conv_desc* d, const void* x, const void* w, void* y, in
 int rn_conv_fwd_bnstats(const rn_conv_desc* d, const void* x, const void* w, void* y, int32_t y_dtype,
                         const void* add_src, const float* bias, float* part, rn_stream_t stream) {
   return rn_conv_fwd_x(d, x, w, y, y_dtype, add_src, bias, nullptr, nullptr, part, stream);
+}
+
+int32_t rn_conv_tile(const rn_conv_desc* d, int32_t mode) {
+  if (!d || d->dtype != RN_BF16 || (mode != 0 && mode != 1)) return 0;
+  const IgemmArgs a = make_igemm_args(d, mode);
+  const int64_t xb = (int64_t)a.N * a.H * a.W * a.C * 2, wb = (int64_t)a.K * a.wrow * 2;
+  return big_tile_cols(a, xb, wb);
 }
 
 int64_t rn_conv_bnstats_blocks(const rn_conv_desc* d) { return ceil_div((int64_t)d->n * d->p * d->q, 128); }

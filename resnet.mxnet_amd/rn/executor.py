@@ -712,11 +712,15 @@ class Executor:
             if op.kind in ("conv", "stem"):
                 producer[id(op.y)] = op
         # default on since the 256-row conv tiles (measured -0.6 % step time with the bwd fusion)
-        if os.environ.get("RN_BN_EPILOGUE_STATS", "1") == "1":
+        # fused only where the producer runs the 256-row tile: the 128-row kernel's epilogue costs
+        # more than the statistics pass it saves (RN_BN_EPILOGUE_STATS=2: every conv producer)
+        stats_mode = os.environ.get("RN_BN_EPILOGUE_STATS", "1")
+        if stats_mode in ("1", "2"):
             for op in plan.ops:
                 if op.kind == "bn" and not op.use_global_stats:
                     src = producer.get(id(op.x))
-                    if src is not None and src.y.c % 8 == 0 and src.y.cp == op.x.cp:
+                    if src is not None and src.y.c % 8 == 0 and src.y.cp == op.x.cp and \
+                            (stats_mode == "2" or self._big_tile(src, 0)):
                         src.bnstats = True
                         op.part_src = src
         for op in plan.ops:
@@ -869,6 +873,14 @@ class Executor:
             self._fwd_infer.extend(I)
         self.stem_ws = self._zeros(stem_ws, self.torch.float32)
 
+    def _big_tile(self, op, mode):
+        """Does conv `op` run its forward (mode 0) / data gradient (mode 1) on the 256-row tile?"""
+        if op.kind != "conv" or self.lib is None:
+            return False
+        x, y = op.x, op.y
+        d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad, op.groups)
+        return int(self.lib.rn_conv_tile(L.C.byref(d), mode)) > 0
+
     def _conv_fwd_call(self, op, d, xptr, res, sp, stats=True):
         """Conv forward; emits the next BatchNorm's statistics when one consumes y (training), and
         applies the producing BatchNorm+ReLU on load when that BN is fused (op.xf)."""
@@ -905,7 +917,9 @@ class Executor:
         wsp = self._p(self.ws)
         self.param_done_at = {}  # param -> index in self._bwd after which its grad is final
         self._gw = {}  # id(tensor) -> last writer of its gradient buffer: ("dgrad", call index, conv op)
-        bwd_fusion = os.environ.get("RN_BN_BWD_FUSION", "1") == "1"  # default on (see RN_BN_EPILOGUE_STATS)
+        # default on where the dgrad runs the 256-row tile (see RN_BN_EPILOGUE_STATS; =2: every dgrad)
+        bwd_fusion = os.environ.get("RN_BN_BWD_FUSION", "1") in ("1", "2")
+        bwd_all = os.environ.get("RN_BN_BWD_FUSION", "1") == "2"
         for op in reversed(plan.ops):
             if op.kind == "softmax":
                 gs.has_value.add(id(op.x))  # dlogits written by the forward softmax call
@@ -961,7 +975,7 @@ class Executor:
                 out, add = (gs.contribute(x) if x.needs_grad else (None, None))
                 w = self._gw.get(id(op.y))
                 if bwd_fusion and w and w[0] == "dgrad" and dy is self._grads.get(id(op.y)) and \
-                        op.y.c % 8 == 0 and op.y.c == op.y.cp:
+                        op.y.c % 8 == 0 and op.y.c == op.y.cp and (bwd_all or self._big_tile(w[2], 1)):
                     # the conv dgrad that completes this BN's output gradient also reduces its backward
                     # (sum dz, sum dz*(x - mean)); the BN then needs only finalize + apply
                     _, ci, cop, cdy, cout, cadd = w
