@@ -296,7 +296,8 @@ const char* rn_last_error(void);
  * (default: occupancy), 3 = diagnostic only:
  * igemm A operand from one L1-resident chunk (wrong results; isolates memory latency),
  * 4 = igemm 256-row tiles (0 auto, 1 off, 2 force 256x256, 3 force 256x128),
- * 5 = wgrad 256-column LDS-DMA tiles (1 on; default off: measured slower),
+ * 5 = wgrad variant (0 auto: 128x128 LDS-DMA tiles where K and the column count exceed 64; 1 = 256-column
+ *     LDS-DMA tiles, measured slower; 3 = the register-staged kernel only),
  * 6 = diagnostic only: wgrad skips its dW epilogue (wrong results; isolates the atomic adds),
  * 7 = igemm 256-row tile schedule experiments (bit mask; 0 = default). */
 int rn_set_tuning(int32_t key, int32_t value);

@@ -1223,12 +1223,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 // columns), bf16, dense, unpadded channels. Both operands are staged by inline-asm LDS-DMA into
 // [64 m][row] images whose 16-byte chunks are XOR-swizzled (swz_tr) by choosing each lane's SOURCE
 // chunk, and read with ds_read_b64_tr_b16 as in wgrad_kernel. NBUF buffers, NBUF-1 M-tiles in flight.
-template <int BMK, int NBUF>
-__global__ __launch_bounds__(512, 1) void wgrad_big_kernel(WgradArgs p) {
-  constexpr int BNC = 256, CE = 8, BKM = 64;
+// BNC = 256: 8 waves, one workgroup per CU; BNC = 128: 4 waves (2 x 2, each 64-128 rows x 64
+// columns), two workgroups per CU.
+template <int BMK, int NBUF, int BNC = 256>
+__global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(WgradArgs p) {
+  constexpr int CE = 8, BKM = 64;
+  constexpr int NWC = BNC / 64, NW = 2 * NWC;              // waves along the columns, waves
   constexpr int A_CPR = BMK / 8, B_CPR = BNC / 8;      // 16-byte chunks per LDS row
   constexpr int A_RPI = 64 / A_CPR, B_RPI = 64 / B_CPR;  // rows per 1 KiB DMA instruction
-  constexpr int AR = BKM / A_RPI / 8, BR = BKM / B_RPI / 8;  // DMA instructions per wave per M-tile
+  constexpr int AR = BKM / A_RPI / NW, BR = BKM / B_RPI / NW;  // DMA instructions per wave per M-tile
   constexpr int LPT = AR + BR;
   constexpr int MI = BMK / 32, NI = 4;
   constexpr int A_SZ = BKM * A_CPR, B_SZ = BKM * B_CPR;  // chunks
@@ -1236,7 +1239,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_big_kernel(WgradArgs p) {
   __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * kStage];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 2, wn = wid & 3;
+  const int wm = wid / NWC, wn = wid % NWC;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   const int per_split = p.nct * p.nkt;
   const int zs = lid / per_split;
@@ -1903,6 +1906,21 @@ int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, f
   // 128-tile kernel on every ResNet-50 layer: with the M split, the fp32 atomic epilogue issues
   // (workgroups x tile area) adds, 4x more per workgroup at 256x256, and that dominates the
   // small-M layers (stage 3-4).
+  if (d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c && g_tune[RN_TUNE_WGRAD_BIG] == 2 &&
+      a.K > 64 && a.ncol_load > 64 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX &&
+      (int64_t)a.M * a.ldy < INT32_MAX) {
+    // 128 x 128 LDS-DMA tiles, 4 waves, two workgroups per CU (default; measured -0.4 % step time
+    // over the register-staged wgrad_kernel, which rn_set_tuning 5 = 3 selects)
+    a.nct = (int)ceil_div(a.ncol_load, 128);
+    a.nkt = (int)ceil_div(a.K, 128);
+    const int64_t tiles = (int64_t)a.nct * a.nkt;
+    const int64_t mtiles = ceil_div(a.M, 64);
+    int64_t split = std::min<int64_t>(std::max<int64_t>(1, 512 / tiles), std::max<int64_t>(1, mtiles / 8));
+    a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
+    split = ceil_div(a.M, a.m_per_split);
+    hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
+    return rn_check_launch("wgrad_dma128");
+  }
   if (d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c && a.K >= 128 && a.ncol_load >= 256 &&
       g_tune[RN_TUNE_WGRAD_BIG] == 1 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX &&
       (int64_t)a.M * a.ldy < INT32_MAX) {

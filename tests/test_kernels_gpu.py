@@ -654,6 +654,7 @@ def test_conv_big_tiles(gpu, mode, case):
     y = torch.zeros((n, P, Q, d.k_pad), dtype=torch.bfloat16, device=gpu)
     dx = torch.zeros((n, h, w, d.c), dtype=torch.bfloat16, device=gpu)
     dw = torch.zeros(k * r * r * c, dtype=torch.float32, device=gpu)
+    dw2 = torch.zeros_like(dw)
     xd, rd, dyd = to_nhwc(x, BF16, gpu), to_nhwc(res, BF16, gpu), to_nhwc(dy, BF16, gpu)  # alive across the calls
     L.call("rn_set_tuning", 4, mode)
     L.call("rn_set_tuning", 5, 1)
@@ -661,11 +662,13 @@ def test_conv_big_tiles(gpu, mode, case):
         L.call("rn_conv_fwd", C.byref(d), p(xd), p(wk), p(y), BF16, p(rd), None, stream())
         L.call("rn_conv_bwd_data", C.byref(d), p(dyd), p(wc), p(dx), None, stream())
         L.call("rn_conv_bwd_filter", C.byref(d), p(xd), p(dyd), p(dw), stream())  # wgrad_big_kernel when eligible
+        L.call("rn_set_tuning", 5, 0)
+        L.call("rn_conv_bwd_filter", C.byref(d), p(xd), p(dyd), p(dw2), stream())  # 128x128 4-wave DMA variant
         torch.cuda.synchronize()
     finally:
         L.call("rn_set_tuning", 4, 0)
         L.call("rn_set_tuning", 5, 0)
     assert rel_err(from_nhwc(y, k), ref) < TOL[BF16]
     assert rel_err(from_nhwc(dx, c), dx_ref) < TOL[BF16]
-    dw_h = dw.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2)
-    assert rel_err(dw_h, dw_ref) < 5e-3
+    for g in (dw, dw2):
+        assert rel_err(g.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2), dw_ref) < 5e-3
