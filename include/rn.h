@@ -67,8 +67,9 @@ int rn_conv_fwd_bnstats(const rn_conv_desc* d, const void* x, const void* w_krsc
                         const void* add_src, const float* bias, float* part, rn_stream_t stream);
 int64_t rn_conv_bnstats_blocks(const rn_conv_desc* d);
 /* Kernel variant the bf16 forward (mode 0, plain: no bias / input transform) or data-gradient
- * (mode 1) of `d` runs: the column count of its 256-row tile (256 or 128), or 0 for the 128-row
- * kernel. Lets a caller enable the BatchNorm epilogue fusions only where they pay. */
+ * (mode 1) of `d` runs: the column count of its 256-row tile (256, 128 or 64), or 0 for the
+ * 128-row kernel. Lets a caller enable the BatchNorm epilogue fusions only where they pay (the
+ * 64-column tile has none: with a fused epilogue those layers run the 128-row kernel). */
 int32_t rn_conv_tile(const rn_conv_desc* d, int32_t mode);
 
 /* rn_conv_bwd_data that also reduces the BatchNorm+ReLU backward of the BN whose output gradient
@@ -295,7 +296,7 @@ const char* rn_last_error(void);
  * 1 = igemm LDS-DMA staging (default off: measured slower), 2 = wgrad split-M target blocks per CU
  * (default: occupancy), 3 = diagnostic only:
  * igemm A operand from one L1-resident chunk (wrong results; isolates memory latency),
- * 4 = igemm 256-row tiles (0 auto, 1 off, 2 force 256x256, 3 force 256x128),
+ * 4 = igemm 256-row tiles (0 auto, 1 off, 2 force 256x256, 3 force 256x128, 5 no 256x64),
  * 5 = wgrad variant (0 auto: 128x128 LDS-DMA tiles where K and the column count exceed 64; 1 = 256-column
  *     LDS-DMA tiles, measured slower; 3 = the register-staged kernel only),
  * 6 = diagnostic only: wgrad skips its dW epilogue (wrong results; isolates the atomic adds),

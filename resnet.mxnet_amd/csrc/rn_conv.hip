@@ -650,21 +650,27 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // EPI: 0 plain; 1 (fwd) BatchNorm statistics of the stored output per 128-row half (one wave row):
 // part[2*mtile + wm][S1 | S2 | pivot][ldo], as igemm_kernel's bn_stats_epilogue; 2 (dgrad) the
 // BatchNorm-backward reduction of the stored gradient: bnred[class][2*mtile + wm][ldo][2].
+// BN = 64 (the 64-channel layers): 4 waves stacked along M (each 64 x 64), two workgroups per CU;
+// plain epilogue only (EPI 0).
 template <int BN, int NBUF, int EPI = 0>
-__global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
+__global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_big_kernel(IgemmArgs p) {
   constexpr int BM = 256, CE = 8, BKE = 64;
-  constexpr int AR = BM / 64, BR = BN / 64;  // DMA rounds per K-tile (64 rows each)
-  constexpr int LPT = AR + BR;               // DMA instructions per thread per K-tile
-  constexpr int WN = BN / 4;                 // wave tile columns
-  constexpr int MI = 8, NI = WN / 16;        // 16x16 accumulators per wave
-  constexpr int kStage = (BM + BN) * 8;      // 16-byte chunks per K-tile
-  constexpr int EP_LD = WN + 4;              // staged fp32 row stride
-  constexpr int EP_WAVE = 64 * EP_LD;        // floats per wave per epilogue half
-  constexpr int kEpChunks = 8 * EP_WAVE / 4;
+  constexpr int NW = BN == 64 ? 4 : 8;           // waves
+  constexpr int WAVES_N = BN == 64 ? 1 : 4, WAVES_M = NW / WAVES_N;
+  constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;  // wave tile
+  constexpr int RPR = NW * 8;                    // rows per DMA round (8 per wave)
+  constexpr int AR = BM / RPR, BR = BN / RPR;    // DMA rounds per K-tile
+  constexpr int LPT = AR + BR;                   // DMA instructions per thread per K-tile
+  constexpr int MI = WM / 16, NI = WN / 16;      // 16x16 accumulators per wave
+  constexpr int kStage = (BM + BN) * 8;          // 16-byte chunks per K-tile
+  constexpr int EP_LD = WN + 4;                  // staged fp32 row stride
+  constexpr int EP_WAVE = 64 * EP_LD;            // floats per wave per epilogue half
+  constexpr int kEpChunks = NW * EP_WAVE / 4;
+  static_assert(BN != 64 || EPI == 0, "the 64-column tile has no BatchNorm epilogue");
   __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * kStage > kEpChunks ? NBUF * kStage : kEpChunks];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 2, wn = wid & 3;
+  const int wm = wid / WAVES_N, wn = wid % WAVES_N;
   const IgemmCls& cl = p.cls[blockIdx.z];
   const int Mc = p.N * cl.Pc * cl.Qc;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
@@ -673,7 +679,7 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
   const int n0 = (lid - mtile * p.ntn) * BN;
   if (m0 >= Mc) {  // (a dgrad parity class with fewer rows): empty BN-reduction partials
     if constexpr (EPI == 2)
-      for (int e = tid; e < 2 * BN; e += 512) {
+      for (int e = tid; e < 2 * BN; e += NW * 64) {
         const int hh = e / BN, col = n0 + e % BN;
         if (col < p.ldo && 2 * mtile + hh < p.mt_max) {
           float* dst = p.bnred + ((int64_t)(blockIdx.z * p.mt_max + 2 * mtile + hh) * p.ldo + col) * 2;
@@ -690,7 +696,7 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
   int a_row[AR], a_h[AR], a_w[AR];  // row offset of tap (0,0); its gathered coordinates
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
-    const int m = m0 + 64 * i + (tid >> 3);
+    const int m = m0 + RPR * i + (tid >> 3);
     if (m < Mc) {
       const int n = fdiv(m, cl.fdPQ);
       const int rem = m - n * cl.Pc * cl.Qc;
@@ -709,7 +715,7 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
   bool b_ok[BR];
 #pragma unroll
   for (int i = 0; i < BR; ++i) {
-    const int col = n0 + 64 * i + (tid >> 3);
+    const int col = n0 + RPR * i + (tid >> 3);
     b_ok[i] = col < p.K;
     b_off[i] = (b_ok[i] ? col : 0) * p.wrow + lch * CE;
   }
@@ -747,10 +753,10 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
   auto piece = [&](int k) __attribute__((always_inline)) {
     if (k < AR) {
       const bool ok = d_cok && (unsigned)(a_h[k] + d_dh) < (unsigned)p.H && (unsigned)(a_w[k] + d_dw) < (unsigned)p.W;
-      dma16_asm(rs_x, d_la + k * 8192, ok ? ((uint32_t)((a_row[k] + d_toffa) * 2) & dmask) : kOob);
+      dma16_asm(rs_x, d_la + k * (RPR * 128), ok ? ((uint32_t)((a_row[k] + d_toffa) * 2) & dmask) : kOob);
     } else {
       const int i = k - AR;
-      dma16_asm(rs_w, d_la + BM * 128 + i * 8192,
+      dma16_asm(rs_w, d_la + BM * 128 + i * (RPR * 128),
                 (d_cok && b_ok[i]) ? ((uint32_t)((b_off[i] + d_toffb) * 2) & dmask) : kOob);
     }
   };
@@ -782,17 +788,21 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const int row = wm * 128 + i * 16 + (lane & 15);
+        const int row = wm * WM + i * 16 + (lane & 15);
         af[i] = As[row * 8 + swz(row, kc)];
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
 #pragma unroll
         for (int j = 0; j < NI; ++j) mfma_slab<bf16_t>(acc[i][j], af[i], bfr[j]);
-        // 256x256 (2 buffers): the DMAs early (slab 0) so they have the longest to land; 256x128
-        // (3 buffers, one more K-tile in flight): spread over both slabs. Measured per layer.
-        const int step = slab * MI + i;
-        if (NBUF == 2 ? step < LPT : ((step & 1) && (step >> 1) < LPT)) piece(NBUF == 2 ? step : step >> 1);
+        // 2 buffers: the DMAs early (over slab 0's groups) so they have the longest to land; 3
+        // buffers (one more K-tile in flight): spread over both slabs. Measured per layer.
+        constexpr int G = NBUF == 2 ? MI : 2 * MI;  // MFMA groups the LPT DMAs are spread over
+        const int g = slab * MI + i;
+        if (g < G) {
+#pragma unroll
+          for (int q = g * LPT / G; q < (g + 1) * LPT / G; ++q) piece(q);
+        }
       }
     }
   };
@@ -821,7 +831,7 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
   bf16_t* __restrict__ yg = reinterpret_cast<bf16_t*>(p.y);
   const int cc = lane % CPR;
   const int col0 = n0 + wn * WN + cc * 8;
-  const bool half_ok = m0 + wm * 128 < Mc;  // this wave row holds at least one output row
+  const bool half_ok = m0 + wm * WM < Mc;  // this wave row holds at least one output row
   // BatchNorm partials of this lane's 8 columns (EPI 1: S1, S2 about the pivot; EPI 2: sum dz,
   // sum dz * (x - mean)), over its rows; the lanes sharing a column chunk are summed at the end
   constexpr int NS = EPI ? 8 : 1;
@@ -838,14 +848,14 @@ __global__ __launch_bounds__(512, 1) void igemm_big_kernel(IgemmArgs p) {
   }
   const bf16_t* __restrict__ bxg = reinterpret_cast<const bf16_t*>(p.bn_x);
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < WM / 64; ++h) {
     int64_t off[CPR];  // this lane's rows: lane / CPR + (64 / CPR) k
     uint4 addv[CPR];
     uint4 xpre[EPI == 2 ? CPR : 1];  // BN input at the same positions (EPI 2), loaded with the residual
 #pragma unroll
     for (int k = 0; k < CPR; ++k) {
       const int r = lane / CPR + (64 / CPR) * k;
-      const int m = m0 + wm * 128 + h * 64 + r;
+      const int m = m0 + wm * WM + h * 64 + r;
       off[k] = -1;
       addv[k] = make_uint4(0, 0, 0, 0);
       if constexpr (EPI == 2) xpre[k] = make_uint4(0, 0, 0, 0);
@@ -1690,8 +1700,13 @@ int big_tile_cols(const IgemmArgs& a, int64_t xb, int64_t wb) {
   int max_taps = 0;
   for (int z = 0; z < a.ncls; ++z) max_taps = std::max(max_taps, a.cls[z].nr * a.cls[z].ns);
   const bool eligible = big != 1 && !a.in_sc && !a.smallc && a.gred == 0 && !g_tune[RN_TUNE_DIAG_IGEMM_L1] &&
-                        !a.bias && xb < INT32_MAX && wb < INT32_MAX && max_taps <= 32 && a.K >= 128;
+                        !a.bias && xb < INT32_MAX && wb < INT32_MAX && max_taps <= 32;
   if (!eligible) return 0;
+  if (a.K <= 64) {  // 4-wave 256x64 tile where the reduction is deep (>= 8 K-tiles: the 3x3 layers);
+                   // on the short 1x1 reductions the 128-row kernel measured faster (rn_set_tuning 4 = 5: never)
+    const int nst = max_taps * (int)ceil_div(a.cblk, 64);
+    return (big == 5 || nst < 8) ? 0 : 64;
+  }
   if (big == 2) return 256;
   if (big == 3) return 128;
   int64_t rows = 0;  // 256-row tiles over all parity classes
@@ -1720,11 +1735,17 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   const bool dma = g_tune[RN_TUNE_IGEMM_DMA] > 0 && !a.in_sc && !b.diag_l1 && xb < INT32_MAX && wb < INT32_MAX &&
                    max_taps <= 64;
   if constexpr (std::is_same<T, bf16_t>::value && std::is_same<OutT, bf16_t>::value) {
+    const int epi = a.stats ? 1 : a.bnred ? 2 : 0;
     const int bn = big_tile_cols(a, xb, wb);
-    if (bn) {
+    if (bn == 64 && epi == 0) {
+      b.ntn = (int)ceil_div(a.K, 64);
+      dim3 grid((unsigned)(ceil_div(maxMc, 256) * b.ntn), 1, a.ncls);
+      hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0>), grid, dim3(256), 0, st, b);
+      return rn_check_launch("igemm_big64");
+    }
+    if (bn >= 128) {
       b.ntn = (int)ceil_div(a.K, bn);
       dim3 grid((unsigned)(ceil_div(maxMc, 256) * b.ntn), 1, a.ncls);
-      const int epi = a.stats ? 1 : a.bnred ? 2 : 0;
 #define RN_BIG(BNV, NB)                                                                                       \
   if (epi == 0) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 0>), grid, dim3(512), 0, st, b);              \
   else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 1>), grid, dim3(512), 0, st, b);         \

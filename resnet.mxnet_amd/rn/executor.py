@@ -879,7 +879,7 @@ class Executor:
             return False
         x, y = op.x, op.y
         d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad, op.groups)
-        return int(self.lib.rn_conv_tile(L.C.byref(d), mode)) > 0
+        return int(self.lib.rn_conv_tile(L.C.byref(d), mode)) >= 128  # the 64-column tile has no BN epilogue
 
     def _conv_fwd_call(self, op, d, xptr, res, sp, stats=True):
         """Conv forward; emits the next BatchNorm's statistics when one consumes y (training), and

@@ -629,6 +629,8 @@ BIG_CASES = [
     (1, 512, 7, 7, 512, 3, 1, 1),      # fewer rows than one tile
     (4, 128, 28, 28, 128, 3, 1, 1),    # several row tiles
     (8, 256, 16, 16, 512, 1, 2, 0),    # wgrad: M split over several workgroups
+    (3, 64, 20, 20, 64, 3, 1, 1),      # 64 columns both ways: the 4-wave 256x64 tile
+    (2, 40, 13, 11, 56, 5, 2, 2),      # 256x64 tile: ragged columns, 25 taps, stride-2 classes
 ]
 
 
