@@ -1968,8 +1968,8 @@ int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, f
   // 128-tile kernel on every ResNet-50 layer: with the M split, the fp32 atomic epilogue issues
   // (workgroups x tile area) adds, 4x more per workgroup at 256x256, and that dominates the
   // small-M layers (stage 3-4).
-  if (d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c && g_tune[RN_TUNE_WGRAD_BIG] == 2 &&
-      a.K > 64 && a.ncol_load > 64 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX &&
+  if (d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c &&
+      (g_tune[RN_TUNE_WGRAD_BIG] == 0 || g_tune[RN_TUNE_WGRAD_BIG] == 2) && a.K > 64 && a.ncol_load > 64 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX &&
       (int64_t)a.M * a.ldy < INT32_MAX) {
     // 128 x 128 LDS-DMA tiles, 4 waves, two workgroups per CU (default; measured -0.4 % step time
     // over the register-staged wgrad_kernel, which rn_set_tuning 5 = 3 selects)

@@ -36,9 +36,21 @@ def load(path, counter):
     return out
 
 
+def aggregate(name):
+    """bench.py's family for a kernel family: every bf16 weight-gradient kernel is one family there."""
+    if name.startswith("wgrad_big_kernel") or name.startswith("wgrad_kernel<bf16"):
+        return "wgrad_kernel<bf16,*>"
+    return None
+
+
 def summarise(base):
     fetch = load(base + "_fetch/run_counter_collection.csv", "FETCH_SIZE")
     write = load(base + "_write/run_counter_collection.csv", "WRITE_SIZE")
+    for src in (fetch, write):
+        for k in list(src):
+            a = aggregate(k)
+            if a:
+                src.setdefault(a, []).extend(src[k])
     res = {}
     for k in sorted(set(fetch) | set(write)):
         f, w = fetch.get(k, []), write.get(k, [])
