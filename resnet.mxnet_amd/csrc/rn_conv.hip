@@ -1968,8 +1968,23 @@ int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, f
   // 128-tile kernel on every ResNet-50 layer: with the M split, the fp32 atomic epilogue issues
   // (workgroups x tile area) adds, 4x more per workgroup at 256x256, and that dominates the
   // small-M layers (stage 3-4).
+  if (d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c && a.K <= 64 && a.ncol_load > 64 &&
+      g_tune[RN_TUNE_WGRAD_BIG] == 4 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX &&
+      (int64_t)a.M * a.ldy < INT32_MAX) {
+    // 64 x 128 LDS-DMA tiles for the 64-channel layers (4 waves, 3 buffers, two workgroups per CU)
+    a.nct = (int)ceil_div(a.ncol_load, 128);
+    a.nkt = 1;
+    const int64_t tiles = a.nct;
+    const int64_t mtiles = ceil_div(a.M, 64);
+    int64_t split = std::min<int64_t>(std::max<int64_t>(1, 512 / tiles), std::max<int64_t>(1, mtiles / 8));
+    a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
+    split = ceil_div(a.M, a.m_per_split);
+    hipLaunchKernelGGL((wgrad_big_kernel<64, 3, 128>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
+    return rn_check_launch("wgrad_dma64");
+  }
   if (d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c &&
-      (g_tune[RN_TUNE_WGRAD_BIG] == 0 || g_tune[RN_TUNE_WGRAD_BIG] == 2) && a.K > 64 && a.ncol_load > 64 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX &&
+      (g_tune[RN_TUNE_WGRAD_BIG] == 0 || g_tune[RN_TUNE_WGRAD_BIG] == 2 || g_tune[RN_TUNE_WGRAD_BIG] == 4) &&
+      a.K > 64 && a.ncol_load > 64 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX &&
       (int64_t)a.M * a.ldy < INT32_MAX) {
     // 128 x 128 LDS-DMA tiles, 4 waves, two workgroups per CU (default; measured -0.4 % step time
     // over the register-staged wgrad_kernel, which rn_set_tuning 5 = 3 selects)

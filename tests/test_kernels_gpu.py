@@ -696,8 +696,8 @@ def test_conv_big_tiles(gpu, mode, case):
         L.call("rn_conv_fwd", C.byref(d), p(xd), p(wk), p(y), BF16, p(rd), None, stream())
         L.call("rn_conv_bwd_data", C.byref(d), p(dyd), p(wc), p(dx), None, stream())
         L.call("rn_conv_bwd_filter", C.byref(d), p(xd), p(dyd), p(dw), stream())  # wgrad_big_kernel when eligible
-        L.call("rn_set_tuning", 5, 0)
-        L.call("rn_conv_bwd_filter", C.byref(d), p(xd), p(dyd), p(dw2), stream())  # 128x128 4-wave DMA variant
+        L.call("rn_set_tuning", 5, 4)  # the LDS-DMA variants incl. the 64x128 one for K <= 64
+        L.call("rn_conv_bwd_filter", C.byref(d), p(xd), p(dyd), p(dw2), stream())
         torch.cuda.synchronize()
     finally:
         L.call("rn_set_tuning", 4, 0)
