@@ -277,6 +277,42 @@ int rn_sgd_mom_update(int32_t ntensors, const int64_t* offsets, const int64_t* n
                       int32_t lowp_dtype, float lr, const float* lr_dev, float momentum,
                       float rescale_grad, float clip, rn_stream_t stream);
 
+/* Compute copies of one parameter tensor written by rn_sgd_mom_update_pack (layouts of
+ * rn_conv_weight_pack, dense convolutions / FullyConnected only). krsc == NULL: plain tensor. */
+typedef struct rn_wpack {
+  void* krsc;     /* [k][rs][c] copy (channel stride c), or NULL                          */
+  void* crsk;     /* [c][rs][kpad] copy, or NULL                                          */
+  int32_t k, rs;  /* output channels, taps                                                */
+  int32_t creal;  /* input channels of the master tensor ([k][rs][creal])                */
+  int32_t c;      /* channel stride of the KRSC copy                                      */
+  int32_t kpad;   /* output-channel stride of the CRSK copy                               */
+  int32_t pad_;
+} rn_wpack;
+
+/* rn_sgd_mom_update fused with the weight packs: the same update, and for every tensor whose
+ * `packs` entry (device table, ntensors entries) names copies, the updated weight written to
+ * them in lowp_dtype -- replaces rn_sgd_mom_update + one rn_conv_weight_pack per layer.
+ * work: device table of nwork int32x4 items, one workgroup each: {tensor, start, 0, 0} = the
+ * 4096 elements from `start` of a tensor without a CRSK copy; {tensor, k0, tap, c0} = the
+ * 64 x 64 (k, c) tile of one tap of a tensor with one (rn_sgd_pack_work builds the table). */
+int rn_sgd_mom_update_pack(int32_t ntensors, const int64_t* offsets, const int64_t* numels,
+                           const float* wds, float* w, const float* g, float* mom,
+                           const rn_wpack* packs, const int32_t* work, int32_t nwork,
+                           int32_t lowp_dtype, float lr, const float* lr_dev, float momentum,
+                           float rescale_grad, float clip, rn_stream_t stream);
+/* Diagnostic twin of rn_sgd_mom_update_pack: every global index is checked against
+ * lim = {nparam, then per tensor the KRSC and CRSK copy sizes}; out-of-range accesses are
+ * skipped and flagged (bit mask) in *flag (device int). */
+int rn_sgd_mom_update_pack_checked(int32_t ntensors, const int64_t* offsets, const int64_t* numels,
+                                   const float* wds, float* w, const float* g, float* mom,
+                                   const rn_wpack* packs, const int32_t* work, int32_t nwork,
+                                   int32_t lowp_dtype, float lr, float momentum, float rescale_grad,
+                                   const int64_t* lim, int32_t* flag, rn_stream_t stream);
+/* Host helper: fills `work` (host memory, capacity max_items x 4) for the tensors described by
+ * numels / packs (host copies); returns the item count, or -1 if max_items is too small. */
+int32_t rn_sgd_pack_work(int32_t ntensors, const int64_t* numels, const rn_wpack* packs, int32_t* work,
+                         int32_t max_items);
+
 /* ---------------------------------------------------------------------------------------
  * Data movement helpers.
  * ------------------------------------------------------------------------------------- */

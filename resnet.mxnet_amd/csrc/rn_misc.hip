@@ -220,6 +220,85 @@ __global__ void sgd_mom_kernel(const int64_t* __restrict__ offs, const int64_t* 
   }
 }
 
+// SGD momentum with the compute copies written in the same pass. A conv/FC master tensor is KRSC
+// over creal channels (index (k*RS + tap)*creal + ci); its copies are KRSC over the channel stride c
+// and CRSK over the output stride kpad (the layouts pack_krsc/pack_crsk write). One workgroup per
+// work item: a 4096-element chunk of a tensor without a CRSK copy, or a 64(k) x 64(ci) tile of one
+// tap, transposed through LDS so both copies are written with coalesced rows.
+// Padding entries of the copies are never touched (zero since the bind-time pack).
+constexpr int kSgdChunk = 4096;
+template <typename LT, bool CHECK = false>
+__global__ __launch_bounds__(256) void sgd_mom_pack_kernel(const int64_t* __restrict__ offs,
+                                                           const float* __restrict__ wds, float* __restrict__ w,
+                                                           const float* __restrict__ g, float* __restrict__ mom,
+                                                           const rn_wpack* __restrict__ packs,
+                                                           const int4* __restrict__ work, const int64_t* numels,
+                                                           float lr, const float* lr_dev, float momentum,
+                                                           float rescale, float clip, const int64_t* lim = nullptr,
+                                                           int* flag = nullptr) {
+  __shared__ LT tile[64][65];
+  const int4 wi = work[blockIdx.x];
+  const int t = wi.x;
+  const int64_t off = offs[t];
+  const float wd = wds[t];
+  const float lrv = lr_dev ? *lr_dev : lr;
+  const rn_wpack pk = packs[t];
+  LT* __restrict__ wk = reinterpret_cast<LT*>(pk.krsc);
+  LT* __restrict__ wc = reinterpret_cast<LT*>(pk.crsk);
+  auto upd = [&](int64_t k) __attribute__((always_inline)) {
+    if (CHECK && (k < 0 || k >= lim[0])) {
+      atomicOr(flag, 1);
+      return 0.f;
+    }
+    float gr = rescale * g[k];
+    if (clip > 0.f) gr = fminf(fmaxf(gr, -clip), clip);
+    const float wv = w[k];
+    const float mv = momentum * mom[k] - lrv * (gr + wd * wv);
+    mom[k] = mv;
+    const float nw = wv + mv;
+    w[k] = nw;
+    return nw;
+  };
+  if (!wc) {  // elementwise chunk [wi.y, wi.y + kSgdChunk)
+    const int n = (int)min<int64_t>(numels[t], (int64_t)wi.y + kSgdChunk);
+    for (int i = wi.y + threadIdx.x; i < n; i += 256) {
+      const float nw = upd(off + i);
+      if (wk) {
+        const int64_t o = (int64_t)(i / pk.creal) * pk.c + i % pk.creal;
+        if (CHECK && (o < 0 || o >= lim[1 + 2 * t])) {
+          atomicOr(flag, 2);
+          continue;
+        }
+        wk[o] = from_f<LT>(nw);
+      }
+    }
+    return;
+  }
+  const int k0 = wi.y, tap = wi.z, c0 = wi.w;
+  const int cl = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int j = 0; j < 16; ++j) {  // rows k0 + r, columns c0 + cl: coalesced over ci
+    const int r = r0 + 4 * j, k = k0 + r, ci = c0 + cl;
+    if (k < pk.k && ci < pk.creal) {
+      const int64_t kt = (int64_t)k * pk.rs + tap;
+      const LT v = from_f<LT>(upd(off + kt * pk.creal + ci));
+      if (CHECK && (kt * pk.c + ci >= lim[1 + 2 * t])) atomicOr(flag, 4);
+      else wk[kt * pk.c + ci] = v;
+      tile[r][cl] = v;
+    }
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int j = 0; j < 16; ++j) {  // rows ci, columns k: coalesced over k
+    const int r = r0 + 4 * j, ci = c0 + r, k = k0 + cl;
+    if (k < pk.k && ci < pk.creal) {
+      const int64_t o = ((int64_t)ci * pk.rs + tap) * pk.kpad + k;
+      if (CHECK && o >= lim[2 + 2 * t]) atomicOr(flag, 8);
+      else wc[o] = tile[cl][r];
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------ layout / casts
 template <typename T>
 __global__ void nchw_to_nhwc_kernel(int n, int c, int h, int w, int cpad, const float* __restrict__ src,
@@ -420,6 +499,70 @@ int rn_sgd_mom_update(int32_t ntensors, const int64_t* offsets, const int64_t* n
     hipLaunchKernelGGL(sgd_mom_kernel<float>, grid, dim3(256), 0, st, offsets, numels, wds, w, g, mom,
                        (float*)w_lowp, lr, lr_dev, momentum, rescale_grad, clip);
   return rn_check_launch("sgd_mom_update");
+}
+
+int rn_sgd_mom_update_pack(int32_t ntensors, const int64_t* offsets, const int64_t* numels, const float* wds,
+                           float* w, const float* g, float* mom, const rn_wpack* packs, const int32_t* work,
+                           int32_t nwork, int32_t lowp_dtype, float lr, const float* lr_dev, float momentum,
+                           float rescale_grad, float clip, rn_stream_t stream) {
+  RN_CHECK_ARG(ntensors > 0 && offsets && numels && wds && w && g && mom && packs && work && nwork > 0,
+               "bad arguments");
+  hipStream_t st = as_stream(stream);
+  const int4* wk = reinterpret_cast<const int4*>(work);
+  if (lowp_dtype == RN_BF16)
+    hipLaunchKernelGGL(sgd_mom_pack_kernel<bf16_t>, dim3(nwork), dim3(256), 0, st, offsets, wds, w, g, mom, packs, wk,
+                       numels, lr, lr_dev, momentum, rescale_grad, clip);
+  else
+    hipLaunchKernelGGL(sgd_mom_pack_kernel<float>, dim3(nwork), dim3(256), 0, st, offsets, wds, w, g, mom, packs, wk,
+                       numels, lr, lr_dev, momentum, rescale_grad, clip);
+  return rn_check_launch("sgd_mom_update_pack");
+}
+
+// Diagnostic: the same kernel with every global index checked against lim = {nparam, then per
+// tensor KRSC and CRSK copy sizes}; out-of-range accesses are skipped and flagged in *flag.
+int rn_sgd_mom_update_pack_checked(int32_t ntensors, const int64_t* offsets, const int64_t* numels, const float* wds,
+                                   float* w, const float* g, float* mom, const rn_wpack* packs, const int32_t* work,
+                                   int32_t nwork, int32_t lowp_dtype, float lr, float momentum, float rescale_grad,
+                                   const int64_t* lim, int32_t* flag, rn_stream_t stream) {
+  RN_CHECK_ARG(ntensors > 0 && nwork > 0 && lim && flag, "bad arguments");
+  hipStream_t st = as_stream(stream);
+  const int4* wk = reinterpret_cast<const int4*>(work);
+  if (lowp_dtype == RN_BF16)
+    hipLaunchKernelGGL((sgd_mom_pack_kernel<bf16_t, true>), dim3(nwork), dim3(256), 0, st, offsets, wds, w, g, mom,
+                       packs, wk, numels, lr, nullptr, momentum, rescale_grad, -1.f, lim, flag);
+  else
+    hipLaunchKernelGGL((sgd_mom_pack_kernel<float, true>), dim3(nwork), dim3(256), 0, st, offsets, wds, w, g, mom,
+                       packs, wk, numels, lr, nullptr, momentum, rescale_grad, -1.f, lim, flag);
+  return rn_check_launch("sgd_mom_update_pack_checked");
+}
+
+int32_t rn_sgd_pack_work(int32_t ntensors, const int64_t* numels, const rn_wpack* packs, int32_t* work,
+                         int32_t max_items) {
+  RN_CHECK_ARG(ntensors > 0 && numels && packs && work, "bad arguments");
+  int32_t n = 0;
+  auto put = [&](int a, int b, int c, int d) {
+    if (n < max_items) {
+      work[4 * n] = a;
+      work[4 * n + 1] = b;
+      work[4 * n + 2] = c;
+      work[4 * n + 3] = d;
+    }
+    ++n;
+  };
+  for (int t = 0; t < ntensors; ++t) {
+    const rn_wpack& p = packs[t];
+    if (p.crsk) {
+      RN_CHECK_ARG((int64_t)p.k * p.rs * p.creal == numels[t], "pack table does not match the tensor size");
+      for (int k0 = 0; k0 < p.k; k0 += 64)
+        for (int tap = 0; tap < p.rs; ++tap)
+          for (int c0 = 0; c0 < p.creal; c0 += 64) put(t, k0, tap, c0);
+    } else {
+      RN_CHECK_ARG(numels[t] < (int64_t)1 << 31, "tensor too large");
+      for (int64_t s = 0; s < numels[t]; s += kSgdChunk) put(t, (int)s, 0, 0);
+    }
+  }
+  RN_CHECK_ARG(n <= max_items, "work table too small");
+  return n;
 }
 
 int rn_nchw_to_nhwc(int32_t n, int32_t c, int32_t h, int32_t w, int32_t c_pad, const float* src, void* dst,

@@ -535,6 +535,9 @@ class Executor:
         self._fwd_train, self._fwd_infer, self._bwd = [], [], []
         # Quantization_int8: activation EMA states initialise from the first training batch
         self._qfirst = L.C.c_int32(1)
+        # SGD writes the dense weights' compute copies itself (rn_sgd_mom_update_pack); 0 = the
+        # separate pack launches after every update
+        self.fuse_packs = os.environ.get("RN_FUSED_PACK", "1") == "1"
         self._build_params()
         self._alloc_acts()
         self._build_forward()
@@ -701,7 +704,9 @@ class Executor:
         sp = self._sp()
         ws_bytes = 64
         self._descs = []  # keep ctypes structs alive
-        self.packs = []   # weight pack calls (after every update)
+        self.packs = []   # weight pack calls (bind time / set_params)
+        self.fused_packs = {}  # param -> rn_wpack fields: copies rewritten by the SGD kernel itself
+        self.unfused_packs = []  # packs that still run after every update (grouped, fake-quantized)
         self.bn_state = {}
         stem_ws = 64
         # BatchNorm statistics straight from the producing conv's epilogue (no separate stats pass)
@@ -761,8 +766,7 @@ class Executor:
                 op.dfull = op.desc = dfull
                 op.x8 = self._zeros(x.n * x.h * x.w * 8, self.tdtype)
                 op.wk = self._zeros(y.c * op.kernel[0] * op.kernel[1] * 8, self.tdtype)
-                self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(dfull), op.wsrc, self._p(op.wk), None,
-                                             sp))
+                self._add_pack(op, dfull, op.wk, None, sp)
                 stem_ws = max(stem_ws, y.h * y.w * y.cp + y.h * op.kernel[1] * y.c + y.c * op.kernel[0] * op.kernel[1] + 64)
                 xnchw = self._in_ptr  # the current input buffer (double-buffered H2D pipeline)
                 op.bnbuf = self._zeros(4 * 8, self.torch.float32)
@@ -795,8 +799,7 @@ class Executor:
                 op.desc = d
                 op.wk = self._zeros(self.lib.rn_conv_pack_numel(L.C.byref(d), 0), self.tdtype)
                 op.wc = self._zeros(self.lib.rn_conv_pack_numel(L.C.byref(d), 1), self.tdtype)
-                self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(d), op.wsrc, self._p(op.wk),
-                                             self._p(op.wc), sp))
+                self._add_pack(op, d, op.wk, op.wc, sp)
                 res = self._p(self.act(op.res)) if op.res is not None else None
                 xin = self._p(self.act(op.xf.x)) if op.xf is not None else self._p(self.act(x))
                 I.append(self._conv_fwd_call(op, d, xin, res, sp, stats=False))
@@ -864,8 +867,7 @@ class Executor:
                 op.desc = d
                 op.wk = self._zeros(op.nh * x.cp, self.tdtype)
                 op.wc = self._zeros(x.cp * _pad8(op.nh), self.tdtype)
-                self.packs.append(self._call("rn_conv_weight_pack", L.C.byref(d), op.wsrc, self._p(op.wk),
-                                             self._p(op.wc), sp))
+                self._add_pack(op, d, op.wk, op.wc, sp)
                 bias = self._pp(op.bias) if op.bias else None
                 c = self._call("rn_conv_fwd", L.C.byref(d), self._p(self.act(x)), self._p(op.wk),
                                self._p(self.act(y)), F32, None, bias, sp)
@@ -921,9 +923,24 @@ class Executor:
         q = op.qweight
         n = int(np.prod(self.plan.param_shape(op.weight)))
         op.qw = self._zeros(n, self.torch.float32)
-        self.packs.append(self._call("rn_quant_int8_fwd", F32, n, self._pp(op.weight), self._p(op.qw),
-                                     self._ap(q["minmax"]), 1, 1, q["ema"], 0, q["nbits"], qwsp, sp))
+        c = self._call("rn_quant_int8_fwd", F32, n, self._pp(op.weight), self._p(op.qw),
+                       self._ap(q["minmax"]), 1, 1, q["ema"], 0, q["nbits"], qwsp, sp)
+        self.packs.append(c)
+        self.unfused_packs.append(c)
         return self._p(op.qw)
+
+    def _add_pack(self, op, d, wk, wc, sp):
+        """Compute copies of op's weight. Dense weights packed straight from the master are
+        rewritten by the fused SGD kernel (rn_sgd_mom_update_pack); the bind-time pack below also
+        writes their zero padding, which that kernel never touches."""
+        c = self._call("rn_conv_weight_pack", L.C.byref(d), op.wsrc, self._p(wk), self._p(wc), sp)
+        self.packs.append(c)
+        if d.groups == 1 and not getattr(op, "qweight", None) and self.fuse_packs:
+            self.fused_packs[op.weight] = (wk.data_ptr() if wk is not None else 0,
+                                           wc.data_ptr() if wc is not None else 0,
+                                           d.k, d.r * d.s, d.c_real, d.c, d.k_pad)
+        else:
+            self.unfused_packs.append(c)
 
     # ------------------------------------------------------------------ backward
     def _build_backward(self):
@@ -1037,7 +1054,10 @@ class Executor:
             elif op.kind == "add":
                 g = dy
                 if op.relu:
+                    # held by the executor: the bound call keeps only the raw pointer (a dropped
+                    # tensor would be recycled by the caching allocator while the plan writes it)
                     gbuf = self._zeros(op.y.numel, self.tdtype)
+                    self._grads[("relu_add", id(op))] = gbuf
                     self._bwd.append(self._call("rn_relu_bwd", op.y.numel, self.dtype, self._p(self.act(op.y)),
                                                 self._p(dy), self._p(gbuf), None, sp))
                     g = gbuf
@@ -1054,6 +1074,27 @@ class Executor:
     # ------------------------------------------------------------------ update
     def _build_update(self):
         self.wpack_calls = list(self.packs)
+        self.opt_packs = None
+        if self.fused_packs:
+            dt = np.dtype([("krsc", "<u8"), ("crsk", "<u8"), ("k", "<i4"), ("rs", "<i4"), ("creal", "<i4"),
+                           ("c", "<i4"), ("kpad", "<i4"), ("pad", "<i4")])
+            tab = np.zeros(len(self.param_order), dtype=dt)
+            for i, nm in enumerate(self.param_order):
+                e = self.fused_packs.get(nm)
+                if e is not None:
+                    tab[i] = e + (0,)
+            nums = np.array([int(np.prod(self.param_shape[n])) for n in self.param_order], dtype=np.int64)
+            cap = int(sum((n + 4095) // 4096 for n in nums) + sum(
+                ((e[2] + 63) // 64) * e[3] * ((e[4] + 63) // 64) for e in self.fused_packs.values()))
+            work = np.zeros((cap, 4), dtype=np.int32)
+            nwork = self.lib.rn_sgd_pack_work(len(nums), nums.ctypes.data_as(L.C.c_void_p),
+                                              tab.ctypes.data_as(L.C.c_void_p), work.ctypes.data_as(L.C.c_void_p),
+                                              cap)
+            if nwork < 0:
+                raise L.RNError("rn_sgd_pack_work: %s" % self.lib.rn_last_error().decode())
+            self.opt_packs = self.torch.from_numpy(tab.view(np.uint8).copy()).to(self.device)
+            self.opt_work = self.torch.from_numpy(work[:nwork].copy()).to(self.device)
+            self.opt_nwork = int(nwork)
 
     # ------------------------------------------------------------------ running
     def _run(self, calls):
@@ -1140,6 +1181,16 @@ class Executor:
         if self._wd_value != wd:
             self.opt_wds.copy_(self.torch.from_numpy(self.wd_mult * np.float32(wd)))
             self._wd_value = wd
+        if self.opt_packs is not None:
+            L.check(self.lib.rn_sgd_mom_update_pack(len(self.param_order), self._p(self.opt_offsets),
+                                                    self._p(self.opt_numels), self._p(self.opt_wds),
+                                                    self._p(self.master), self._p(self.grad), self._p(self.mom),
+                                                    self._p(self.opt_packs), self._p(self.opt_work),
+                                                    self.opt_nwork, self.dtype, float(lr), None,
+                                                    float(momentum), float(rescale_grad), float(clip), self._sp()),
+                    "rn_sgd_mom_update_pack")
+            self._run(self.unfused_packs)
+            return
         L.check(self.lib.rn_sgd_mom_update(len(self.param_order), self._p(self.opt_offsets),
                                            self._p(self.opt_numels), self._p(self.opt_wds), self._p(self.master),
                                            self._p(self.grad), self._p(self.mom), None, F32, float(lr), None,

@@ -73,6 +73,11 @@ SIGNATURES = {
     "rn_softmax_output": (_i32, [_i32, _i32, _i32, _i32, _P, _P, _P, _P, _f32, _P, _P]),
     "rn_col_sum": (_i32, [_i32, _i64, _i32, _i32, _P, _P, _i32, _P]),
     "rn_sgd_mom_update": (_i32, [_i32, _P, _P, _P, _P, _P, _P, _P, _i32, _f32, _P, _f32, _f32, _f32, _P]),
+    "rn_sgd_mom_update_pack": (_i32, [_i32, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _i32, _f32, _P, _f32, _f32, _f32,
+                                      _P]),
+    "rn_sgd_mom_update_pack_checked": (_i32, [_i32, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _i32, _f32, _f32, _f32, _P,
+                                              _P, _P]),
+    "rn_sgd_pack_work": (_i32, [_i32, _P, _P, _P, _i32]),
     "rn_nchw_to_nhwc": (_i32, [_i32, _i32, _i32, _i32, _i32, _P, _P, _i32, _P]),
     "rn_cast": (_i32, [_i64, _P, _i32, _P, _i32, _P]),
     "rn_eltwise_add": (_i32, [_i64, _i32, _P, _P, _P, _i32, _P]),

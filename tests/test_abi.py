@@ -40,3 +40,30 @@ def test_host_side_validation_and_errors():
     pd = L.PoolDesc(dtype=L.RN_BF16, n=2, h=112, w=112, c=64, r=3, s=3, stride_h=2, stride_w=2, pad_h=1, pad_w=1,
                     type=L.RN_POOL_MAX, global_pool=0)
     assert lib.rn_pool_desc_init(C.byref(pd)) == 0 and (pd.p, pd.q) == (56, 56)
+
+
+def test_sgd_pack_work_table():
+    """Host-side work table of rn_sgd_mom_update_pack: 4096-element chunks for tensors without a
+    CRSK copy, 64 x 64 (k, c) tiles per tap for the others; every element covered exactly once."""
+    import numpy as np
+    lib = L.load()
+    dt = np.dtype([("krsc", "<u8"), ("crsk", "<u8"), ("k", "<i4"), ("rs", "<i4"), ("creal", "<i4"),
+                   ("c", "<i4"), ("kpad", "<i4"), ("pad", "<i4")])
+    assert dt.itemsize == 40
+    tab = np.zeros(3, dtype=dt)
+    tab[1] = (1, 1, 100, 9, 70, 72, 104, 0)   # conv 3x3, ragged k and c
+    tab[2] = (1, 0, 16, 49, 3, 8, 16, 0)      # stem: KRSC copy only -> chunks
+    nums = np.array([5000, 100 * 9 * 70, 16 * 49 * 3], dtype=np.int64)
+    work = np.zeros((64, 4), dtype=np.int32)
+    P = lambda a: a.ctypes.data_as(C.c_void_p)
+    n = lib.rn_sgd_pack_work(3, P(nums), P(tab), P(work), 64)
+    assert n == 2 + 2 * 9 * 2 + 1, n
+    w = work[:n]
+    assert [tuple(r) for r in w[:2]] == [(0, 0, 0, 0), (0, 4096, 0, 0)]
+    cover = np.zeros((100, 9, 70), dtype=np.int32)
+    for t, k0, tap, c0 in w[w[:, 0] == 1]:
+        cover[k0:k0 + 64, tap, c0:c0 + 64] += 1
+    assert (cover == 1).all()
+    assert lib.rn_sgd_pack_work(3, P(nums), P(tab), P(work), 4) == -1
+    tab[1]["k"] = 99  # size mismatch is refused
+    assert lib.rn_sgd_pack_work(3, P(nums), P(tab), P(work), 64) == -1

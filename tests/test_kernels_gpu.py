@@ -281,6 +281,73 @@ def test_sgd_momentum(gpu):
 
 
 @pytest.mark.parametrize("dtype", [F32, BF16])
+def test_sgd_update_pack(gpu, dtype):
+    """rn_sgd_mom_update_pack = rn_sgd_mom_update followed by rn_conv_weight_pack of every dense
+    conv / FC tensor, bit for bit (padding entries of the copies untouched)."""
+    rng = np.random.default_rng(11)
+    # (name, conv desc args or None): a 3x3 conv with padded channels, the stem (c=8 over 3), an FC
+    # with a ragged output count, a BN gamma
+    specs = [("c3_weight", (dtype, 2, 24, 5, 5, 40, 3, 3, 1, 1)), ("g_gamma", None),
+             ("stem_weight", (dtype, 2, 8, 9, 9, 16, 7, 7, 2, 3, 3)), ("fc_weight", (dtype, 2, 64, 1, 1, 1000, 1, 1, 1, 0))]
+    descs, sizes = [], []
+    for nm, a in specs:
+        if a is None:
+            descs.append(None)
+            sizes.append(40)
+            continue
+        d = conv_desc(*a[:10], c_real=a[10] if len(a) > 10 else None)
+        descs.append(d)
+        sizes.append(int(d.k * d.r * d.s * d.c_real))
+    offs = np.cumsum([0] + [((s + 3) // 4) * 4 for s in sizes])[:-1]
+    total = int(offs[-1] + sizes[-1] + 4)
+    t = lambda a, dt=torch.float32: torch.tensor(a, dtype=dt, device=gpu)
+    w, g, m = (rng.standard_normal(total).astype(np.float32) for _ in range(3))
+    wd = np.array([1e-4, 0.0, 1e-4, 1e-4], dtype=np.float32)
+    offs_d, sizes_d, wds_d = t(offs, torch.int64), t(sizes, torch.int64), t(wd)
+    tab = np.zeros(len(specs), dtype=[("krsc", "<u8"), ("crsk", "<u8"), ("k", "<i4"), ("rs", "<i4"),
+                                      ("creal", "<i4"), ("c", "<i4"), ("kpad", "<i4"), ("pad", "<i4")])
+    outs = []
+    for i, d in enumerate(descs):
+        if d is None:
+            outs.append(None)
+            continue
+        # copies prefilled with a sentinel: the padding must keep it
+        pair = [torch.full((int(L.load().rn_conv_pack_numel(C.byref(d), j)),), 7.0, dtype=tdt(dtype), device=gpu)
+                for j in (0, 1)]
+        ref = [x.clone() for x in pair]
+        outs.append((pair, ref))
+        tab[i] = (pair[0].data_ptr(), pair[1].data_ptr(), d.k, d.r * d.s, d.c_real, d.c, d.k_pad, 0)
+    tab_d = torch.from_numpy(tab.view(np.uint8).copy()).to(gpu)
+    work = np.zeros((4096, 4), dtype=np.int32)
+    nwork = L.load().rn_sgd_pack_work(len(specs), np.asarray(sizes, np.int64).ctypes.data_as(C.c_void_p),
+                                      tab.ctypes.data_as(C.c_void_p), work.ctypes.data_as(C.c_void_p), 4096)
+    assert nwork > 0
+    work_d = torch.from_numpy(work[:nwork].copy()).to(gpu)
+    args = lambda wv, mv: (p(offs_d), p(sizes_d), p(wds_d), p(wv), p(gd), p(mv))
+    gd = t(g)
+    w1, m1, w2, m2 = t(w), t(m), t(w), t(m)
+    sc = (C.c_float(0.05), None, C.c_float(0.9), C.c_float(1 / 128.), C.c_float(-1.0), stream())
+    L.call("rn_sgd_mom_update", len(specs), *args(w1, m1), None, F32, *sc)
+    for i, d in enumerate(descs):
+        if d is not None:
+            ref = outs[i][1]
+            L.call("rn_conv_weight_pack", C.byref(d), C.c_void_p(w1.data_ptr() + 4 * int(offs[i])), p(ref[0]),
+                   p(ref[1]), stream())
+    L.call("rn_sgd_mom_update_pack", len(specs), *args(w2, m2), p(tab_d), p(work_d), nwork, dtype, *sc)
+    torch.cuda.synchronize()
+    assert torch.equal(w1, w2) and torch.equal(m1, m2)
+    for o in outs:
+        if o is None:
+            continue
+        pair, ref = o
+        # reference pack zero-fills the padding; the fused kernel leaves the sentinel there
+        for a, b in zip(pair, ref):
+            pad = b == 0
+            assert torch.equal(a[~pad], b[~pad])
+            assert bool((a[pad] == 7.0).all())
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
 def test_quant_int8(gpu, dtype):
     rng = np.random.default_rng(10)
     n = 4096

@@ -175,3 +175,54 @@ def test_plan_bn_bwd_fusion_default(monkeypatch):
     assert counts() == (48, 48, 2)
     monkeypatch.setenv("RN_BN_BWD_FUSION", "0")
     assert counts() == (0, 0, 50)
+
+
+def _live_tensors(ex):
+    """Every torch tensor the executor (or its plan's ops) keeps a reference to."""
+    import torch
+    seen, out = set(), []
+
+    def walk(o, depth=0):
+        if depth > 4 or id(o) in seen:
+            return
+        seen.add(id(o))
+        if isinstance(o, torch.Tensor):
+            out.append(o)
+        elif isinstance(o, dict):
+            for v in o.values():
+                walk(v, depth + 1)
+        elif isinstance(o, (list, tuple)):
+            for v in o:
+                walk(v, depth + 1)
+    for v in vars(ex).values():
+        walk(v)
+    for op in ex.plan.ops:
+        for v in vars(op).values():
+            walk(v)
+    return out
+
+
+@pytest.mark.parametrize("graph", ["resnet20", "resnext", "resnet_int8"])
+def test_bound_pointers_are_owned(graph):
+    """Every device pointer a bound call carries lies inside a tensor the executor keeps alive
+    (a dropped temporary is recycled by the caching allocator while the plan still writes it)."""
+    import ctypes as C
+    sym, shp = {
+        "resnet20": (graphs.resnet20_cifar(), (4, 3, 32, 32)),
+        "resnext": (graphs.resnext([1, 1, 1, 1], 4, [64, 256, 512, 1024, 2048], 16, "float32", 32), (2, 3, 64, 64)),
+        "resnet_int8": (graphs.resnet_int8([1, 1, 1, 1], 4, [64, 256, 512, 1024, 2048], 16), (2, 3, 64, 64)),
+    }[graph]
+    ex = Executor(Plan(sym, [("data", shp)], [("softmax_label", (shp[0],))]), "cpu")
+    spans = sorted((t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()) for t in _live_tensors(ex))
+    starts = [s for s, _ in spans]
+    import bisect
+    lists = [ex._fwd_train, ex._fwd_infer, ex._bwd, ex.wpack_calls, getattr(ex, "unfused_packs", [])]
+    n = 0
+    for lst in lists:
+        for name, fn, args in lst:
+            for a in args:
+                if isinstance(a, C.c_void_p) and a.value and a is not ex._spv:
+                    i = bisect.bisect_right(starts, a.value) - 1
+                    assert i >= 0 and a.value < spans[i][1], (name, hex(a.value))
+                    n += 1
+    assert n > 100

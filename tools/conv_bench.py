@@ -45,7 +45,7 @@ def main():
     modes = a.only.split(",")
     tot = {m: 0.0 for m in modes}
     flops_tot = 0.0
-    print("%-26s %3s %-22s %-5s" % ("layer", "n", "shape", "") + "".join("%18s" % m for m in modes))
+    print("%-26s %3s %-22s %-5s" % ("layer", "n", "shape", "") + "".join("%23s" % m for m in modes))
     for key, (name, cnt) in shapes.items():
         if a.filter and a.filter not in name:
             continue
@@ -69,6 +69,9 @@ def main():
             "wgrad": lambda: lib.rn_conv_bwd_filter(C.byref(d), P(x), P(yv), P(dw), st),
         }
         flops = 2.0 * n * d.p * d.q * k * (c // g) * kern[0] * kern[1]
+        # algorithmic HBM bytes (bf16): x + w + y (+ residual for fwd); per-mode roofline time
+        xb, yb, wb = 2.0 * n * h * w * c, 2.0 * n * d.p * d.q * k, 2.0 * k * kern[0] * kern[1] * (c // g)
+        algb = {"fwd": xb + wb + yb * (2 if res else 1), "dgrad": yb + wb + xb, "wgrad": xb + yb + 2 * wb}
         row = "%-26s %3d %-22s %-5s" % (name[:26], cnt, "%dx%dx%d>%d k%d s%d" % (h, w, c, k, kern[0], stride[0]),
                                        "g%d" % g if g > 1 else ("+res" if res else ""))
         for m in modes:
@@ -96,7 +99,8 @@ def main():
                 torch.cuda.synchronize()
                 ms = sum(x.elapsed_time(y) for x, y in evs) / a.iters
             tot[m] += ms * cnt
-            row += "%8.1fus %6.0fT" % (ms * 1e3, flops / ms / 1e9)
+            roof = max(flops / 2.5e15, algb[m] / 8e12) * 1e3
+            row += "%8.1fus %6.0fT %3.0f%%" % (ms * 1e3, flops / ms / 1e9, 100 * roof / ms)
         flops_tot += flops * cnt
         print(row, flush=True)
     print("per-step totals: " + "  ".join("%s %.3f ms" % (m, tot[m]) for m in modes) +

@@ -9,7 +9,7 @@ import sys
 def main(path):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if "sgd_mom_kernel" in r["Kernel_Name"]]
+    idx = [i for i, r in enumerate(rows) if "sgd_mom" in r["Kernel_Name"]]
     a, b = idx[-2] + 1, idx[-1] + 1
     fam = collections.defaultdict(float)
     cnt = collections.Counter()
