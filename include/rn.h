@@ -66,6 +66,9 @@ int rn_conv_fwd(const rn_conv_desc* d, const void* x, const void* w_krsc, void* 
 int rn_conv_fwd_bnstats(const rn_conv_desc* d, const void* x, const void* w_krsc, void* y, int32_t y_dtype,
                         const void* add_src, const float* bias, float* part, rn_stream_t stream);
 int64_t rn_conv_bnstats_blocks(const rn_conv_desc* d);
+/* Rows each BatchNorm partial block of the conv kernel covers (mode 0 fwd / 1 dgrad): 128, or half
+ * the tile rows of the 256/224-row tiles. rn_bn_fwd_train_part's rows_blk. */
+int32_t rn_conv_bn_part_rows(const rn_conv_desc* d, int32_t mode);
 /* Kernel variant the bf16 forward (mode 0, plain: no bias / input transform) or data-gradient
  * (mode 1) of `d` runs: the column count of its 256-row tile (256, 128 or 64), or 0 for the
  * 128-row kernel. Lets a caller enable the BatchNorm epilogue fusions only where they pay (the
@@ -357,7 +360,9 @@ const char* rn_last_error(void);
  * 5 = wgrad variant (0 auto: 128x128 LDS-DMA tiles where K and the column count exceed 64; 1 = 256-column
  *     LDS-DMA tiles, measured slower; 3 = the register-staged kernel only),
  * 6 = diagnostic only: wgrad skips its dW epilogue (wrong results; isolates the atomic adds),
- * 7 = igemm 256-row tile schedule experiments (bit mask; 0 = default). */
+ * 7 = igemm 256-row tile schedule experiments (bit mask; 0 = default),
+ * 8 = igemm 256-row tile MFMA shape (0 = 32x32x16, 1 = 16x16x32),
+ * 9 = igemm 224-row tiles for the 256/128-column tiles (0 = on, 1 = 256 rows). */
 int rn_set_tuning(int32_t key, int32_t value);
 int32_t rn_version(void);
 /* Number of compute units of the current device (for split heuristics / reporting). */

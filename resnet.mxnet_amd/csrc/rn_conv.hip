@@ -74,6 +74,15 @@ struct IgemmArgs {
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ (row & 7); }
+// swizzle for 32x32x16 fragment reads (32 lanes read 32 consecutive rows at one chunk): the
+// 16-lane ds_read_b128 groups {0-3,12-15,20-27} / {4-11,16-19,28-31} then cover 16 distinct
+// 16-byte slots of a 256-byte line pair (row & 15 distinct within each group)
+__device__ __forceinline__ int swz32(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+typedef float v16f __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ void mfma32(v16f& acc, const uint4& a, const uint4& b) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(v8s, a), __builtin_bit_cast(v8s, b), acc, 0, 0, 0);
+}
 
 // LDS-DMA (buffer_load ... lds) of one 16-byte chunk per lane: the LDS destination is the
 // wave-uniform base + 16 * lane; an out-of-range voffset reads zeros (halo / ragged edges).
@@ -610,7 +619,9 @@ __device__ __forceinline__ v4i make_rsrc(const void* base, uint32_t bytes) {
 }
 
 // one 16-byte LDS-DMA per lane into the wave-uniform LDS byte address lds (+16 * lane); M0 is
-// compiler-reserved, so it is saved and restored inside the statement
+// compiler-reserved, so it is saved and restored inside the statement. No "memory" clobber: the
+// LDS it writes is ordered by the explicit wait_vmcnt + barrier (which carry one), and without it
+// the compiler keeps kernel arguments in SGPRs and schedules the fragment reads across the DMAs.
 __device__ __forceinline__ void dma16_asm(const v4i& rsrc, uint32_t lds, uint32_t voff) {
   uint32_t keep;
   lds = __builtin_amdgcn_readfirstlane(lds);  // free when already scalar; M0 is written by an SALU move
@@ -621,8 +632,7 @@ __device__ __forceinline__ void dma16_asm(const v4i& rsrc, uint32_t lds, uint32_
       "buffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(voff), "s"(lds), "s"(rsrc)
-      : "memory");
+      : "v"(voff), "s"(lds), "s"(rsrc));
 }
 
 // the same through global_load_lds_dwordx4 with a per-lane 64-bit source address (no buffer
@@ -657,17 +667,28 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // BatchNorm-backward reduction of the stored gradient: bnred[class][2*mtile + wm][ldo][2].
 // BN = 64 (the 64-channel layers): 4 waves stacked along M (each 64 x 64), two workgroups per CU;
 // plain epilogue only (EPI 0).
-template <int BN, int NBUF, int EPI = 0>
+// M32: v_mfma_f32_32x32x16_bf16 (32-cycle MFMAs: three times the issue shadow of the 16x16x32
+// form for the fragment reads, DMA address arithmetic and waits of the same K-tile) with the
+// swz32 LDS image; else v_mfma_f32_16x16x32_bf16 with swz.
+// BM: tile rows, 256 or 224 (16x16 MFMAs only: 112 rows per wave row). M = N*P*Q is 256 * 49 * 4^j
+// for every ResNet-50 layer at batch 256, so 256-row tiles leave a last round of 196 / 256 workgroups
+// on every grid; 224-row tiles (7 / 8 of the rows) fill 224 / 256. The A region of the LDS stage
+// keeps 256 rows (the DMA rounds of rows >= BM read zeros).
+template <int BN, int NBUF, int EPI = 0, bool M32 = false, int BM = 256>
 __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_big_kernel(IgemmArgs p) {
-  constexpr int BM = 256, CE = 8, BKE = 64;
+  constexpr int BMA = 256, CE = 8, BKE = 64;
   constexpr int NW = BN == 64 ? 4 : 8;           // waves
   constexpr int WAVES_N = BN == 64 ? 1 : 4, WAVES_M = NW / WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;  // wave tile
   constexpr int RPR = NW * 8;                    // rows per DMA round (8 per wave)
-  constexpr int AR = BM / RPR, BR = BN / RPR;    // DMA rounds per K-tile
+  constexpr int AR = BMA / RPR, BR = BN / RPR;   // DMA rounds per K-tile
   constexpr int LPT = AR + BR;                   // DMA instructions per thread per K-tile
-  constexpr int MI = WM / 16, NI = WN / 16;      // 16x16 accumulators per wave
-  constexpr int kStage = (BM + BN) * 8;          // 16-byte chunks per K-tile
+  constexpr int FM = M32 ? 32 : 16;              // MFMA tile edge
+  constexpr int MI = WM / FM, NI = WN / FM;      // accumulators per wave
+  constexpr int NCH = (WM + 63) / 64;            // 64-row epilogue chunks per wave
+  static_assert(WM % FM == 0 && (BM == 256 || !M32) && (BM == 256 || BN != 64), "tile shape");
+  using AccT = typename std::conditional<M32, v16f, v4f>::type;
+  constexpr int kStage = (BMA + BN) * 8;         // 16-byte chunks per K-tile
   constexpr int EP_LD = WN + 4;                  // staged fp32 row stride
   constexpr int EP_WAVE = 64 * EP_LD;            // floats per wave per epilogue half
   constexpr int kEpChunks = NW * EP_WAVE / 4;
@@ -697,12 +718,12 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
 
   // DMA lane -> (row 8*wid + lane/8 (+64 i), LDS slot lane&7); it fetches the source chunk that the
   // XOR read-swizzle expects in that slot
-  const int lch = (lane & 7) ^ ((lane >> 3) & 7);
+  const int lch = M32 ? (lane & 7) ^ ((4 * wid + (lane >> 4)) & 7) : (lane & 7) ^ ((lane >> 3) & 7);
   int a_row[AR], a_h[AR], a_w[AR];  // row offset of tap (0,0); its gathered coordinates
 #pragma unroll
   for (int i = 0; i < AR; ++i) {
     const int m = m0 + RPR * i + (tid >> 3);
-    if (m < Mc) {
+    if (m < Mc && RPR * i + (tid >> 3) < BM) {
       const int n = fdiv(m, cl.fdPQ);
       const int rem = m - n * cl.Pc * cl.Qc;
       const int ii = fdiv(rem, cl.fdQ);
@@ -761,9 +782,14 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
       dma16_asm(rs_x, d_la + k * (RPR * 128), ok ? ((uint32_t)((a_row[k] + d_toffa) * 2) & dmask) : kOob);
     } else {
       const int i = k - AR;
-      dma16_asm(rs_w, d_la + BM * 128 + i * (RPR * 128),
+      dma16_asm(rs_w, d_la + BMA * 128 + i * (RPR * 128),
                 (d_cok && b_ok[i]) ? ((uint32_t)((b_off[i] + d_toffb) * 2) & dmask) : kOob);
     }
+  };
+  // diagnostic (rn_set_tuning 7 bit 8): no DMAs inside the main loop (wrong results; isolates their cost)
+  const bool loop_dma = !(p.sched & 8);
+  auto lpiece = [&](int k) __attribute__((always_inline)) {
+    if (loop_dma) piece(k);
   };
   auto issue = [&](int buf) __attribute__((always_inline)) {
     prep(buf);
@@ -771,42 +797,53 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
     for (int k = 0; k < LPT; ++k) piece(k);
   };
 
-  v4f acc[MI][NI];
+  AccT acc[MI][NI];
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NI; ++j) acc[i][j] = AccT{};
 
   // the MFMAs of K-tile `buf`, with the next K-tile's DMAs between the first MFMA groups
   // (inline asm is a scheduling boundary: each DMA's address arithmetic overlaps the MFMAs around it)
   auto compute = [&](int buf) __attribute__((always_inline)) {
     const uint4* As = smem + buf * kStage;
-    const uint4* Bs = As + BM * 8;
-#pragma unroll
-    for (int slab = 0; slab < 2; ++slab) {
-      uint4 af[MI], bfr[NI];
-      const int kc = slab * 4 + (lane >> 4);
+    const uint4* Bs = As + BMA * 8;
+    // k-steps per K-tile: 4 of 16 (32x32x16: lane half h = lane >> 5 holds chunk 2 ks + h of its
+    // row) or 2 of 32 (16x16x32: lane quarter q = lane >> 4 holds chunk 4 ks + q). Fragments are
+    // double-buffered in registers: k-step ks + 1 is read while ks multiplies.
+    constexpr int KS = M32 ? 4 : 2;
+    uint4 af[2][MI], bfr[2][NI];
+    auto ldf = [&](int ks) __attribute__((always_inline)) {
+      const int kc = M32 ? 2 * ks + (lane >> 5) : 4 * ks + (lane >> 4);
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const int row = wn * WN + j * 16 + (lane & 15);
-        bfr[j] = Bs[row * 8 + swz(row, kc)];
+        const int row = wn * WN + j * FM + (lane & (FM - 1));
+        bfr[ks & 1][j] = Bs[row * 8 + (M32 ? swz32(row, kc) : swz(row, kc))];
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const int row = wm * WM + i * 16 + (lane & 15);
-        af[i] = As[row * 8 + swz(row, kc)];
+        const int row = wm * WM + i * FM + (lane & (FM - 1));
+        af[ks & 1][i] = As[row * 8 + (M32 ? swz32(row, kc) : swz(row, kc))];
       }
+    };
+    ldf(0);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 1 < KS) ldf(ks + 1);
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
 #pragma unroll
-        for (int j = 0; j < NI; ++j) mfma_slab<bf16_t>(acc[i][j], af[i], bfr[j]);
-        // 2 buffers: the DMAs early (over slab 0's groups) so they have the longest to land; 3
-        // buffers (one more K-tile in flight): spread over both slabs. Measured per layer.
-        constexpr int G = NBUF == 2 ? MI : 2 * MI;  // MFMA groups the LPT DMAs are spread over
-        const int g = slab * MI + i;
+        for (int j = 0; j < NI; ++j) {
+          if constexpr (M32) mfma32(acc[i][j], af[ks & 1][i], bfr[ks & 1][j]);
+          else mfma_slab<bf16_t>(acc[i][j], af[ks & 1][i], bfr[ks & 1][j]);
+        }
+        // 2 buffers: the DMAs over the first half of the K-tile's MFMA groups, so they have the
+        // longest to land; 3 buffers (one more K-tile in flight): spread over all of them
+        constexpr int G = NBUF == 2 ? KS / 2 * MI : KS * MI;
+        const int g = ks * MI + i;
         if (g < G) {
 #pragma unroll
-          for (int q = g * LPT / G; q < (g + 1) * LPT / G; ++q) piece(q);
+          for (int q = g * LPT / G; q < (g + 1) * LPT / G; ++q) lpiece(q);
         }
       }
     }
@@ -853,7 +890,9 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   }
   const bf16_t* __restrict__ bxg = reinterpret_cast<const bf16_t*>(p.bn_x);
 #pragma unroll
-  for (int h = 0; h < WM / 64; ++h) {
+  for (int h = 0; h < NCH; ++h) {
+    constexpr int kLast = WM - 64 * (NCH - 1);  // rows of the last chunk (48 for 112-row waves)
+    const int rows_h = h + 1 < NCH ? 64 : kLast;
     int64_t off[CPR];  // this lane's rows: lane / CPR + (64 / CPR) k
     uint4 addv[CPR];
     uint4 xpre[EPI == 2 ? CPR : 1];  // BN input at the same positions (EPI 2), loaded with the residual
@@ -864,7 +903,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
       off[k] = -1;
       addv[k] = make_uint4(0, 0, 0, 0);
       if constexpr (EPI == 2) xpre[k] = make_uint4(0, 0, 0, 0);
-      if (m < Mc && col0 < p.K) {
+      if (m < Mc && col0 < p.K && r < rows_h) {
         const int n = fdiv(m, cl.fdPQ);
         const int rem = m - n * cl.Pc * cl.Qc;
         const int ii = fdiv(rem, cl.fdQ);
@@ -876,12 +915,25 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
       }
     }
     if (h > 0) __syncthreads();  // the first half's staged rows have been read
+    if constexpr (M32) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < NI; ++j)
+        for (int j = 0; j < NI; ++j)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) ep[(i * 16 + (lane >> 4) * 4 + e) * EP_LD + j * 16 + (lane & 15)] = acc[h * 4 + i][j][e];
+          for (int e = 0; e < 16; ++e)
+            ep[(i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * EP_LD + j * 32 + (lane & 31)] =
+                acc[h * 2 + i][j][e];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (h * 4 + i < MI)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              ep[(i * 16 + (lane >> 4) * 4 + e) * EP_LD + j * 16 + (lane & 15)] = acc[h * 4 + i][j][e];
+    }
     __syncthreads();
     if constexpr (EPI == 1) {
       if (h == 0) {  // pivot: the BN's moving mean (accumulated sums), else the wave row's first
@@ -1732,6 +1784,18 @@ int big_tile_cols(const IgemmArgs& a, int64_t xb, int64_t wb) {
   return (a.K >= 256 && rows * ceil_div(a.K, 256) >= 192) ? 256 : 128;
 }
 
+// Rows of the 256-row-family tile for `bn` columns: 224 (16x16 MFMAs) unless rn_set_tuning 9 = 1,
+// or the 64-column tile. The BatchNorm epilogue partials cover one wave row (half the tile).
+int big_tile_rows(int bn) { return (bn >= 128 && g_tune[RN_TUNE_IGEMM_ROWS] != 1) ? 224 : 256; }
+
+// rows per BatchNorm partial block of the conv kernel these arguments select
+int bn_part_rows(const IgemmArgs& a, bool bf16) {
+  if (!bf16) return 128;
+  const int64_t xb = (int64_t)a.N * a.H * a.W * a.C * 2, wb = (int64_t)a.K * a.wrow * 2;
+  const int bn = big_tile_cols(a, xb, wb);
+  return bn >= 128 ? big_tile_rows(bn) / 2 : 128;
+}
+
 template <typename T, typename OutT>
 int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   RN_CHECK_ARG((int64_t)a.N * a.H * a.W * a.C < (1ll << 31), "gathered tensor exceeds 2^31 elements");
@@ -1756,23 +1820,38 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
     const int epi = a.stats ? 1 : a.bnred ? 2 : a.bnacc ? (a.bn_x ? 2 : 1) : 0;
     const int bn = big_tile_cols(a, xb, wb);
     RN_CHECK_ARG(!a.bnacc || bn >= 128, "accumulated BatchNorm sums need the 256-row tile (rn_conv_tile >= 128)");
+    const bool m32 = g_tune[RN_TUNE_IGEMM_MFMA] != 1;
     if (bn == 64 && epi == 0) {
       b.ntn = (int)ceil_div(a.K, 64);
       dim3 grid((unsigned)(ceil_div(maxMc, 256) * b.ntn), 1, a.ncls);
-      hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0>), grid, dim3(256), 0, st, b);
+      if (m32) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true>), grid, dim3(256), 0, st, b);
+      else hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, false>), grid, dim3(256), 0, st, b);
       return rn_check_launch("igemm_big64");
     }
     if (bn >= 128) {
+      const int bm = big_tile_rows(bn);
+      RN_CHECK_ARG(!(a.stats || a.bnred) || bm / 2 == bn_part_rows(a, true), "BN partial rows mismatch");
+      if (a.bnred) b.mt_max = (int)ceil_div(maxMc, bm / 2);
       b.ntn = (int)ceil_div(a.K, bn);
-      dim3 grid((unsigned)(ceil_div(maxMc, 256) * b.ntn), 1, a.ncls);
-#define RN_BIG(BNV, NB)                                                                                       \
-  if (epi == 0) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 0>), grid, dim3(512), 0, st, b);              \
-  else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 1>), grid, dim3(512), 0, st, b);         \
-  else hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 2>), grid, dim3(512), 0, st, b);
-      if (bn == 256) {
-        RN_BIG(256, 2)
+      dim3 grid((unsigned)(ceil_div(maxMc, bm) * b.ntn), 1, a.ncls);
+#define RN_BIG(BNV, NB, M, R)                                                                                 \
+  if (epi == 0) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 0, M, R>), grid, dim3(512), 0, st, b);        \
+  else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 1, M, R>), grid, dim3(512), 0, st, b);   \
+  else hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 2, M, R>), grid, dim3(512), 0, st, b);
+      if (bm == 224) {
+        if (bn == 256) {
+          RN_BIG(256, 2, false, 224)
+        } else {
+          RN_BIG(128, 3, false, 224)
+        }
+      } else if (bn == 256 && m32) {
+        RN_BIG(256, 2, true, 256)
+      } else if (bn == 256) {
+        RN_BIG(256, 2, false, 256)
+      } else if (m32) {
+        RN_BIG(128, 3, true, 256)
       } else {
-        RN_BIG(128, 3)
+        RN_BIG(128, 3, false, 256)
       }
 #undef RN_BIG
       return rn_check_launch("igemm_big");
@@ -1898,13 +1977,20 @@ int32_t rn_conv_tile(const rn_conv_desc* d, int32_t mode) {
   return big_tile_cols(a, xb, wb);
 }
 
-int64_t rn_conv_bnstats_blocks(const rn_conv_desc* d) { return ceil_div((int64_t)d->n * d->p * d->q, 128); }
+int32_t rn_conv_bn_part_rows(const rn_conv_desc* d, int32_t mode) {
+  if (!d || (mode != 0 && mode != 1)) return 0;
+  return bn_part_rows(make_igemm_args(d, mode), d->dtype == RN_BF16);
+}
+
+int64_t rn_conv_bnstats_blocks(const rn_conv_desc* d) {
+  return ceil_div((int64_t)d->n * d->p * d->q, rn_conv_bn_part_rows(d, 0));
+}
 
 int64_t rn_conv_bnred_blocks(const rn_conv_desc* d) {
   IgemmArgs a = make_igemm_args(d, 1);
   int maxMc = 0;
   for (int z = 0; z < a.ncls; ++z) maxMc = std::max(maxMc, a.N * a.cls[z].Pc * a.cls[z].Qc);
-  return (int64_t)a.ncls * ceil_div(maxMc, 128);
+  return (int64_t)a.ncls * ceil_div(maxMc, bn_part_rows(a, d->dtype == RN_BF16));
 }
 
 int rn_conv_bwd_data_bnred(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx, const void* add_src,

@@ -822,7 +822,7 @@ class Executor:
                 elif op.part_src is not None:
                     s_ = op.part_src
                     F.append(self._call("rn_bn_fwd_train_part", L.C.byref(op.desc), self._p(s_.part), s_.part_blocks,
-                                        128, s_.y.cp, self._p(self.act(x)), yptr, gamma,
+                                        s_.part_rows, s_.y.cp, self._p(self.act(x)), yptr, gamma,
                                         self._pp(op.beta), self._ap(op.mean), self._ap(op.var), op.sm, op.si, op.sc,
                                         op.sh, wsp, sp))
                 else:
@@ -909,6 +909,7 @@ class Executor:
         if stats and op.bnstats:
             if getattr(op, "part", None) is None:
                 op.part_blocks = int(self.lib.rn_conv_bnstats_blocks(L.C.byref(d)))
+                op.part_rows = int(self.lib.rn_conv_bn_part_rows(L.C.byref(d), 0))
                 op.part = self._zeros(op.part_blocks * 3 * op.y.cp, self.torch.float32)
             part = self._p(op.part)
         if sc is None and part is None:

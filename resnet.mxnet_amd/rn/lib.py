@@ -41,6 +41,7 @@ SIGNATURES = {
     "rn_conv_fwd": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P]),
     "rn_conv_fwd_bnstats": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P]),
     "rn_conv_bnstats_blocks": (_i64, [_P]),
+    "rn_conv_bn_part_rows": (_i32, [_P, _i32]),
     "rn_conv_tile": (_i32, [_P, _i32]),
     "rn_conv_fwd_x": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_filter_x": (_i32, [_P, _P, _P, _P, _P, _P, _P]),

@@ -487,6 +487,17 @@ def test_stem_quant(gpu):
     assert rel_err(dbeta.cpu().numpy(), dbeta_ref) < 1e-4
 
 
+@pytest.fixture(params=[(0, 0), (1, 0), (1, 1)], ids=["rows224", "rows256_mfma32", "rows256_mfma16"])
+def tile_variant(request):
+    """igemm 256-row-family variants: rn_set_tuning 9 (224-row tiles on/off) x 8 (MFMA shape)."""
+    rows, mfma = request.param
+    L.call("rn_set_tuning", 9, rows)
+    L.call("rn_set_tuning", 8, mfma)
+    yield request.param
+    L.call("rn_set_tuning", 9, 0)
+    L.call("rn_set_tuning", 8, 0)
+
+
 @pytest.fixture(params=[0, 2], ids=["auto", "big256"])
 def big_tiles(request):
     """rn_set_tuning 4 (igemm 256-row tiles): automatic choice, or 256x256 forced where eligible."""
@@ -499,7 +510,7 @@ def big_tiles(request):
 @pytest.mark.parametrize("case", [(3, 32, 13, 11, 48, 3, 2, 1), (2, 64, 14, 14, 256, 1, 1, 0), (2, 16, 9, 9, 64, 1, 1, 0),
                                   (3, 128, 20, 20, 256, 3, 1, 1)])
 @pytest.mark.parametrize("acc", [False, True], ids=["partials", "fp64acc"])
-def test_conv_bnstats_epilogue(gpu, dtype, case, big_tiles, acc):
+def test_conv_bnstats_epilogue(gpu, dtype, case, big_tiles, acc, tile_variant):
     """BatchNorm statistics emitted by the conv epilogue (rn_conv_fwd_bnstats, with the fused
     residual add) and merged by rn_bn_fwd_train_part == a BatchNorm over the stored conv output.
     acc: the fp64-accumulated variant (rn_conv_fwd_bnacc + rn_bn_fwd_train_acc, 256-row tiles)."""
@@ -546,7 +557,7 @@ def test_conv_bnstats_epilogue(gpu, dtype, case, big_tiles, acc):
         L.call("rn_bn_fwd_train_acc", C.byref(bd), p(bacc), p(mm), p(y), p(yb), p(g_d), p(b_d), p(mm), p(mv),
                p(sm), p(si), p(sc), p(sh), stream())
     else:
-        L.call("rn_bn_fwd_train_part", C.byref(bd), p(part), nblk, 128, d.k_pad, p(y), p(yb), p(g_d), p(b_d), p(mm),
+        L.call("rn_bn_fwd_train_part", C.byref(bd), p(part), nblk, lib.rn_conv_bn_part_rows(C.byref(d), 0), d.k_pad, p(y), p(yb), p(g_d), p(b_d), p(mm),
                p(mv), p(sm), p(si), p(sc), p(sh), p(ws), stream())
     torch.cuda.synchronize()
     if acc:
@@ -653,7 +664,7 @@ def test_conv_bnrelu_on_load(gpu, dtype, case):
 @pytest.mark.parametrize("case", [(2, 64, 14, 14, 128, 3, 1, 1), (2, 128, 14, 14, 256, 1, 2, 0),
                                   (3, 32, 13, 11, 48, 3, 2, 1), (3, 256, 20, 20, 128, 3, 2, 1)])
 @pytest.mark.parametrize("acc", [False, True], ids=["partials", "fp64acc"])
-def test_dgrad_bn_backward_fusion(gpu, dtype, case, big_tiles, acc):
+def test_dgrad_bn_backward_fusion(gpu, dtype, case, big_tiles, acc, tile_variant):
     """rn_conv_bwd_data_bnred + rn_bn_bwd_part == conv dgrad followed by the BatchNorm+ReLU backward
     of the BN that produced the conv's input (pre-activation units)."""
     n, c, h, w, k, r, st, pd = case
@@ -735,7 +746,7 @@ BIG_CASES = [
 
 @pytest.mark.parametrize("mode", [2, 3])
 @pytest.mark.parametrize("case", BIG_CASES)
-def test_conv_big_tiles(gpu, mode, case):
+def test_conv_big_tiles(gpu, mode, case, tile_variant):
     """igemm_big_kernel (rn_set_tuning 4: 2 = 256x256, 3 = 256x128) for fwd + residual and dgrad;
     wgrad_big_kernel (rn_set_tuning 5 = 1; >= 128 output channels, >= 256 columns) for the weight gradient."""
     n, c, h, w, k, r, st, pd = case

@@ -1,5 +1,7 @@
-"""Map igemm/wgrad dispatch durations of the last training step in a rocprofv3 kernel trace
-onto the ResNet-50 layers (plan call order), and print per-layer TFLOP/s. CPU-only tool."""
+"""Map the conv dispatch durations (igemm*/wgrad* kernels) of the LAST training step in a rocprofv3
+kernel trace onto the ResNet-50 layers (plan call order) and print per-layer TFLOP/s and the
+fraction of each layer's own roofline max(FLOP/2.5 PF, algorithmic bytes/8 TB/s). CPU-only tool.
+usage: python tools/trace_layers.py <run_kernel_trace.csv> [batch]"""
 import csv
 import os
 import sys
@@ -9,29 +11,41 @@ sys.path[:0] = [REPO, os.path.join(REPO, "resnet.mxnet_amd")]
 from rn import graphs  # noqa: E402
 from rn.executor import Executor, Plan  # noqa: E402
 
-trace = sys.argv[1]
-batch = int(sys.argv[2]) if len(sys.argv) > 2 else 256
-plan = Plan(graphs.resnet50(), [("data", (batch, 3, 224, 224))], [("softmax_label", (batch,))])
-ex = Executor(plan, "cpu")
-calls = [(n, a) for n, f, a in ex._fwd_train + ex._bwd if n in ("rn_conv_fwd", "rn_conv_bwd_data", "rn_conv_bwd_filter")]
-names = {}
-for op in plan.ops:
-    if hasattr(op, "desc"):
-        names[id(op.desc)] = op.name
-    if hasattr(op, "d1"):
-        names[id(op.d1)] = op.name
-rows = [r for r in csv.DictReader(open(trace)) if "igemm_kernel" in r["Kernel_Name"] or "wgrad_kernel" in r["Kernel_Name"]]
-rows = rows[-len(calls):]
-tot = {}
-out = []
-for (n, a), r in zip(calls, rows):
-    d = a[0]._obj
-    flops = 2 * d.n * d.p * d.q * d.k * d.c_real * d.r * d.s
-    us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-    lname = names.get(id(d), "?")
-    kind = {"rn_conv_fwd": "fwd", "rn_conv_bwd_data": "dgrad", "rn_conv_bwd_filter": "wgrad"}[n]
-    out.append((us, lname, kind, flops / us / 1e6, d.n * d.p * d.q, d.k, d.c_real, d.r))
-    tot[kind] = tot.get(kind, 0) + us
-for us, lname, kind, tf, m, k, c, r in sorted(out, reverse=True)[:40]:
-    print("%8.1f us  %-28s %-5s %7.1f TF  M=%d K=%d C=%d R=%d" % (us, lname, kind, tf, m, k, c, r))
-print({k: round(v / 1e3, 3) for k, v in tot.items()}, "ms")
+CONV_CALLS = ("rn_conv_fwd", "rn_conv_fwd_bnstats", "rn_conv_fwd_x", "rn_conv_fwd_bnacc", "rn_conv_bwd_data",
+              "rn_conv_bwd_data_bnred", "rn_conv_bwd_data_bnacc", "rn_conv_bwd_filter", "rn_conv_bwd_filter_x")
+
+
+def main():
+    trace = sys.argv[1]
+    batch = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+    plan = Plan(graphs.resnet50(), [("data", (batch, 3, 224, 224))], [("softmax_label", (batch,))])
+    ex = Executor(plan, "cpu")
+    names = {}
+    for op in plan.ops:
+        for attr in ("desc", "dfull", "d1"):
+            if hasattr(op, attr):
+                names[id(getattr(op, attr))] = op.name
+    calls = [(n, a) for n, f, a in ex._fwd_train + ex._bwd if n in CONV_CALLS]
+    rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
+    step_end = [i for i, r in enumerate(rows) if "sgd_mom" in r["Kernel_Name"]]
+    rows = rows[step_end[-2] + 1:step_end[-1]]
+    rows = [r for r in rows if "igemm" in r["Kernel_Name"] or "wgrad" in r["Kernel_Name"]]
+    assert len(rows) == len(calls), (len(rows), len(calls))
+    tot, out = {}, []
+    for (n, a), r in zip(calls, rows):
+        d = a[0]._obj
+        flops = 2.0 * d.n * d.p * d.q * d.k * (d.c_real // d.groups) * d.r * d.s
+        xb, yb, wb = 2.0 * d.n * d.h * d.w * d.c, 2.0 * d.n * d.p * d.q * d.k_pad, 2.0 * d.k * d.r * d.s * d.c
+        kind = "wgrad" if "filter" in n else "dgrad" if "bwd_data" in n else "fwd"
+        algb = xb + yb + (2 * wb if kind == "wgrad" else wb)
+        us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+        roof = max(flops / 2.5e15, algb / 8e12) * 1e6
+        out.append((us, names.get(id(d), "?"), kind, flops / us / 1e6, roof / us, r["Kernel_Name"].split("(")[0][-40:]))
+        tot[kind] = tot.get(kind, 0) + us
+    for us, lname, kind, tf, fr, kn in sorted(out, reverse=True):
+        print("%8.1f us  %-22s %-5s %7.1f TF %4.0f%%  %s" % (us, lname, kind, tf, 100 * fr, kn))
+    print({k: round(v / 1e3, 3) for k, v in tot.items()}, "ms")
+
+
+if __name__ == "__main__":
+    main()
