@@ -674,7 +674,10 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // for every ResNet-50 layer at batch 256, so 256-row tiles leave a last round of 196 / 256 workgroups
 // on every grid; 224-row tiles (7 / 8 of the rows) fill 224 / 256. The A region of the LDS stage
 // keeps 256 rows (the DMA rounds of rows >= BM read zeros).
-template <int BN, int NBUF, int EPI = 0, bool M32 = false, int BM = 256>
+// SC: the stem's small-C mode (C = 8 = one 16-byte chunk per tap, the flattened reduction
+// k = tap * 8 + c): each DMA lane's chunk of a K-tile is its own tap, so the gathered row offset and
+// the in-image test are per lane (64-column tile only).
+template <int BN, int NBUF, int EPI = 0, bool M32 = false, int BM = 256, bool SC = false>
 __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_big_kernel(IgemmArgs p) {
   constexpr int BMA = 256, CE = 8, BKE = 64;
   constexpr int NW = BN == 64 ? 4 : 8;           // waves
@@ -686,7 +689,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   constexpr int FM = M32 ? 32 : 16;              // MFMA tile edge
   constexpr int MI = WM / FM, NI = WN / FM;      // accumulators per wave
   constexpr int NCH = (WM + 63) / 64;            // 64-row epilogue chunks per wave
-  static_assert(WM % FM == 0 && (BM == 256 || !M32) && (BM == 256 || BN != 64), "tile shape");
+  static_assert(WM % FM == 0 && (BM == 256 || !M32) && (BM == 256 || BN != 64) && (!SC || BN == 64), "tile shape");
   using AccT = typename std::conditional<M32, v16f, v4f>::type;
   constexpr int kStage = (BMA + BN) * 8;         // 16-byte chunks per K-tile
   constexpr int EP_LD = WN + 4;                  // staged fp32 row stride
@@ -730,7 +733,8 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
       const int jj = rem - ii * cl.Qc;
       a_h[i] = ii * p.hmul + cl.hb0 + cl.hoff0;
       a_w[i] = jj * p.wmul + cl.wb0 + cl.woff0;
-      a_row[i] = ((n * p.H + a_h[i]) * p.W + a_w[i]) * p.C + lch * CE;  // may point before the image: masked
+      // may point before the image: masked (SC: the lane's chunk is a tap, not a channel block)
+      a_row[i] = ((n * p.H + a_h[i]) * p.W + a_w[i]) * p.C + (SC ? 0 : lch * CE);
     } else {
       a_h[i] = -(1 << 28);  // never inside the image
       a_w[i] = 0;
@@ -750,7 +754,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);  // this wave's 8 rows
 
   const int ncb = (p.cblk + BKE - 1) / BKE;
-  const int nstage = cl.nr * cl.ns * ncb;
+  const int nstage = SC ? (p.rs * CE + BKE - 1) / BKE : cl.nr * cl.ns * ncb;
   int st_tr = 0, st_ts = 0, st_cb = 0, st_n = 0;
   // one K-tile's DMAs: prep() fixes the tile's uniform offsets, piece(k) issues DMA k (A rounds
   // first, then B). A tile past the range issues zero-fill DMAs (kOob) into a buffer nobody reads,
@@ -760,6 +764,18 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   uint32_t d_la = 0;
   const uint32_t dmask = (p.sched & 2) ? 0xFFF0u : 0xFFFFFFFFu;  // diagnostic: L2-resident sources
   auto prep = [&](int buf) __attribute__((always_inline)) {
+    if constexpr (SC) {  // K-tile t: lane chunk lch is tap 8 t + lch (all 8 channels of it)
+      const int t = st_n++;
+      const int tap = t * (BKE / CE) + lch;
+      const int r = (int)fdiv((uint32_t)tap, p.fdS);
+      d_cok = t < nstage && tap < p.rs;
+      d_dh = r;
+      d_dw = tap - r * p.S;
+      d_toffa = (d_dh * p.W + d_dw) * p.C;
+      d_toffb = t * BKE;
+      d_la = lds0 + buf * (kStage * 16);
+      return;
+    }
     const int tr = st_tr, ts = st_ts, cb = st_cb;
     const bool live = st_n++ < nstage;
     if (++st_cb == ncb) {
@@ -1444,7 +1460,9 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
   }
   wait_vmcnt<0>();
 
-  // D[row = k][col] -> fp32 atomic add into dw (dense, unpadded: ldw = ncol)
+  // D[row = k][col] -> fp32 atomic add into dw (dense, unpadded: ldw = ncol); padded channels (the
+  // stem's 3 of 8) keep c < creal
+  const bool padded = p.creal != p.C;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1454,7 +1472,13 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         const int col = n0 + wn * 64 + j * 16 + (lane & 15);
-        if (col < p.ncol) atomicAdd(p.dw + (int64_t)k * p.ldw + col, acc[i][j][e]);
+        if (!padded) {
+          if (col < p.ncol) atomicAdd(p.dw + (int64_t)k * p.ldw + col, acc[i][j][e]);
+        } else if (col < p.ncol_load) {
+          const int tap = fdiv(col, p.fdC);
+          const int c = col - tap * p.C;
+          if (c < p.creal) atomicAdd(p.dw + (int64_t)k * p.ldw + tap * p.creal + c, acc[i][j][e]);
+        }
       }
     }
 }
@@ -1620,16 +1644,40 @@ __global__ void stem_clip_grad_kernel(const float* __restrict__ x, const float* 
   }
 }
 
-// S[p][q][k] = sum_n dy[n][p][q][k]
+// S[p][q][k] = sum_n dy[n][p][q][k]: thread per 16-byte chunk of one image (kpad is a multiple of
+// the chunk), 8 images in flight per thread (a plain HBM-bound reduction over the batch)
 template <typename T>
-__global__ void stem_sum_n_kernel(const T* __restrict__ dy, float* __restrict__ ws, int N, int PQ,
-                                  int kpad) {
+__global__ __launch_bounds__(256) void stem_sum_n_kernel(const T* __restrict__ dy, float* __restrict__ ws, int N,
+                                                         int PQ, int kpad) {
+  constexpr int CE = 16 / sizeof(T);
   const int64_t total = (int64_t)PQ * kpad;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float acc = 0.f;
-    for (int n = 0; n < N; ++n) acc += to_f(dy[(int64_t)n * total + i]);
-    ws[i] = acc;
+  const int64_t nch = total / CE;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nch; i += (int64_t)gridDim.x * blockDim.x) {
+    float acc[CE];
+#pragma unroll
+    for (int e = 0; e < CE; ++e) acc[e] = 0.f;
+    const uint4* src = reinterpret_cast<const uint4*>(dy) + i;
+    int n = 0;
+    for (; n + 8 <= N; n += 8) {
+      uint4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(n + u) * nch];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        float f[CE];
+        chunk_to_f(v[u], f, (const T*)nullptr);
+#pragma unroll
+        for (int e = 0; e < CE; ++e) acc[e] += f[e];
+      }
+    }
+    for (; n < N; ++n) {
+      float f[CE];
+      chunk_to_f(src[(int64_t)n * nch], f, (const T*)nullptr);
+#pragma unroll
+      for (int e = 0; e < CE; ++e) acc[e] += f[e];
+    }
+#pragma unroll
+    for (int e = 0; e < CE; ++e) ws[i * CE + e] = acc[e];
   }
 }
 // separable rectangle sums: Tq[p][s][k] = sum_{q in V(s)} S[p][q][k];
@@ -1769,7 +1817,10 @@ int big_tile_cols(const IgemmArgs& a, int64_t xb, int64_t wb) {
   const int big = g_tune[RN_TUNE_IGEMM_BIG];
   int max_taps = 0;
   for (int z = 0; z < a.ncls; ++z) max_taps = std::max(max_taps, a.cls[z].nr * a.cls[z].ns);
-  const bool eligible = big != 1 && !a.in_sc && !a.smallc && a.gred == 0 && !g_tune[RN_TUNE_DIAG_IGEMM_L1] &&
+  if (a.smallc)  // the stem (C = 8): the 256x64 tile in its small-C mode (rn_set_tuning 4 = 1 or 5: never)
+    return (big != 1 && big != 5 && a.C == 8 && a.K <= 64 && !a.in_sc && !a.bias && !g_tune[RN_TUNE_DIAG_IGEMM_L1] &&
+            xb < INT32_MAX && wb < INT32_MAX) ? 64 : 0;
+  const bool eligible = big != 1 && !a.in_sc && a.gred == 0 && !g_tune[RN_TUNE_DIAG_IGEMM_L1] &&
                         !a.bias && xb < INT32_MAX && wb < INT32_MAX && max_taps <= 32;
   if (!eligible) return 0;
   if (a.K <= 64) {  // 4-wave 256x64 tile where the reduction is deep (>= 8 K-tiles: the 3x3 layers);
@@ -1824,7 +1875,8 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
     if (bn == 64 && epi == 0) {
       b.ntn = (int)ceil_div(a.K, 64);
       dim3 grid((unsigned)(ceil_div(maxMc, 256) * b.ntn), 1, a.ncls);
-      if (m32) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true>), grid, dim3(256), 0, st, b);
+      if (a.smallc) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, true>), grid, dim3(256), 0, st, b);
+      else if (m32) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true>), grid, dim3(256), 0, st, b);
       else hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, false>), grid, dim3(256), 0, st, b);
       return rn_check_launch("igemm_big64");
     }
@@ -2054,9 +2106,11 @@ int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, f
   // 128-tile kernel on every ResNet-50 layer: with the M split, the fp32 atomic epilogue issues
   // (workgroups x tile area) adds, 4x more per workgroup at 256x256, and that dominates the
   // small-M layers (stage 3-4).
-  if (d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c && a.K <= 64 && a.ncol_load > 64 &&
-      g_tune[RN_TUNE_WGRAD_BIG] == 4 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX &&
-      (int64_t)a.M * a.ldy < INT32_MAX) {
+  // (default for the stem's padded channels, c_real < c = 8; rn_set_tuning 5 = 4 for every 64-channel layer)
+  const bool stem_dma = d->c_real < d->c && d->c == 8 && g_tune[RN_TUNE_WGRAD_BIG] != 3;
+  if (d->dtype == RN_BF16 && !grouped && !in_scale && (d->c_real == d->c || stem_dma) && a.K <= 64 &&
+      a.ncol_load > 64 && (g_tune[RN_TUNE_WGRAD_BIG] == 4 || stem_dma) &&
+      (int64_t)d->n * d->h * d->w * d->c < INT32_MAX && (int64_t)a.M * a.ldy < INT32_MAX) {
     // 64 x 128 LDS-DMA tiles for the 64-channel layers (4 waves, 3 buffers, two workgroups per CU)
     a.nct = (int)ceil_div(a.ncol_load, 128);
     a.nkt = 1;
@@ -2259,11 +2313,12 @@ int rn_stem_shift_grad(const rn_conv_desc* d, const void* dy, const float* wm, f
   hipStream_t st = as_stream(stream);
   const int PQ = d->p * d->q;
   const int64_t total = (int64_t)PQ * d->k_pad;
+  RN_CHECK_ARG(d->k_pad % 8 == 0, "k_pad must be a multiple of 8");
   if (d->dtype == RN_BF16)
-    hipLaunchKernelGGL(stem_sum_n_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st,
+    hipLaunchKernelGGL(stem_sum_n_kernel<bf16_t>, dim3(grid_for(total / 8)), dim3(256), 0, st,
                        (const bf16_t*)dy, ws, d->n, PQ, d->k_pad);
   else
-    hipLaunchKernelGGL(stem_sum_n_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st,
+    hipLaunchKernelGGL(stem_sum_n_kernel<float>, dim3(grid_for(total / 4)), dim3(256), 0, st,
                        (const float*)dy, ws, d->n, PQ, d->k_pad);
   float* tq = ws + total;
   const int ntq = d->p * d->s * d->k;
