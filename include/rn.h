@@ -115,6 +115,13 @@ int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, 
 int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, float* dw,
                        rn_stream_t stream);
 
+/* rn_conv_bwd_filter with a workspace for the split-M partial tiles: the large-tile LDS-DMA kernels
+ * store each split's tile into ws (no atomics) and a reduction pass adds the splits into dw.
+ * rn_conv_wgrad_ws_bytes(d) = the bytes that takes (0: this conv's kernel adds with atomics);
+ * a smaller ws falls back to the atomic epilogue. ws: 16-byte aligned, device memory. */
+int64_t rn_conv_wgrad_ws_bytes(const rn_conv_desc* d);
+int rn_conv_bwd_filter_ws(const rn_conv_desc* d, const void* x, const void* dy, float* dw, void* ws,
+                          int64_t ws_bytes, rn_stream_t stream);
 /* rn_conv_bwd_filter over the same BN+ReLU-on-load input as rn_conv_fwd_x. */
 int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, float* dw, const float* in_scale,
                          const float* in_shift, rn_stream_t stream);

@@ -1066,6 +1066,8 @@ struct WgradArgs {
   int creal;                  // logical input channels (< C: padded stride, dw keeps c < creal)
   int nct, nkt;               // column tiles, k tiles (grid = splits * nkt * nct)
   int diag_noepi;             // diagnostic (rn_set_tuning 6): skip the dW epilogue (wrong results)
+  float* slab;                // nullable (LDS-DMA kernels): the split's tile stored into slab[split][K][ldw]
+                              // (no atomics; wgrad_slab_reduce_kernel sums the splits into dw)
   const float* in_sc;         // nullable: BN+ReLU applied to the gathered x while staging
   const float* in_sh;
   FastDiv fdQ, fdPQ, fdC, fdS;  // fdC divides by cblk (dense: C)
@@ -1462,6 +1464,23 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
 
   // D[row = k][col] -> fp32 atomic add into dw (dense, unpadded: ldw = ncol); padded channels (the
   // stem's 3 of 8) keep c < creal
+  if (p.diag_noepi) return;  // diagnostic (rn_set_tuning 6): no dW epilogue (wrong results)
+  if (p.slab) {  // plain stores of this split's partial tile (rows of 16 columns: 64-byte segments)
+    float* dst = p.slab + (int64_t)zs * p.K * p.ldw;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int k = k0 + wm * (BMK / 2) + i * 16 + (lane >> 4) * 4 + e;
+        if (k >= p.K) continue;
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int col = n0 + wn * 64 + j * 16 + (lane & 15);
+          if (col < p.ncol) dst[(int64_t)k * p.ldw + col] = acc[i][j][e];
+        }
+      }
+    return;
+  }
   const bool padded = p.creal != p.C;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -1481,6 +1500,36 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
         }
       }
     }
+}
+
+// dw[i] += sum_z slab[z][i] (the split-M partial tiles of wgrad_big_kernel), float4 per thread
+__global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __restrict__ slab, int nsplit,
+                                                                int64_t n, float* __restrict__ dw) {
+  const int64_t n4 = n / 4;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    float4 a = reinterpret_cast<const float4*>(dw)[i];
+    int z = 0;
+    for (; z + 4 <= nsplit; z += 4) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = reinterpret_cast<const float4*>(slab + (int64_t)(z + u) * n)[i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w;
+      }
+    }
+    for (; z < nsplit; ++z) {
+      const float4 v = reinterpret_cast<const float4*>(slab + (int64_t)z * n)[i];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    reinterpret_cast<float4*>(dw)[i] = a;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < n - n4 * 4) {  // tail
+    const int64_t i = n4 * 4 + threadIdx.x;
+    float a = dw[i];
+    for (int z = 0; z < nsplit; ++z) a += slab[(int64_t)z * n + i];
+    dw[i] = a;
+  }
 }
 
 // ------------------------------------------------------------------------------ helpers
@@ -2069,9 +2118,15 @@ int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, 
   return rn_conv_bwd_data_bnred(d, dy, w_crsk, dx, add_src, nullptr, nullptr, nullptr, nullptr, 0, nullptr, stream);
 }
 
-int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, float* dw, const float* in_scale,
-                         const float* in_shift, rn_stream_t stream) {
-  RN_CHECK_ARG(d && x && dy && dw, "null argument");
+}  // extern "C"
+
+namespace {
+// The weight-gradient kernel choice for d. launch == false: only *ws_need (bytes of split-M partial
+// slabs the chosen kernel stores when given a workspace; 0 = it adds into dw with atomics).
+int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* dw, const float* in_scale,
+                   const float* in_shift, float* ws, int64_t ws_bytes, int64_t* ws_need, bool launch,
+                   hipStream_t st) {
+  if (ws_need) *ws_need = 0;
   RN_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "in_scale / in_shift must both be set");
   RN_CHECK_ARG(!in_scale || d->groups == 1, "input transform on a grouped conv");
 
@@ -2099,7 +2154,25 @@ int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, f
   a.diag_noepi = g_tune[RN_TUNE_DIAG_WGRAD_NOEPI];
   a.fdQ = make_fastdiv(d->q); a.fdPQ = make_fastdiv(d->p * d->q);
   a.fdC = make_fastdiv(a.cblk); a.fdS = make_fastdiv(d->s);
-  hipStream_t st = as_stream(stream);
+  // split-M partial slabs (plain stores + wgrad_slab_reduce_kernel) instead of fp32 atomics: 2 x the
+  // slab bytes at streaming rates vs the slab bytes at the chip's ~1.3 TB/s atomic rate
+  const bool slab_ok = d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c;
+  auto finish = [&](int64_t split, const char* what) -> int {
+    const int64_t need = slab_ok ? split * a.K * (int64_t)a.ldw * 4 : 0;
+    if (ws_need) *ws_need = need;
+    if (!launch) return 0;
+    if (rn_check_launch(what)) return -1;
+    if (a.slab) {
+      const int64_t n = (int64_t)a.K * a.ldw;
+      hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, a.slab, (int)split, n, dw);
+      return rn_check_launch("wgrad_slab_reduce");
+    }
+    return 0;
+  };
+  auto use_slab = [&](int64_t split) {
+    const int64_t need = split * a.K * (int64_t)a.ldw * 4;
+    a.slab = (slab_ok && ws && ws_bytes >= need) ? ws : nullptr;
+  };
   // 256-column, 8-wave LDS-DMA tiles (rn_set_tuning 5: 1 = on, default off) for dense bf16 layers
   // with >= 128 output channels and >= 256 columns; the M range is split so that the grid is one
   // round of one workgroup per CU, with >= 4 M-tiles per workgroup. Measured slower than the
@@ -2119,28 +2192,40 @@ int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, f
     int64_t split = std::min<int64_t>(std::max<int64_t>(1, 512 / tiles), std::max<int64_t>(1, mtiles / 8));
     a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
     split = ceil_div(a.M, a.m_per_split);
+    if (!launch) return finish(split, "wgrad_dma64");
+    use_slab(split);
     hipLaunchKernelGGL((wgrad_big_kernel<64, 3, 128>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
-    return rn_check_launch("wgrad_dma64");
+    return finish(split, "wgrad_dma64");
   }
-  if (d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c &&
+  // with a slab workspace (rn_conv_bwd_filter_ws) the 256-column 8-wave tiles below are the default
+  // for >= 128 output channels and >= 256 columns: their main loop is the faster one, and the
+  // 4x larger per-workgroup tile no longer costs atomics
+  const bool big256 = (g_tune[RN_TUNE_WGRAD_BIG] == 1 || (g_tune[RN_TUNE_WGRAD_BIG] == 0 && slab_ok && ws)) &&
+                      d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c && a.K >= 128 &&
+                      a.ncol_load >= 256 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX &&
+                      (int64_t)a.M * a.ldy < INT32_MAX;
+  if (d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c && !big256 &&
       (g_tune[RN_TUNE_WGRAD_BIG] == 0 || g_tune[RN_TUNE_WGRAD_BIG] == 2 || g_tune[RN_TUNE_WGRAD_BIG] == 4) &&
       a.K > 64 && a.ncol_load > 64 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX &&
       (int64_t)a.M * a.ldy < INT32_MAX) {
     // 128 x 128 LDS-DMA tiles, 4 waves, two workgroups per CU (default; measured -0.4 % step time
-    // over the register-staged wgrad_kernel, which rn_set_tuning 5 = 3 selects)
+    // over the register-staged wgrad_kernel, which rn_set_tuning 5 = 3 selects). The M split targets
+    // rn_set_tuning 2 workgroups per CU (default 2): every workgroup adds its tile into dw with
+    // fp32 atomics, so the atomic traffic is (workgroups x 64 KB).
     a.nct = (int)ceil_div(a.ncol_load, 128);
     a.nkt = (int)ceil_div(a.K, 128);
     const int64_t tiles = (int64_t)a.nct * a.nkt;
     const int64_t mtiles = ceil_div(a.M, 64);
-    int64_t split = std::min<int64_t>(std::max<int64_t>(1, 512 / tiles), std::max<int64_t>(1, mtiles / 8));
+    const int64_t target = 256 * (g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU] > 0 ? g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU] : 2);
+    int64_t split = std::min<int64_t>(std::max<int64_t>(1, target / tiles), std::max<int64_t>(1, mtiles / 8));
     a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
     split = ceil_div(a.M, a.m_per_split);
+    if (!launch) return finish(split, "wgrad_dma128");
+    use_slab(split);
     hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
-    return rn_check_launch("wgrad_dma128");
+    return finish(split, "wgrad_dma128");
   }
-  if (d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c && a.K >= 128 && a.ncol_load >= 256 &&
-      g_tune[RN_TUNE_WGRAD_BIG] == 1 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX &&
-      (int64_t)a.M * a.ldy < INT32_MAX) {
+  if (big256) {
     const int bmk = a.K >= 256 ? 256 : 128;
     a.nct = (int)ceil_div(a.ncol_load, 256);
     a.nkt = (int)ceil_div(a.K, bmk);
@@ -2149,10 +2234,12 @@ int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, f
     int64_t split = std::min<int64_t>(std::max<int64_t>(1, 256 / tiles), std::max<int64_t>(1, mtiles / 4));
     a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
     split = ceil_div(a.M, a.m_per_split);
+    if (!launch) return finish(split, "wgrad_big");
+    use_slab(split);
     dim3 grid((unsigned)(tiles * split));
     if (bmk == 256) hipLaunchKernelGGL((wgrad_big_kernel<256, 2>), grid, dim3(512), 0, st, a);
     else hipLaunchKernelGGL((wgrad_big_kernel<128, 3>), grid, dim3(512), 0, st, a);
-    return rn_check_launch("wgrad_big");
+    return finish(split, "wgrad_big");
   }
   // 64-wide tiles where K or the column count is <= 64 (stage-1 layers): a 128 tile would spend
   // half (or three quarters) of its MFMAs on zero rows / columns
@@ -2175,6 +2262,7 @@ int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, f
   a.nct = (int)ceil_div(a.ncol_load, bnc);
   a.nkt = (int)ceil_div(a.K, bmk);
   dim3 grid((unsigned)(a.nct * a.nkt * split));
+  if (!launch) return 0;
   if (grouped) {
     if (d->dtype == RN_BF16)
       hipLaunchKernelGGL((wgrad_kernel<bf16_t, RN_GROUP_BLOCK, RN_GROUP_BLOCK>), grid, dim3(256), 0, st, a);
@@ -2188,6 +2276,33 @@ int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, f
     else launch_wgrad_tiles<float, false>(bmk, bnc, grid, st, a);
   }
   return rn_check_launch("wgrad");
+}
+}  // namespace
+
+extern "C" {
+
+int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, float* dw, const float* in_scale,
+                         const float* in_shift, rn_stream_t stream) {
+  RN_CHECK_ARG(d && x && dy && dw, "null argument");
+  return wgrad_dispatch(d, x, dy, dw, in_scale, in_shift, nullptr, 0, nullptr, true, as_stream(stream));
+}
+
+int64_t rn_conv_wgrad_ws_bytes(const rn_conv_desc* d) {
+  if (!d) return -1;
+  int64_t need = 0;
+  if (wgrad_dispatch(d, nullptr, nullptr, nullptr, nullptr, nullptr, reinterpret_cast<float*>(16), INT64_MAX, &need,
+                     false, nullptr))
+    return -1;
+  return need;
+}
+
+int rn_conv_bwd_filter_ws(const rn_conv_desc* d, const void* x, const void* dy, float* dw, void* ws, int64_t ws_bytes,
+                          rn_stream_t stream) {
+  RN_CHECK_ARG(d && x && dy && dw, "null argument");
+  RN_CHECK_ARG(ws_bytes >= 0 && (ws || ws_bytes == 0), "bad workspace");
+  RN_CHECK_ARG(((uintptr_t)ws & 15) == 0, "workspace must be 16-byte aligned");
+  return wgrad_dispatch(d, x, dy, dw, nullptr, nullptr, reinterpret_cast<float*>(ws), ws_bytes, nullptr, true,
+                        as_stream(stream));
 }
 
 int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, float* dw, rn_stream_t stream) {

@@ -944,6 +944,13 @@ class Executor:
             self.unfused_packs.append(c)
 
     # ------------------------------------------------------------------ backward
+    def _wgrad_call(self, d, x, dy, dw, sp):
+        """rn_conv_bwd_filter, through the split-M slab workspace where the kernel uses one."""
+        if self.wgrad_ws is not None and int(self.lib.rn_conv_wgrad_ws_bytes(L.C.byref(d))) > 0:
+            return self._call("rn_conv_bwd_filter_ws", L.C.byref(d), x, dy, dw, self._p(self.wgrad_ws),
+                              self.wgrad_ws_bytes, sp)
+        return self._call("rn_conv_bwd_filter", L.C.byref(d), x, dy, dw, sp)
+
     def _build_backward(self):
         plan = self.plan
         sp = self._sp()
@@ -954,6 +961,15 @@ class Executor:
         # default on where the dgrad runs the 256-row tile (see RN_BN_EPILOGUE_STATS; =2: every dgrad)
         bwd_fusion = os.environ.get("RN_BN_BWD_FUSION", "1") in ("1", "2")
         bwd_all = os.environ.get("RN_BN_BWD_FUSION", "1") == "2"
+        # one workspace for the weight gradients' split-M partial tiles (rn_conv_bwd_filter_ws),
+        # sized for the largest layer; the backward runs the layers one after another on one stream
+        self.wgrad_ws, self.wgrad_ws_bytes = None, 0
+        if os.environ.get("RN_WGRAD_SLAB", "1") == "1":
+            need = [int(self.lib.rn_conv_wgrad_ws_bytes(L.C.byref(op.desc))) for op in plan.ops
+                    if op.kind in ("conv", "fc") and getattr(op, "desc", None) is not None]
+            self.wgrad_ws_bytes = max(need + [0])
+            if self.wgrad_ws_bytes > 0:
+                self.wgrad_ws = self._zeros(self.wgrad_ws_bytes // 4, self.torch.float32)
         for op in reversed(plan.ops):
             if op.kind == "softmax":
                 gs.has_value.add(id(op.x))  # dlogits written by the forward softmax call
@@ -963,8 +979,7 @@ class Executor:
                 continue
             if op.kind == "fc":
                 x = op.x
-                self._bwd.append(self._call("rn_conv_bwd_filter", L.C.byref(op.desc), self._p(self.act(x)),
-                                            self._p(dy), self._gp(op.weight), sp))
+                self._bwd.append(self._wgrad_call(op.desc, self._p(self.act(x)), self._p(dy), self._gp(op.weight), sp))
                 if op.bias:
                     self._bwd.append(self._call("rn_col_sum", self.dtype, x.n, op.nh, _pad8(op.nh), self._p(dy),
                                                 self._gp(op.bias), 0, sp))
@@ -980,8 +995,8 @@ class Executor:
                     self._bwd.append(self._call("rn_conv_bwd_filter_x", L.C.byref(op.desc), self._p(self.act(op.xf.x)),
                                                 self._p(dy), self._gp(op.weight), op.xf.sc, op.xf.sh, sp))
                 else:
-                    self._bwd.append(self._call("rn_conv_bwd_filter", L.C.byref(op.desc), self._p(self.act(x)),
-                                                self._p(dy), self._gp(op.weight), sp))
+                    self._bwd.append(self._wgrad_call(op.desc, self._p(self.act(x)), self._p(dy), self._gp(op.weight),
+                                                      sp))
                 self.param_done_at[op.weight] = len(self._bwd)
                 if x.needs_grad:
                     out, add = gs.contribute(x)

@@ -776,11 +776,21 @@ def test_conv_big_tiles(gpu, mode, case, tile_variant):
         L.call("rn_conv_bwd_filter", C.byref(d), p(xd), p(dyd), p(dw), stream())  # wgrad_big_kernel when eligible
         L.call("rn_set_tuning", 5, 4)  # the LDS-DMA variants incl. the 64x128 one for K <= 64
         L.call("rn_conv_bwd_filter", C.byref(d), p(xd), p(dyd), p(dw2), stream())
+        L.call("rn_set_tuning", 5, 0)
+        # split-M partial slabs + reduction (default tiles with a workspace), and a too-small
+        # workspace (falls back to the atomic epilogue); dw is accumulated into (+=)
+        need = L.load().rn_conv_wgrad_ws_bytes(C.byref(d))
+        ws = torch.full((max(need, 16) // 4 + 4,), float("nan"), dtype=torch.float32, device=gpu)
+        dw3 = torch.full_like(dw, 0.5)
+        dw4 = torch.zeros_like(dw)
+        L.call("rn_conv_bwd_filter_ws", C.byref(d), p(xd), p(dyd), p(dw3), p(ws), need, stream())
+        L.call("rn_conv_bwd_filter_ws", C.byref(d), p(xd), p(dyd), p(dw4), p(ws), max(need - 4, 0), stream())
         torch.cuda.synchronize()
     finally:
         L.call("rn_set_tuning", 4, 0)
         L.call("rn_set_tuning", 5, 0)
     assert rel_err(from_nhwc(y, k), ref) < TOL[BF16]
     assert rel_err(from_nhwc(dx, c), dx_ref) < TOL[BF16]
-    for g in (dw, dw2):
+    dw3 -= 0.5
+    for g in (dw, dw2, dw3, dw4):
         assert rel_err(g.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2), dw_ref) < 5e-3

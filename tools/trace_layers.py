@@ -12,7 +12,7 @@ from rn import graphs  # noqa: E402
 from rn.executor import Executor, Plan  # noqa: E402
 
 CONV_CALLS = ("rn_conv_fwd", "rn_conv_fwd_bnstats", "rn_conv_fwd_x", "rn_conv_fwd_bnacc", "rn_conv_bwd_data",
-              "rn_conv_bwd_data_bnred", "rn_conv_bwd_data_bnacc", "rn_conv_bwd_filter", "rn_conv_bwd_filter_x")
+              "rn_conv_bwd_data_bnred", "rn_conv_bwd_data_bnacc", "rn_conv_bwd_filter", "rn_conv_bwd_filter_x", "rn_conv_bwd_filter_ws")
 
 
 def main():
@@ -29,7 +29,14 @@ def main():
     rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
     step_end = [i for i, r in enumerate(rows) if "sgd_mom" in r["Kernel_Name"]]
     rows = rows[step_end[-2] + 1:step_end[-1]]
-    rows = [r for r in rows if "igemm" in r["Kernel_Name"] or "wgrad" in r["Kernel_Name"]]
+    conv_rows = []
+    for r in rows:  # a slab reduction pass belongs to the weight gradient launched just before it
+        if "slab_reduce" in r["Kernel_Name"] and conv_rows:
+            conv_rows[-1] = dict(conv_rows[-1], End_Timestamp=str(int(conv_rows[-1]["End_Timestamp"]) + int(
+                r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+        elif "igemm" in r["Kernel_Name"] or "wgrad" in r["Kernel_Name"]:
+            conv_rows.append(r)
+    rows = conv_rows
     assert len(rows) == len(calls), (len(rows), len(calls))
     tot, out = {}, []
     for (n, a), r in zip(calls, rows):
