@@ -51,7 +51,7 @@ def conv_call_bytes(ex, name, args):
     if name in ("rn_conv_bwd_data", "rn_conv_bwd_data_bnred"):
         bnx = x if name == "rn_conv_bwd_data_bnred" else 0  # the fused BN-backward reduction reads the BN input
         return y + w + x + (x if args[4] is not None else 0) + bnx
-    return x + y + 2 * d.k * d.r * d.s * d.c_real * 4  # wgrad: fp32 dW read-modify-write
+    return x + y + 2 * d.k * d.r * d.s * d.c_real * 4  # wgrad: fp32 dW read-modify-write (slabs not counted)
 
 
 def pmc_traffic(family):
@@ -73,7 +73,7 @@ DGRAD_CALLS = ("rn_conv_bwd_data", "rn_conv_bwd_data_bnred")
 
 
 def family_of(ex, name, args):
-    if name == "rn_conv_bwd_filter":
+    if name in ("rn_conv_bwd_filter", "rn_conv_bwd_filter_ws"):  # _ws: its slab reduction pass included
         return "wgrad_kernel<bf16,*>" if ex.dtype == 0 else "wgrad_kernel<f32,*>"
     if name in FWD_CALLS + DGRAD_CALLS:
         d = args[0]._obj
@@ -83,8 +83,9 @@ def family_of(ex, name, args):
         plain = dgrad or (args[6] is None and (name != "rn_conv_fwd_x" or args[7] is None))
         # the library's own choice (rn_conv_tile), so the family always matches the kernel that runs
         big = ex.lib.rn_conv_tile(args[0], 1 if dgrad else 0) if (ex.dtype == 0 and not out_f32 and plain) else 0
-        if big:
-            return "igemm_big_kernel<256x%d>" % big
+        if big:  # tile rows: 256, or 224 (the BN partial blocks are half the tile rows)
+            rows = 2 * ex.lib.rn_conv_bn_part_rows(args[0], 1 if dgrad else 0) if big >= 128 else 256
+            return "igemm_big_kernel<%dx%d>" % (rows, big)
         tile = "128x64" if ncol <= 64 else "128x128"
         return "igemm_kernel<bf16,%s,%s>" % ("f32" if out_f32 else "bf16", tile)
     return None

@@ -62,11 +62,13 @@ def main():
         wc = torch.empty(lib.rn_conv_pack_numel(C.byref(d), 1), device=dev, dtype=torch.bfloat16)
         dw = torch.zeros(wm.numel(), device=dev)
         P = lambda t: C.c_void_p(t.data_ptr())
+        ws_bytes = int(lib.rn_conv_wgrad_ws_bytes(C.byref(d)))  # split-M slab workspace, as the executor uses
+        ws = torch.empty(max(ws_bytes, 16) // 4, device=dev)
         L.check(lib.rn_conv_weight_pack(C.byref(d), P(wm), P(wk), P(wc), st), "pack")
         calls = {
             "fwd": lambda: lib.rn_conv_fwd(C.byref(d), P(x), P(wk), P(y), L.RN_BF16, P(yv) if res else None, None, st),
             "dgrad": lambda: lib.rn_conv_bwd_data(C.byref(d), P(yv), P(wc), P(dx), None, st),
-            "wgrad": lambda: lib.rn_conv_bwd_filter(C.byref(d), P(x), P(yv), P(dw), st),
+            "wgrad": lambda: lib.rn_conv_bwd_filter_ws(C.byref(d), P(x), P(yv), P(dw), P(ws), ws_bytes, st),
         }
         flops = 2.0 * n * d.p * d.q * k * (c // g) * kern[0] * kern[1]
         # algorithmic HBM bytes (bf16): x + w + y (+ residual for fwd); per-mode roofline time

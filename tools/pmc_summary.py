@@ -10,9 +10,9 @@ import csv, json, re, sys, collections
 
 
 def family(name):
-    m = re.search(r"igemm_big_kernel<(\d+),", name)
+    m = re.search(r"igemm_big_kernel<(\d+), \d+, \d+(?:, (?:true|false), (\d+))?", name)
     if m:
-        return "igemm_big_kernel<256x%s>" % m.group(1)
+        return "igemm_big_kernel<%sx%s>" % (m.group(2) or "256", m.group(1))
     m = re.search(r"(igemm_kernel|wgrad_kernel)<([^>]*)>", name)
     if m:
         args = [a.strip() for a in m.group(2).split(",")]
