@@ -881,6 +881,16 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   }
   wait_vmcnt<0>();  // the zero-fill DMAs past the range land before the epilogue reuses the buffers
   __syncthreads();  // the epilogue reuses the staging buffers
+  if (p.sched & 16) {  // diagnostic (rn_set_tuning 7 bit 16): no epilogue, one store per wave keeps
+                       // the accumulators live (wrong results; isolates the epilogue's cost)
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) t += acc[i][j][0];
+    if (lane == 0) reinterpret_cast<float*>(p.y)[blockIdx.x] = t;
+    return;
+  }
 
   // ---- epilogue: per wave, 64 accumulator rows at a time through LDS, then 16-byte row chunks
   constexpr int CPR = WN / 8;  // 16-byte output chunks per wave row
@@ -974,7 +984,8 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
           for (int e = 0; e < 8; ++e) v[e] += a[e];
         }
         const uint4 out = f_to_chunk(v, (const bf16_t*)nullptr);
-        *reinterpret_cast<uint4*>(yg + off[k]) = out;
+        if (!(p.sched & 32) || (out.x & 0xFFFF) == 0x7FC1)  // diagnostic bit 32: no output stores
+          *reinterpret_cast<uint4*>(yg + off[k]) = out;
         if constexpr (EPI != 0) {  // on the stored (rounded) values, as a separate pass would read them
           float g[8];
           chunk_to_f(out, g, (const bf16_t*)nullptr);
