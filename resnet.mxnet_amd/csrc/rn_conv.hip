@@ -1749,12 +1749,20 @@ __global__ void stem_colsum_kernel(const float* __restrict__ ws, float* __restri
   const int k = idx % K;
   const int s = (idx / K) % S;
   const int pp = idx / (K * S);
-  float acc = 0.f;
-  for (int q = 0; q < Q; ++q) {
-    const int w = q * sw - pw + s;
-    if (w >= 0 && w < W) acc += ws[((int64_t)pp * Q + q) * kpad + k];
+  // the in-bounds output columns of tap s: 0 <= q*sw - pw + s < W (a contiguous range)
+  const int qlo = max(0, (pw - s + sw - 1) / sw);  // (a negative numerator only gives values <= 0)
+  const int qhi = W - 1 + pw - s < 0 ? -1 : min(Q - 1, (W - 1 + pw - s) / sw);
+  const float* src = ws + (int64_t)pp * Q * kpad + k;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;  // independent chains: the loads overlap
+  int q = qlo;
+  for (; q + 3 <= qhi; q += 4) {
+    a0 += src[(int64_t)q * kpad];
+    a1 += src[(int64_t)(q + 1) * kpad];
+    a2 += src[(int64_t)(q + 2) * kpad];
+    a3 += src[(int64_t)(q + 3) * kpad];
   }
-  tq[idx] = acc;
+  for (; q <= qhi; ++q) a0 += src[(int64_t)q * kpad];
+  tq[idx] = (a0 + a1) + (a2 + a3);
 }
 __global__ void stem_tap_sum_kernel(const float* __restrict__ tq, float* __restrict__ g, int K, int R, int S, int H,
                                     int P, int sh, int ph) {
@@ -1763,12 +1771,20 @@ __global__ void stem_tap_sum_kernel(const float* __restrict__ tq, float* __restr
   const int k = idx / (R * S);
   const int tap = idx % (R * S);
   const int r = tap / S, s = tap % S;
-  float acc = 0.f;
-  for (int pp = 0; pp < P; ++pp) {
-    const int h = pp * sh - ph + r;
-    if (h >= 0 && h < H) acc += tq[((int64_t)pp * S + s) * K + k];
+  const int plo = max(0, (ph - r + sh - 1) / sh);
+  const int phi = H - 1 + ph - r < 0 ? -1 : min(P - 1, (H - 1 + ph - r) / sh);
+  const float* src = tq + (int64_t)s * K + k;
+  const int64_t step = (int64_t)S * K;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int pp = plo;
+  for (; pp + 3 <= phi; pp += 4) {
+    a0 += src[pp * step];
+    a1 += src[(pp + 1) * step];
+    a2 += src[(pp + 2) * step];
+    a3 += src[(pp + 3) * step];
   }
-  g[idx] = acc;
+  for (; pp <= phi; ++pp) a0 += src[pp * step];
+  g[idx] = (a0 + a1) + (a2 + a3);
 }
 __global__ void stem_shift_reduce_kernel(const float* __restrict__ g, const float* __restrict__ wm,
                                          float* __restrict__ dbeta, int K, int RS, int C) {

@@ -31,6 +31,7 @@ int grid1d(int64_t total, int block = 256, int cap = 8192) {
 // ------------------------------------------------------------------------------ pooling
 struct PoolArgs {
   int n, h, w, c, r, s, sh, sw, ph, pw, p, q, type;
+  FastDiv fd_cpr, fd_a, fd_b;  // chunks per pixel; fwd: q, p / bwd: w, h (32-bit index math)
 };
 
 // forward: thread per (output pixel, chunk). Max: first maximal tap in (r, s) scan order,
@@ -41,14 +42,14 @@ __global__ void pool_fwd_kernel(PoolArgs a, const T* __restrict__ x, T* __restri
                                 uint8_t* __restrict__ argmax) {
   constexpr int CE = 16 / sizeof(T);
   const int cpr = a.c / CE;
-  const int64_t total = (int64_t)a.n * a.p * a.q * cpr;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int cc = (int)(i % cpr);
-    const int64_t pix = i / cpr;
-    const int qq = (int)(pix % a.q);
-    const int pp = (int)((pix / a.q) % a.p);
-    const int n = (int)(pix / ((int64_t)a.q * a.p));
+  const uint32_t total = (uint32_t)a.n * a.p * a.q * cpr;  // host-checked < 2^31
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t pix = fdiv(i, a.fd_cpr);
+    const int cc = (int)(i - pix * cpr);
+    const uint32_t t = fdiv(pix, a.fd_a);
+    const int qq = (int)(pix - t * a.q);
+    const uint32_t n = fdiv(t, a.fd_b);
+    const int pp = (int)(t - n * a.p);
     float best[CE];
     int arg[CE];
 #pragma unroll
@@ -82,9 +83,12 @@ __global__ void pool_fwd_kernel(PoolArgs a, const T* __restrict__ x, T* __restri
       const float inv = 1.f / (float)(a.r * a.s);
 #pragma unroll
       for (int e = 0; e < CE; ++e) best[e] *= inv;
-    } else if (argmax) {
+    } else if (argmax) {  // the chunk's CE tap indices in one 8- or 4-byte store
+      uint64_t packed = 0;
 #pragma unroll
-      for (int e = 0; e < CE; ++e) argmax[pix * a.c + cc * CE + e] = (uint8_t)arg[e];
+      for (int e = 0; e < CE; ++e) packed |= (uint64_t)(uint8_t)arg[e] << (8 * e);
+      if (CE == 8) *reinterpret_cast<uint64_t*>(argmax + pix * a.c + cc * CE) = packed;
+      else *reinterpret_cast<uint32_t*>(argmax + pix * a.c + cc * CE) = (uint32_t)packed;
     }
     reinterpret_cast<uint4*>(y)[i] = f_to_chunk(best, (const T*)nullptr);
   }
@@ -96,15 +100,15 @@ __global__ void pool_bwd_kernel(PoolArgs a, const T* __restrict__ dy, const uint
                                 T* __restrict__ dx, const T* __restrict__ add) {
   constexpr int CE = 16 / sizeof(T);
   const int cpr = a.c / CE;
-  const int64_t total = (int64_t)a.n * a.h * a.w * cpr;
+  const uint32_t total = (uint32_t)a.n * a.h * a.w * cpr;  // host-checked < 2^31
   const float inv = 1.f / (float)(a.r * a.s);
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    const int cc = (int)(i % cpr);
-    const int64_t pix = i / cpr;
-    const int ww = (int)(pix % a.w);
-    const int hh = (int)((pix / a.w) % a.h);
-    const int n = (int)(pix / ((int64_t)a.w * a.h));
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t pix = fdiv(i, a.fd_cpr);
+    const int cc = (int)(i - pix * cpr);
+    const uint32_t t = fdiv(pix, a.fd_a);
+    const int ww = (int)(pix - t * a.w);
+    const uint32_t n = fdiv(t, a.fd_b);
+    const int hh = (int)(t - n * a.h);
     float acc[CE];
     if (add) chunk_to_f(reinterpret_cast<const uint4*>(add)[i], acc, (const T*)nullptr);
     else
@@ -125,10 +129,12 @@ __global__ void pool_bwd_kernel(PoolArgs a, const T* __restrict__ dy, const uint
         const int64_t obase = (((int64_t)n * a.p + pp) * a.q + qq) * a.c + cc * CE;
         float g[CE];
         chunk_to_f(*reinterpret_cast<const uint4*>(dy + obase), g, (const T*)nullptr);
-        if (a.type == RN_POOL_MAX) {
+        if (a.type == RN_POOL_MAX) {  // the chunk's CE tap indices in one 8- or 4-byte load
+          const uint64_t am = CE == 8 ? *reinterpret_cast<const uint64_t*>(argmax + obase)
+                                      : (uint64_t)*reinterpret_cast<const uint32_t*>(argmax + obase);
 #pragma unroll
           for (int e = 0; e < CE; ++e)
-            if (argmax[obase + e] == tap) acc[e] += g[e];
+            if ((int)((am >> (8 * e)) & 0xFF) == tap) acc[e] += g[e];
         } else {
 #pragma unroll
           for (int e = 0; e < CE; ++e) acc[e] += g[e] * inv;
@@ -431,6 +437,10 @@ int rn_pool_desc_init(rn_pool_desc* d) {
 int rn_pool_fwd(const rn_pool_desc* d, const void* x, void* y, uint8_t* argmax, rn_stream_t stream) {
   RN_CHECK_ARG(d && x && y, "null argument");
   PoolArgs a{d->n, d->h, d->w, d->c, d->r, d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, d->p, d->q, d->type};
+  a.fd_cpr = make_fastdiv(d->c / (d->dtype == RN_BF16 ? 8 : 4));
+  a.fd_a = make_fastdiv(d->q);
+  a.fd_b = make_fastdiv(d->p);
+  RN_CHECK_ARG((int64_t)d->n * d->h * d->w * d->c < INT32_MAX, "pooling tensor exceeds 2^31 elements");
   hipStream_t st = as_stream(stream);
   const int64_t total = (int64_t)d->n * d->p * d->q * d->c / 8;
   if (d->dtype == RN_BF16)
@@ -447,6 +457,10 @@ int rn_pool_bwd(const rn_pool_desc* d, const void* dy, const uint8_t* argmax, vo
   RN_CHECK_ARG(d && dy && dx, "null argument");
   RN_CHECK_ARG(d->type != RN_POOL_MAX || argmax, "max pool backward needs argmax");
   PoolArgs a{d->n, d->h, d->w, d->c, d->r, d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, d->p, d->q, d->type};
+  a.fd_cpr = make_fastdiv(d->c / (d->dtype == RN_BF16 ? 8 : 4));
+  a.fd_a = make_fastdiv(d->w);
+  a.fd_b = make_fastdiv(d->h);
+  RN_CHECK_ARG((int64_t)d->n * d->h * d->w * d->c < INT32_MAX, "pooling tensor exceeds 2^31 elements");
   hipStream_t st = as_stream(stream);
   const int64_t total = (int64_t)d->n * d->h * d->w * d->c / 8;
   if (d->dtype == RN_BF16)
