@@ -205,6 +205,9 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--image", type=int, default=224)
     ap.add_argument("--precision", default="bfloat16")
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "resnext50", "resnet50_int8"],
+                    help="BASELINE.json configs: resnet50 = C2/C3 (the headline), resnext50 = C4 "
+                         "(32x4d, grouped convs), resnet50_int8 = C5 (symbol/resnet_int8.py QAT graph)")
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=8)
@@ -230,7 +233,11 @@ def main():
         rdist.init_from_env("nccl")
     import torch.distributed as dist
 
-    sym = graphs.resnet50()
+    sym = {"resnet50": graphs.resnet50, "resnext50": graphs.resnext50_32x4d,
+           "resnet50_int8": graphs.resnet50_int8}[a.model]()
+    model_name = {"resnet50": "resnet50_v2", "resnext50": "resnext50_32x4d", "resnet50_int8": "resnet50_v2_int8"}[a.model]
+    workload = {"resnet50": "ResNet-50 v2 (symbol/resnet.py)", "resnext50": "ResNeXt-50 32x4d (symbol/resnext.py)",
+                "resnet50_int8": "ResNet-50 v2 int8 QAT (symbol/resnet_int8.py)"}[a.model]
     mod = mx.mod.Module(sym, context=[mx.gpu(local)], precision=a.precision)
     shp = (a.batch, 3, a.image, a.image)
     mod.bind(data_shapes=[("data", shp)], label_shapes=[("softmax_label", (a.batch,))], for_training=True)
@@ -319,9 +326,10 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "images/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if a.precision.startswith("bf") else "fp32",
-            "data": "synthetic (seeded U(-1,1) 224x224 images, random labels; Xavier-init ResNet-50 v2)",
-            "config": {"workload": "ResNet-50 v2 (symbol/resnet.py) train step, batch %d/GPU, %dx%d" % (
-                a.batch, a.image, a.image), "model": "resnet50_v2", "global_batch": a.batch * world,
+            "data": "synthetic (seeded U(-1,1) %dx%d images, random labels; Xavier-init %s)" % (
+                a.image, a.image, workload.split(" (")[0]),
+            "config": {"workload": "%s train step, batch %d/GPU, %dx%d" % (
+                workload, a.batch, a.image, a.image), "model": model_name, "global_batch": a.batch * world,
                 "seq_len": None, "parallelism": "dp%d" % world, "per_gpu_images_per_sec": round(value / world, 2)},
             "roofline": {"bound": "mfma", "kernel": dom, "launches_per_step": len(timer.idx),
                          "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
@@ -338,7 +346,7 @@ def main():
             "inputs": "pinned host batch copied every step (PCIe-inclusive)" if a.host_input else
                       "resident in HBM",
         }
-        if world == 1 and not a.no_cpu_baseline:
+        if world == 1 and not a.no_cpu_baseline and a.model == "resnet50":
             try:
                 out["cpu_baseline"] = cpu_baseline(a.cpu_batch, a.cpu_steps)
                 out["cpu_baseline_c1"] = cpu_baseline_c1()
