@@ -203,6 +203,25 @@ int rn_bn_fwd_train(const rn_bn_desc* d, const void* x, void* y, const float* ga
 int rn_stem_prepare(const rn_bn_desc* d, const float* x_nchw, int32_t n, int32_t c, int32_t h, int32_t w, void* out,
                     int32_t mode, const float* gamma, const float* beta, float* moving_mean, float* moving_var,
                     float* save_mean, float* save_invstd, float* scale, float* shift, void* ws, rn_stream_t stream);
+/* The same as the zero-bordered NHWC4 image out[n][h + ph][w + pw][4] of hp x wp pixels (bf16; the
+ * caller zeroes the border once) that the padded-NHWC4 stem path reads. */
+int rn_stem_prepare_p4(const rn_bn_desc* d, const float* x_nchw, int32_t n, int32_t c, int32_t h, int32_t w,
+                       void* out, int32_t hp, int32_t wp, int32_t ph, int32_t pw, int32_t mode,
+                       const float* gamma, const float* beta, float* moving_mean, float* moving_var,
+                       float* save_mean, float* save_invstd, float* scale, float* shift, void* ws,
+                       rn_stream_t stream);
+/* conv0 over that image (bf16, c_real <= 4, k <= 64, r, s <= 8): the reduction runs over
+ * k = (r * 8 + s) * 4 + c (rows and taps padded to 8, channels to 4: 256 instead of the NHWC-8
+ * layout's r * s * 8), with no in-image tests (the border is zero). d: the conv0 descriptor
+ * (c = 8 as for rn_stem_prepare, c_real = 3); hp >= (p-1)*stride_h + 8, wp >= (q-1)*stride_w + 8.
+ * w4: [k][8][8][4] from rn_stem_weight_pack_p4 (master [k][r][s][c_real] fp32).
+ * rn_stem_conv_wgrad_p4 ADDS dW into dw ([k][r][s][c_real] fp32). */
+int32_t rn_stem_p4_supported(const rn_conv_desc* d, int32_t hp, int32_t wp);
+int rn_stem_weight_pack_p4(const rn_conv_desc* d, const float* w_master, void* w4, rn_stream_t stream);
+int rn_stem_conv_fwd_p4(const rn_conv_desc* d, const void* x4, const void* w4, void* y, int32_t hp, int32_t wp,
+                        rn_stream_t stream);
+int rn_stem_conv_wgrad_p4(const rn_conv_desc* d, const void* x4, const void* dy, float* dw, int32_t hp,
+                          int32_t wp, rn_stream_t stream);
 
 /* rn_bn_fwd_train with the batch statistics already reduced per row block by the producer
  * (rn_conv_fwd_bnstats): fp64 merge of part[nblk][3][ld] -> coefficients, moving stats, then

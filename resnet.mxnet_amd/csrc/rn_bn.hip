@@ -711,9 +711,62 @@ int rn_bn_fwd_train_part(const rn_bn_desc* d, const float* part, int64_t nblk, i
   return bn_apply_t<float>(d, x, y, scale, shift, st);
 }
 
+namespace {
+// the affine-transformed batch as the zero-bordered NHWC4 image: out[n][h + ph][w + pw][4] (bf16) of
+// an image of hp x wp pixels whose border the caller zeroed once; thread per pixel, 8-byte stores
+__global__ __launch_bounds__(256) void stem_to_nhwc4p_kernel(const float* __restrict__ x, int64_t npix, int c, int h,
+                                                             int w, int hp, int wp, int ph, int pw,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift, bf16_t* __restrict__ out) {
+  const int hw = h * w;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < npix; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t img = i / hw;
+    const int pix = (int)(i - img * hw);
+    const int hh = pix / w, ww = pix - hh * w;
+    uint32_t packed[2] = {0u, 0u};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float f = 0.f;
+      if (e < c) {
+        f = x[(img * c + e) * hw + pix];
+        if (scale) f = fmaf(f, scale[e], shift[e]);
+      }
+      packed[e >> 1] |= (uint32_t)f2bf(f) << (16 * (e & 1));
+    }
+    const int64_t o = ((img * hp + hh + ph) * wp + ww + pw) * 4;
+    *reinterpret_cast<uint2*>(out + o) = make_uint2(packed[0], packed[1]);
+  }
+}
+
+int stem_prepare_impl(const rn_bn_desc* d, const float* x, int32_t n, int32_t c, int32_t h, int32_t w, void* out,
+                      int32_t p4, int32_t hp, int32_t wp, int32_t ph, int32_t pw, int32_t mode, const float* gamma,
+                      const float* beta, float* moving_mean, float* moving_var, float* save_mean, float* save_invstd,
+                      float* scale, float* shift, void* ws, rn_stream_t stream);
+}  // namespace
+
 int rn_stem_prepare(const rn_bn_desc* d, const float* x, int32_t n, int32_t c, int32_t h, int32_t w, void* out,
                     int32_t mode, const float* gamma, const float* beta, float* moving_mean, float* moving_var,
                     float* save_mean, float* save_invstd, float* scale, float* shift, void* ws, rn_stream_t stream) {
+  return stem_prepare_impl(d, x, n, c, h, w, out, 0, 0, 0, 0, 0, mode, gamma, beta, moving_mean, moving_var,
+                           save_mean, save_invstd, scale, shift, ws, stream);
+}
+
+int rn_stem_prepare_p4(const rn_bn_desc* d, const float* x, int32_t n, int32_t c, int32_t h, int32_t w, void* out,
+                       int32_t hp, int32_t wp, int32_t ph, int32_t pw, int32_t mode, const float* gamma,
+                       const float* beta, float* moving_mean, float* moving_var, float* save_mean, float* save_invstd,
+                       float* scale, float* shift, void* ws, rn_stream_t stream) {
+  RN_CHECK_ARG(c <= 4 && ph >= 0 && pw >= 0 && hp >= h + ph && wp >= w + pw, "bad padded-image geometry");
+  RN_CHECK_ARG(d && d->dtype == RN_BF16, "the padded NHWC4 image is bf16");
+  return stem_prepare_impl(d, x, n, c, h, w, out, 1, hp, wp, ph, pw, mode, gamma, beta, moving_mean, moving_var,
+                           save_mean, save_invstd, scale, shift, ws, stream);
+}
+}  // extern "C"
+
+namespace {
+int stem_prepare_impl(const rn_bn_desc* d, const float* x, int32_t n, int32_t c, int32_t h, int32_t w, void* out,
+                      int32_t p4, int32_t hp, int32_t wp, int32_t ph, int32_t pw, int32_t mode, const float* gamma,
+                      const float* beta, float* moving_mean, float* moving_var, float* save_mean, float* save_invstd,
+                      float* scale, float* shift, void* ws, rn_stream_t stream) {
   RN_CHECK_ARG(d && x && out && c >= 1 && c <= 8 && n > 0 && h > 0 && w > 0, "bad arguments");
   RN_CHECK_ARG(d->c == 8 && d->c_real == c && d->m == (int64_t)n * h * w, "desc must describe the NHWC-8 copy");
   RN_CHECK_ARG(mode == 2 || (beta && scale && shift), "affine outputs required");
@@ -738,6 +791,11 @@ int rn_stem_prepare(const rn_bn_desc* d, const float* x, int32_t n, int32_t c, i
   const float* sh = mode == 2 ? nullptr : shift;
   const int64_t npix = (int64_t)n * hw;
   const int grid = (int)std::min<int64_t>((npix + 255) / 256, 65536);
+  if (p4) {
+    hipLaunchKernelGGL(stem_to_nhwc4p_kernel, dim3(grid), dim3(256), 0, st, x, npix, c, h, w, hp, wp, ph, pw, sc, sh,
+                       (bf16_t*)out);
+    return rn_check_launch("stem_prepare_p4");
+  }
   if (d->dtype == RN_BF16)
     hipLaunchKernelGGL(stem_to_nhwc8_kernel<bf16_t>, dim3(grid), dim3(256), 0, st, x, npix, c, hw, sc, sh,
                        (bf16_t*)out);
@@ -746,6 +804,9 @@ int rn_stem_prepare(const rn_bn_desc* d, const float* x, int32_t n, int32_t c, i
                        (float*)out);
   return rn_check_launch("stem_prepare");
 }
+}  // namespace
+
+extern "C" {
 
 int rn_bn_bwd_part(const rn_bn_desc* d, const float* part, int64_t nrb, const void* x, const void* dy, void* dx,
                    const void* add_src, const float* gamma, const float* save_mean, const float* save_invstd,

@@ -674,10 +674,12 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // for every ResNet-50 layer at batch 256, so 256-row tiles leave a last round of 196 / 256 workgroups
 // on every grid; 224-row tiles (7 / 8 of the rows) fill 224 / 256. The A region of the LDS stage
 // keeps 256 rows (the DMA rounds of rows >= BM read zeros).
-// SC: the stem's small-C mode (C = 8 = one 16-byte chunk per tap, the flattened reduction
-// k = tap * 8 + c): each DMA lane's chunk of a K-tile is its own tap, so the gathered row offset and
-// the in-image test are per lane (64-column tile only).
-template <int BN, int NBUF, int EPI = 0, bool M32 = false, int BM = 256, bool SC = false>
+// SC: the stem's small-C modes (64-column tile only), where a DMA lane's chunk of a K-tile is its own
+// tap, so the gathered row offset (and the in-image test) is per lane. SC 1: NHWC with C = 8 (one
+// tap per 16-byte chunk, k = tap * 8 + c). SC 2: the padded NHWC4 image of rn_stem_prepare_p4 (zero
+// border, so no in-image test): k = (r * 8 + s) * 4 + c over r, s < 8 (tap 7 of a row and row 7
+// have zero weights), a chunk = taps (r, 2 j) and (r, 2 j + 1), K-tile t = rows 2 t, 2 t + 1.
+template <int BN, int NBUF, int EPI = 0, bool M32 = false, int BM = 256, int SC = 0>
 __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_big_kernel(IgemmArgs p) {
   constexpr int BMA = 256, CE = 8, BKE = 64;
   constexpr int NW = BN == 64 ? 4 : 8;           // waves
@@ -735,6 +737,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
       a_w[i] = jj * p.wmul + cl.wb0 + cl.woff0;
       // may point before the image: masked (SC: the lane's chunk is a tap, not a channel block)
       a_row[i] = ((n * p.H + a_h[i]) * p.W + a_w[i]) * p.C + (SC ? 0 : lch * CE);
+      if (SC == 2) a_row[i] = ((n * p.H + ii * p.hmul) * p.W + jj * p.wmul) * 4;  // padded image: no offsets
     } else {
       a_h[i] = -(1 << 28);  // never inside the image
       a_w[i] = 0;
@@ -754,7 +757,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * 1024);  // this wave's 8 rows
 
   const int ncb = (p.cblk + BKE - 1) / BKE;
-  const int nstage = SC ? (p.rs * CE + BKE - 1) / BKE : cl.nr * cl.ns * ncb;
+  const int nstage = SC == 2 ? 4 : SC ? (p.rs * CE + BKE - 1) / BKE : cl.nr * cl.ns * ncb;
   int st_tr = 0, st_ts = 0, st_cb = 0, st_n = 0;
   // one K-tile's DMAs: prep() fixes the tile's uniform offsets, piece(k) issues DMA k (A rounds
   // first, then B). A tile past the range issues zero-fill DMAs (kOob) into a buffer nobody reads,
@@ -764,7 +767,17 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   uint32_t d_la = 0;
   const uint32_t dmask = (p.sched & 2) ? 0xFFF0u : 0xFFFFFFFFu;  // diagnostic: L2-resident sources
   auto prep = [&](int buf) __attribute__((always_inline)) {
-    if constexpr (SC) {  // K-tile t: lane chunk lch is tap 8 t + lch (all 8 channels of it)
+    if constexpr (SC == 2) {  // K-tile t: lane chunk lch is row 2 t + lch / 4, taps 2 (lch % 4) + {0, 1}
+      const int t = st_n++;
+      d_cok = t < nstage;
+      d_dh = 0;  // (the padded image needs no in-image test: a_h / a_w are inside it)
+      d_dw = 0;
+      d_toffa = ((2 * t + (lch >> 2)) * p.W + 2 * (lch & 3)) * 4;
+      d_toffb = t * BKE;
+      d_la = lds0 + buf * (kStage * 16);
+      return;
+    }
+    if constexpr (SC == 1) {  // K-tile t: lane chunk lch is tap 8 t + lch (all 8 channels of it)
       const int t = st_n++;
       const int tap = t * (BKE / CE) + lch;
       const int r = (int)fdiv((uint32_t)tap, p.fdS);
@@ -1077,6 +1090,8 @@ struct WgradArgs {
   int creal;                  // logical input channels (< C: padded stride, dw keeps c < creal)
   int nct, nkt;               // column tiles, k tiles (grid = splits * nkt * nct)
   int diag_noepi;             // diagnostic (rn_set_tuning 6): skip the dW epilogue (wrong results)
+  int p4;                     // the stem's padded NHWC4 image (rn_stem_prepare_p4): column = (r*8 + s)*4 + c,
+                              // r, s < 8; dW keeps r < R, s < S, c < creal ([K][R][S][creal])
   float* slab;                // nullable (LDS-DMA kernels): the split's tile stored into slab[split][K][ldw]
                               // (no atomics; wgrad_slab_reduce_kernel sums the splits into dw)
   const float* in_sc;         // nullable: BN+ReLU applied to the gathered x while staging
@@ -1375,7 +1390,11 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
     b_row[j] = (wid * BR + j) * B_RPI + lane / B_CPR;
     const int slot = lane % B_CPR;
     const int col = n0 + 8 * (slot ^ (swz_tr(b_row[j]) & (B_CPR - 1)));
-    if (col < p.ncol_load) {
+    if (col < p.ncol_load && p.p4) {  // chunk = taps (r, s), (r, s + 1) of the padded image
+      b_ch[j] = 0;
+      b_h[j] = col >> 5;
+      b_w[j] = (col >> 2) & 7;
+    } else if (col < p.ncol_load) {
       const int tap = fdiv(col, p.fdC);
       b_ch[j] = col - tap * p.C;
       const int r = fdiv(tap, p.fdS);
@@ -1504,6 +1523,10 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
         const int col = n0 + wn * 64 + j * 16 + (lane & 15);
         if (!padded) {
           if (col < p.ncol) atomicAdd(p.dw + (int64_t)k * p.ldw + col, acc[i][j][e]);
+        } else if (p.p4) {  // column (r*8 + s)*4 + c of the padded NHWC4 image
+          const int c = col & 3, s = (col >> 2) & 7, r = col >> 5;
+          if (c < p.creal && s < p.S && r < p.R)
+            atomicAdd(p.dw + (int64_t)k * p.ldw + (r * p.S + s) * p.creal + c, acc[i][j][e]);
         } else if (col < p.ncol_load) {
           const int tap = fdiv(col, p.fdC);
           const int c = col - tap * p.C;
@@ -1951,7 +1974,7 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
     if (bn == 64 && epi == 0) {
       b.ntn = (int)ceil_div(a.K, 64);
       dim3 grid((unsigned)(ceil_div(maxMc, 256) * b.ntn), 1, a.ncls);
-      if (a.smallc) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, true>), grid, dim3(256), 0, st, b);
+      if (a.smallc) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, 1>), grid, dim3(256), 0, st, b);
       else if (m32) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true>), grid, dim3(256), 0, st, b);
       else hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, false>), grid, dim3(256), 0, st, b);
       return rn_check_launch("igemm_big64");
@@ -2334,6 +2357,86 @@ int rn_conv_bwd_filter_ws(const rn_conv_desc* d, const void* x, const void* dy, 
 
 int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, float* dw, rn_stream_t stream) {
   return rn_conv_bwd_filter_x(d, x, dy, dw, nullptr, nullptr, stream);
+}
+
+// ---------------------------------------------------------------- stem over the padded NHWC4 image
+namespace {
+bool stem_p4_ok(const rn_conv_desc* d, int32_t hp, int32_t wp) {
+  return d && d->dtype == RN_BF16 && d->groups == 1 && d->c_real <= 4 && d->k <= 64 && d->r <= 8 && d->s <= 8 &&
+         hp >= (d->p - 1) * d->stride_h + 8 && wp >= (d->q - 1) * d->stride_w + 8 &&
+         (int64_t)d->n * hp * wp * 4 < INT32_MAX;
+}
+}  // namespace
+
+__global__ void stem_pack_p4_kernel(const float* __restrict__ wm, bf16_t* __restrict__ out, int K, int R, int S,
+                                    int creal) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // out[k][r<8][s<8][c<4]
+  if (i >= K * 256) return;
+  const int c = i & 3, s = (i >> 2) & 7, r = (i >> 5) & 7, k = i >> 8;
+  const float v = (c < creal && s < S && r < R) ? wm[((int64_t)(k * R + r) * S + s) * creal + c] : 0.f;
+  out[i] = f2bf(v);
+}
+
+int32_t rn_stem_p4_supported(const rn_conv_desc* d, int32_t hp, int32_t wp) { return stem_p4_ok(d, hp, wp) ? 1 : 0; }
+
+int rn_stem_weight_pack_p4(const rn_conv_desc* d, const float* wm, void* w4, rn_stream_t stream) {
+  RN_CHECK_ARG(d && wm && w4 && d->dtype == RN_BF16 && d->c_real <= 4 && d->r <= 8 && d->s <= 8, "bad arguments");
+  hipLaunchKernelGGL(stem_pack_p4_kernel, dim3((d->k * 256 + 255) / 256), dim3(256), 0, as_stream(stream), wm,
+                     (bf16_t*)w4, d->k, d->r, d->s, d->c_real);
+  return rn_check_launch("stem_weight_pack_p4");
+}
+
+int rn_stem_conv_fwd_p4(const rn_conv_desc* d, const void* x4, const void* w4, void* y, int32_t hp, int32_t wp,
+                        rn_stream_t stream) {
+  RN_CHECK_ARG(x4 && w4 && y, "null argument");
+  RN_CHECK_ARG(stem_p4_ok(d, hp, wp), "unsupported stem shape for the padded NHWC4 path");
+  IgemmArgs a{};
+  a.x = x4; a.w = w4; a.y = y;
+  a.N = d->n; a.H = hp; a.W = wp; a.C = 4; a.P = d->p; a.Q = d->q; a.K = d->k; a.ldo = d->k_pad;
+  a.S = 8; a.wrow = 256; a.hmul = d->stride_h; a.wmul = d->stride_w;
+  a.ostep_h = 1; a.ostep_w = 1; a.cblk = 4;
+  a.ncls = 1;
+  IgemmCls& c = a.cls[0];
+  c.Pc = d->p; c.Qc = d->q; c.nr = 1; c.ns = 1;
+  c.fdQ = make_fastdiv(c.Qc); c.fdPQ = make_fastdiv(c.Pc * c.Qc);
+  a.x_bytes = (int)((int64_t)d->n * hp * wp * 4 * 2);
+  a.w_bytes = d->k * 256 * 2;
+  a.sched = g_tune[RN_TUNE_IGEMM_SCHED];
+  a.ntn = 1;
+  const int64_t M = (int64_t)d->n * d->p * d->q;
+  hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, 2>), dim3((unsigned)ceil_div(M, 256)), dim3(256), 0,
+                     as_stream(stream), a);
+  return rn_check_launch("stem_conv_fwd_p4");
+}
+
+int rn_stem_conv_wgrad_p4(const rn_conv_desc* d, const void* x4, const void* dy, float* dw, int32_t hp, int32_t wp,
+                          rn_stream_t stream) {
+  RN_CHECK_ARG(x4 && dy && dw, "null argument");
+  RN_CHECK_ARG(stem_p4_ok(d, hp, wp), "unsupported stem shape for the padded NHWC4 path");
+  RN_CHECK_ARG((int64_t)d->n * d->p * d->q * d->k_pad < INT32_MAX, "dy exceeds 2^31 elements");
+  WgradArgs a{};
+  a.x = x4; a.dy = dy; a.dw = dw;
+  a.N = d->n; a.H = hp; a.W = wp; a.C = 4; a.P = d->p; a.Q = d->q; a.K = d->k;
+  a.ldy = d->k_pad; a.R = d->r; a.S = d->s; a.sh = d->stride_h; a.sw = d->stride_w; a.ph = 0; a.pw = 0;
+  a.ncol_load = 256;
+  a.ncol = d->r * d->s * d->c_real;
+  a.ldw = a.ncol;
+  a.cblk = 4;
+  a.creal = d->c_real;
+  a.p4 = 1;
+  a.M = d->n * d->p * d->q;
+  a.fdQ = make_fastdiv(d->q); a.fdPQ = make_fastdiv(d->p * d->q);
+  a.fdC = make_fastdiv(4); a.fdS = make_fastdiv(8);
+  a.nct = 2;
+  a.nkt = 1;
+  const int64_t tiles = a.nct;
+  const int64_t mtiles = ceil_div(a.M, 64);
+  int64_t split = std::min<int64_t>(std::max<int64_t>(1, 512 / tiles), std::max<int64_t>(1, mtiles / 8));
+  a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
+  split = ceil_div(a.M, a.m_per_split);
+  hipLaunchKernelGGL((wgrad_big_kernel<64, 3, 128>), dim3((unsigned)(tiles * split)), dim3(256), 0, as_stream(stream),
+                     a);
+  return rn_check_launch("stem_conv_wgrad_p4");
 }
 
 int rn_conv_weight_pack(const rn_conv_desc* d, const float* wm, void* w_krsc, void* w_crsk,

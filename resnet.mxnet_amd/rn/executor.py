@@ -764,9 +764,24 @@ class Executor:
                 dfull = self._conv_desc(x.n, x.h, x.w, 8, x.c, y.c, op.kernel, op.stride, op.pad)
                 assert (dfull.p, dfull.q) == (y.h, y.w), (op.name, dfull.p, dfull.q, y.h, y.w)
                 op.dfull = op.desc = dfull
-                op.x8 = self._zeros(x.n * x.h * x.w * 8, self.tdtype)
-                op.wk = self._zeros(y.c * op.kernel[0] * op.kernel[1] * 8, self.tdtype)
-                self._add_pack(op, dfull, op.wk, None, sp)
+                # bf16 (not int8-quantized): the zero-bordered NHWC4 image instead of NHWC-8 (the
+                # reduction runs over 8x8 taps x 4 channels = 256 instead of 7x7 x 8 = 392, and no
+                # in-image tests); its border is zeroed here once, the prepare pass writes the inside
+                hp = max(x.h + 2 * op.pad[0], (dfull.p - 1) * op.stride[0] + 8)
+                wp = max(x.w + 2 * op.pad[1], (dfull.q - 1) * op.stride[1] + 8)
+                op.p4 = None
+                if self.dtype == BF16 and not op.quant and os.environ.get("RN_STEM_P4", "1") == "1" and \
+                        self.lib.rn_stem_p4_supported(L.C.byref(dfull), hp, wp):
+                    op.p4 = (hp, wp)
+                    op.x8 = self._zeros(x.n * hp * wp * 4, self.tdtype)
+                    op.wk = self._zeros(y.c * 256, self.tdtype)
+                    c_ = self._call("rn_stem_weight_pack_p4", L.C.byref(dfull), op.wsrc, self._p(op.wk), sp)
+                    self.packs.append(c_)
+                    self.unfused_packs.append(c_)
+                else:
+                    op.x8 = self._zeros(x.n * x.h * x.w * 8, self.tdtype)
+                    op.wk = self._zeros(y.c * op.kernel[0] * op.kernel[1] * 8, self.tdtype)
+                    self._add_pack(op, dfull, op.wk, None, sp)
                 stem_ws = max(stem_ws, y.h * y.w * y.cp + y.h * op.kernel[1] * y.c + y.c * op.kernel[0] * op.kernel[1] + 64)
                 xnchw = self._in_ptr  # the current input buffer (double-buffered H2D pipeline)
                 op.bnbuf = self._zeros(4 * 8, self.torch.float32)
@@ -781,17 +796,28 @@ class Executor:
                     bnargs = (None, None, None, None)
                     mode_f = mode_i = 2
                 for lst, mode in ((F, mode_f), (I, mode_i)):
-                    lst.append(self._call("rn_stem_prepare", L.C.byref(op.bn_desc), xnchw, x.n, x.c, x.h, x.w,
-                                          self._p(op.x8), mode, *bnargs, sm, si, sc, sh, wsp, sp))
+                    if op.p4:
+                        lst.append(self._call("rn_stem_prepare_p4", L.C.byref(op.bn_desc), xnchw, x.n, x.c, x.h, x.w,
+                                              self._p(op.x8), op.p4[0], op.p4[1], op.pad[0], op.pad[1], mode,
+                                              *bnargs, sm, si, sc, sh, wsp, sp))
+                    else:
+                        lst.append(self._call("rn_stem_prepare", L.C.byref(op.bn_desc), xnchw, x.n, x.c, x.h, x.w,
+                                              self._p(op.x8), mode, *bnargs, sm, si, sc, sh, wsp, sp))
                 if op.quant:
                     q = op.quant
                     for lst, tr in ((F, 1), (I, 0)):
                         lst.append(self._call("rn_quant_int8_fwd", self.dtype, x.n * x.h * x.w * 8, self._p(op.x8),
                                               self._p(op.x8), self._ap(q["minmax"]), 0, tr, q["ema"], self._qfirst,
                                               q["nbits"], qwsp, sp))
-                I.append(self._call("rn_conv_fwd", L.C.byref(dfull), self._p(op.x8), self._p(op.wk),
-                                    self._p(self.act(y)), self.dtype, None, None, sp))
-                F.append(self._conv_fwd_call(op, dfull, self._p(op.x8), None, sp))
+                if op.p4:
+                    c_ = self._call("rn_stem_conv_fwd_p4", L.C.byref(dfull), self._p(op.x8), self._p(op.wk),
+                                    self._p(self.act(y)), op.p4[0], op.p4[1], sp)
+                    I.append(c_)
+                    F.append(c_)
+                else:
+                    I.append(self._call("rn_conv_fwd", L.C.byref(dfull), self._p(op.x8), self._p(op.wk),
+                                        self._p(self.act(y)), self.dtype, None, None, sp))
+                    F.append(self._conv_fwd_call(op, dfull, self._p(op.x8), None, sp))
             elif op.kind == "conv":
                 x, y = op.x, op.y
                 d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad, op.groups)
@@ -1006,8 +1032,12 @@ class Executor:
                 if op.res is not None and op.res.needs_grad:
                     gs.alias(op.res, dy)
             elif op.kind == "stem":
-                self._bwd.append(self._call("rn_conv_bwd_filter", L.C.byref(op.dfull), self._p(op.x8), self._p(dy),
-                                            self._gp(op.weight), sp))
+                if op.p4:
+                    self._bwd.append(self._call("rn_stem_conv_wgrad_p4", L.C.byref(op.dfull), self._p(op.x8),
+                                                self._p(dy), self._gp(op.weight), op.p4[0], op.p4[1], sp))
+                else:
+                    self._bwd.append(self._call("rn_conv_bwd_filter", L.C.byref(op.dfull), self._p(op.x8),
+                                                self._p(dy), self._gp(op.weight), sp))
                 self.param_done_at[op.weight] = len(self._bwd)
                 if op.bn:
                     self._bwd.append(self._call("rn_stem_shift_grad", L.C.byref(op.dfull), self._p(dy),

@@ -60,6 +60,12 @@ SIGNATURES = {
     "rn_conv_pack_numel": (_i64, [_P, _i32]),
     "rn_conv_weight_pack": (_i32, [_P, _P, _P, _P, _P]),
     "rn_stem_prepare": (_i32, [_P, _P, _i32, _i32, _i32, _i32, _P, _i32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "rn_stem_prepare_p4": (_i32, [_P, _P, _i32, _i32, _i32, _i32, _P, _i32, _i32, _i32, _i32, _i32, _P, _P, _P, _P,
+                                  _P, _P, _P, _P, _P, _P]),
+    "rn_stem_p4_supported": (_i32, [_P, _i32, _i32]),
+    "rn_stem_weight_pack_p4": (_i32, [_P, _P, _P, _P]),
+    "rn_stem_conv_fwd_p4": (_i32, [_P, _P, _P, _P, _i32, _i32, _P]),
+    "rn_stem_conv_wgrad_p4": (_i32, [_P, _P, _P, _P, _i32, _i32, _P]),
     "rn_im2col_nchw": (_i32, [_P, _P, _P, _P, _P, _i32, _P]),
     "rn_im2col_nchw_quant": (_i32, [_P, _P, _P, _P, _P, _i32, _f32, _i32, _i32, _P, _P, _i32, _P]),
     "rn_stem_quant_clip_grad": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -660,6 +660,52 @@ def test_conv_bnrelu_on_load(gpu, dtype, case):
         (TOL[dtype] if dtype == F32 else 5e-3)
 
 
+@pytest.mark.parametrize("mode", [0, 2])
+@pytest.mark.parametrize("geom", [(2, 3, 20, 16, 64, 7, 2, 3), (3, 3, 18, 14, 24, 7, 2, 3), (2, 3, 12, 12, 40, 5, 1, 2)])
+def test_stem_padded_nhwc4(gpu, mode, geom):
+    """The bf16 stem over the zero-bordered NHWC4 image: rn_stem_prepare_p4 (bn_data in training
+    mode or none), conv0 fwd (rn_stem_conv_fwd_p4) and wgrad (rn_stem_conv_wgrad_p4, adds into dw)
+    against the oracle on the values the device stores; ragged output counts and odd sizes."""
+    n, c, h, w, k, r, st, pd = geom
+    rng = np.random.default_rng(23)
+    x = rng.uniform(-1, 1, (n, c, h, w)).astype(np.float32) * 2 + 0.5
+    gamma, beta = np.ones(c), rng.standard_normal(c) * 0.1
+    xa = ops.bn_train_fwd(x.astype(np.float64), gamma, beta, 2e-5, True)[0] if mode == 0 else x.astype(np.float64)
+    d = conv_desc(BF16, n, 8, h, w, k, r, r, st, pd, c_real=c)
+    hp = max(h + 2 * pd, (d.p - 1) * st + 8)
+    wp = max(w + 2 * pd, (d.q - 1) * st + 8)
+    assert L.load().rn_stem_p4_supported(C.byref(d), hp, wp) == 1
+    bd = L.BNDesc(dtype=BF16, m=n * h * w, c=8, c_real=c, eps=2e-5, momentum=0.9, fix_gamma=1, relu=0)
+    f = lambda a: torch.tensor(np.asarray(a, np.float32), device=gpu)
+    g_d, b_d, mm, mv = f(gamma), f(beta), f(np.zeros(c)), f(np.ones(c))
+    sm, si, sc, sh = [torch.zeros(8, dtype=torch.float32, device=gpu) for _ in range(4)]
+    ws = torch.zeros(4096 + 64, dtype=torch.float32, device=gpu)
+    x4 = torch.zeros(n * hp * wp * 4, dtype=torch.bfloat16, device=gpu)
+    L.call("rn_stem_prepare_p4", C.byref(bd), p(f(x)), n, c, h, w, p(x4), hp, wp, pd, pd, mode, p(g_d), p(b_d),
+           p(mm), p(mv), p(sm), p(si), p(sc), p(sh), p(ws), stream())
+    torch.cuda.synchronize()
+    img = x4.float().cpu().numpy().reshape(n, hp, wp, 4)
+    inner = img[:, pd:pd + h, pd:pd + w, :c].transpose(0, 3, 1, 2).astype(np.float64)
+    border = img.copy()
+    border[:, pd:pd + h, pd:pd + w, :c] = 0
+    assert not border.any()  # zero border and zero fourth channel
+    assert rel_err(inner, xa) < 8e-3
+    wt = bf16_round(rng.standard_normal((k, c, r, r)) * 0.1)
+    w4 = torch.full((k * 256,), 7.0, dtype=torch.bfloat16, device=gpu)
+    L.call("rn_stem_weight_pack_p4", C.byref(d), p(_master_krsc(wt, gpu)), p(w4), stream())
+    y = torch.zeros((n, d.p, d.q, d.k_pad), dtype=torch.bfloat16, device=gpu)
+    L.call("rn_stem_conv_fwd_p4", C.byref(d), p(x4), p(w4), p(y), hp, wp, stream())
+    dy = bf16_round(rng.standard_normal((n, k, d.p, d.q)))
+    dw = torch.full((k * r * r * c,), 0.25, dtype=torch.float32, device=gpu)
+    L.call("rn_stem_conv_wgrad_p4", C.byref(d), p(x4), p(to_nhwc(dy, BF16, gpu)), p(dw), hp, wp, stream())
+    torch.cuda.synchronize()
+    y_ref = ops.conv2d_fwd(inner, wt, (st, st), (pd, pd))
+    _, dw_ref = ops.conv2d_bwd(inner, wt, dy, (st, st), (pd, pd))
+    assert rel_err(from_nhwc(y, k), y_ref) < TOL[BF16]
+    got = dw.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2) - 0.25
+    assert rel_err(got, dw_ref) < 5e-3
+
+
 @pytest.mark.parametrize("dtype", [F32, BF16])
 @pytest.mark.parametrize("case", [(2, 64, 14, 14, 128, 3, 1, 1), (2, 128, 14, 14, 256, 1, 2, 0),
                                   (3, 32, 13, 11, 48, 3, 2, 1), (3, 256, 20, 20, 128, 3, 2, 1)])

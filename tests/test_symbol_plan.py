@@ -90,7 +90,8 @@ def test_plan_resnext_grouped():
     assert abs(p.train_flops() / 1e9 - 6437.6) < 0.1
     ex = Executor(Plan(graphs.resnext50_32x4d(), [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")
     names = [c[0] for c in ex._bwd]
-    assert sum(n.startswith("rn_conv_bwd_filter") for n in names) == 54  # 53 conv + fc1
+    # 52 conv + fc1 weight gradients, and the stem's (the padded-NHWC4 kernel in bf16)
+    assert sum(n.startswith("rn_conv_bwd_filter") or n == "rn_stem_conv_wgrad_p4" for n in names) == 54
 
 
 def test_plan_rejects_unsupported():
@@ -107,7 +108,9 @@ def test_executor_dry_run(dtype):
     p = Plan(sym, [("data", (2, 3, 64, 64))], [("softmax_label", (2,))], dtype=dtype)
     ex = Executor(p, "cpu")
     names = [c[0] for c in ex._bwd]
-    assert sum(n.startswith("rn_conv_bwd_filter") for n in names) == 54
+    # the stem's weight gradient runs on the padded-NHWC4 kernel in bf16
+    assert sum(n.startswith("rn_conv_bwd_filter") for n in names) == (54 if dtype == "float32" else 53)
+    assert names.count("rn_stem_conv_wgrad_p4") == (0 if dtype == "float32" else 1)
     assert sum(n.startswith("rn_conv_bwd_data") for n in names) == 53
     # BN-backward reductions fused where the dgrad runs the 256-row tile (bf16 only)
     assert names.count("rn_conv_bwd_data_bnred") == (0 if dtype == "float32" else 41)
