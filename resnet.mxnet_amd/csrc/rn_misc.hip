@@ -57,6 +57,32 @@ __global__ void pool_fwd_kernel(PoolArgs a, const T* __restrict__ x, T* __restri
       best[e] = a.type == RN_POOL_MAX ? -INFINITY : 0.f;
       arg[e] = 0;
     }
+    if (a.type == RN_POOL_MAX && a.r == 3 && a.s == 3) {
+      // the ResNet stem pool: all 9 window loads issued before the first max (clamped addresses,
+      // out-of-image taps masked), so they are in flight together
+      uint4 v[9];
+      bool ok[9];
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const int hh = pp * a.sh - a.ph + r, ww = qq * a.sw - a.pw + s;
+          ok[r * 3 + s] = (unsigned)hh < (unsigned)a.h && (unsigned)ww < (unsigned)a.w;
+          const int hc = ok[r * 3 + s] ? hh : 0, wc = ok[r * 3 + s] ? ww : 0;
+          v[r * 3 + s] = *reinterpret_cast<const uint4*>(x + (((int64_t)n * a.h + hc) * a.w + wc) * a.c + cc * CE);
+        }
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        float f[CE];
+        chunk_to_f(v[t], f, (const T*)nullptr);
+#pragma unroll
+        for (int e = 0; e < CE; ++e)
+          if (ok[t] && f[e] > best[e]) {
+            best[e] = f[e];
+            arg[e] = t;
+          }
+      }
+    } else
     for (int r = 0; r < a.r; ++r) {
       const int hh = pp * a.sh - a.ph + r;
       if (hh < 0 || hh >= a.h) continue;
@@ -121,6 +147,34 @@ __global__ void pool_bwd_kernel(PoolArgs a, const T* __restrict__ dy, const uint
     int qlo = ww + a.pw - a.s + 1;
     qlo = qlo <= 0 ? 0 : (qlo + a.sw - 1) / a.sw;
     const int qhi = min(a.q - 1, (ww + a.pw) / a.sw);
+    if (a.type == RN_POOL_MAX && a.r == 3 && a.s == 3 && a.sh == 2 && a.sw == 2) {
+      // 3x3 / stride 2: at most 2 x 2 windows hold this pixel; their dy chunks and tap indices are
+      // loaded together (clamped addresses, masked), then added in the generic order
+      uint4 g4[4];
+      uint64_t am4[4];
+      bool ok4[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int pp = plo + (u >> 1), qq = qlo + (u & 1);
+        ok4[u] = pp <= phi && qq <= qhi;
+        const int64_t obase = (((int64_t)n * a.p + (ok4[u] ? pp : 0)) * a.q + (ok4[u] ? qq : 0)) * a.c + cc * CE;
+        g4[u] = *reinterpret_cast<const uint4*>(dy + obase);
+        am4[u] = CE == 8 ? *reinterpret_cast<const uint64_t*>(argmax + obase)
+                         : (uint64_t)*reinterpret_cast<const uint32_t*>(argmax + obase);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int pp = plo + (u >> 1), qq = qlo + (u & 1);
+        const int tap = (hh - (pp * 2 - a.ph)) * 3 + (ww - (qq * 2 - a.pw));
+        float g[CE];
+        chunk_to_f(g4[u], g, (const T*)nullptr);
+#pragma unroll
+        for (int e = 0; e < CE; ++e)
+          if (ok4[u] && (int)((am4[u] >> (8 * e)) & 0xFF) == tap) acc[e] += g[e];
+      }
+      reinterpret_cast<uint4*>(dx)[i] = f_to_chunk(acc, (const T*)nullptr);
+      continue;
+    }
     for (int pp = plo; pp <= phi; ++pp) {
       const int r = hh - (pp * a.sh - a.ph);
       for (int qq = qlo; qq <= qhi; ++qq) {
