@@ -697,7 +697,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   constexpr int EP_LD = WN + 4;                  // staged fp32 row stride
   constexpr int EP_WAVE = 64 * EP_LD;            // floats per wave per epilogue half
   constexpr int kEpChunks = NW * EP_WAVE / 4;
-  static_assert(BN != 64 || EPI == 0, "the 64-column tile has no BatchNorm epilogue");
+  static_assert(BN != 64 || !SC || EPI == 0, "the stem modes have no BatchNorm epilogue");
   __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * kStage > kEpChunks ? NBUF * kStage : kEpChunks];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -710,10 +710,10 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   const int n0 = (lid - mtile * p.ntn) * BN;
   if (m0 >= Mc) {  // (a dgrad parity class with fewer rows): empty BN-reduction partials
     if (EPI == 2 && !p.bnacc)
-      for (int e = tid; e < 2 * BN; e += NW * 64) {
+      for (int e = tid; e < WAVES_M * BN; e += NW * 64) {
         const int hh = e / BN, col = n0 + e % BN;
-        if (col < p.ldo && 2 * mtile + hh < p.mt_max) {
-          float* dst = p.bnred + ((int64_t)(blockIdx.z * p.mt_max + 2 * mtile + hh) * p.ldo + col) * 2;
+        if (col < p.ldo && WAVES_M * mtile + hh < p.mt_max) {
+          float* dst = p.bnred + ((int64_t)(blockIdx.z * p.mt_max + WAVES_M * mtile + hh) * p.ldo + col) * 2;
           dst[0] = 0.f;
           dst[1] = 0.f;
         }
@@ -1052,7 +1052,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
       }
     } else if (lane < CPR) {
       const int c0 = n0 + wn * WN + lane * 8;
-      const int blk = 2 * mtile + wm;
+      const int blk = WAVES_M * mtile + wm;  // one partial per wave row
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int col = c0 + e;
@@ -1943,7 +1943,7 @@ int bn_part_rows(const IgemmArgs& a, bool bf16) {
   if (!bf16) return 128;
   const int64_t xb = (int64_t)a.N * a.H * a.W * a.C * 2, wb = (int64_t)a.K * a.wrow * 2;
   const int bn = big_tile_cols(a, xb, wb);
-  return bn >= 128 ? big_tile_rows(bn) / 2 : 128;
+  return bn >= 128 ? big_tile_rows(bn) / 2 : bn == 64 ? 64 : 128;  // one wave row: 2 x 2 / 4 x 1 waves
 }
 
 template <typename T, typename OutT>
@@ -1971,10 +1971,13 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
     const int bn = big_tile_cols(a, xb, wb);
     RN_CHECK_ARG(!a.bnacc || bn >= 128, "accumulated BatchNorm sums need the 256-row tile (rn_conv_tile >= 128)");
     const bool m32 = g_tune[RN_TUNE_IGEMM_MFMA] != 1;
-    if (bn == 64 && epi == 0) {
+    if (bn == 64 && !a.bnacc && (epi == 0 || !a.smallc)) {
       b.ntn = (int)ceil_div(a.K, 64);
+      if (a.bnred) b.mt_max = (int)ceil_div(maxMc, 64);  // BN partials per 64-row wave row
       dim3 grid((unsigned)(ceil_div(maxMc, 256) * b.ntn), 1, a.ncls);
       if (a.smallc) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, 1>), grid, dim3(256), 0, st, b);
+      else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 1, true>), grid, dim3(256), 0, st, b);
+      else if (epi == 2) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 2, true>), grid, dim3(256), 0, st, b);
       else if (m32) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true>), grid, dim3(256), 0, st, b);
       else hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, false>), grid, dim3(256), 0, st, b);
       return rn_check_launch("igemm_big64");

@@ -733,7 +733,7 @@ class Executor:
                         # (the device-scope fp64 atomics cost more than the merge they replace)
                         op.bnacc = None
                         if self.dtype == BF16 and os.environ.get("RN_BN_ACC", "0") == "1" and \
-                                self._big_tile(src, 0) and getattr(src, "xf", None) is None:
+                                self._big_tile(src, 0, 128) and getattr(src, "xf", None) is None:
                             op.bnacc = self._zeros(L.RN_BN_ACC_REPLICAS * 2 * op.x.cp, self.torch.float64)
                             src.stats_bn = op
         for op in plan.ops:
@@ -913,13 +913,17 @@ class Executor:
             self._fwd_infer.extend(I)
         self.stem_ws = self._zeros(stem_ws, self.torch.float32)
 
-    def _big_tile(self, op, mode):
-        """Does conv `op` run its forward (mode 0) / data gradient (mode 1) on the 256-row tile?"""
+    def _big_tile(self, op, mode, min_cols=None):
+        """Does conv `op` run its forward (mode 0) / data gradient (mode 1) on a 256/224-row LDS-DMA
+        tile of at least min_cols columns (the BN epilogue fusions run there; the fp64-accumulated
+        variant on the 128/256-column tiles only)?"""
         if op.kind != "conv" or self.lib is None:
             return False
+        if min_cols is None:  # RN_BN_FUSION_MIN_COLS=64: also on the 64-column tile (opt-in: measured
+            min_cols = int(os.environ.get("RN_BN_FUSION_MIN_COLS", "128"))  # 0.6 % slower per step)
         x, y = op.x, op.y
         d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad, op.groups)
-        return int(self.lib.rn_conv_tile(L.C.byref(d), mode)) >= 128  # the 64-column tile has no BN epilogue
+        return int(self.lib.rn_conv_tile(L.C.byref(d), mode)) >= min_cols
 
     def _conv_fwd_call(self, op, d, xptr, res, sp, stats=True):
         """Conv forward; emits the next BatchNorm's statistics when one consumes y (training), and
@@ -1058,7 +1062,7 @@ class Executor:
                     # the conv dgrad that completes this BN's output gradient also reduces its backward
                     # (sum dz, sum dz*(x - mean)); the BN then needs only finalize + apply
                     _, ci, cop, cdy, cout, cadd = w
-                    if self.dtype == BF16 and os.environ.get("RN_BN_ACC", "0") == "1" and self._big_tile(cop, 1):
+                    if self.dtype == BF16 and os.environ.get("RN_BN_ACC", "0") == "1" and self._big_tile(cop, 1, 128):
                         op.bnacc2 = self._zeros(L.RN_BN_ACC_REPLICAS * 2 * op.y.cp, self.torch.float64)
                         self._bwd[ci] = self._call("rn_conv_bwd_data_bnacc", L.C.byref(cop.desc), self._p(cdy),
                                                    self._p(cop.wc), self._p(cout), self._p(cadd),
