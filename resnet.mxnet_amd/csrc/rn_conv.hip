@@ -721,6 +721,9 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
     return;
   }
 
+  // grouped conv (ResNeXt, 64-column tile = one RN_GROUP_BLOCK): the block's columns touch groups
+  // n0/gcol.., whose input channels start at cbase (dense: gcol = 2^30, cbase = 0)
+  const int cbase = (n0 / p.gcol) * p.gred;
   // DMA lane -> (row 8*wid + lane/8 (+64 i), LDS slot lane&7); it fetches the source chunk that the
   // XOR read-swizzle expects in that slot
   const int lch = M32 ? (lane & 7) ^ ((4 * wid + (lane >> 4)) & 7) : (lane & 7) ^ ((lane >> 3) & 7);
@@ -736,7 +739,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
       a_h[i] = ii * p.hmul + cl.hb0 + cl.hoff0;
       a_w[i] = jj * p.wmul + cl.wb0 + cl.woff0;
       // may point before the image: masked (SC: the lane's chunk is a tap, not a channel block)
-      a_row[i] = ((n * p.H + a_h[i]) * p.W + a_w[i]) * p.C + (SC ? 0 : lch * CE);
+      a_row[i] = ((n * p.H + a_h[i]) * p.W + a_w[i]) * p.C + (SC ? 0 : cbase + lch * CE);
       if (SC == 2) a_row[i] = ((n * p.H + ii * p.hmul) * p.W + jj * p.wmul) * 4;  // padded image: no offsets
     } else {
       a_h[i] = -(1 << 28);  // never inside the image
@@ -798,7 +801,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
         ++st_tr;
       }
     }
-    d_cok = live && cb * BKE + lch * CE < p.cblk;
+    d_cok = live && cb * BKE + lch * CE < p.cblk && cbase + cb * BKE + lch * CE < p.C;
     d_dh = p.hinc * tr;
     d_dw = p.winc * ts;
     d_toffa = (d_dh * p.W + d_dw) * p.C + cb * BKE;
@@ -1916,6 +1919,11 @@ int big_tile_cols(const IgemmArgs& a, int64_t xb, int64_t wb) {
   const int big = g_tune[RN_TUNE_IGEMM_BIG];
   int max_taps = 0;
   for (int z = 0; z < a.ncls; ++z) max_taps = std::max(max_taps, a.cls[z].nr * a.cls[z].ns);
+  if (a.gred > 0) {  // grouped (ResNeXt): the 256x64 tile over one RN_GROUP_BLOCK column block, deep reductions
+    const int nst = max_taps * (int)ceil_div(a.cblk, 64);
+    return (big != 1 && big != 5 && RN_GROUP_BLOCK == 64 && !a.in_sc && !a.bias && !g_tune[RN_TUNE_DIAG_IGEMM_L1] &&
+            xb < INT32_MAX && wb < INT32_MAX && max_taps <= 32 && nst >= 8) ? 64 : 0;
+  }
   if (a.smallc)  // the stem (C = 8): the 256x64 tile in its small-C mode (rn_set_tuning 4 = 1 or 5: never)
     return (big != 1 && big != 5 && a.C == 8 && a.K <= 64 && !a.in_sc && !a.bias && !g_tune[RN_TUNE_DIAG_IGEMM_L1] &&
             xb < INT32_MAX && wb < INT32_MAX) ? 64 : 0;
@@ -2397,7 +2405,7 @@ int rn_stem_conv_fwd_p4(const rn_conv_desc* d, const void* x4, const void* w4, v
   a.x = x4; a.w = w4; a.y = y;
   a.N = d->n; a.H = hp; a.W = wp; a.C = 4; a.P = d->p; a.Q = d->q; a.K = d->k; a.ldo = d->k_pad;
   a.S = 8; a.wrow = 256; a.hmul = d->stride_h; a.wmul = d->stride_w;
-  a.ostep_h = 1; a.ostep_w = 1; a.cblk = 4;
+  a.ostep_h = 1; a.ostep_w = 1; a.cblk = 4; a.gcol = 1 << 30; a.gred = 0;
   a.ncls = 1;
   IgemmCls& c = a.cls[0];
   c.Pc = d->p; c.Qc = d->q; c.nr = 1; c.ns = 1;
