@@ -12,7 +12,8 @@ from rn import graphs  # noqa: E402
 from rn.executor import Executor, Plan  # noqa: E402
 
 CONV_CALLS = ("rn_conv_fwd", "rn_conv_fwd_bnstats", "rn_conv_fwd_x", "rn_conv_fwd_bnacc", "rn_conv_bwd_data",
-              "rn_conv_bwd_data_bnred", "rn_conv_bwd_data_bnacc", "rn_conv_bwd_filter", "rn_conv_bwd_filter_x", "rn_conv_bwd_filter_ws")
+              "rn_conv_bwd_data_bnred", "rn_conv_bwd_data_bnacc", "rn_conv_bwd_filter", "rn_conv_bwd_filter_x", "rn_conv_bwd_filter_ws",
+              "rn_stem_conv_fwd_p4", "rn_stem_conv_wgrad_p4")
 
 
 def main():
@@ -43,7 +44,7 @@ def main():
         d = a[0]._obj
         flops = 2.0 * d.n * d.p * d.q * d.k * (d.c_real // d.groups) * d.r * d.s
         xb, yb, wb = 2.0 * d.n * d.h * d.w * d.c, 2.0 * d.n * d.p * d.q * d.k_pad, 2.0 * d.k * d.r * d.s * d.c
-        kind = "wgrad" if "filter" in n else "dgrad" if "bwd_data" in n else "fwd"
+        kind = "wgrad" if ("filter" in n or "wgrad" in n) else "dgrad" if "bwd_data" in n else "fwd"
         algb = xb + yb + (2 * wb if kind == "wgrad" else wb)
         us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         roof = max(flops / 2.5e15, algb / 8e12) * 1e6
