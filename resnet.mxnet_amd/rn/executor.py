@@ -529,6 +529,16 @@ class Executor:
         # whenever a call list runs: the plan then follows the caller's stream -- torch ops, RCCL
         # ordering and HIP-graph capture (torch.cuda.graph) all see the same stream
         self._spv = L.C.c_void_p(0)
+        # weight gradients run on a second stream (RN_WGRAD_STREAM=0: all on one): each forks from
+        # the compute stream right before it (its dy is final there, its x was final since the
+        # forward) and the backward joins it at the end, so a layer's wgrad overlaps the next
+        # layers' dgrad / BatchNorm kernels and fills the CUs their last rounds leave idle
+        self._spv2 = L.C.c_void_p(0)
+        self._side_stream = None
+        if not self.dry_run and os.environ.get("RN_WGRAD_STREAM", "1") == "1":
+            self._side_stream = torch.cuda.Stream(device=self.device)
+        self._side_idx = set()
+        self.side_enabled = True  # False: the side-stream calls run on the compute stream (serialised timing)
         self._sync_stream()
         self._acts = {}
         self._grads = {}
@@ -542,6 +552,7 @@ class Executor:
         self._alloc_acts()
         self._build_forward()
         self._build_backward()
+        self._route_wgrads()
         self._build_update()
         self.bucket_bytes = bucket_bytes
         self.num_update = 0
@@ -690,6 +701,30 @@ class Executor:
     def _sync_stream(self):
         if not self.dry_run:
             self._spv.value = self.torch.cuda.current_stream(self.device).cuda_stream
+            if self._side_stream is not None:
+                self._spv2.value = self._side_stream.cuda_stream if self.side_enabled else self._spv.value
+
+    WGRAD_CALLS = ("rn_conv_bwd_filter", "rn_conv_bwd_filter_ws", "rn_conv_bwd_filter_x", "rn_stem_conv_wgrad_p4")
+
+    def _route_wgrads(self):
+        """Bind the weight-gradient calls of the backward plan to the side stream."""
+        if self._side_stream is None:
+            return
+        for i, (name, fn, args) in enumerate(self._bwd):
+            if name in self.WGRAD_CALLS and args and args[-1] is self._spv:
+                self._bwd[i] = (name, fn, args[:-1] + (self._spv2,))
+                self._side_idx.add(i)
+
+    def _fork(self):
+        """The side stream continues after everything enqueued on the compute stream so far."""
+        ev = self.torch.cuda.Event()
+        ev.record(self.torch.cuda.current_stream(self.device))
+        self._side_stream.wait_event(ev)
+
+    def _join(self):
+        ev = self.torch.cuda.Event()
+        ev.record(self._side_stream)
+        self.torch.cuda.current_stream(self.device).wait_event(ev)
 
     def _conv_desc(self, n, h, w, c, c_real, k, kernel, stride, pad, groups=1):
         d = L.ConvDesc(dtype=self.dtype, n=n, h=h, w=w, c=c, c_real=c_real, k=k, k_pad=_pad8(k), r=kernel[0],
@@ -1207,19 +1242,30 @@ class Executor:
     def backward(self, hooks=None):
         self._sync_stream()
         self.grad.zero_()
-        if not hooks:
+        side = self._side_stream if (self._side_idx and self.side_enabled) else None
+        if not hooks and side is None:
             self._run(self._bwd)
             self._mark_input_read()
             return
-        # hooks: {bwd index -> callable}, e.g. RCCL bucket all-reduce launches
-        calls = self._bwd
-        for i, (name, fn, args) in enumerate(calls):
+        # hooks: {bwd index -> callable}, e.g. RCCL bucket all-reduce launches; with the wgrad side
+        # stream a hook runs on it after a fork, so its collective follows both streams' writes
+        hooks = hooks or {}
+        for i, (name, fn, args) in enumerate(self._bwd):
+            if side is not None and i in self._side_idx:
+                self._fork()
             r = fn(*args)
             if r != 0:
                 raise L.RNError("%s: %s" % (name, self.lib.rn_last_error().decode()))
             h = hooks.get(i + 1)
             if h is not None:
-                h()
+                if side is not None:
+                    self._fork()
+                    with self.torch.cuda.stream(side):
+                        h()
+                else:
+                    h()
+        if side is not None:
+            self._join()
         self._mark_input_read()
 
     def repack_weights(self):
