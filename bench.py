@@ -268,7 +268,23 @@ def main():
     pinned = mx.io.DataBatch(data=[mx.nd.array(data, ctx=mx.Context("cpu_pinned", 0))],
                              label=[mx.nd.array(label, ctx=mx.Context("cpu_pinned", 0))])
 
+    # the data-gradient chain on a high-priority stream when the weight gradients run beside it
+    # (RN_MAIN_PRIORITY=0: the default stream): the hardware then prefers the chain's workgroups
+    # and the side stream fills what is left
+    main_stream = None
+    if getattr(ex, "_side_stream", None) is not None and os.environ.get("RN_MAIN_PRIORITY", "1") == "1":
+        lo, hi = torch.cuda.Stream.priority_range()
+        main_stream = torch.cuda.Stream(priority=min(lo, hi))
+        torch.cuda.synchronize()
+
     def step():
+        if main_stream is not None:
+            with torch.cuda.stream(main_stream):
+                mod.forward(pinned if a.host_input else None, is_train=True)
+                mod.backward()
+                mod.update()
+            torch.cuda.current_stream().wait_stream(main_stream)
+            return
         mod.forward(pinned if a.host_input else None, is_train=True)
         mod.backward()
         mod.update()
