@@ -236,9 +236,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # (RN_DIST_BACKEND=gloo with more ranks than GPUs: a rehearsal of the N > 1 path on a one-GPU box)
+    torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
     if world > 1:
-        rdist.init_from_env("nccl")
+        rdist.init_from_env(os.environ.get("RN_DIST_BACKEND", "nccl"))
     import torch.distributed as dist
 
     sym = {"resnet50": graphs.resnet50, "resnext50": graphs.resnext50_32x4d,
@@ -246,7 +247,7 @@ def main():
     model_name = {"resnet50": "resnet50_v2", "resnext50": "resnext50_32x4d", "resnet50_int8": "resnet50_v2_int8"}[a.model]
     workload = {"resnet50": "ResNet-50 v2 (symbol/resnet.py)", "resnext50": "ResNeXt-50 32x4d (symbol/resnext.py)",
                 "resnet50_int8": "ResNet-50 v2 int8 QAT (symbol/resnet_int8.py)"}[a.model]
-    mod = mx.mod.Module(sym, context=[mx.gpu(local)], precision=a.precision)
+    mod = mx.mod.Module(sym, context=[mx.gpu(local % max(1, torch.cuda.device_count()))], precision=a.precision)
     shp = (a.batch, 3, a.image, a.image)
     mod.bind(data_shapes=[("data", shp)], label_shapes=[("softmax_label", (a.batch,))], for_training=True)
     mx.random.seed(2)
