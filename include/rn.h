@@ -388,7 +388,10 @@ const char* rn_last_error(void);
  * 6 = diagnostic only: wgrad skips its dW epilogue (wrong results; isolates the atomic adds),
  * 7 = igemm 256-row tile schedule experiments (bit mask; 0 = default),
  * 8 = igemm 256-row tile MFMA shape (0 = 32x32x16, 1 = 16x16x32),
- * 9 = igemm 224-row tiles for the 256/128-column tiles (0 = on, 1 = 256 rows). */
+ * 9 = igemm 224-row tiles for the 256/128-column tiles (0 = on, 1 = 256 rows),
+ * 10 = igemm 256-row-family persistent grid: workgroups (a multiple of 8) that walk the tiles of a
+ *      larger grid, so one tile's output stores drain while the next tile loads (default 512; 0 = one
+ *      tile per workgroup). */
 int rn_set_tuning(int32_t key, int32_t value);
 int32_t rn_version(void);
 /* Number of compute units of the current device (for split heuristics / reporting). */

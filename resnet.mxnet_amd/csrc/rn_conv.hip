@@ -56,6 +56,7 @@ struct IgemmArgs {
   int smallc, lgc, rs; // fwd over C < one stage (the stem's 8 channels): k = tap*C + c flattened
   int diag_l1;         // diagnostic (rn_set_tuning 3): every A row reads the same L1-resident chunk
   int sched;           // igemm_big_kernel schedule experiments (rn_set_tuning 7, bit mask)
+  int ntiles;          // igemm_big_kernel persistent mode: tiles per class (0: one tile per workgroup)
   int x_bytes, w_bytes;  // LDS-DMA buffer descriptors
   // dgrad only, nullable: the BatchNorm-backward reduction of the gradient this conv completes
   // (sum dz, sum dz*(x - mean), dz = dy * relu'(bn(x))) per output block -> bnred[blk][ldo][2]
@@ -704,7 +705,12 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   const int wm = wid / WAVES_N, wn = wid % WAVES_N;
   const IgemmCls& cl = p.cls[blockIdx.z];
   const int Mc = p.N * cl.Pc * cl.Qc;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  // persistent mode (p.ntiles > 0, rn_set_tuning 10): each workgroup walks the tiles v = blockIdx.x +
+  // k * gridDim.x (gridDim.x a multiple of 8: v stays on this XCD's contiguous tile range), so one
+  // tile's output stores drain while the next tile's first K-tiles load
+  const int total = p.ntiles > 0 ? p.ntiles : (int)gridDim.x;
+  for (int v = blockIdx.x; v < total; v += gridDim.x) {
+  const int lid = xcd_remap(v, total);
   const int mtile = lid / p.ntn;
   const int m0 = mtile * BM;
   const int n0 = (lid - mtile * p.ntn) * BN;
@@ -718,7 +724,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
           dst[1] = 0.f;
         }
       }
-    return;
+    continue;
   }
 
   // grouped conv (ResNeXt, 64-column tile = one RN_GROUP_BLOCK): the block's columns touch groups
@@ -905,7 +911,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
 #pragma unroll
       for (int j = 0; j < NI; ++j) t += acc[i][j][0];
     if (lane == 0) reinterpret_cast<float*>(p.y)[blockIdx.x] = t;
-    return;
+    continue;
   }
 
   // ---- epilogue: per wave, 64 accumulator rows at a time through LDS, then 16-byte row chunks
@@ -1075,6 +1081,8 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
         }
       }
     }
+  }
+  __syncthreads();  // (persistent) the epilogue's LDS reads end before the next tile's DMAs
   }
 }
 
@@ -1979,10 +1987,20 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
     const int bn = big_tile_cols(a, xb, wb);
     RN_CHECK_ARG(!a.bnacc || bn >= 128, "accumulated BatchNorm sums need the 256-row tile (rn_conv_tile >= 128)");
     const bool m32 = g_tune[RN_TUNE_IGEMM_MFMA] != 1;
+    // persistent tiles (rn_set_tuning 10 = workgroups, a multiple of 8): only where the grid is larger
+    b.ntiles = 0;
+    auto persist = [&](dim3& grid) {
+      const int g = g_tune[RN_TUNE_IGEMM_PERSIST] / 8 * 8;
+      if (g > 0 && (int)grid.x > g) {
+        b.ntiles = (int)grid.x;
+        grid.x = (unsigned)g;
+      }
+    };
     if (bn == 64 && !a.bnacc && (epi == 0 || !a.smallc)) {
       b.ntn = (int)ceil_div(a.K, 64);
       if (a.bnred) b.mt_max = (int)ceil_div(maxMc, 64);  // BN partials per 64-row wave row
       dim3 grid((unsigned)(ceil_div(maxMc, 256) * b.ntn), 1, a.ncls);
+      persist(grid);
       if (a.smallc) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, 1>), grid, dim3(256), 0, st, b);
       else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 1, true>), grid, dim3(256), 0, st, b);
       else if (epi == 2) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 2, true>), grid, dim3(256), 0, st, b);
@@ -1996,6 +2014,7 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
       if (a.bnred) b.mt_max = (int)ceil_div(maxMc, bm / 2);
       b.ntn = (int)ceil_div(a.K, bn);
       dim3 grid((unsigned)(ceil_div(maxMc, bm) * b.ntn), 1, a.ncls);
+      persist(grid);
 #define RN_BIG(BNV, NB, M, R)                                                                                 \
   if (epi == 0) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 0, M, R>), grid, dim3(512), 0, st, b);        \
   else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 1, M, R>), grid, dim3(512), 0, st, b);   \

@@ -487,15 +487,19 @@ def test_stem_quant(gpu):
     assert rel_err(dbeta.cpu().numpy(), dbeta_ref) < 1e-4
 
 
-@pytest.fixture(params=[(0, 0), (1, 0), (1, 1)], ids=["rows224", "rows256_mfma32", "rows256_mfma16"])
+@pytest.fixture(params=[(0, 0, 512), (0, 0, 8), (1, 0, 0), (1, 1, 512)],
+                ids=["rows224", "rows224_persist8", "rows256_mfma32", "rows256_mfma16"])
 def tile_variant(request):
-    """igemm 256-row-family variants: rn_set_tuning 9 (224-row tiles on/off) x 8 (MFMA shape)."""
-    rows, mfma = request.param
+    """igemm 256-row-family variants: rn_set_tuning 9 (224-row tiles on/off) x 8 (MFMA shape) x 10
+    (persistent grid: 8 workgroups walk every tile of these small grids; 0 = one tile each)."""
+    rows, mfma, persist = request.param
     L.call("rn_set_tuning", 9, rows)
     L.call("rn_set_tuning", 8, mfma)
+    L.call("rn_set_tuning", 10, persist)
     yield request.param
     L.call("rn_set_tuning", 9, 0)
     L.call("rn_set_tuning", 8, 0)
+    L.call("rn_set_tuning", 10, 512)
 
 
 @pytest.fixture(params=[0, 2], ids=["auto", "big256"])
