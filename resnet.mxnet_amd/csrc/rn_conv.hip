@@ -910,7 +910,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j) t += acc[i][j][0];
-    if (lane == 0) reinterpret_cast<float*>(p.y)[blockIdx.x] = t;
+    if (lane == 0) reinterpret_cast<float*>(p.y)[v] = t;  // one slot per tile (persistent mode walks several)
     continue;
   }
 

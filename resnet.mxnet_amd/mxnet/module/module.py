@@ -7,9 +7,13 @@ forward / backward / update -> librn kernels; gradients all-reduced over RCCL in
 backward runs (one process per GPU), then the fused SGD kernel on every rank.
 
 Multi-device contexts: MXNet splits the batch evenly over `context` (core/solver.py:58-61,
-train.py:34). Here each device is its own process; when the torchrun world size equals
-len(context), rank r computes slice r of every batch (per-slice BN statistics, summed
-gradients -- the same semantics), so train.py's gpu_list runs unchanged under torchrun.
+train.py:34). Here each device is its own process:
+  * under torchrun with world size == len(context), rank r computes slice r of every batch
+    (per-slice BN statistics, summed gradients -- the same semantics);
+  * one process given several contexts (the reference's own `python train.py`, script/train.sh:3)
+    gets a MultiDeviceModule (module/multidev.py) that spawns one worker per device at bind and runs
+    that same slice path in them, the optimizer, metrics and schedule staying in the caller.
+RN_DRY_RUN=1 binds the call plan on the CPU without launching anything (host-plumbing tests).
 """
 import logging
 import os
@@ -41,12 +45,35 @@ def _dist():
     return None
 
 
+_MultiDeviceModule = None
+
+
 class BatchEndParam:
     def __init__(self, epoch, nbatch, eval_metric, locals=None):
         self.epoch, self.nbatch, self.eval_metric, self.locals = epoch, nbatch, eval_metric, locals
 
 
+def _torchrun_world():
+    """World size of an enclosing torchrun / torch.distributed launch (1 outside one)."""
+    d = _dist()
+    if d is not None:
+        return d.get_world_size()
+    return int(os.environ.get("WORLD_SIZE", "1"))
+
+
 class Module:
+    def __new__(cls, symbol=None, data_names=("data",), label_names=("softmax_label",), logger=logging, context=None,
+                *args, **kwargs):
+        # several contexts in one process outside a torchrun launch: the reference's own
+        # `python train.py` with gpu_list (train.py:34, core/solver.py:58-61) -> one worker per device
+        if cls is Module and context is not None and len(_as_list(context)) > 1 and _torchrun_world() == 1:
+            from .multidev import make_module_class
+            global _MultiDeviceModule
+            if _MultiDeviceModule is None:
+                _MultiDeviceModule = make_module_class(Module)
+            return super().__new__(_MultiDeviceModule)
+        return super().__new__(cls)
+
     def __init__(self, symbol, data_names=("data",), label_names=("softmax_label",), logger=logging, context=None,
                  work_load_list=None, fixed_param_names=None, state_names=None, group2ctxs=None,
                  compression_params=None, precision=None):
@@ -123,13 +150,13 @@ class Module:
         if len(ctxs) > 1 and world == len(ctxs):
             self._slice = (local_rank, len(ctxs))
             ctx = ctxs[local_rank]
+        elif len(ctxs) > 1:
+            # (one process with several contexts outside torchrun is the MultiDeviceModule)
+            raise MXNetError("Module: %d contexts under a distributed launch of %d processes; MXNet's per-device "
+                             "split needs one process per context (world size == len(context))" % (len(ctxs), world))
         else:
-            if len(ctxs) > 1:
-                self.logger.warning("Module: %d contexts in one process; running the whole batch on %s "
-                                    "(launch one process per GPU with torchrun for MXNet's per-device split)",
-                                    len(ctxs), ctxs[0])
             self._slice = None
-            ctx = ctxs[local_rank % len(ctxs)] if world > 1 and len(ctxs) > 1 else ctxs[0]
+            ctx = ctxs[0]
         self._ctx = ctx
         self._total_batch = dshapes[0][1][0]
         nsl = self._slice[1] if self._slice else 1
@@ -138,10 +165,14 @@ class Module:
         per = lambda shp: (shp[0] // nsl,) + tuple(shp[1:])
         pd = [(n, per(s)) for n, s in dshapes]
         pl = [(n, per(s)) for n, s in lshapes]
-        import torch
-        torch.cuda.set_device(ctx.device_id)
+        from .multidev import dry_run
         plan = Plan(self._symbol, pd, pl, dtype=self.precision, for_training=for_training)
-        self._exec = Executor(plan, ctx.torch_device())
+        if dry_run():  # RN_DRY_RUN=1: the call plan on the CPU, nothing launched (host-plumbing tests)
+            self._exec = Executor(plan, "cpu")
+        else:
+            import torch
+            torch.cuda.set_device(ctx.device_id)
+            self._exec = Executor(plan, ctx.torch_device())
         self.binded = True
 
     # ------------------------------------------------------------------ params
@@ -243,9 +274,12 @@ class Module:
         self._kv = kv
         params = dict(optimizer_params)
         batch = self._total_batch
-        if kv is not None and kv.type.startswith("dist") and "_sync" in kv.type or \
-                (kv is not None and kv.type in ("dist_sync_device",)):
-            batch *= kv.num_workers
+        if kv is not None and kv.type.startswith("dist") and "_sync" in kv.type:
+            # MXNet: rescale = 1 / (batch x MXNet workers). In slice mode the bound batch is already the
+            # global one (each rank runs one device's slice of it, as MXNet's one worker drives all of
+            # len(context) devices), so only the processes beyond one per context count as workers.
+            workers = kv.num_workers // len(self._context) if self._slice is not None else kv.num_workers
+            batch *= max(1, workers)
         params.setdefault("rescale_grad", 1.0 / batch)
         idx2name = {i: n for i, n in enumerate(self._exec.plan.param_names)}
         self._optimizer = opt.create(optimizer, param_idx2name=idx2name, **params)
@@ -293,17 +327,26 @@ class Module:
             raise MXNetError("head gradients are not supported (SoftmaxOutput is a loss head)")
         ex = self._exec
         ex.backward(hooks=self._reducer.hooks() if self._reducer else None)
+        if self._reducer is not None:
+            self._reducer.launched_step = True  # every bucket was launched by its backward hook
 
     def update(self):
-        ex = self._exec
-        if self._reducer is not None:
-            if not self._reducer.works:
-                self._reducer.launch_all()
-            self._reducer.wait()
         o = self._optimizer
         lr = o.step_lr()
         clip = o.clip_gradient if o.clip_gradient is not None else -1.0
-        ex.sgd_update(lr, o.wd, getattr(o, "momentum", 0.0), o.rescale_grad, clip)
+        self._update_with(lr, o.wd, getattr(o, "momentum", 0.0), o.rescale_grad, clip)
+
+    def _update_with(self, lr, wd, momentum, rescale_grad, clip):
+        """kvstore push(sum) + SGD + pull: the summed gradient, then the fused update on this device."""
+        ex = self._exec
+        if self._reducer is not None:
+            # exactly one all-reduce per backward: launched by the hooks (or here, when backward ran
+            # without them), waited for here even if the caller already waited
+            if not self._reducer.launched_step:
+                self._reducer.launch_all()
+            self._reducer.wait()
+            self._reducer.launched_step = False
+        ex.sgd_update(lr, wd, momentum, rescale_grad, clip)
 
     def get_outputs(self, merge_multi_context=True):
         return [nd.NDArray(self._exec.output(i), self._ctx) for i in range(len(self._exec.plan.outputs))]

@@ -35,6 +35,7 @@ class BucketAllReducer:
         self.buckets = list(buckets)  # [(start, end, launch_after_call_index)]
         self.group = group
         self.works = []
+        self.launched_step = False  # set by Module.backward once the hooks launched every bucket
 
     def hooks(self):
         h = {}

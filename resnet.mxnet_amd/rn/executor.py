@@ -515,7 +515,9 @@ class _GradState:
 class Executor:
     """Device buffers + bound C calls for one Plan on one GPU."""
 
-    def __init__(self, plan, device, bucket_bytes=25 << 20):
+    def __init__(self, plan, device, bucket_bytes=None):
+        if bucket_bytes is None:  # RCCL all-reduce bucket size (RN_BUCKET_MB, default 25 MB)
+            bucket_bytes = int(float(os.environ.get("RN_BUCKET_MB", "25")) * (1 << 20))
         import torch
         self.torch = torch
         self.plan = plan
@@ -538,6 +540,7 @@ class Executor:
         if not self.dry_run and os.environ.get("RN_WGRAD_STREAM", "1") == "1":
             self._side_stream = torch.cuda.Stream(device=self.device)
         self._side_idx = set()
+        self._events = {}
         self.side_enabled = True  # False: the side-stream calls run on the compute stream (serialised timing)
         self._sync_stream()
         self._acts = {}
@@ -707,22 +710,37 @@ class Executor:
     WGRAD_CALLS = ("rn_conv_bwd_filter", "rn_conv_bwd_filter_ws", "rn_conv_bwd_filter_x", "rn_stem_conv_wgrad_p4")
 
     def _route_wgrads(self):
-        """Bind the weight-gradient calls of the backward plan to the side stream."""
+        """Bind the weight-gradient calls of the backward plan to the side stream.
+
+        Invariant: the shared split-M slab workspace (self.wgrad_ws) is used by these calls only, so
+        with the side stream on it is touched by that one stream, in plan order."""
         if self._side_stream is None:
             return
+        ws = self.wgrad_ws.data_ptr() if self.wgrad_ws is not None else None
         for i, (name, fn, args) in enumerate(self._bwd):
             if name in self.WGRAD_CALLS and args and args[-1] is self._spv:
                 self._bwd[i] = (name, fn, args[:-1] + (self._spv2,))
                 self._side_idx.add(i)
+            elif ws is not None and any(isinstance(a, L.C.c_void_p) and a.value == ws for a in args):
+                raise PlanError("%s uses the weight-gradient slab workspace but is not routed to the side "
+                                "stream" % name)
 
-    def _fork(self):
+    def _event(self, key):
+        """One persistent HIP event per fork / join point of the backward plan (re-recorded every
+        step): no event is created or destroyed while a stream may still wait on it."""
+        ev = self._events.get(key)
+        if ev is None:
+            ev = self._events[key] = self.torch.cuda.Event()
+        return ev
+
+    def _fork(self, key):
         """The side stream continues after everything enqueued on the compute stream so far."""
-        ev = self.torch.cuda.Event()
+        ev = self._event(("fork", key))
         ev.record(self.torch.cuda.current_stream(self.device))
         self._side_stream.wait_event(ev)
 
     def _join(self):
-        ev = self.torch.cuda.Event()
+        ev = self._event(("join",))
         ev.record(self._side_stream)
         self.torch.cuda.current_stream(self.device).wait_event(ev)
 
@@ -1027,7 +1045,9 @@ class Executor:
         bwd_fusion = os.environ.get("RN_BN_BWD_FUSION", "1") in ("1", "2")
         bwd_all = os.environ.get("RN_BN_BWD_FUSION", "1") == "2"
         # one workspace for the weight gradients' split-M partial tiles (rn_conv_bwd_filter_ws),
-        # sized for the largest layer; the backward runs the layers one after another on one stream
+        # sized for the largest layer. Shared safely because every call using it is a weight-gradient
+        # call, and those all run in plan order on ONE stream (the side stream when it is on:
+        # _route_wgrads enforces this)
         self.wgrad_ws, self.wgrad_ws_bytes = None, 0
         if os.environ.get("RN_WGRAD_SLAB", "1") == "1":
             need = [int(self.lib.rn_conv_wgrad_ws_bytes(L.C.byref(op.desc))) for op in plan.ops
@@ -1183,6 +1203,8 @@ class Executor:
 
     # ------------------------------------------------------------------ running
     def _run(self, calls):
+        if self.dry_run:  # the plan only (CPU tests): nothing is launched
+            return
         for name, fn, args in calls:
             r = fn(*args)
             if r != 0:
@@ -1252,14 +1274,14 @@ class Executor:
         hooks = hooks or {}
         for i, (name, fn, args) in enumerate(self._bwd):
             if side is not None and i in self._side_idx:
-                self._fork()
-            r = fn(*args)
+                self._fork(i)
+            r = 0 if self.dry_run else fn(*args)
             if r != 0:
                 raise L.RNError("%s: %s" % (name, self.lib.rn_last_error().decode()))
             h = hooks.get(i + 1)
             if h is not None:
                 if side is not None:
-                    self._fork()
+                    self._fork(("hook", i))
                     with self.torch.cuda.stream(side):
                         h()
                 else:
@@ -1274,6 +1296,8 @@ class Executor:
 
     def sgd_update(self, lr, wd, momentum, rescale_grad, clip=-1.0):
         self._sync_stream()
+        if self.dry_run:
+            return
         if self._wd_value != wd:
             self.opt_wds.copy_(self.torch.from_numpy(self.wd_mult * np.float32(wd)))
             self._wd_value = wd
