@@ -17,5 +17,5 @@ vectors or fixtures for this path. Every MXNet-interna
 restated here is taken from the public MXNet 1.x code base and listed in oracle/ops.py, and
 the restatement is cross-checked against an independent torch-CPU fp64 implementation in
 tests/test_oracle.py. The committed fixtures under tests/golden/ pin THIS oracle from now on
-(made by oracle/gen_golden.py).
+(made by tests/golden/make_golden.py).
 """

@@ -106,6 +106,8 @@ class _Worker:
         self.mod.set_params(arg, aux)
 
     def grads(self):
+        if self.mod._reducer is not None:  # the summed gradient (update() waits again: no-op)
+            self.mod._reducer.wait()
         ex = self.mod.executor
         return {n: ex.get_param(n, grad=True) for n in ex.plan.param_names}
 
