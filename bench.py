@@ -11,8 +11,11 @@ Rank 0 prints ONE JSON line (contract in the task statement), including
                  / average launch duration from HIP events around every launch of that family
                  (eager mode: inside the timed region; HIP-graph mode: in one eager step right
                  after it, graph nodes carry no timing events), vs the dense bf16 MFMA peak
-  cpu_baseline : the numpy oracle (oracle/, "port") timing a bounded sample of the same step
-                 on the host cores (rank 0, N=1 only)
+  roofline     : "bound" from the family's algorithmic FLOP/byte vs the 312.5 FLOP/B ridge (2.5 PF
+                 bf16 / 8 TB/s); both the MFMA and the HBM fraction are reported
+  pcie_inclusive: the same step fed the iterator's pinned host batch every step (not `value`)
+  cpu_baseline : torch-CPU fp32 (oneDNN) restatement of the same step (oracle/torch_cpu.py,
+                 "port") on every host core, batch 32 (rank 0, N=1 only)
 """
 import argparse
 import ctypes as C
@@ -28,6 +31,8 @@ for _p in (REPO, os.path.join(REPO, "resnet.mxnet_amd")):
 
 METRIC = "images/sec/GPU ResNet-50 224px bf16 bs256; 1→8 GPU scaling"
 PEAK_BF16_TFLOPS = 2500.0
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: 8 TB/s spec (6.3 TB/s achievable)
+RIDGE = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)  # 312.5 FLOP/B: below it a kernel is HBM-bound
 
 
 def conv_call_flops(name, args):
@@ -166,42 +171,29 @@ def calibrate_families(torch, ex, mod):
     return out
 
 
-def cpu_baseline(batch=8, steps=2, image=224):
-    """Time the numpy oracle (fp32) on a bounded sample of the same training step."""
-    import numpy as np
+def cpu_baseline(batch=32, steps=2, image=224):
+    """SURVEY.md 8d / BASELINE.md 3: the reference's MXNet CPU executor cannot run here, so its
+    closest analogue -- torch-CPU fp32 functional ops (oneDNN, MXNet's MKL-DNN counterpart) on every
+    host core -- runs the identical ResNet-50 v2 graph and Solver step (oracle/torch_cpu.py) on a
+    bounded sample: batch 32 at 224x224, 1 warm-up + `steps` timed steps."""
     from oracle import net as onet
-    g = onet.resnet50_imagenet()
-    args, aux = onet.init_params(g, dtype=np.float32)
-    moms = {k: np.zeros_like(v) for k, v in args.items()}
-    data, label = onet.synthetic_batch(batch, (3, image, image), 1000, dtype=np.float32)
-    onet.train_step(g, args, aux, moms, data, label, 0.1)  # warm-up (allocations, BLAS threads)
-    t0 = time.time()
-    for _ in range(steps):
-        onet.train_step(g, args, aux, moms, data, label, 0.1)
-    dt = time.time() - t0
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    return {"value": round(batch * steps / dt, 3), "unit": "images/sec", "cores": cores, "kind": "port",
-            "sample": "numpy fp32 oracle ResNet-50 v2 train step (fwd+bwd+SGD), batch %d at %dx%d, %d timed steps "
-                      "after 1 warm-up (%.1f s)" % (batch, image, image, steps, dt)}
+    from oracle import torch_cpu
+    ips, dt, cores, _ = torch_cpu.time_step(onet.resnet50_imagenet(), batch, image, 1000, steps)
+    return {"value": round(ips, 3), "unit": "images/sec", "cores": cores, "kind": "port",
+            "cpu_model": torch_cpu.cpu_model(),
+            "sample": "torch-CPU fp32 (oneDNN) ResNet-50 v2 train step (fwd + bwd + MXNet SGD), batch %d at %dx%d, "
+                      "%d timed steps after 1 warm-up (%.1f s), %d threads" % (batch, image, image, steps, dt, cores)}
 
 
-def cpu_baseline_c1(batch=128, steps=3):
+def cpu_baseline_c1(batch=128, steps=20):
     """BASELINE.json configs[0]: ResNet-20 CIFAR-10 32x32, batch 128 -- the reference's own CPU case --
-    as the numpy fp32 oracle step on the host cores."""
-    import numpy as np
+    as the same torch-CPU fp32 step on every host core (3 warm-up + `steps` timed)."""
     from oracle import net as onet
-    g = onet.resnet20_cifar()
-    args, aux = onet.init_params(g, dtype=np.float32)
-    moms = {k: np.zeros_like(v) for k, v in args.items()}
-    data, label = onet.synthetic_batch(batch, (3, 32, 32), 10, dtype=np.float32)
-    onet.train_step(g, args, aux, moms, data, label, 0.1)
-    t0 = time.time()
-    for _ in range(steps):
-        onet.train_step(g, args, aux, moms, data, label, 0.1)
-    dt = time.time() - t0
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
-    return {"value": round(batch * steps / dt, 3), "unit": "images/sec", "cores": cores, "kind": "port",
-            "sample": "numpy fp32 oracle ResNet-20 CIFAR-10 train step, batch %d at 32x32, %d timed steps (%.1f s)"
+    from oracle import torch_cpu
+    ips, dt, cores, _ = torch_cpu.time_step(onet.resnet20_cifar(), batch, 32, 10, steps, warmup=3)
+    return {"value": round(ips, 3), "unit": "images/sec", "cores": cores, "kind": "port",
+            "cpu_model": torch_cpu.cpu_model(),
+            "sample": "torch-CPU fp32 ResNet-20 CIFAR-10 train step, batch %d at 32x32, %d timed steps (%.1f s)"
                       % (batch, steps, dt)}
 
 
@@ -218,8 +210,10 @@ def main():
                          "(32x4d, grouped convs), resnet50_int8 = C5 (symbol/resnet_int8.py QAT graph)")
     ap.add_argument("--bucket-mb", type=float, default=25.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=8)
+    ap.add_argument("--cpu-batch", type=int, default=32)
     ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--pcie-steps", type=int, default=None,
+                    help="steps of the PCIe-inclusive leg (default: steps / 2; 0 skips it)")
     ap.add_argument("--host-input", action="store_true",
                     help="feed the pinned host batch through Module.forward every step (PCIe-inclusive "
                          "rate, the solver's own loop; not the headline value)")
@@ -278,15 +272,15 @@ def main():
         main_stream = torch.cuda.Stream(priority=min(lo, hi))
         torch.cuda.synchronize()
 
-    def step():
+    def step(feed=pinned if a.host_input else None):
         if main_stream is not None:
             with torch.cuda.stream(main_stream):
-                mod.forward(pinned if a.host_input else None, is_train=True)
+                mod.forward(feed, is_train=True)
                 mod.backward()
                 mod.update()
             torch.cuda.current_stream().wait_stream(main_stream)
             return
-        mod.forward(pinned if a.host_input else None, is_train=True)
+        mod.forward(feed, is_train=True)
         mod.backward()
         mod.update()
 
@@ -339,6 +333,29 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     fam_ms, fam_n = timer.result()
+    # PCIe-inclusive rate (never `value`): the solver's own loop feeds the iterator's pinned host
+    # batch every step (core/solver.py:115, data/imagenet.py:17-18) -- copied H2D on the copy
+    # stream, double-buffered, overlapping the previous step
+    pcie = None
+    psteps = a.steps // 2 if a.pcie_steps is None else a.pcie_steps
+    if psteps > 0 and not a.host_input:
+        for _ in range(2):
+            step(pinned)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(psteps):
+            step(pinned)
+        torch.cuda.synchronize()
+        pel = time.perf_counter() - t1
+        if world > 1:
+            t = torch.tensor([pel], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            pel = float(t.item())
+        pcie = {"value": round(a.batch * world * psteps / pel, 2), "unit": "images/sec", "steps": psteps,
+                "ms_per_step": round(pel / psteps * 1e3, 3),
+                "inputs": "pinned host NCHW fp32 batch copied H2D every step (eager launches)"}
     prob = mod.get_outputs()[0].asnumpy()
     finite = bool(np.isfinite(prob).all())
 
@@ -349,9 +366,17 @@ def main():
         flops_step = ex.plan.train_flops()
         per_launch_flops = timer.flops / max(1, len(timer.idx))
         avg_ms = fam_ms / max(fam_n, 1)
-        achieved = per_launch_flops / (avg_ms * 1e-3) / 1e12
         traffic, traffic_src = pmc_traffic(dom)
         alg_bytes = timer.bytes / max(1, len(timer.idx))
+        # which roofline binds this family: its algorithmic FLOP per algorithmic byte vs the ridge
+        intensity = per_launch_flops / max(alg_bytes, 1.0)
+        bound = "mfma" if intensity >= RIDGE else "hbm"
+        tflops = per_launch_flops / (avg_ms * 1e-3) / 1e12
+        gbs = alg_bytes / (avg_ms * 1e-3) / 1e9
+        achieved, peak, unit = (tflops, PEAK_BF16_TFLOPS, "TFLOP/s") if bound == "mfma" else \
+            (gbs, PEAK_HBM_GBS, "GB/s")
+        solo_tf = per_launch_flops / (solo_ms * 1e-3) / 1e12
+        solo_gbs = alg_bytes / (solo_ms * 1e-3) / 1e9
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "images/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
@@ -361,18 +386,22 @@ def main():
             "config": {"workload": "%s train step, batch %d/GPU, %dx%d" % (
                 workload, a.batch, a.image, a.image), "model": model_name, "global_batch": a.batch * world,
                 "seq_len": None, "parallelism": "dp%d" % world, "per_gpu_images_per_sec": round(value / world, 2)},
-            "roofline": {"bound": "mfma", "kernel": dom, "launches_per_step": len(timer.idx),
-                         "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / PEAK_BF16_TFLOPS, 4),
+            "roofline": {"bound": bound, "kernel": dom, "launches_per_step": len(timer.idx),
+                         "achieved": round(achieved, 2), "peak": peak, "unit": unit,
+                         "frac": round(achieved / peak, 4),
                          "traffic": round(traffic) if traffic else None, "traffic_unit": "HBM bytes/launch",
                          "traffic_source": traffic_src, "algorithmic_bytes": round(alg_bytes),
                          "flops_per_launch": round(per_launch_flops),
+                         "intensity_flop_per_byte": round(intensity, 1), "ridge_flop_per_byte": round(RIDGE, 1),
+                         # both rooflines of the family, whichever binds
+                         "mfma_achieved_tflops": round(tflops, 2), "mfma_frac": round(tflops / PEAK_BF16_TFLOPS, 4),
+                         "hbm_achieved_gbs": round(gbs, 1), "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
                          "avg_launch_ms": round(avg_ms, 4),
                          # the same launches in the serialised calibration step (no weight gradient
                          # sharing the CUs): the kernel's own rate
                          "solo_avg_launch_ms": round(solo_ms, 4),
-                         "solo_achieved": round(per_launch_flops / (solo_ms * 1e-3) / 1e12, 2),
-                         "solo_frac": round(per_launch_flops / (solo_ms * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+                         "solo_mfma_frac": round(solo_tf / PEAK_BF16_TFLOPS, 4),
+                         "solo_hbm_frac": round(solo_gbs / PEAK_HBM_GBS, 4),
                          "concurrent_streams": 2 if (ex._side_idx and ex.side_enabled) else 1,
                          "step_tflops": round(flops_step / (ms_step * 1e-3) / 1e12, 2),
                          "step_frac": round(flops_step / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
@@ -381,6 +410,7 @@ def main():
             "hip_graph": bool(use_graph),
             "inputs": "pinned host batch copied every step (PCIe-inclusive)" if a.host_input else
                       "resident in HBM",
+            "pcie_inclusive": pcie,
         }
         if world == 1 and not a.no_cpu_baseline and a.model == "resnet50":
             try:

@@ -16,6 +16,15 @@ CONV_CALLS = ("rn_conv_fwd", "rn_conv_fwd_bnstats", "rn_conv_fwd_x", "rn_conv_fw
               "rn_stem_conv_fwd_p4", "rn_stem_conv_wgrad_p4")
 
 
+def kernel_short(name):
+    """'void (anonymous namespace)::igemm_big_kernel<256, 2, 1, false, 224, 0>(IgemmArgs)' ->
+    'igemm_big_kernel<256, 2, 1, false, 224, 0>'."""
+    name = name.replace("(anonymous namespace)::", "")
+    if name.startswith("void "):
+        name = name[5:]
+    return name.split("(")[0].replace("unsigned short", "bf16")[:48]
+
+
 def main():
     trace = sys.argv[1]
     batch = int(sys.argv[2]) if len(sys.argv) > 2 else 256
@@ -27,7 +36,9 @@ def main():
             if hasattr(op, attr):
                 names[id(getattr(op, attr))] = op.name
     calls = [(n, a) for n, f, a in ex._fwd_train + ex._bwd if n in CONV_CALLS]
-    rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"]))
+    # host submission order (Dispatch_Id) = the plan's call order on both streams; start times are
+    # not, once the weight gradients run on the side stream beside the data-gradient chain
+    rows = sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Dispatch_Id"]))
     step_end = [i for i, r in enumerate(rows) if "sgd_mom" in r["Kernel_Name"]]
     rows = rows[step_end[-2] + 1:step_end[-1]]
     conv_rows = []
@@ -48,7 +59,7 @@ def main():
         algb = xb + yb + (2 * wb if kind == "wgrad" else wb)
         us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         roof = max(flops / 2.5e15, algb / 8e12) * 1e6
-        out.append((us, names.get(id(d), "?"), kind, flops / us / 1e6, roof / us, r["Kernel_Name"].split("(")[0][-40:]))
+        out.append((us, names.get(id(d), "?"), kind, flops / us / 1e6, roof / us, kernel_short(r["Kernel_Name"])))
         tot[kind] = tot.get(kind, 0) + us
     for us, lname, kind, tf, fr, kn in sorted(out, reverse=True):
         print("%8.1f us  %-22s %-5s %7.1f TF %4.0f%%  %s" % (us, lname, kind, tf, 100 * fr, kn))
