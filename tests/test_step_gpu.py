@@ -157,6 +157,36 @@ def test_resnet_int8_fp32_small(gpu):
         assert abs(v.item() - ref["quant_state"][k]) <= 1e-6 * ref["quant_state"][k], k
 
 
+def test_resnet_int8_fp32_full_units(gpu):
+    """resnet_int8 with the full ResNet-50 [3,4,6,3] units (the C5 graph at 64x64, batch 4): the
+    same replayed parity as the one-unit case above, 53 quantized convs + fc1."""
+    from rn import graphs
+    cfg = ([3, 4, 6, 3], 4, [64, 256, 512, 1024, 2048], 16)
+    g = onet.resnet_int8(*cfg)
+    args, aux = oracle_state(g)
+    data, label = onet.synthetic_batch(4, (3, 64, 64), 16)
+    res = module_step(graphs.resnet_int8(*cfg), args, aux, data, label, "float32")
+    qv = res["quant_values"][0]
+    assert len(qv) == 2 * 54
+    errs, ref = replayed_parity(res, g, args, aux, data, label, quant_values=qv)
+    assert max_rel(res["prob"][0], ref["prob"][0]) < 1e-4
+    _assert_replayed(errs)
+
+
+def test_resnext50_fp32_full_units(gpu):
+    """ResNeXt-50 32x4d with its full [3,4,6,3] units (the C4 graph at 64x64, batch 4), ReLU
+    decisions replayed: probabilities 1e-4, every gradient max(1e-4, 4x numpy-fp32 error)."""
+    from rn import graphs
+    cfg = ([3, 4, 6, 3], 4, [64, 256, 512, 1024, 2048], 16)
+    g = onet.resnext(*cfg, num_group=32)
+    args, aux = oracle_state(g)
+    data, label = onet.synthetic_batch(4, (3, 64, 64), 16)
+    res = module_step(graphs.resnext(*cfg, "float32", 32), args, aux, data, label, "float32")
+    errs, ref = replayed_parity(res, g, args, aux, data, label)
+    assert max_rel(res["prob"][0], ref["prob"][0]) < 1e-4
+    _assert_replayed(errs)
+
+
 def test_resnet_int8_bf16_loss_trajectory(gpu):
     from rn import graphs
     cfg = ([1, 1, 1, 1], 4, [64, 256, 512, 1024, 2048], 16)
