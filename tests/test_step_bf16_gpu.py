@@ -11,10 +11,11 @@ several tiles per workgroup.
 Reference: the numpy oracle in fp64 (symbol/resnet.py:77-121 restated) and its bf16-storage
 emulation (oracle.net.forward storage='bf16': weights and every stored activation rounded to
 bf16, fp64 arithmetic). A deep random-init ResNet at small spatial size is chaotic under rounding
-(DESIGN.md 4), so the device is judged against the noise bf16 storage itself creates: over all 157
-gradient tensors (step_util.grad_summary) the device's distance to fp64 must stay within a small
-factor of the bf16 emulation's own distance to fp64, with absolute bars on top; probabilities
-within the bf16 bar of the emulation; updated weights within the same bar.
+(DESIGN.md 4): unreplayed, bf16 storage alone leaves gradients at cosine ~0.26 to fp64, and the
+device must be no more chaotic than that. With the device's ReLU decisions replayed in both oracle
+runs the gradients are well conditioned: over all 157 tensors (step_util.grad_summary) the
+device's distance to fp64 must stay within 4x the bf16 emulation's own distance (with absolute
+floors), probabilities and loss likewise, updated weights within the gradient bar.
 
 Full size: one 224x224 / 256-image step checked through size-independent properties -- finite
 outputs, BatchNorm moving statistics of channel subsets against a host recompute from the device's
@@ -59,25 +60,35 @@ def test_resnet50_bf16_step_gradients(gpu, tiles):
     finally:
         L.check(lib.rn_set_tuning(4, 0), "tune")
         L.check(lib.rn_set_tuning(10, 512), "tune")
+    masks = res["relu_masks"][0]
+    # (1) unreplayed: at 2 images of 112x112 a random-init ResNet-50 is chaotic under ANY rounding
+    # (thousands of ReLU decisions flip; measured: the bf16 emulation's own gradients have cosine
+    # ~0.26 to fp64). The device must be exactly as chaotic as bf16 storage is, no more.
     ref = oracle_step(g, args, aux, data, label)
     emu = oracle_step(g, args, aux, data, label, storage="bf16")
-    s_dev = grad_summary(res["grads"][0], ref["grads"][0])
-    s_emu = grad_summary(emu["grads"][0], ref["grads"][0])
-    p_dev = max_rel(res["prob"][0], ref["prob"][0])
-    p_emu = max_rel(emu["prob"][0], ref["prob"][0])
-    print("device vs fp64:", s_dev, "prob", p_dev)
-    print("bf16 emulation vs fp64:", s_emu, "prob", p_emu)
-    assert s_dev["cos"] > 0.98 and s_dev["cos"] > 1 - 4 * (1 - s_emu["cos"]) - 2e-3, (s_dev, s_emu)
-    assert s_dev["fro"] < max(4 * s_emu["fro"], 0.05), (s_dev, s_emu)
-    assert s_dev["median"] < max(4 * s_emu["median"], 0.05), (s_dev, s_emu)
-    assert s_dev["p95"] < max(4 * s_emu["p95"], 0.15), (s_dev, s_emu)
-    assert p_dev < max(4 * p_emu, 0.03), (p_dev, p_emu)
-    loss_dev, loss_ref = ce_loss(res["prob"][0], label), ce_loss(ref["prob"][0], label)
+    raw_dev = grad_summary(res["grads"][0], ref["grads"][0])
+    raw_emu = grad_summary(emu["grads"][0], ref["grads"][0])
+    # (2) replayed: the same ReLU decisions in all three (the device's, step_util.gpu_relu_masks),
+    # then the gradients are well conditioned and the device must match the fp64 oracle within a
+    # small factor of what bf16 storage alone costs
+    ref_m = oracle_step(g, args, aux, data, label, relu_masks=masks)
+    emu_m = oracle_step(g, args, aux, data, label, storage="bf16", relu_masks=masks)
+    s_dev = grad_summary(res["grads"][0], ref_m["grads"][0])
+    s_emu = grad_summary(emu_m["grads"][0], ref_m["grads"][0])
+    p_dev = max_rel(res["prob"][0], ref_m["prob"][0])
+    p_emu = max_rel(emu_m["prob"][0], ref_m["prob"][0])
+    print("unreplayed  device vs fp64:", raw_dev, " bf16 emulation vs fp64:", raw_emu)
+    print("replayed    device vs fp64:", s_dev, "prob", p_dev, " bf16 emulation vs fp64:", s_emu, "prob", p_emu)
+    assert raw_dev["median"] < 1.5 * raw_emu["median"] + 0.1, (raw_dev, raw_emu)
+    assert s_dev["cos"] > 0.995 and 1 - s_dev["cos"] < 4 * (1 - s_emu["cos"]) + 1e-3, (s_dev, s_emu)
+    for k, floor in (("fro", 0.02), ("median", 0.02), ("p95", 0.05)):
+        assert s_dev[k] < max(4 * s_emu[k], floor), (k, s_dev, s_emu)
+    assert p_dev < max(4 * p_emu, 2e-2), (p_dev, p_emu)
+    loss_dev, loss_ref = ce_loss(res["prob"][0], label), ce_loss(ref_m["prob"][0], label)
     assert abs(loss_dev - loss_ref) < 0.02 * loss_ref, (loss_dev, loss_ref)
-    # the SGD step on fp32 master weights: beta / bias updates are -lr*g/B, so they carry the
-    # gradient bar; every other tensor moved by less than its bf16 noise
-    worst = max(fro_rel(res["args"][n], ref["args"][n]) for n in ref["args"])
-    assert worst < 0.05, worst
+    # the SGD step on fp32 master weights inherits the gradient bar
+    worst = sorted(fro_rel(res["args"][n], ref_m["args"][n]) for n in ref_m["args"])
+    assert worst[len(worst) // 2] < 0.02 and worst[-1] < 0.1, worst[-5:]
 
 
 def test_resnet50_bf16_full_size_properties(gpu):
