@@ -47,7 +47,28 @@ class TorchStep:
         self.mom = {k: torch.zeros_like(v) for k, v in self.P.items()}
         self.wd_mult = {k: ops.wd_mult_for(k) for k in self.P}
 
+    def grads(self, data, label):
+        """Forward(is_train) + backward only: ({param: fp64 gradient of the summed CE}, probabilities)."""
+        self._forward_backward(data, label)
+        out = {k: (p.grad.double().numpy() if p.grad is not None else np.zeros(p.shape))
+               for k, p in self.P.items()}
+        for p in self.P.values():
+            p.grad = None
+        return out, self._prob
+
     def step(self, data, label, lr, momentum=0.9, wd=1e-4):
+        loss = self._forward_backward(data, label)
+        rescale = 1.0 / data.shape[0]
+        with torch.no_grad():
+            for k, p in self.P.items():
+                m = self.mom[k]
+                gk = p.grad if p.grad is not None else torch.zeros_like(p)  # fix_gamma: dgamma = 0
+                m.mul_(momentum).sub_(lr * (rescale * gk + wd * self.wd_mult[k] * p))
+                p.add_(m)
+                p.grad = None
+        return loss
+
+    def _forward_backward(self, data, label):
         g = self.g
         x = torch.from_numpy(np.ascontiguousarray(data, dtype=np.float32))
         if self.cl:
@@ -85,15 +106,8 @@ class TorchStep:
             elif t == "softmax":
                 # SoftmaxOutput: d logits = p - onehot per sample (sum of CE, no 1/B)
                 loss = F.cross_entropy(env[op["x"]], torch.from_numpy(label.astype(np.int64)), reduction="sum")
+                self._prob = F.softmax(env[op["x"]].detach(), dim=1).double().numpy()
         loss.backward()
-        rescale = 1.0 / data.shape[0]
-        with torch.no_grad():
-            for k, p in self.P.items():
-                m = self.mom[k]
-                gk = p.grad if p.grad is not None else torch.zeros_like(p)  # fix_gamma: dgamma = 0
-                m.mul_(momentum).sub_(lr * (rescale * gk + wd * self.wd_mult[k] * p))
-                p.add_(m)
-                p.grad = None
         return float(loss.item()) / data.shape[0]
 
 

@@ -79,16 +79,40 @@ def test_resnet50_bf16_step_gradients(gpu, tiles):
     p_emu = max_rel(emu_m["prob"][0], ref_m["prob"][0])
     print("unreplayed  device vs fp64:", raw_dev, " bf16 emulation vs fp64:", raw_emu)
     print("replayed    device vs fp64:", s_dev, "prob", p_dev, " bf16 emulation vs fp64:", s_emu, "prob", p_emu)
+    # measured (r02): even replayed, bf16 storage moves this ill-conditioned network's gradients by
+    # ~46 % per tensor (BN backward over 32 elements per channel at stage 4 cancels heavily): both
+    # bars say "the device is as accurate as ideal bf16 storage", not an absolute accuracy
     assert raw_dev["median"] < 1.5 * raw_emu["median"] + 0.1, (raw_dev, raw_emu)
-    assert s_dev["cos"] > 0.995 and 1 - s_dev["cos"] < 4 * (1 - s_emu["cos"]) + 1e-3, (s_dev, s_emu)
-    for k, floor in (("fro", 0.02), ("median", 0.02), ("p95", 0.05)):
-        assert s_dev[k] < max(4 * s_emu[k], floor), (k, s_dev, s_emu)
-    assert p_dev < max(4 * p_emu, 2e-2), (p_dev, p_emu)
-    loss_dev, loss_ref = ce_loss(res["prob"][0], label), ce_loss(ref_m["prob"][0], label)
-    assert abs(loss_dev - loss_ref) < 0.02 * loss_ref, (loss_dev, loss_ref)
-    # the SGD step on fp32 master weights inherits the gradient bar
-    worst = sorted(fro_rel(res["args"][n], ref_m["args"][n]) for n in ref_m["args"])
-    assert worst[len(worst) // 2] < 0.02 and worst[-1] < 0.1, worst[-5:]
+    assert 1 - s_dev["cos"] < 1.5 * (1 - s_emu["cos"]) + 0.01, (s_dev, s_emu)
+    for k in ("fro", "median", "p95"):
+        assert s_dev[k] < 1.5 * s_emu[k] + 0.02, (k, s_dev, s_emu)
+    assert p_dev < 2 * p_emu + 0.02, (p_dev, p_emu)
+
+
+def test_resnet50_bf16_full_size_gradients(gpu):
+    """The exact bench configuration -- 256 images at 224x224, no tuning override -- against the
+    torch-CPU fp32 restatement of the same step (oracle/torch_cpu.py, itself pinned to the numpy
+    oracle): at this size BatchNorm averages over >= 12,544 elements per channel, the network is
+    well conditioned and bf16 storage costs ~1 % per gradient tensor, so absolute bars apply."""
+    from oracle import torch_cpu
+    g = onet.resnet50_imagenet()
+    args, aux = onet.init_params(g, dtype=np.float32)
+    data, label = onet.synthetic_batch(256, (3, 224, 224), 1000, dtype=np.float32)
+    from rn import graphs
+    with torch.cuda.stream(_prio_stream()):
+        res = module_step(graphs.resnet50(), args, aux, data, label, "bfloat16")
+    torch.cuda.synchronize()
+    del res["mod"]
+    torch.cuda.empty_cache()
+    st = torch_cpu.TorchStep(g, args, aux)
+    grads, prob = st.grads(data, label)
+    s = grad_summary(res["grads"][0], grads)
+    p = max_rel(res["prob"][0], prob)
+    worst = sorted((fro_rel(res["grads"][0][n], grads[n]), n) for n in grads)[-5:]
+    print("bench config vs torch-CPU fp32:", s, "prob", p, "worst", worst)
+    assert s["cos"] > 0.999 and s["fro"] < 0.03 and s["median"] < 0.03 and s["p95"] < 0.08, s
+    assert p < 0.03, p
+    assert abs(ce_loss(res["prob"][0], label) - ce_loss(prob, label)) < 0.01 * ce_loss(prob, label)
 
 
 def test_resnet50_bf16_full_size_properties(gpu):
