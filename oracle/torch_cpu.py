@@ -32,9 +32,12 @@ def cpu_model():
 class TorchStep:
     """Parameters, momenta and BN moving statistics of one graph, stepped in fp32 on the CPU."""
 
-    def __init__(self, graph, args, aux, channels_last=True):
+    def __init__(self, graph, args, aux, channels_last=True, storage=None):
         self.g = graph
         self.cl = channels_last
+        # storage='bf16': conv / BN / pooling outputs and conv weights rounded to bf16 as they are
+        # stored (the bf16-storage emulation of oracle.net.forward), fp32 arithmetic in between
+        self.rnd = (lambda t: t.to(torch.bfloat16).to(torch.float32)) if storage == "bf16" else (lambda t: t)
         fmt = torch.channels_last if channels_last else torch.contiguous_format
 
         def mk(v):
@@ -78,15 +81,16 @@ class TorchStep:
         for op in g.ops:
             t = op["op"]
             if t == "conv":
-                env[op["y"]] = F.conv2d(env[op["x"]], self.P[op["name"] + "_weight"], stride=op["stride"],
-                                        padding=op["pad"], groups=op["groups"])
+                env[op["y"]] = self.rnd(F.conv2d(env[op["x"]], self.rnd(self.P[op["name"] + "_weight"]),
+                                                 stride=op["stride"], padding=op["pad"], groups=op["groups"]))
             elif t == "bn":
                 nm = op["name"]
                 xin = env[op["x"]]
                 gam = self.P[nm + "_gamma"]
                 if op["fix_gamma"]:
                     gam = torch.ones_like(gam)
-                env[op["y"]] = F.batch_norm(xin, None, None, gam, self.P[nm + "_beta"], training=True, eps=op["eps"])
+                env[op["y"]] = self.rnd(F.batch_norm(xin, None, None, gam, self.P[nm + "_beta"], training=True,
+                                                     eps=op["eps"]))
                 with torch.no_grad():  # MXNet moving stats: biased batch variance, m = 0.9 m + 0.1 batch
                     var, mean = torch.var_mean(xin, dim=(0, 2, 3), unbiased=False)
                     mm, mv = self.aux[nm + "_moving_mean"], self.aux[nm + "_moving_var"]
@@ -97,12 +101,12 @@ class TorchStep:
             elif t == "maxpool":
                 env[op["y"]] = F.max_pool2d(env[op["x"]], op["kernel"], op["stride"], op["pad"])
             elif t == "gap":
-                env[op["y"]] = env[op["x"]].mean(dim=(2, 3), keepdim=True)
+                env[op["y"]] = self.rnd(env[op["x"]].mean(dim=(2, 3), keepdim=True))
             elif t == "fc":
                 env[op["y"]] = F.linear(env[op["x"]].flatten(1), self.P[op["name"] + "_weight"],
                                         self.P[op["name"] + "_bias"])
             elif t == "add":
-                env[op["y"]] = env[op["a"]] + env[op["b"]]
+                env[op["y"]] = self.rnd(env[op["a"]] + env[op["b"]])
             elif t == "softmax":
                 # SoftmaxOutput: d logits = p - onehot per sample (sum of CE, no 1/B)
                 loss = F.cross_entropy(env[op["x"]], torch.from_numpy(label.astype(np.int64)), reduction="sum")

@@ -104,14 +104,19 @@ def test_resnet50_bf16_full_size_gradients(gpu):
     torch.cuda.synchronize()
     del res["mod"]
     torch.cuda.empty_cache()
-    st = torch_cpu.TorchStep(g, args, aux)
-    grads, prob = st.grads(data, label)
+    grads, prob = torch_cpu.TorchStep(g, args, aux).grads(data, label)
+    egrads, eprob = torch_cpu.TorchStep(g, args, aux, storage="bf16").grads(data, label)
     s = grad_summary(res["grads"][0], grads)
-    p = max_rel(res["prob"][0], prob)
-    worst = sorted((fro_rel(res["grads"][0][n], grads[n]), n) for n in grads)[-5:]
-    print("bench config vs torch-CPU fp32:", s, "prob", p, "worst", worst)
-    assert s["cos"] > 0.999 and s["fro"] < 0.03 and s["median"] < 0.03 and s["p95"] < 0.08, s
-    assert p < 0.03, p
+    se = grad_summary(egrads, grads)
+    p, pe = max_rel(res["prob"][0], prob), max_rel(eprob, prob)
+    print("bench config vs torch-CPU fp32:", s, "prob", p)
+    print("torch-CPU bf16-storage emulation vs fp32:", se, "prob", pe)
+    # the random-init network is chaotic under bf16 rounding even at this size: the device must be
+    # no further from fp32 than ideal bf16 storage is
+    assert 1 - s["cos"] < 1.5 * (1 - se["cos"]) + 0.01, (s, se)
+    for k in ("fro", "median", "p95"):
+        assert s[k] < 1.5 * se[k] + 0.02, (k, s, se)
+    assert p < 2 * pe + 0.02, (p, pe)
     assert abs(ce_loss(res["prob"][0], label) - ce_loss(prob, label)) < 0.01 * ce_loss(prob, label)
 
 
