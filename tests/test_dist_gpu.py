@@ -75,10 +75,16 @@ def _worker(rank, world, port, graph, precision, mode, q):
         # this rank's local gradient first, before the process group exists (no exchange), from the
         # weights rank 0 will broadcast (seed 3)
         ml = make("device", 3, [mx.gpu(0)], shp)
-        ml.forward(batch, is_train=True)
-        ml.backward()
-        exl = ml.executor
-        g_local = {n: exl.get_param(n, grad=True).copy() for n in exl.plan.param_names}
+        g_runs = []
+        for _ in range(2):  # twice: the local gradient itself must repeat (no race inside the step)
+            ml.forward(batch, is_train=True)
+            ml.backward()
+            exl = ml.executor
+            g_runs.append({n: exl.get_param(n, grad=True).copy() for n in exl.plan.param_names})
+        g_local = g_runs[0]
+        rep = max(float(np.abs(g_runs[1][n] - g_local[n]).max()) / max(1e-6, float(np.abs(g_local[n]).max()))
+                  for n in g_local)
+        assert rep <= (1e-5 if precision == "float32" else 2e-2), ("local gradient does not repeat", rep)
         del ml, exl
         rdist.init_from_env("gloo")
         if mode == "slice":

@@ -1,7 +1,10 @@
-"""Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes per kernel family.
+"""Summarise rocprofv3 --pmc passes (tools/pmc_bench.sh) per kernel family and for the last step.
 
 Usage: python tools/pmc_summary.py gpurun_out/pmc_<tag>  [--json out.json]
-Reads <dir>_fetch/run_counter_collection.csv and <dir>_write/run_counter_collection.csv.
+Reads <dir>_fetch/, <dir>_write/ and (when present) <dir>_sq/run_counter_collection.csv.
+MFMA utilisation = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs) (rocprofv3's
+MfmaUtil formula: GRBM_GUI_ACTIVE comes summed over the 8 XCDs); LDS bank-conflict share =
+SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE (extra cycles / all LDS-array cycles).
 Units: rocprofv3 reports both counters in KiB. gfx950 correction (MI355X_MICROARCH.md, HBM
 section): FETCH_SIZE counts half the bytes of a 16-B/lane streaming read -> doubled here;
 WRITE_SIZE is exact for 16-B stores and fp32 atomics.
@@ -60,10 +63,93 @@ def summarise(base):
     return res
 
 
+SQ = ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE", "SQ_LDS_BANK_CONFLICT", "SQ_LDS_IDX_ACTIVE",
+      "SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_INSTS_LDS")
+
+
+def load_dispatches(path):
+    """{dispatch id: {"name", "start", counters...}} from a counter-collection csv."""
+    out = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            d = out.setdefault(int(row["Dispatch_Id"]), {"name": row["Kernel_Name"],
+                                                          "start": int(row["Start_Timestamp"])})
+            d[row["Counter_Name"]] = d.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+    return out
+
+
+def last_step_bytes(base):
+    """HBM bytes of the last training step: 2 x FETCH_SIZE + WRITE_SIZE summed over its dispatches."""
+    tot = 0.0
+    for name, counter, scale in (("fetch", "FETCH_SIZE", 2.0), ("write", "WRITE_SIZE", 1.0)):
+        rows = sorted(load_dispatches(base + "_%s/run_counter_collection.csv" % name).values(),
+                      key=lambda d: d["start"])
+        sgd = [i for i, d in enumerate(rows) if "sgd_mom" in d["name"]]
+        if len(sgd) < 2:
+            return None
+        tot += scale * 1024.0 * sum(d.get(counter, 0.0) for d in rows[sgd[-2] + 1:sgd[-1] + 1])
+    return tot
+
+
+def sq_ratios(acc):
+    simd_cycles = acc.get("GRBM_GUI_ACTIVE", 0.0) / 8.0 * 1024.0
+    return {"mfma_util": acc.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) / simd_cycles if simd_cycles else None,
+            "lds_conflict_share": (acc.get("SQ_LDS_BANK_CONFLICT", 0.0) / acc["SQ_LDS_IDX_ACTIVE"]
+                                   if acc.get("SQ_LDS_IDX_ACTIVE") else None),
+            "mfma_bf16_tflop": acc.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) * 512 / 1e12,
+            "busy_ms_at_2.4GHz": acc.get("GRBM_GUI_ACTIVE", 0.0) / 8.0 / 2.4e9 * 1e3}
+
+
+def summarise_sq(base):
+    """Per family (summed over launches) and over the last training step (dispatches between the
+    last two SGD launches): MFMA utilisation of the kernels' own busy time, LDS conflict share."""
+    path = base + "_sq/run_counter_collection.csv"
+    try:
+        disp = load_dispatches(path)
+    except FileNotFoundError:
+        return None
+    rows = sorted(disp.values(), key=lambda d: d["start"])
+    sgd = [i for i, d in enumerate(rows) if "sgd_mom" in d["name"]]
+    fam = collections.defaultdict(lambda: collections.defaultdict(float))
+    step = collections.defaultdict(float)
+    for i, d in enumerate(rows):
+        f = family(d["name"])
+        a = aggregate(f)
+        for k in SQ:
+            fam[f][k] += d.get(k, 0.0)
+            if a:
+                fam[a][k] += d.get(k, 0.0)
+            if len(sgd) >= 2 and sgd[-2] < i <= sgd[-1]:
+                step[k] += d.get(k, 0.0)
+        fam[f]["launches"] += 1
+        if a:
+            fam[a]["launches"] += 1
+    out = {"families": {k: dict(sq_ratios(v), launches=int(v["launches"])) for k, v in fam.items()}}
+    if step:
+        out["last_step"] = sq_ratios(step)
+    return out
+
+
 if __name__ == "__main__":
     base = sys.argv[1]
     res = summarise(base)
-    for k, v in sorted(res.items(), key=lambda kv: -kv[1]["hbm_bytes"] * kv[1]["launches"]):
+    sq = summarise_sq(base)
+    sb = last_step_bytes(base)
+    if sb:
+        print("last step HBM bytes (2 x FETCH_SIZE + WRITE_SIZE): %.2f GB" % (sb / 1e9))
+    if sq:
+        print("last step (kernels serialised under PMC): MFMA util %.3f of the kernels' busy time, "
+              "%.1f TFLOP bf16 MFMA, busy %.2f ms at 2.4 GHz, LDS conflict share %.3f" % (
+                  sq["last_step"]["mfma_util"], sq["last_step"]["mfma_bf16_tflop"],
+                  sq["last_step"]["busy_ms_at_2.4GHz"], sq["last_step"]["lds_conflict_share"] or 0))
+        for k, v in sorted(sq["families"].items(), key=lambda kv: -kv[1]["busy_ms_at_2.4GHz"]):
+            if v["mfma_util"] is None:
+                continue
+            print("  %-42s n=%5d MFMA util %.3f  LDS conflict %.3f  busy %.2f ms" % (
+                k, v["launches"], v["mfma_util"], v["lds_conflict_share"] or 0, v["busy_ms_at_2.4GHz"]))
+        res = {"hbm": res, "sq": sq, "last_step_hbm_bytes": sb}
+    hbm = res["hbm"] if sq else res
+    for k, v in sorted(hbm.items(), key=lambda kv: -kv[1]["hbm_bytes"] * kv[1]["launches"]):
         print("%-42s n=%5d fetch %9.2f MB  write %9.2f MB  per launch" %
               (k, v["launches"], v["fetch_bytes"] / 1e6, v["write_bytes"] / 1e6))
     if "--json" in sys.argv:

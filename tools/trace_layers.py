@@ -10,6 +10,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "resnet.mxnet_amd")]
 from rn import graphs  # noqa: E402
 from rn.executor import Executor, Plan  # noqa: E402
+from bench import conv_call_bytes  # noqa: E402
 
 CONV_CALLS = ("rn_conv_fwd", "rn_conv_fwd_bnstats", "rn_conv_fwd_x", "rn_conv_fwd_bnacc", "rn_conv_bwd_data",
               "rn_conv_bwd_data_bnred", "rn_conv_bwd_data_bnacc", "rn_conv_bwd_filter", "rn_conv_bwd_filter_x", "rn_conv_bwd_filter_ws",
@@ -54,16 +55,23 @@ def main():
     for (n, a), r in zip(calls, rows):
         d = a[0]._obj
         flops = 2.0 * d.n * d.p * d.q * d.k * (d.c_real // d.groups) * d.r * d.s
-        xb, yb, wb = 2.0 * d.n * d.h * d.w * d.c, 2.0 * d.n * d.p * d.q * d.k_pad, 2.0 * d.k * d.r * d.s * d.c
         kind = "wgrad" if ("filter" in n or "wgrad" in n) else "dgrad" if "bwd_data" in n else "fwd"
-        algb = xb + yb + (2 * wb if kind == "wgrad" else wb)
+        # algorithmic bytes as bench.py counts them: every operand once, + residual / BN input reads
+        algb = float(conv_call_bytes(ex, n, a)) if n.startswith("rn_conv") else \
+            2.0 * (d.n * d.h * d.w * d.c + d.n * d.p * d.q * d.k_pad) + 8.0 * d.k * d.r * d.s * d.c
         us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
         roof = max(flops / 2.5e15, algb / 8e12) * 1e6
-        out.append((us, names.get(id(d), "?"), kind, flops / us / 1e6, roof / us, kernel_short(r["Kernel_Name"])))
+        out.append((us, names.get(id(d), "?"), kind, flops / us / 1e6, algb / us / 1e6, roof / us,
+                    flops / algb, kernel_short(r["Kernel_Name"])))
         tot[kind] = tot.get(kind, 0) + us
-    for us, lname, kind, tf, fr, kn in sorted(out, reverse=True):
-        print("%8.1f us  %-22s %-5s %7.1f TF %4.0f%%  %s" % (us, lname, kind, tf, 100 * fr, kn))
+    print("    time  layer                  kind    TFLOP/s   TB/s  roof%  FLOP/B  kernel")
+    for us, lname, kind, tf, tb, fr, ai, kn in sorted(out, reverse=True):
+        print("%8.1f us  %-22s %-5s %7.1f TF %5.2f %4.0f%% %6.0f  %s" % (us, lname, kind, tf, tb, 100 * fr, ai, kn))
     print({k: round(v / 1e3, 3) for k, v in tot.items()}, "ms")
+    # time above a practical bound: memory-side layers at 5.5 TB/s, MFMA-side at 60 % of peak
+    excess = sum(max(0.0, o[0] - max(o[3] * o[0] / 2.5e3 / 0.6 * 0 + (o[0] * o[4] / 5.5), 0)) for o in out)
+    print("time above max(bytes / 5.5 TB/s, FLOP / 1.5 PF): %.3f ms" % (sum(
+        max(0.0, o[0] - max(o[0] * o[4] / 5.5, o[0] * o[3] / 1.5e3)) for o in out) / 1e3))
 
 
 if __name__ == "__main__":
