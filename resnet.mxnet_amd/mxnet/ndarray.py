@@ -44,7 +44,10 @@ class NDArray:
         if isinstance(self._data, np.ndarray):
             t = torch.from_numpy(np.ascontiguousarray(self._data))
             if self._ctx.device_type == "cpu_pinned":
-                t = t.pin_memory()
+                # page-locked for the H2D copy stream; a host without a GPU has nothing to pin for
+                # (RN_DRY_RUN plans on the CPU)
+                if torch.cuda.is_available():
+                    t = t.pin_memory()
                 self._data = t
             return t
         return self._data
