@@ -345,6 +345,15 @@ int32_t rn_sgd_pack_work(int32_t ntensors, const int64_t* numels, const rn_wpack
 /* ---------------------------------------------------------------------------------------
  * Data movement helpers.
  * ------------------------------------------------------------------------------------- */
+/* Backward through [relu o] BN with GLOBAL statistics (use_global_stats=True; config.fix_bn ->
+ * core/graph_optimize.py:114-157 fix_bn, train.py:106-109): the forward normalised with the moving
+ * statistics (rn_bn_fwd_infer wrote scale/shift), which are constants: dz as in rn_bn_bwd,
+ * dgamma = sum(dz*xhat) (0 if fix_gamma), dbeta = sum(dz), dx = gamma/sqrt(moving_var+eps)*dz
+ * (+ add_src), xhat = (x - moving_mean)/sqrt(moving_var+eps). Moving statistics are not updated. */
+int rn_bn_bwd_global(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const void* add_src,
+                     const float* gamma, const float* moving_mean, const float* moving_var,
+                     const float* scale, const float* shift, float* dgamma, float* dbeta, void* ws,
+                     rn_stream_t stream);
 /* NCHW fp32 -> NHWC dtype with channel stride c_pad (zero padding). */
 int rn_nchw_to_nhwc(int32_t n, int32_t c, int32_t h, int32_t w, int32_t c_pad, const float* src,
                     void* dst, int32_t dst_dtype, rn_stream_t stream);

@@ -37,7 +37,7 @@ class Graph:
         c = self.chan[x]
         self.add_param(name + "_weight", (k, c // groups) + tuple(kernel))
         self.ops.append(dict(op="conv", name=name, x=x, y=name, k=k, kernel=kernel, stride=stride, pad=pad,
-                             groups=groups, quant=quant))
+                             groups=groups, quant=quant, qname=None, wbits=8, abits=8))
         self.chan[name] = k
         return name
 
@@ -70,7 +70,7 @@ class Graph:
         c = self.chan[x]
         self.add_param(name + "_weight", (nh, c))
         self.add_param(name + "_bias", (nh,))
-        self.ops.append(dict(op="fc", name=name, x=x, y=name, nh=nh, quant=quant))
+        self.ops.append(dict(op="fc", name=name, x=x, y=name, nh=nh, quant=quant, qname=None, wbits=8, abits=8))
         self.chan[name] = nh
         return name
 
@@ -226,6 +226,35 @@ def resnext50_32x4d(num_classes=1000):
 
 
 # ----------------------------------------------------------------------------- execution
+def fix_bn(graph):
+    """core/graph_optimize.py:114-157 (config.fix_bn, train.py:106-109, test.py:45-48): every
+    BatchNorm switched to use_global_stats=True. Returns a new Graph (ops copied)."""
+    g = Graph()
+    g.params, g.aux, g.chan = dict(graph.params), dict(graph.aux), dict(graph.chan)
+    g.ops = [dict(op, global_stats=True) if op["op"] == "bn" else dict(op) for op in graph.ops]
+    return g
+
+
+def attach_quant(graph, skip=None, wbits=8, abits=8):
+    """core/graph_optimize.py:199-292 (config.quantize_flag, train.py:111-120) restricted to
+    Quantization_int8 on Convolution / FullyConnected: every conv / fc input and weight gets a
+    fake-quant node except the first skip[op] of each kind in graph order (skip_quantize_counts,
+    edict_config.py default {'Convolution': 1, 'FullyConnected': 1}); one node per quantized tensor,
+    named after it, shared by all its consumers. Returns a new Graph."""
+    skip = dict(skip or {})
+    seen = {"conv": 0, "fc": 0}
+    g = Graph()
+    g.params, g.aux, g.chan = dict(graph.params), dict(graph.aux), dict(graph.chan)
+    for op in graph.ops:
+        op = dict(op)
+        if op["op"] in ("conv", "fc"):
+            seen[op["op"]] += 1
+            if seen[op["op"]] > skip.get(op["op"], 0):
+                op.update(quant=True, qname=op["x"], wbits=wbits, abits=abits)
+        g.ops.append(op)
+    return g
+
+
 def init_params(graph, seed=2, dtype=np.float64):
     """Xavier(gaussian, in, 2) in graph (MXNet arg) order from numpy.random.default_rng(seed)."""
     rng = np.random.default_rng(seed)
@@ -248,6 +277,7 @@ def forward(graph, args, aux, data, label, is_train=True, quant_state=None, firs
     env = {"data": data}
     tape = []
     qs = quant_state if quant_state is not None else {}
+    qdone = {}
     for op in graph.ops:
         t = op["op"]
         if t == "conv" or t == "fc":
@@ -255,12 +285,22 @@ def forward(graph, args, aux, data, label, is_train=True, quant_state=None, firs
             w = args[op["name"] + "_weight"]
             rec = dict(op=op)
             if op["quant"]:
-                key = op["name"] + "_data_minmax"
-                xq, mm = ops.quant_int8_act(x, qs.get(key, 0.0), is_train, first_batch or key not in qs)
+                # the data quantizer node: '<conv>_data' (int8_api.py:133-136), or the quantized tensor's
+                # own name when attach_quantize_node shares one node between its consumers
+                # (core/graph_optimize.py:247-252): it runs (and updates its EMA) once per forward
+                qn = op.get("qname") or op["name"] + "_data"
+                key = qn + "_minmax"
+                if qn in qdone:
+                    xq, mm = qdone[qn]
+                else:
+                    xq, mm = ops.quant_int8_act(x, qs.get(key, 0.0), is_train, first_batch or key not in qs,
+                                                nbits=op.get("abits", 8))
+                    if quant_values is not None:
+                        xq = quant_values.get(qn, xq).reshape(xq.shape).astype(xq.dtype)
+                    qdone[qn] = (xq, mm)
                 qs[key] = mm
-                wq, _ = ops.quant_int8_weight(w)
+                wq, _ = ops.quant_int8_weight(w, nbits=op.get("wbits", 8))
                 if quant_values is not None:
-                    xq = quant_values.get(op["name"] + "_data", xq).reshape(xq.shape).astype(xq.dtype)
                     wq = quant_values.get(op["name"] + "_weight", wq).reshape(wq.shape).astype(wq.dtype)
                 rec.update(xraw=x, t=mm)
                 x, w = xq, wq
@@ -277,7 +317,11 @@ def forward(graph, args, aux, data, label, is_train=True, quant_state=None, firs
         elif t == "bn":
             x = env[op["x"]]
             nm = op["name"]
-            if is_train:
+            if is_train and op.get("global_stats"):
+                y, cache = ops.bn_global_fwd(x, args[nm + "_gamma"], args[nm + "_beta"], aux[nm + "_moving_mean"],
+                                             aux[nm + "_moving_var"], op["eps"], op["fix_gamma"])
+                tape.append(dict(op=op, gcache=cache))
+            elif is_train:
                 y, cache = ops.bn_train_fwd(x, args[nm + "_gamma"], args[nm + "_beta"], op["eps"], op["fix_gamma"])
                 aux[nm + "_moving_mean"], aux[nm + "_moving_var"] = ops.bn_moving_update(
                     aux[nm + "_moving_mean"], aux[nm + "_moving_var"], cache[3], cache[4], op["momentum"])
@@ -355,7 +399,10 @@ def backward(graph, args, fwd_state, grad_scale=1.0, keep=None):
             grads[op["name"] + "_bias"] = db
             acc(op["x"], dxf.reshape(dxf.shape[0], -1, 1, 1))
         elif t == "bn":
-            dx, dgamma, dbeta = ops.bn_train_bwd(dy, rec["cache"], op["fix_gamma"])
+            if "gcache" in rec:
+                dx, dgamma, dbeta = ops.bn_global_bwd(dy, rec["gcache"], op["fix_gamma"])
+            else:
+                dx, dgamma, dbeta = ops.bn_train_bwd(dy, rec["cache"], op["fix_gamma"])
             grads[op["name"] + "_gamma"] = dgamma
             grads[op["name"] + "_beta"] = dbeta
             if op["x"] != "data":

@@ -128,6 +128,28 @@ def bn_infer_fwd(x, gamma, beta, moving_mean, moving_var, eps, fix_gamma):
     return (x - moving_mean.reshape(shp)) / np.sqrt(moving_var.reshape(shp) + eps) * g.reshape(shp) + beta.reshape(shp)
 
 
+def bn_global_fwd(x, gamma, beta, moving_mean, moving_var, eps, fix_gamma):
+    """BatchNorm(use_global_stats=True) in training (fix_bn, core/graph_optimize.py:114-157;
+    MXNet 1.x batch_norm backward, un-vendored): normalised with the moving statistics, which are
+    constants (no moving-stat update). Returns y, cache."""
+    shp = (1, -1, 1, 1) if x.ndim == 4 else (1, -1)
+    invstd = 1.0 / np.sqrt(moving_var + eps)
+    g = np.ones_like(gamma) if fix_gamma else gamma
+    xhat = (x - moving_mean.reshape(shp)) * invstd.reshape(shp)
+    return xhat * g.reshape(shp) + beta.reshape(shp), (xhat, invstd, g)
+
+
+def bn_global_bwd(dy, cache, fix_gamma):
+    """dx = gamma*invstd*dy (no batch-statistic terms), dgamma = sum(dy*xhat), dbeta = sum(dy)."""
+    xhat, invstd, g = cache
+    axes = (0, 2, 3) if dy.ndim == 4 else (0,)
+    shp = (1, -1, 1, 1) if dy.ndim == 4 else (1, -1)
+    dbeta = dy.sum(axis=axes)
+    dg_raw = (dy * xhat).sum(axis=axes)
+    dgamma = np.zeros_like(dg_raw) if fix_gamma else dg_raw
+    return (g * invstd).reshape(shp) * dy, dgamma, dbeta
+
+
 # ----------------------------------------------------------------------------- activation
 def relu_fwd(x):
     return np.maximum(x, 0)

@@ -506,7 +506,9 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
                                                               const float* __restrict__ gamma,
                                                               const float* __restrict__ save_mean,
                                                               const float* __restrict__ save_invstd, float* dgamma,
-                                                              float* dbeta, float* __restrict__ coef) {
+                                                              float* dbeta, float* __restrict__ coef,
+                                                              const float* __restrict__ global_var = nullptr,
+                                                              float global_eps = 0.f) {
   const int ch = blockIdx.x;
   double s = 0.0, q = 0.0;
   for (int b = threadIdx.x; b < nrb; b += blockDim.x) {
@@ -523,14 +525,18 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
     coef[ch * 4 + 3] = 0.f;
     return;
   }
-  const double invstd = save_invstd[ch];
+  // global statistics (use_global_stats, fix_bn: core/graph_optimize.py:114-157): save_invstd is
+  // null, the normalisation used the moving statistics (save_mean = moving mean, invstd from the
+  // moving variance and global_eps) and they are constants of the graph: dx = g*invstd*dz
+  const bool global = save_invstd == nullptr;
+  const double invstd = global ? 1.0 / sqrt((double)global_var[ch] + (double)global_eps) : (double)save_invstd[ch];
   const double g = fix_gamma ? 1.0 : (double)gamma[ch];
   const double dg_raw = q * invstd;  // sum dz * xhat
   if (dbeta) dbeta[ch] = (float)s;
   if (dgamma) dgamma[ch] = fix_gamma ? 0.f : (float)dg_raw;
   coef[ch * 4 + 0] = (float)(g * invstd);
-  coef[ch * 4 + 1] = (float)(s / (double)m);
-  coef[ch * 4 + 2] = (float)(g * invstd * invstd * dg_raw / (double)m);
+  coef[ch * 4 + 1] = global ? 0.f : (float)(s / (double)m);
+  coef[ch * 4 + 2] = global ? 0.f : (float)(g * invstd * invstd * dg_raw / (double)m);
   coef[ch * 4 + 3] = save_mean[ch];
 }
 
@@ -631,7 +637,7 @@ int bn_apply_t(const rn_bn_desc* d, const void* x, void* y, const float* scale, 
 template <typename T>
 int bn_bwd_t(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const void* add, const float* gamma,
              const float* smean, const float* sinv, const float* scale, const float* shift, float* dgamma,
-             float* dbeta, void* ws, hipStream_t st) {
+             float* dbeta, void* ws, hipStream_t st, const float* global_var = nullptr) {
   Geo g = make_geo<T>(d->m, d->c);
   float* part = reinterpret_cast<float*>(ws);
   float* coef = part + (int64_t)g.nrb * d->c * 2;
@@ -643,7 +649,8 @@ int bn_bwd_t(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(g.gx, g.nrb), dim3(kThreads), 0, st, (const T*)x,
                        (const T*)dy, d->m, d->c, g.ct, g.rows_per_block, smean, scale, shift, part);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(d->c), dim3(256), 0, st, part, g.nrb, d->m, d->c,
-                     d->c_real, d->fix_gamma, gamma, smean, sinv, dgamma, dbeta, coef);
+                     d->c_real, d->fix_gamma, gamma, smean, global_var ? nullptr : sinv, dgamma, dbeta, coef,
+                     global_var, d->eps);
   if (dx) {
     if (d->relu) launch_bwd_apply<T, true>(d, x, dy, dx, add, coef, scale, shift, st);
     else launch_bwd_apply<T, false>(d, x, dy, dx, add, coef, scale, shift, st);
@@ -907,6 +914,20 @@ int rn_bn_bwd(const rn_bn_desc* d, const void* x, const void* dy, void* dx, cons
                             ws, st);
   return bn_bwd_t<float>(d, x, dy, dx, add_src, gamma, save_mean, save_invstd, scale, shift, dgamma, dbeta, ws,
                          st);
+}
+
+int rn_bn_bwd_global(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const void* add_src,
+                     const float* gamma, const float* moving_mean, const float* moving_var, const float* scale,
+                     const float* shift, float* dgamma, float* dbeta, void* ws, rn_stream_t stream) {
+  if (check_bn(d)) return -1;
+  RN_CHECK_ARG(x && dy && moving_mean && moving_var && scale && shift && ws, "null argument");
+  RN_CHECK_ARG(d->fix_gamma || gamma, "gamma required unless fix_gamma");
+  hipStream_t st = as_stream(stream);
+  if (d->dtype == RN_BF16)
+    return bn_bwd_t<bf16_t>(d, x, dy, dx, add_src, gamma, moving_mean, nullptr, scale, shift, dgamma, dbeta, ws,
+                            st, moving_var);
+  return bn_bwd_t<float>(d, x, dy, dx, add_src, gamma, moving_mean, nullptr, scale, shift, dgamma, dbeta, ws, st,
+                         moving_var);
 }
 
 }  // extern "C"

@@ -124,5 +124,40 @@ def load_checkpoint(prefix, epoch):
 
 
 class FeedForward:
-    def __init__(self, *args, **kwargs):
-        raise MXNetError("mx.model.FeedForward (deprecated eval API, test.py) is not provided; use mx.mod.Module")
+    """The legacy model API as test.py:64-71 drives it: FeedForward(symbol, ctx, arg_params=...,
+    aux_params=...).score(val_iter). Evaluation only (fit is Module's / Solver's job): a Module bound
+    for inference on the iterator's shapes, parameters the symbol does not use are ignored like
+    MXNet's FeedForward._init_params does."""
+
+    def __init__(self, symbol, ctx=None, num_epoch=None, epoch_size=None, optimizer="sgd", initializer=None,
+                 numpy_batch_size=128, arg_params=None, aux_params=None, allow_extra_params=False,
+                 begin_epoch=0, **kwargs):
+        from .context import gpu
+        self.symbol = symbol
+        self.ctx = ctx if ctx is not None else gpu(0)
+        self.arg_params, self.aux_params = arg_params, aux_params
+        self._mod = None
+        self._shapes = None
+
+    def _module(self, it):
+        from .module import Module
+        shapes = (tuple(it.provide_data), tuple(it.provide_label or ()))
+        if self._mod is None or self._shapes != shapes:
+            data_names = [d[0] if isinstance(d, tuple) else d.name for d in it.provide_data]
+            label_names = [d[0] if isinstance(d, tuple) else d.name for d in (it.provide_label or [])]
+            mod = Module(self.symbol, data_names=data_names, label_names=label_names, context=self.ctx)
+            mod.bind(it.provide_data, it.provide_label, for_training=False)
+            mod.init_params(arg_params=self.arg_params, aux_params=self.aux_params, allow_missing=False,
+                            allow_extra=True)
+            self._mod, self._shapes = mod, shapes
+        return self._mod
+
+    def score(self, X, eval_metric="acc", num_batch=None, batch_end_callback=None, reset=True):
+        """The metric's value over X (FeedForward.score returns eval_metric.get()[1])."""
+        from . import metric
+        m = eval_metric if isinstance(eval_metric, metric.EvalMetric) else metric.create(eval_metric)
+        self._module(X).score(X, m, num_batch=num_batch, batch_end_callback=batch_end_callback, reset=reset)
+        return m.get()[1]
+
+    def predict(self, X, num_batch=None, return_data=False, reset=True):
+        return self._module(X).predict(X, num_batch=num_batch, reset=reset).asnumpy()

@@ -2,7 +2,9 @@
 
 Covers what the reference's hot path touches: mx.nd.array(..., ctx=cpu_pinned) in the synthetic
 iterator (data/imagenet.py:17-18), asnumpy() on outputs/labels in metrics, waitall(), save/load of
-parameter dicts for checkpoints. Math helpers used only inside Python CustomOps are not provided.
+parameter dicts for checkpoints, and the host-side parameter arithmetic of the graph passes
+(core/graph_optimize.py:76-86: `-=`, `*`, `/`, `mx.nd.sqrt`, `expand_dims`, `[:] = v`). Math
+helpers used only inside Python CustomOps are not provided.
 """
 import numpy as np
 
@@ -103,6 +105,66 @@ class NDArray:
     def __len__(self):
         return self.shape[0]
 
+    # --- host arithmetic (numpy semantics, fp32 results like MXNet's default dtype)
+    def _binary(self, other, fn):
+        b = other.asnumpy() if isinstance(other, NDArray) else other
+        return NDArray(np.asarray(fn(self.asnumpy(), b), dtype=np.float32), self._ctx)
+
+    def _inplace(self, other, fn):
+        r = self._binary(other, fn).asnumpy()
+        if isinstance(self._data, np.ndarray) and self._data.shape == r.shape:
+            self._data[...] = r
+        elif isinstance(self._data, np.ndarray):
+            self._data = r
+        else:
+            self[:] = r
+        return self
+
+    def __add__(self, o):
+        return self._binary(o, np.add)
+
+    def __radd__(self, o):
+        return self._binary(o, lambda a, b: np.add(b, a))
+
+    def __sub__(self, o):
+        return self._binary(o, np.subtract)
+
+    def __rsub__(self, o):
+        return self._binary(o, lambda a, b: np.subtract(b, a))
+
+    def __mul__(self, o):
+        return self._binary(o, np.multiply)
+
+    def __rmul__(self, o):
+        return self._binary(o, lambda a, b: np.multiply(b, a))
+
+    def __truediv__(self, o):
+        return self._binary(o, np.divide)
+
+    def __rtruediv__(self, o):
+        return self._binary(o, lambda a, b: np.divide(b, a))
+
+    def __neg__(self):
+        return NDArray(-self.asnumpy(), self._ctx)
+
+    def __iadd__(self, o):
+        return self._inplace(o, np.add)
+
+    def __isub__(self, o):
+        return self._inplace(o, np.subtract)
+
+    def __imul__(self, o):
+        return self._inplace(o, np.multiply)
+
+    def __itruediv__(self, o):
+        return self._inplace(o, np.divide)
+
+    def expand_dims(self, axis):
+        return NDArray(np.expand_dims(self.asnumpy(), axis), self._ctx)
+
+    def squeeze(self, axis=None):
+        return NDArray(np.squeeze(self.asnumpy(), axis), self._ctx)
+
     def __repr__(self):
         return "\n%s\n<NDArray %s @%s>" % (self.asnumpy(), "x".join(map(str, self.shape)), self._ctx)
 
@@ -123,6 +185,14 @@ def ones(shape, ctx=None, dtype=np.float32):
 
 def empty(shape, ctx=None, dtype=np.float32):
     return zeros(shape, ctx, dtype)
+
+
+def sqrt(x):
+    return NDArray(np.sqrt(x.asnumpy()).astype(np.float32), x.context)
+
+
+def expand_dims(x, axis):
+    return x.expand_dims(axis)
 
 
 def waitall():

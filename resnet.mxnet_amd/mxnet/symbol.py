@@ -109,6 +109,9 @@ _reg(OpSpec("_Plus", ["lhs", "rhs"], hint="_plus"))
 _reg(OpSpec("elemwise_add", ["lhs", "rhs"], hint="_plus"))
 _reg(OpSpec("broadcast_add", ["lhs", "rhs"], hint="broadcast_add"))
 _reg(OpSpec("_contrib_Quantization_int8", ["data"], lambda n: ["minmax"], hint="quantization_int8"))
+# the fork's per-channel scale (data * scaler, scaler (1,C,1,1)): what merge_bn folds a BatchNorm into
+# (core/graph_optimize.py:90-93)
+_reg(OpSpec("_contrib_BroadcastScale", ["data", "scaler"], hint="broadcastscale"))
 _reg(OpSpec("Custom", lambda n: ["data"], hint="custom"))
 
 
@@ -404,11 +407,20 @@ def _infer_node(n, shapes, partial):
     elif op == "SoftmaxOutput":
         _set(shapes, ins[1], (dshape[0],))
         _set(shapes, (n, 0), dshape)
-    elif op in ("_Plus", "broadcast_add", "ElementWiseSum"):
+    elif op in ("_Plus", "ElementWiseSum"):
         for i in ins[1:]:
             s = _shape(shapes, i)
             if s is None:
                 _set(shapes, i, dshape)
+        _set(shapes, (n, 0), dshape)
+    elif op in ("broadcast_add", "_contrib_BroadcastScale"):
+        other = _shape(shapes, ins[1])
+        if other is None:
+            # an unshaped per-channel operand (NCHW): (1, C, 1, 1)
+            other = (1, dshape[1]) + (1,) * (len(dshape) - 2) if op == "_contrib_BroadcastScale" else dshape
+            _set(shapes, ins[1], other)
+        if len(other) != len(dshape) or any(o not in (1, d) for o, d in zip(other, dshape)):
+            raise MXNetError("%s: operand shape %s does not broadcast to %s" % (n.name, other, dshape))
         _set(shapes, (n, 0), dshape)
     elif op == "Concat":
         dim = int(_parse(n.attrs.get("dim", 1)))
@@ -467,7 +479,9 @@ def _create(opname, pos_inputs, kwargs, name, attr=None):
             raise MXNetError("%s: input %s must be a single-output symbol" % (name, an))
         inputs.append(s._outputs[0])
     for an in spec.aux_names(node):
-        s = sym_kwargs.pop(an, None)
+        # aux states may come positionally after the arguments (BatchNorm(*children) in the graph passes
+        # of core/graph_optimize.py:95) or by keyword
+        s = pos.pop(0) if pos else sym_kwargs.pop(an, None)
         if s is None:
             s = Variable("%s_%s" % (name, an))
         inputs.append(s._outputs[0])
@@ -533,6 +547,7 @@ def Group(symbols):
 
 class _Contrib:
     Quantization_int8 = staticmethod(_make("_contrib_Quantization_int8"))
+    BroadcastScale = staticmethod(_make("_contrib_BroadcastScale"))
 
     def __getattr__(self, item):
         raise MXNetError("contrib operator %s is not provided by this runtime" % item)

@@ -285,6 +285,8 @@ class Plan:
                 if relu_node is not None:
                     self.alias[id(relu_node)] = id(n)
                     done.add(id(relu_node))
+            elif op in ("_contrib_BroadcastScale", "broadcast_add"):
+                self._lower_affine(n, cons, done)
             elif op == "Pooling":
                 self._lower_pool(n)
                 done.add(id(n))
@@ -421,6 +423,59 @@ class Plan:
                                momentum=float(_parse(n.attrs.get("momentum", 0.9))),
                                fix_gamma=bool(_parse(n.attrs.get("fix_gamma", True))),
                                use_global_stats=bool(_parse(n.attrs.get("use_global_stats", False)))))
+
+    def _chan_param(self, node_idx, c):
+        """Name of a per-channel parameter Variable ((C,) or (1,C,1,1)), else None."""
+        v = node_idx[0]
+        shp = self.shapes.get((id(v), node_idx[1]))
+        if v.op != "null" or v.name in self.data_names or shp is None:
+            return None
+        if int(np.prod(shp)) != c or (len(shp) == 4 and shp[1] != c):
+            return None
+        return v.name
+
+    def _lower_affine(self, n, cons, done):
+        """Per-channel affine y = [relu](x * scale + bias): the BroadcastScale -> broadcast_add pair that
+        merge_bn folds an inference BatchNorm into (core/graph_optimize.py:90-93), a standalone
+        broadcast_add of a per-channel parameter, or (two same-shape tensors) a plain add."""
+        x = self.tensor(n.inputs[0][0])
+        c = x.c
+        scale = bias = None
+        last = n
+        if n.op == "_contrib_BroadcastScale":
+            scale = self._chan_param(n.inputs[1], c)
+            if scale is None:
+                raise PlanError("%s: BroadcastScale needs a per-channel (1,C,1,1) scaler Variable" % n.name)
+            cl = cons.get(id(n), [])
+            if len(cl) == 1 and cl[0] is not None and cl[0].op == "broadcast_add" and cl[0].inputs[0][0] is n:
+                bias = self._chan_param(cl[0].inputs[1], c)
+                if bias is not None:
+                    last = cl[0]
+        else:
+            bias = self._chan_param(n.inputs[1], c)
+            if bias is None:
+                other = self.tensor(n.inputs[1][0])
+                if other.shape != x.shape:
+                    raise PlanError("%s: broadcast_add of %s and %s not supported" % (n.name, x.shape, other.shape))
+                y = self._new_tensor(n, self.shape_of(n))
+                self.ops.append(PlanOp("add", n.name, a=x, b=other, y=y, relu=False, relu_name=None))
+                done.add(id(n))
+                return
+        if x.kind != "act":
+            raise PlanError("%s: per-channel affine over a non-activation tensor" % n.name)
+        cl = cons.get(id(last), [])
+        relu_node = None
+        if len(cl) == 1 and cl[0] is not None and cl[0].op == "Activation" and \
+                _parse(cl[0].attrs.get("act_type")) == "relu":
+            relu_node = cl[0]
+        y = self._new_tensor(n, self.shape_of(n))
+        self.ops.append(PlanOp("affine", n.name, x=x, y=y, gamma=scale, beta=bias, relu=relu_node is not None,
+                               relu_name=relu_node.name if relu_node is not None else None))
+        done.add(id(n))
+        for extra in (last, relu_node):
+            if extra is not None and extra is not n:
+                self.alias[id(extra)] = id(n)
+                done.add(id(extra))
 
     def _lower_pool(self, n):
         x = self.tensor(n.inputs[0][0])
@@ -795,6 +850,10 @@ class Executor:
                              momentum=op.momentum, fix_gamma=int(op.fix_gamma), relu=int(op.relu))
                 ws_bytes = max(ws_bytes, self.lib.rn_bn_workspace_bytes(L.C.byref(d)))
                 op.desc = d
+            elif op.kind == "affine":
+                d = L.BNDesc(dtype=self.dtype, m=op.x.rows, c=op.x.cp, c_real=op.x.c, eps=0.0, momentum=0.0,
+                             fix_gamma=0, relu=int(op.relu))
+                ws_bytes = max(ws_bytes, self.lib.rn_bn_workspace_bytes(L.C.byref(d)))
             elif op.kind == "stem":
                 x = op.x
                 b = op.bn or {}
@@ -909,6 +968,27 @@ class Executor:
                                         yptr, gamma, self._pp(op.beta), self._ap(op.mean),
                                         self._ap(op.var), op.sm, op.si, op.sc, op.sh, wsp, sp))
                 I.append(infer)
+            elif op.kind == "affine":
+                # y = [relu](x*scale + bias) with per-channel parameters copied into channel-padded
+                # coefficient vectors each forward (set_params / SGD may change them)
+                x, y = op.x, op.y
+                c = x.cp
+                op.buf = self._zeros(4 * c, self.torch.float32)
+                if op.gamma is None:
+                    op.buf[:x.c] = 1.0
+                op.sc, op.sh, op.zero, op.one = [L.C.c_void_p(op.buf.data_ptr() + 4 * c * i) for i in range(4)]
+                op.buf[3 * c:3 * c + x.c] = 1.0
+                op.desc = L.BNDesc(dtype=self.dtype, m=x.rows, c=c, c_real=x.c, eps=0.0, momentum=0.0,
+                                   fix_gamma=int(op.gamma is None), relu=int(op.relu))
+                for nm, dst in ((op.gamma, op.sc), (op.beta, op.sh)):
+                    if nm is not None:
+                        c_ = self._call("rn_cast", x.c, self._pp(nm), F32, dst, F32, sp)
+                        F.append(c_)
+                        I.append(c_)
+                c_ = self._call("rn_bn_apply", L.C.byref(op.desc), self._p(self.act(x)), self._p(self.act(y)),
+                                op.sc, op.sh, sp)
+                F.append(c_)
+                I.append(c_)
             elif op.kind == "relu":
                 c = self._call("rn_eltwise_add", op.x.numel, self.dtype, self._p(self.act(op.x)), None,
                                self._p(self.act(op.y)), 1, sp)
@@ -1112,7 +1192,13 @@ class Executor:
                 x = op.x
                 out, add = (gs.contribute(x) if x.needs_grad else (None, None))
                 w = self._gw.get(id(op.y))
-                if bwd_fusion and w and w[0] == "dgrad" and dy is self._grads.get(id(op.y)) and \
+                if op.use_global_stats:
+                    # moving statistics are constants of the graph (fix_bn): dx = gamma*invstd*dz
+                    self._bwd.append(self._call("rn_bn_bwd_global", L.C.byref(op.desc), self._p(self.act(x)),
+                                                self._p(dy), self._p(out), self._p(add), self._pp(op.gamma),
+                                                self._ap(op.mean), self._ap(op.var), op.sc, op.sh,
+                                                self._gp(op.gamma), self._gp(op.beta), wsp, sp))
+                elif bwd_fusion and w and w[0] == "dgrad" and dy is self._grads.get(id(op.y)) and \
                         op.y.c % 8 == 0 and op.y.c == op.y.cp and (bwd_all or self._big_tile(w[2], 1)):
                     # the conv dgrad that completes this BN's output gradient also reduces its backward
                     # (sum dz, sum dz*(x - mean)); the BN then needs only finalize + apply
@@ -1145,6 +1231,21 @@ class Executor:
                                                 op.sh, self._gp(op.gamma), self._gp(op.beta), wsp, sp))
                 self.param_done_at[op.gamma] = len(self._bwd)
                 self.param_done_at[op.beta] = len(self._bwd)
+            elif op.kind == "affine":
+                # the global-statistics BN backward with mean 0, variance 1, eps 0: dz = dy*[y > 0],
+                # dscale = sum(dz*x), dbias = sum(dz), dx = scale*dz
+                x = op.x
+                out, add = (gs.contribute(x) if x.needs_grad else (None, None))
+                if op.gamma is None or op.beta is None:
+                    op.gscratch = self._zeros(x.cp, self.torch.float32)
+                dg = self._gp(op.gamma) if op.gamma is not None else self._p(op.gscratch)
+                db = self._gp(op.beta) if op.beta is not None else self._p(op.gscratch)
+                self._bwd.append(self._call("rn_bn_bwd_global", L.C.byref(op.desc), self._p(self.act(x)),
+                                            self._p(dy), self._p(out), self._p(add), op.sc, op.zero, op.one,
+                                            op.sc, op.sh, dg, db, wsp, sp))
+                for nm in (op.gamma, op.beta):
+                    if nm is not None:
+                        self.param_done_at[nm] = len(self._bwd)
             elif op.kind == "quant":
                 if op.x.needs_grad:
                     out, add = gs.contribute(op.x)
