@@ -74,6 +74,20 @@ int32_t rn_conv_bn_part_rows(const rn_conv_desc* d, int32_t mode);
  * 128-row kernel. Lets a caller enable the BatchNorm epilogue fusions only where they pay (the
  * 64-column tile has none: with a fused epilogue those layers run the 128-row kernel). */
 int32_t rn_conv_tile(const rn_conv_desc* d, int32_t mode);
+/* Int8 forward of a quantized convolution (resnet_int8 / attach_quantize_node graphs: conv over
+ * Quantization_int8(data) and Quantization_int8(weight), symbol/int8_api.py:120-151). x_codes /
+ * w_codes are the int8 codes (value = code * unit; NHWC / KRSC, channel stride d->c bytes, a multiple
+ * of 16) and x_unit / w_unit device pointers to the per-tensor units: y = unit_x * unit_w * sum of
+ * int8 products, accumulated exactly in int32 by v_mfma_i32_16x16x64_i8 (+ add_src), stored as
+ * y_dtype. part (nullable): the BatchNorm statistics partials of y as rn_conv_fwd_bnstats, with
+ * rn_conv_bn_part_rows(d, 2) rows per block; rn_conv_tile(d, 2) is this kernel's tile columns. */
+int rn_conv_fwd_i8(const rn_conv_desc* d, const void* x_codes, const void* w_codes, void* y, int32_t y_dtype,
+                   const void* add_src, const float* x_unit, const float* w_unit, float* part,
+                   rn_stream_t stream);
+/* w_codes[k][r][s][c] = round(w[k][r][s][c] / unit) (int8, zero for c >= c_real): the int8 compute
+ * copy of a per-tensor quantized weight from the fp32 master (unit from rn_quant_int8_fwd_codes). */
+int rn_conv_weight_pack_i8(const rn_conv_desc* d, const float* w_master, const float* unit, void* w_codes,
+                           rn_stream_t stream);
 #define RN_BN_ACC_REPLICAS 64
 /* As rn_conv_fwd_bnstats / rn_conv_bwd_data_bnred, with the BatchNorm sums accumulated straight into
  * acc = double[RN_BN_ACC_REPLICAS][2][k_pad (fwd) | c (dgrad)] by fp64 atomic adds, each workgroup
@@ -378,6 +392,12 @@ int rn_relu_bwd(int64_t n, int32_t dtype, const void* y, const void* dy, void* d
 int rn_quant_int8_fwd(int32_t dtype, int64_t n, const void* x, void* out, float* minmax,
                       int32_t is_weight, int32_t is_train, float ema_decay, int32_t first_batch,
                       int32_t nbits, float* ws, rn_stream_t stream);
+/* rn_quant_int8_fwd that also writes the int8 codes round(clip(x)/unit) (codes nullable: values
+ * only; n a multiple of 16 when set) and unit[0] = t/qmax (kept for the int8 convolution; nbits <= 8).
+ * out (nullable when codes is set) gets the fake-quantized values as rn_quant_int8_fwd. */
+int rn_quant_int8_fwd_codes(int32_t dtype, int64_t n, const void* x, void* out, void* codes, float* unit,
+                            float* minmax, int32_t is_weight, int32_t is_train, float ema_decay,
+                            int32_t first_batch, int32_t nbits, float* ws, rn_stream_t stream);
 /* STE backward: dx = dy (weights) or dy * (|x| <= t) (activations). */
 int rn_quant_int8_bwd(int32_t dtype, int64_t n, const void* x, const void* dy, void* dx,
                       const float* minmax, int32_t is_weight, const void* add_src,

@@ -69,6 +69,10 @@ struct IgemmArgs {
   // moving mean); EPI 2: sum dz, sum dz * (x - mean).
   double* bnacc;
   const float* bnpiv;
+  // int8 forward (igemm_big_kernel Q8): per-tensor quantization units of the int8 codes in x and w
+  // (Quantization_int8: value = code * unit); the int32 accumulators are scaled by their product
+  const float* qunit_x;
+  const float* qunit_w;
   FastDiv fdS;
   int ncls;
   IgemmCls cls[4];
@@ -675,14 +679,20 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // for every ResNet-50 layer at batch 256, so 256-row tiles leave a last round of 196 / 256 workgroups
 // on every grid; 224-row tiles (7 / 8 of the rows) fill 224 / 256. The A region of the LDS stage
 // keeps 256 rows (the DMA rounds of rows >= BM read zeros).
+// Q8: int8 operands (the int8 codes of Quantization_int8, symbol/int8_api.py:120-171), 128-deep
+// K-tiles of the same 128-byte rows, v_mfma_i32_16x16x64_i8 (exact int32 sums; the A and B fragments
+// take the same 16-byte chunks as the bf16 form, so the LDS images and reads are unchanged), the
+// accumulators scaled by unit_x * unit_w in the epilogue; output bf16 (Q8 1) or fp32 (Q8 2).
 // SC: the stem's small-C modes (64-column tile only), where a DMA lane's chunk of a K-tile is its own
 // tap, so the gathered row offset (and the in-image test) is per lane. SC 1: NHWC with C = 8 (one
 // tap per 16-byte chunk, k = tap * 8 + c). SC 2: the padded NHWC4 image of rn_stem_prepare_p4 (zero
 // border, so no in-image test): k = (r * 8 + s) * 4 + c over r, s < 8 (tap 7 of a row and row 7
 // have zero weights), a chunk = taps (r, 2 j) and (r, 2 j + 1), K-tile t = rows 2 t, 2 t + 1.
-template <int BN, int NBUF, int EPI = 0, bool M32 = false, int BM = 256, int SC = 0>
+template <int BN, int NBUF, int EPI = 0, bool M32 = false, int BM = 256, int SC = 0, int Q8 = 0>
 __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_big_kernel(IgemmArgs p) {
-  constexpr int BMA = 256, CE = 8, BKE = 64;
+  constexpr int ES = Q8 ? 1 : 2;                 // operand bytes per element
+  constexpr int BMA = 256, CE = 16 / ES, BKE = 128 / ES;
+  using OutT = typename std::conditional<Q8 == 2, float, bf16_t>::type;
   constexpr int NW = BN == 64 ? 4 : 8;           // waves
   constexpr int WAVES_N = BN == 64 ? 1 : 4, WAVES_M = NW / WAVES_N;
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;  // wave tile
@@ -693,7 +703,8 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   constexpr int MI = WM / FM, NI = WN / FM;      // accumulators per wave
   constexpr int NCH = (WM + 63) / 64;            // 64-row epilogue chunks per wave
   static_assert(WM % FM == 0 && (BM == 256 || !M32) && (BM == 256 || BN != 64) && (!SC || BN == 64), "tile shape");
-  using AccT = typename std::conditional<M32, v16f, v4f>::type;
+  static_assert(!Q8 || (!M32 && !SC && EPI != 2), "int8: 16x16x64 MFMAs, forward only");
+  using AccT = typename std::conditional<Q8 != 0, v4i, typename std::conditional<M32, v16f, v4f>::type>::type;
   constexpr int kStage = (BMA + BN) * 8;         // 16-byte chunks per K-tile
   constexpr int EP_LD = WN + 4;                  // staged fp32 row stride
   constexpr int EP_WAVE = 64 * EP_LD;            // floats per wave per epilogue half
@@ -817,11 +828,11 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   auto piece = [&](int k) __attribute__((always_inline)) {
     if (k < AR) {
       const bool ok = d_cok && (unsigned)(a_h[k] + d_dh) < (unsigned)p.H && (unsigned)(a_w[k] + d_dw) < (unsigned)p.W;
-      dma16_asm(rs_x, d_la + k * (RPR * 128), ok ? ((uint32_t)((a_row[k] + d_toffa) * 2) & dmask) : kOob);
+      dma16_asm(rs_x, d_la + k * (RPR * 128), ok ? ((uint32_t)((a_row[k] + d_toffa) * ES) & dmask) : kOob);
     } else {
       const int i = k - AR;
       dma16_asm(rs_w, d_la + BMA * 128 + i * (RPR * 128),
-                (d_cok && b_ok[i]) ? ((uint32_t)((b_off[i] + d_toffb) * 2) & dmask) : kOob);
+                (d_cok && b_ok[i]) ? ((uint32_t)((b_off[i] + d_toffb) * ES) & dmask) : kOob);
     }
   };
   // diagnostic (rn_set_tuning 7 bit 8): no DMAs inside the main loop (wrong results; isolates their cost)
@@ -872,8 +883,15 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
       for (int i = 0; i < MI; ++i) {
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          if constexpr (M32) mfma32(acc[i][j], af[ks & 1][i], bfr[ks & 1][j]);
-          else mfma_slab<bf16_t>(acc[i][j], af[ks & 1][i], bfr[ks & 1][j]);
+          if constexpr (Q8) {
+            const uint4 a8 = af[ks & 1][i], b8 = bfr[ks & 1][j];
+            acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(*reinterpret_cast<const v4i*>(&a8),
+                                                               *reinterpret_cast<const v4i*>(&b8), acc[i][j], 0, 0, 0);
+          } else if constexpr (M32) {
+            mfma32(acc[i][j], af[ks & 1][i], bfr[ks & 1][j]);
+          } else {
+            mfma_slab<bf16_t>(acc[i][j], af[ks & 1][i], bfr[ks & 1][j]);
+          }
         }
         // 2 buffers: the DMAs over the first half of the K-tile's MFMA groups, so they have the
         // longest to land; 3 buffers (one more K-tile in flight): spread over all of them
@@ -909,16 +927,18 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < NI; ++j) t += acc[i][j][0];
+      for (int j = 0; j < NI; ++j) t += (float)acc[i][j][0];
     if (lane == 0) reinterpret_cast<float*>(p.y)[v] = t;  // one slot per tile (persistent mode walks several)
     continue;
   }
 
   // ---- epilogue: per wave, 64 accumulator rows at a time through LDS, then 16-byte row chunks
-  constexpr int CPR = WN / 8;  // 16-byte output chunks per wave row
+  constexpr int CPR = WN / 8;  // 8-column output chunks per wave row
+  constexpr int AW = sizeof(OutT) / 2;  // 16-byte pieces per 8-column chunk (bf16 1, fp32 2)
+  const float qscale = Q8 ? p.qunit_x[0] * p.qunit_w[0] : 1.f;
   float* ep = reinterpret_cast<float*>(smem) + wid * EP_WAVE;
-  const bf16_t* __restrict__ ag = reinterpret_cast<const bf16_t*>(p.add);
-  bf16_t* __restrict__ yg = reinterpret_cast<bf16_t*>(p.y);
+  const OutT* __restrict__ ag = reinterpret_cast<const OutT*>(p.add);
+  OutT* __restrict__ yg = reinterpret_cast<OutT*>(p.y);
   const int cc = lane % CPR;
   const int col0 = n0 + wn * WN + cc * 8;
   const bool half_ok = m0 + wm * WM < Mc;  // this wave row holds at least one output row
@@ -942,14 +962,15 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
     constexpr int kLast = WM - 64 * (NCH - 1);  // rows of the last chunk (48 for 112-row waves)
     const int rows_h = h + 1 < NCH ? 64 : kLast;
     int64_t off[CPR];  // this lane's rows: lane / CPR + (64 / CPR) k
-    uint4 addv[CPR];
+    uint4 addv[CPR][AW];
     uint4 xpre[EPI == 2 ? CPR : 1];  // BN input at the same positions (EPI 2), loaded with the residual
 #pragma unroll
     for (int k = 0; k < CPR; ++k) {
       const int r = lane / CPR + (64 / CPR) * k;
       const int m = m0 + wm * WM + h * 64 + r;
       off[k] = -1;
-      addv[k] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < AW; ++u) addv[k][u] = make_uint4(0, 0, 0, 0);
       if constexpr (EPI == 2) xpre[k] = make_uint4(0, 0, 0, 0);
       if (m < Mc && col0 < p.K && r < rows_h) {
         const int n = fdiv(m, cl.fdPQ);
@@ -957,7 +978,9 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
         const int ii = fdiv(rem, cl.fdQ);
         const int jj = rem - ii * cl.Qc;
         off[k] = ((int64_t)(n * p.P + cl.a + p.ostep_h * ii) * p.Q + cl.b + p.ostep_w * jj) * p.ldo + col0;
-        if (ag && col0 + 8 <= p.K) addv[k] = *reinterpret_cast<const uint4*>(ag + off[k]);
+        if (ag && col0 + 8 <= p.K)
+#pragma unroll
+          for (int u = 0; u < AW; ++u) addv[k][u] = reinterpret_cast<const uint4*>(ag + off[k])[u];
         if constexpr (EPI == 2)
           if (col0 + 8 <= p.K) xpre[k] = *reinterpret_cast<const uint4*>(bxg + off[k]);
       }
@@ -980,7 +1003,8 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
           for (int j = 0; j < NI; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              ep[(i * 16 + (lane >> 4) * 4 + e) * EP_LD + j * 16 + (lane & 15)] = acc[h * 4 + i][j][e];
+              ep[(i * 16 + (lane >> 4) * 4 + e) * EP_LD + j * 16 + (lane & 15)] =
+                  Q8 ? (float)acc[h * 4 + i][j][e] * qscale : (float)acc[h * 4 + i][j][e];
     }
     __syncthreads();
     if constexpr (EPI == 1) {
@@ -988,7 +1012,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
                      // (rounded) conv value of each column
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          piv[e] = p.bnacc ? (col0 + e < p.K ? p.bnpiv[col0 + e] : 0.f) : to_f(from_f<bf16_t>(ep[cc * 8 + e]));
+          piv[e] = p.bnacc ? (col0 + e < p.K ? p.bnpiv[col0 + e] : 0.f) : to_f(from_f<OutT>(ep[cc * 8 + e]));
       }
     }
 #pragma unroll
@@ -1001,16 +1025,21 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
       if (col0 + 8 <= p.K) {
         if (ag) {
           float a[8];
-          chunk_to_f(addv[k], a, (const bf16_t*)nullptr);
+#pragma unroll
+          for (int u = 0; u < AW; ++u) chunk_to_f(addv[k][u], a + u * (8 / AW), (const OutT*)nullptr);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += a[e];
         }
-        const uint4 out = f_to_chunk(v, (const bf16_t*)nullptr);
-        if (!(p.sched & 32) || (out.x & 0xFFFF) == 0x7FC1)  // diagnostic bit 32: no output stores
-          *reinterpret_cast<uint4*>(yg + off[k]) = out;
+        uint4 out[AW];
+#pragma unroll
+        for (int u = 0; u < AW; ++u) out[u] = f_to_chunk(v + u * (8 / AW), (const OutT*)nullptr);
+        if (!(p.sched & 32) || (out[0].x & 0xFFFF) == 0x7FC1)  // diagnostic bit 32: no output stores
+#pragma unroll
+          for (int u = 0; u < AW; ++u) reinterpret_cast<uint4*>(yg + off[k])[u] = out[u];
         if constexpr (EPI != 0) {  // on the stored (rounded) values, as a separate pass would read them
           float g[8];
-          chunk_to_f(out, g, (const bf16_t*)nullptr);
+#pragma unroll
+          for (int u = 0; u < AW; ++u) chunk_to_f(out[u], g + u * (8 / AW), (const OutT*)nullptr);
           if constexpr (EPI == 1) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
@@ -1035,7 +1064,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
           if (col0 + e < p.K) {
             float o = v[e];
             if (ag) o += to_f(ag[off[k] + e]);
-            yg[off[k] + e] = from_f<bf16_t>(o);
+            yg[off[k] + e] = from_f<OutT>(o);
           }
       }
     }
@@ -2052,6 +2081,72 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   return rn_check_launch("igemm");
 }
 
+// int8 forward tile columns: the 4-wave 256x64 tile for <= 64 output channels, else the bf16 family's
+// rule (256 columns when the output has >= 256 and the grid keeps >= 192 tiles, else 128)
+int i8_tile_cols(const IgemmArgs& a) {
+  if (a.K <= 64) return 64;
+  const int64_t rows = ceil_div((int64_t)a.N * a.cls[0].Pc * a.cls[0].Qc, 256);
+  return (a.K >= 256 && rows * ceil_div(a.K, 256) >= 192) ? 256 : 128;
+}
+
+// int8 codes (Q8) on igemm_big_kernel: x / w are int8 with channel strides in bytes
+int launch_igemm_i8(const IgemmArgs& a, bool f32out, hipStream_t st) {
+  const int64_t xb = (int64_t)a.N * a.H * a.W * a.C, wb = (int64_t)a.K * a.wrow;
+  RN_CHECK_ARG(xb < INT32_MAX && wb < INT32_MAX, "int8 operands exceed 32-bit buffer offsets");
+  RN_CHECK_ARG(a.C % 16 == 0 && a.gred == 0 && !a.smallc && !a.in_sc && !a.bias && a.ncls == 1,
+               "int8 convolution: dense, channel stride a multiple of 16, no bias / input transform");
+  RN_CHECK_ARG(a.cls[0].nr * a.cls[0].ns <= 32, "int8 convolution: at most 32 taps");
+  const int Mc = a.N * a.cls[0].Pc * a.cls[0].Qc;
+  if (Mc == 0) return 0;
+  IgemmArgs b = a;
+  b.sched = g_tune[RN_TUNE_IGEMM_SCHED];
+  b.x_bytes = (int)xb;
+  b.w_bytes = (int)wb;
+  b.ntiles = 0;
+  const int epi = a.stats ? 1 : 0;
+  const int bn = i8_tile_cols(a);
+  const int bm = bn == 64 ? 256 : 224;
+  b.ntn = (int)ceil_div(a.K, bn);
+  dim3 grid((unsigned)(ceil_div(Mc, bm) * b.ntn), 1, 1);
+  const int g = g_tune[RN_TUNE_IGEMM_PERSIST] / 8 * 8;
+  if (g > 0 && (int)grid.x > g) {
+    b.ntiles = (int)grid.x;
+    grid.x = (unsigned)g;
+  }
+#define RN_I8(BNV, NB, R, T)                                                                                        \
+  if (f32out) {                                                                                                    \
+    if (epi) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 1, false, R, 0, 2>), grid, dim3(T), 0, st, b);        \
+    else hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 0, false, R, 0, 2>), grid, dim3(T), 0, st, b);            \
+  } else {                                                                                                         \
+    if (epi) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 1, false, R, 0, 1>), grid, dim3(T), 0, st, b);        \
+    else hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 0, false, R, 0, 1>), grid, dim3(T), 0, st, b);            \
+  }
+  if (bn == 64) {
+    RN_I8(64, 2, 256, 256)
+  } else if (bn == 128) {
+    RN_I8(128, 3, 224, 512)
+  } else {
+    RN_I8(256, 2, 224, 512)
+  }
+#undef RN_I8
+  return rn_check_launch("igemm_i8");
+}
+
+// int8 codes of the KRSC compute copy: round(w / unit) (Quantization_int8 weight path, per tensor:
+// symbol/quant_ops.py:17-31, unit = max|w| / qmax), zero in the channel padding
+__global__ void pack_krsc_i8_kernel(const float* __restrict__ wm, const float* __restrict__ unit,
+                                    int8_t* __restrict__ out, int K, int RS, int creal, int c) {
+  const float u = *unit;
+  const int64_t total = (int64_t)K * RS * c;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int ci = (int)(i % c);
+    const int64_t kt = i / c;
+    const float v = ci < creal ? wm[kt * creal + ci] : 0.f;
+    out[i] = (int8_t)(u > 0.f ? (int)roundf(v / u) : 0);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -2119,6 +2214,30 @@ int rn_conv_fwd_x(const rn_conv_desc* d, const void* x, const void* w, void* y, 
   return launch_igemm<float, float>(a, st);
 }
 
+int rn_conv_fwd_i8(const rn_conv_desc* d, const void* x_codes, const void* w_codes, void* y, int32_t y_dtype,
+                   const void* add_src, const float* x_unit, const float* w_unit, float* part,
+                   rn_stream_t stream) {
+  RN_CHECK_ARG(d && x_codes && w_codes && y && x_unit && w_unit, "null argument");
+  RN_CHECK_ARG(d->groups <= 1, "int8 convolution is dense");
+  RN_CHECK_ARG(y_dtype == RN_BF16 || y_dtype == RN_F32, "bad output dtype");
+  RN_CHECK_ARG(!part || d->k % 8 == 0, "BatchNorm statistics need whole 8-channel chunks");
+  IgemmArgs a = make_igemm_args(d, 0);
+  a.smallc = 0;
+  a.x = x_codes; a.w = w_codes; a.y = y; a.add = add_src; a.bias = nullptr; a.stats = part;
+  a.qunit_x = x_unit; a.qunit_w = w_unit;
+  return launch_igemm_i8(a, y_dtype == RN_F32, as_stream(stream));
+}
+
+int rn_conv_weight_pack_i8(const rn_conv_desc* d, const float* w_master, const float* unit, void* w_codes,
+                           rn_stream_t stream) {
+  RN_CHECK_ARG(d && w_master && unit && w_codes, "null argument");
+  RN_CHECK_ARG(d->groups <= 1, "int8 convolution is dense");
+  const int64_t total = (int64_t)d->k * d->r * d->s * d->c;
+  hipLaunchKernelGGL(pack_krsc_i8_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), w_master, unit,
+                     (int8_t*)w_codes, d->k, d->r * d->s, d->c_real, d->c);
+  return rn_check_launch("weight_pack_i8");
+}
+
 int rn_conv_fwd(const rn_conv_desc* d, const void* x, const void* w, void* y, int32_t y_dtype,
                 const void* add_src, const float* bias, rn_stream_t stream) {
   return rn_conv_fwd_x(d, x, w, y, y_dtype, add_src, bias, nullptr, nullptr, nullptr, stream);
@@ -2152,6 +2271,7 @@ int rn_conv_bwd_data_bnacc(const rn_conv_desc* d, const void* dy, const void* w_
 }
 
 int32_t rn_conv_tile(const rn_conv_desc* d, int32_t mode) {
+  if (d && mode == 2 && d->groups <= 1) return i8_tile_cols(make_igemm_args(d, 0));  // int8 forward
   if (!d || d->dtype != RN_BF16 || (mode != 0 && mode != 1)) return 0;
   const IgemmArgs a = make_igemm_args(d, mode);
   const int64_t xb = (int64_t)a.N * a.H * a.W * a.C * 2, wb = (int64_t)a.K * a.wrow * 2;
@@ -2159,6 +2279,7 @@ int32_t rn_conv_tile(const rn_conv_desc* d, int32_t mode) {
 }
 
 int32_t rn_conv_bn_part_rows(const rn_conv_desc* d, int32_t mode) {
+  if (d && mode == 2) return rn_conv_tile(d, 2) == 64 ? 64 : 112;  // int8 forward: one wave row
   if (!d || (mode != 0 && mode != 1)) return 0;
   return bn_part_rows(make_igemm_args(d, mode), d->dtype == RN_BF16);
 }

@@ -437,6 +437,40 @@ __global__ void quant_apply_kernel(int64_t n, const T* __restrict__ x, T* __rest
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     out[i] = from_f<T>(quant_value(to_f(x[i]), t, qmax, clip));
 }
+// fake-quantized values AND their int8 codes, 16 elements (one 16-byte code chunk) per thread:
+// code = round(clip(v) / unit) (the value quant_value returns is code * unit), unit[0] = t / qmax
+template <typename T>
+__global__ void quant_codes_kernel(int64_t nchunk, const T* __restrict__ x, T* __restrict__ out,
+                                   int8_t* __restrict__ codes, const float* __restrict__ thr, float qmax, int clip,
+                                   float* __restrict__ unit_out) {
+  const float t = *thr;
+  const float unit = t / qmax;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && unit_out) *unit_out = unit;
+  constexpr int CE = 16 / sizeof(T);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nchunk; i += (int64_t)gridDim.x * blockDim.x) {
+    uint32_t cw[4];
+#pragma unroll
+    for (int h = 0; h < 16 / CE; ++h) {
+      float f[CE];
+      chunk_to_f(reinterpret_cast<const uint4*>(x)[i * (16 / CE) + h], f, (const T*)nullptr);
+#pragma unroll
+      for (int e = 0; e < CE; ++e) {
+        float v = clip ? fminf(fmaxf(f[e], -t), t) : f[e];
+        const float q = unit > 0.f ? roundf(v / unit) : 0.f;
+        f[e] = q * unit;
+        const int j = h * CE + e;
+        const uint32_t b = (uint32_t)(uint8_t)(int8_t)(int)q;
+        if ((j & 3) == 0) cw[j >> 2] = b;
+        else cw[j >> 2] |= b << (8 * (j & 3));
+      }
+      if (out) reinterpret_cast<uint4*>(out)[i * (16 / CE) + h] = f_to_chunk(f, (const T*)nullptr);
+    }
+    reinterpret_cast<uint4*>(codes)[i] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+  }
+}
+__global__ void quant_unit_kernel(const float* __restrict__ thr, float qmax, float* __restrict__ unit_out) {
+  *unit_out = *thr / qmax;
+}
 template <typename T>
 __global__ void quant_bwd_kernel(int64_t n, const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx,
                                  const float* __restrict__ minmax, int is_weight, const T* __restrict__ add) {
@@ -729,6 +763,46 @@ int rn_quant_int8_fwd(int32_t dtype, int64_t n, const void* x, void* out, float*
     hipLaunchKernelGGL(quant_apply_kernel<float>, dim3(grid1d(n)), dim3(256), 0, st, n, (const float*)x,
                        (float*)out, thr, qmax, clip);
   return rn_check_launch("quant_int8_fwd");
+}
+
+int rn_quant_int8_fwd_codes(int32_t dtype, int64_t n, const void* x, void* out, void* codes, float* unit,
+                            float* minmax, int32_t is_weight, int32_t is_train, float ema_decay, int32_t first_batch,
+                            int32_t nbits, float* ws, rn_stream_t stream) {
+  RN_CHECK_ARG(x && ws && unit && n > 0 && (out || codes), "bad arguments");
+  RN_CHECK_ARG(nbits >= 2 && nbits <= 8, "int8 codes need nbits <= 8");
+  RN_CHECK_ARG(!codes || n % 16 == 0, "int8 codes: n must be a multiple of 16");
+  if (!codes) {  // the fake-quantized values (and the unit) only
+    if (rn_quant_int8_fwd(dtype, n, x, out, minmax, is_weight, is_train, ema_decay, first_batch, nbits, ws, stream))
+      return -1;
+    hipLaunchKernelGGL(quant_unit_kernel, dim3(1), dim3(1), 0, as_stream(stream), ws + 1,
+                       (float)((1 << (nbits - 1)) - 1), unit);
+    return rn_check_launch("quant_int8_unit");
+  }
+  RN_CHECK_ARG(is_weight || minmax, "activation quantization needs the minmax state");
+  hipStream_t st = as_stream(stream);
+  const float qmax = (float)((1 << (nbits - 1)) - 1);
+  float* curmax = ws;
+  float* thr = ws + 1;
+  hipMemsetAsync(curmax, 0, sizeof(float), st);
+  if (is_weight || is_train) {
+    if (dtype == RN_BF16)
+      hipLaunchKernelGGL(absmax_kernel<bf16_t>, dim3(grid1d(n, 256, 1024)), dim3(256), 0, st, n, (const bf16_t*)x,
+                         curmax);
+    else
+      hipLaunchKernelGGL(absmax_kernel<float>, dim3(grid1d(n, 256, 1024)), dim3(256), 0, st, n, (const float*)x,
+                         curmax);
+  }
+  hipLaunchKernelGGL(quant_state_kernel, dim3(1), dim3(1), 0, st, curmax, minmax, is_weight, is_train, ema_decay,
+                     first_batch, thr);
+  const int clip = is_weight ? 0 : 1;
+  const int64_t nc = n / 16;
+  if (dtype == RN_BF16)
+    hipLaunchKernelGGL(quant_codes_kernel<bf16_t>, dim3(grid1d(nc)), dim3(256), 0, st, nc, (const bf16_t*)x,
+                       (bf16_t*)out, (int8_t*)codes, thr, qmax, clip, unit);
+  else
+    hipLaunchKernelGGL(quant_codes_kernel<float>, dim3(grid1d(nc)), dim3(256), 0, st, nc, (const float*)x,
+                       (float*)out, (int8_t*)codes, thr, qmax, clip, unit);
+  return rn_check_launch("quant_int8_fwd_codes");
 }
 
 int rn_quant_int8_bwd(int32_t dtype, int64_t n, const void* x, const void* dy, void* dx, const float* minmax,

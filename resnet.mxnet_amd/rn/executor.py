@@ -306,6 +306,28 @@ class Plan:
                 raise PlanError("operator %s (%s) is not supported by the MI355X runtime" % (op, n.name))
         self.outputs = [self.tensor(n) for n, _ in self.symbol._outputs]
         self._fuse_bn_apply()
+        self._mark_int8()
+
+    def _mark_int8(self):
+        """Quantized convolutions (a Quantization_int8 on both the data and the weight: resnet_int8,
+        attach_quantize_node) whose input quantizer can also emit int8 codes run their forward on the
+        int8 MFMAs (rn_conv_fwd_i8): exact integer sums of the codes, scaled by the two units, instead
+        of bf16 / fp32 products of the fake-quantized values. RN_INT8_MFMA=0: the fake-quant path."""
+        producer = {id(op.y): op for op in self.ops if op.kind == "quant"}
+        on = os.environ.get("RN_INT8_MFMA", "1") != "0"
+        for op in self.ops:
+            if op.kind == "quant":
+                op.emit_codes = False
+        for op in self.ops:
+            if op.kind != "conv":
+                continue
+            q = producer.get(id(op.x))
+            op.int8 = bool(on and op.qweight is not None and q is not None and op.groups == 1 and
+                           op.x.cp % 16 == 0 and q.q["nbits"] <= 8 and op.qweight["nbits"] <= 8 and
+                           getattr(op, "xf", None) is None)
+            op.qsrc = q if op.int8 else None
+            if op.int8:
+                q.emit_codes = True
 
     def _fuse_bn_apply(self):
         """BatchNorm+ReLU whose output feeds ONLY 1x1 convolutions (act1 -> conv1 / sc, act3 -> conv3
@@ -935,9 +957,21 @@ class Executor:
                 d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad, op.groups)
                 assert (d.p, d.q) == (y.h, y.w), (op.name, d.p, d.q, y.h, y.w)
                 op.desc = d
-                op.wk = self._zeros(self.lib.rn_conv_pack_numel(L.C.byref(d), 0), self.tdtype)
                 op.wc = self._zeros(self.lib.rn_conv_pack_numel(L.C.byref(d), 1), self.tdtype)
-                self._add_pack(op, d, op.wk, op.wc, sp)
+                if getattr(op, "int8", False):
+                    # forward copy: the int8 codes (KRSC); the data-gradient copy stays the
+                    # fake-quantized values in the compute dtype (STE backward)
+                    op.wk = None
+                    self._add_pack(op, d, None, op.wc, sp)
+                    op.wk8 = self.torch.zeros(int(self.lib.rn_conv_pack_numel(L.C.byref(d), 0)),
+                                              dtype=self.torch.int8, device=self.device)
+                    c_ = self._call("rn_conv_weight_pack_i8", L.C.byref(d), self._pp(op.weight), self._p(op.wunit),
+                                    self._p(op.wk8), sp)
+                    self.packs.append(c_)
+                    self.unfused_packs.append(c_)
+                else:
+                    op.wk = self._zeros(self.lib.rn_conv_pack_numel(L.C.byref(d), 0), self.tdtype)
+                    self._add_pack(op, d, op.wk, op.wc, sp)
                 res = self._p(self.act(op.res)) if op.res is not None else None
                 xin = self._p(self.act(op.xf.x)) if op.xf is not None else self._p(self.act(x))
                 I.append(self._conv_fwd_call(op, d, xin, res, sp, stats=False))
@@ -996,10 +1030,19 @@ class Executor:
                 I.append(c)
             elif op.kind == "quant":
                 q = op.q
+                if op.emit_codes:  # + the int8 codes and unit the consumers' int8 forward reads
+                    op.codes = self.torch.zeros(op.x.numel, dtype=self.torch.int8, device=self.device)
+                    op.unit = self._zeros(1, self.torch.float32)
                 for lst, tr in ((F, 1), (I, 0)):
-                    lst.append(self._call("rn_quant_int8_fwd", self.dtype, op.x.numel, self._p(self.act(op.x)),
-                                          self._p(self.act(op.y)), self._ap(q["minmax"]), 0, tr, q["ema"],
-                                          self._qfirst, q["nbits"], qwsp, sp))
+                    if op.emit_codes:
+                        lst.append(self._call("rn_quant_int8_fwd_codes", self.dtype, op.x.numel,
+                                              self._p(self.act(op.x)), self._p(self.act(op.y)), self._p(op.codes),
+                                              self._p(op.unit), self._ap(q["minmax"]), 0, tr, q["ema"],
+                                              self._qfirst, q["nbits"], qwsp, sp))
+                    else:
+                        lst.append(self._call("rn_quant_int8_fwd", self.dtype, op.x.numel, self._p(self.act(op.x)),
+                                              self._p(self.act(op.y)), self._ap(q["minmax"]), 0, tr, q["ema"],
+                                              self._qfirst, q["nbits"], qwsp, sp))
             elif op.kind == "add":
                 c = self._call("rn_eltwise_add", op.y.numel, self.dtype, self._p(self.act(op.a)),
                                self._p(self.act(op.b)), self._p(self.act(op.y)), int(op.relu), sp)
@@ -1052,6 +1095,11 @@ class Executor:
         variant on the 128/256-column tiles only)?"""
         if op.kind != "conv" or self.lib is None:
             return False
+        if getattr(op, "int8", False):  # the int8 forward's tile (mode 0 only)
+            x, y = op.x, op.y
+            d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad, op.groups)
+            mc = min_cols if min_cols is not None else int(os.environ.get("RN_BN_FUSION_MIN_COLS", "128"))
+            return mode == 0 and int(self.lib.rn_conv_tile(L.C.byref(d), 2)) >= mc
         if min_cols is None:  # RN_BN_FUSION_MIN_COLS=64: also on the 64-column tile (opt-in: measured
             min_cols = int(os.environ.get("RN_BN_FUSION_MIN_COLS", "128"))  # 0.6 % slower per step)
         x, y = op.x, op.y
@@ -1062,6 +1110,16 @@ class Executor:
         """Conv forward; emits the next BatchNorm's statistics when one consumes y (training), and
         applies the producing BatchNorm+ReLU on load when that BN is fused (op.xf)."""
         y = self._p(self.act(op.y))
+        if getattr(op, "int8", False):
+            part = None
+            if stats and op.bnstats:
+                if getattr(op, "part", None) is None:
+                    op.part_rows = int(self.lib.rn_conv_bn_part_rows(L.C.byref(d), 2))
+                    op.part_blocks = -(-op.y.rows // op.part_rows)
+                    op.part = self._zeros(op.part_blocks * 3 * op.y.cp, self.torch.float32)
+                part = self._p(op.part)
+            return self._call("rn_conv_fwd_i8", L.C.byref(d), self._p(op.qsrc.codes), self._p(op.wk8), y,
+                              self.dtype, res, self._p(op.qsrc.unit), self._p(op.wunit), part, sp)
         xf = getattr(op, "xf", None)
         sc, sh = (xf.sc, xf.sh) if xf is not None else (None, None)
         part = None
@@ -1087,8 +1145,13 @@ class Executor:
         q = op.qweight
         n = int(np.prod(self.plan.param_shape(op.weight)))
         op.qw = self._zeros(n, self.torch.float32)
-        c = self._call("rn_quant_int8_fwd", F32, n, self._pp(op.weight), self._p(op.qw),
-                       self._ap(q["minmax"]), 1, 1, q["ema"], 0, q["nbits"], qwsp, sp)
+        if getattr(op, "int8", False):  # also keeps the unit for the int8 codes of the forward copy
+            op.wunit = self._zeros(1, self.torch.float32)
+            c = self._call("rn_quant_int8_fwd_codes", F32, n, self._pp(op.weight), self._p(op.qw), None,
+                           self._p(op.wunit), self._ap(q["minmax"]), 1, 1, q["ema"], 0, q["nbits"], qwsp, sp)
+        else:
+            c = self._call("rn_quant_int8_fwd", F32, n, self._pp(op.weight), self._p(op.qw),
+                           self._ap(q["minmax"]), 1, 1, q["ema"], 0, q["nbits"], qwsp, sp)
         self.packs.append(c)
         self.unfused_packs.append(c)
         return self._p(op.qw)

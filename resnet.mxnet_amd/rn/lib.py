@@ -43,6 +43,8 @@ SIGNATURES = {
     "rn_conv_bnstats_blocks": (_i64, [_P]),
     "rn_conv_bn_part_rows": (_i32, [_P, _i32]),
     "rn_conv_tile": (_i32, [_P, _i32]),
+    "rn_conv_fwd_i8": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P, _P]),
+    "rn_conv_weight_pack_i8": (_i32, [_P, _P, _P, _P, _P]),
     "rn_conv_fwd_x": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_filter_x": (_i32, [_P, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_data_bnred": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P, _P]),
@@ -93,6 +95,7 @@ SIGNATURES = {
     "rn_eltwise_add": (_i32, [_i64, _i32, _P, _P, _P, _i32, _P]),
     "rn_relu_bwd": (_i32, [_i64, _i32, _P, _P, _P, _P, _P]),
     "rn_quant_int8_fwd": (_i32, [_i32, _i64, _P, _P, _P, _i32, _i32, _f32, _i32, _i32, _P, _P]),
+    "rn_quant_int8_fwd_codes": (_i32, [_i32, _i64, _P, _P, _P, _P, _P, _i32, _i32, _f32, _i32, _i32, _P, _P]),
     "rn_quant_int8_bwd": (_i32, [_i32, _i64, _P, _P, _P, _P, _i32, _P, _P]),
     "rn_set_tuning": (_i32, [_i32, _i32]),
     "rn_last_error": (C.c_char_p, []),

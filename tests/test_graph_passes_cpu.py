@@ -145,6 +145,34 @@ def test_attach_quantize_node_graph_and_plan(dry):
     assert sum(1 for n in q.list_auxiliary_states() if n.endswith("_minmax")) == 100
 
 
+def test_int8_forward_plan(dry, monkeypatch):
+    """Quantized convs whose data quantizer is a separate op run the int8 MFMA forward (rn_conv_fwd_i8)
+    fed by the quantizer's codes (rn_quant_int8_fwd_codes); the stem (quantizer folded into its
+    im2col) and fc1 stay on the fake-quant path; RN_INT8_MFMA=0 turns it off."""
+    shape = (2, 3, 64, 64)
+    for sym, nconv in ((graphs.resnet_int8(*R50_SMALL.values()), 52),
+                       (attach_quantize_node(graphs.resnet(**R50_SMALL), shape_dict(graphs.resnet(**R50_SMALL), shape,
+                                                                                     (2,)),
+                                             QSET["weight"], QSET["act"], ("Convolution", "FullyConnected"),
+                                             {"Convolution": 1, "FullyConnected": 1}), 52)):
+        for prec in ("float32", "bfloat16"):
+            ex = _bind(sym, shape, precision=prec).executor
+            convs = [op for op in ex.plan.ops if op.kind == "conv"]
+            assert len(convs) == nconv and all(op.int8 for op in convs)
+            names = _call_names(ex._fwd_train)
+            assert names.count("rn_conv_fwd_i8") == nconv
+            # only the stem and fc1 keep a fake-quant / float forward
+            assert sum(1 for nm in names if nm.startswith("rn_conv_fwd") and nm != "rn_conv_fwd_i8") <= 2
+            assert _call_names(ex._fwd_infer).count("rn_conv_fwd_i8") == nconv
+            qops = [op for op in ex.plan.ops if op.kind == "quant"]
+            # every conv's data quantizer emits codes (fc1's, in resnet_int8, does not)
+            assert names.count("rn_quant_int8_fwd_codes") == sum(op.emit_codes for op in qops) >= len(qops) - 1
+            assert _call_names(ex.packs).count("rn_conv_weight_pack_i8") == nconv
+    monkeypatch.setenv("RN_INT8_MFMA", "0")
+    ex = _bind(graphs.resnet_int8(*R50_SMALL.values()), shape).executor
+    assert "rn_conv_fwd_i8" not in _call_names(ex._fwd_train)
+
+
 # ----------------------------------------------------------------------------- oracle restatements
 def test_oracle_attach_quant_equals_resnet_int8():
     """attach_quant with nothing skipped (8 bits) computes what resnet_int8's graph computes (same

@@ -1,0 +1,162 @@
+"""Int8 MFMA forward of quantized convolutions (rn_conv_fwd_i8, v_mfma_i32_16x16x64_i8) and the int8
+codes of Quantization_int8 (rn_quant_int8_fwd_codes, rn_conv_weight_pack_i8).
+
+The reference computes a quantized conv in fp32 on fake-quantized values (symbol/int8_api.py:120-151,
+values code * unit, symbol/quant_ops.py:17-31, clip_grad_quantization_int8.py:37-54). On the integer
+grid the sum of code products is exact; the kernel keeps it exact in int32 and applies unit_x * unit_w
+once. Bars: the integer sums exactly (fp32 output with unit 1, |sum| < 2^24); with real units, fp32
+output within 2 ulp-scale (4e-7 relative) of the fp64 value, bf16 output within bf16 rounding (2^-8);
+codes and units bit-identical to the fake-quant values the same call writes (value == code * unit).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ops
+from rn import lib as L
+from gpu_util import BF16, F32, conv_desc, from_nhwc, p, rel_err, stream, tdt, to_nhwc
+
+pytestmark = pytest.mark.gpu
+
+CASES = [
+    # n, c, h, w, k, r, stride, pad  (c a multiple of 16)
+    (2, 64, 14, 14, 64, 1, 1, 0),      # 64-column tile
+    (2, 64, 14, 14, 256, 1, 1, 0),     # 224 x 128 / 256 tiles
+    (2, 128, 14, 14, 128, 3, 1, 1),    # 3x3: 9 taps x one 128-deep K-tile
+    (3, 256, 9, 7, 512, 3, 2, 1),      # strided 3x3, ragged M
+    (2, 32, 8, 8, 24, 1, 1, 0),        # ragged K (24 columns), partial K-tile
+    (1, 512, 7, 7, 2048, 1, 1, 0),     # stage-4 conv3 shape
+    (2, 64, 56, 56, 256, 1, 1, 0),     # many tiles: persistent walk
+]
+
+
+def _codes(rng, shape, qmax=127):
+    return rng.integers(-qmax, qmax + 1, size=shape)
+
+
+def _run(gpu, case, y_dtype, ux, uw, res=None, part=None):
+    n, c, h, w, k, r, st, pd = case
+    rng = np.random.default_rng(sum(case))
+    xc = _codes(rng, (n, c, h, w))
+    wc = _codes(rng, (k, c, r, r))
+    d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd)
+    assert d.c % 16 == 0
+    xd = torch.from_numpy(np.ascontiguousarray(xc.transpose(0, 2, 3, 1)).astype(np.int8)).to(gpu)
+    wd = torch.from_numpy(np.ascontiguousarray(wc.transpose(0, 2, 3, 1)).astype(np.int8)).reshape(-1).to(gpu)
+    P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+    y = torch.zeros((n, P, Q, d.k_pad), dtype=tdt(y_dtype), device=gpu)
+    uxd = torch.tensor([ux], dtype=torch.float32, device=gpu)
+    uwd = torch.tensor([uw], dtype=torch.float32, device=gpu)
+    rd = to_nhwc(res, y_dtype, gpu) if res is not None else None
+    L.call("rn_conv_fwd_i8", C.byref(d), p(xd), p(wd), p(y), y_dtype, p(rd), p(uxd), p(uwd), p(part), stream())
+    torch.cuda.synchronize()
+    exact = ops.conv2d_fwd(xc.astype(np.float64), wc.astype(np.float64), (st, st), (pd, pd))  # exact integers
+    return d, from_nhwc(y, k), exact
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_int8_conv_exact_integer_sums(gpu, case):
+    _, y, exact = _run(gpu, case, F32, 1.0, 1.0)
+    assert np.abs(exact).max() < 2 ** 24
+    np.testing.assert_array_equal(y, exact)
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("y_dtype", [F32, BF16])
+@pytest.mark.parametrize("persist", [512, 8], ids=["persist512", "persist8"])
+def test_int8_conv_scaled_residual(gpu, case, y_dtype, persist):
+    n, c, h, w, k, r, st, pd = case
+    L.call("rn_set_tuning", 10, persist)
+    try:
+        P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+        res = np.random.default_rng(3).standard_normal((n, k, P, Q))
+        if y_dtype == BF16:
+            res = from_nhwc(to_nhwc(res, BF16, "cpu"), k)
+        ux, uw = 0.0123, 0.00071
+        _, y, exact = _run(gpu, case, y_dtype, ux, uw, res=res)
+    finally:
+        L.call("rn_set_tuning", 10, 512)
+    ref = exact * (np.float64(np.float32(ux)) * np.float64(np.float32(uw))) + res
+    assert rel_err(y, ref) < (4e-7 if y_dtype == F32 else 2 ** -8), rel_err(y, ref)
+
+
+@pytest.mark.parametrize("case", [CASES[1], CASES[2], CASES[0]])
+@pytest.mark.parametrize("y_dtype", [F32, BF16])
+def test_int8_conv_bnstats_epilogue(gpu, case, y_dtype):
+    """BatchNorm statistics partials of the int8 conv's stored output (rn_conv_bn_part_rows(d, 2))
+    merged by rn_bn_fwd_train_part == the batch mean / variance of that output."""
+    n, c, h, w, k, r, st, pd = case
+    lib = L.load()
+    d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd)
+    rows = lib.rn_conv_bn_part_rows(C.byref(d), 2)
+    assert rows in (64, 112)
+    P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+    nblk = -(-(n * P * Q) // rows)
+    part = torch.zeros(nblk * 3 * d.k_pad, dtype=torch.float32, device=gpu)
+    _, y, _ = _run(gpu, case, y_dtype, 0.01, 0.002, part=part)
+    bd = L.BNDesc(dtype=y_dtype, m=n * P * Q, c=d.k_pad, c_real=k, eps=1e-5, momentum=0.9, fix_gamma=0, relu=0)
+    f = lambda a: torch.tensor(np.pad(a, (0, d.k_pad - k)), dtype=torch.float32, device=gpu)
+    g_d, b_d, mm, mv = f(np.ones(k)), f(np.zeros(k)), f(np.zeros(k)), f(np.ones(k))
+    sm, si, sc, sh = [torch.zeros(d.k_pad, dtype=torch.float32, device=gpu) for _ in range(4)]
+    ws = torch.zeros(lib.rn_bn_workspace_bytes(C.byref(bd)) // 4 + 16, dtype=torch.float32, device=gpu)
+    ydev = to_nhwc(y, y_dtype, gpu, d.k_pad)
+    yb = torch.zeros_like(ydev)
+    L.call("rn_bn_fwd_train_part", C.byref(bd), p(part), nblk, rows, d.k_pad, p(ydev), p(yb), p(g_d), p(b_d), p(mm),
+           p(mv), p(sm), p(si), p(sc), p(sh), p(ws), stream())
+    torch.cuda.synchronize()
+    assert rel_err(sm.cpu().numpy()[:k], y.mean(axis=(0, 2, 3))) < 1e-5
+    var = y.var(axis=(0, 2, 3))
+    assert rel_err(1.0 / si.cpu().numpy()[:k] ** 2 - 1e-5, var) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("is_weight", [0, 1])
+def test_quant_codes_match_values(gpu, dtype, is_weight):
+    """rn_quant_int8_fwd_codes: the fake-quantized output equals rn_quant_int8_fwd's, and equals
+    code * unit (fp32; for bf16 its rounding); the EMA state updates as the plain call does."""
+    rng = np.random.default_rng(7)
+    n = 4096
+    x = torch.tensor(rng.standard_normal(n) * 2.0, dtype=tdt(dtype), device=gpu)
+    out1 = torch.zeros_like(x)
+    out2 = torch.zeros_like(x)
+    codes = torch.zeros(n, dtype=torch.int8, device=gpu)
+    unit = torch.zeros(1, dtype=torch.float32, device=gpu)
+    ws = torch.zeros(4096, dtype=torch.float32, device=gpu)
+    mm1 = torch.tensor([1.5], dtype=torch.float32, device=gpu)
+    mm2 = mm1.clone()
+    L.call("rn_quant_int8_fwd", dtype, n, p(x), p(out1), p(mm1), is_weight, 1, 0.99, 0, 8, p(ws), stream())
+    L.call("rn_quant_int8_fwd_codes", dtype, n, p(x), p(out2), p(codes), p(unit), p(mm2), is_weight, 1, 0.99, 0, 8,
+           p(ws), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out2)
+    assert torch.equal(mm1, mm2)
+    u = unit.item()
+    t = (x.abs().max().item() if is_weight else mm2.item())
+    assert u == np.float32(np.float32(t) / np.float32(127))
+    val = codes.cpu().numpy().astype(np.float32) * np.float32(u)
+    want = torch.tensor(val).to(tdt(dtype)).float().numpy()
+    np.testing.assert_array_equal(out2.float().cpu().numpy(), want)
+    assert np.abs(codes.cpu().numpy()).max() <= 127
+
+
+def test_weight_pack_i8(gpu):
+    rng = np.random.default_rng(9)
+    k, c, r = 40, 48, 3
+    d = conv_desc(BF16, 1, c, 8, 8, k, r, r, 1, 1)
+    wt = rng.standard_normal((k, c, r, r)).astype(np.float32)
+    master = torch.from_numpy(np.ascontiguousarray(wt.transpose(0, 2, 3, 1))).reshape(-1).to(gpu)
+    qw = torch.zeros_like(master)
+    unit = torch.zeros(1, dtype=torch.float32, device=gpu)
+    ws = torch.zeros(4096, dtype=torch.float32, device=gpu)
+    L.call("rn_quant_int8_fwd_codes", F32, master.numel(), p(master), p(qw), None, p(unit), None, 1, 1, 0.99, 0, 8,
+           p(ws), stream())
+    wk8 = torch.zeros(k * r * r * d.c, dtype=torch.int8, device=gpu)
+    L.call("rn_conv_weight_pack_i8", C.byref(d), p(master), p(unit), p(wk8), stream())
+    torch.cuda.synchronize()
+    codes = wk8.cpu().numpy().reshape(k, r, r, d.c)
+    assert not codes[..., c:].any()
+    u = np.float32(unit.item())
+    qv = qw.cpu().numpy().reshape(k, r, r, c)
+    np.testing.assert_array_equal(codes[..., :c].astype(np.float32) * u, qv)

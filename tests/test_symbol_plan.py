@@ -145,7 +145,10 @@ def test_plan_int8_quantization():
                        [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")
     names = [c[0] for c in ex._bwd]
     assert names.count("rn_quant_int8_bwd") == 17 and names.count("rn_stem_quant_clip_grad") == 1
-    assert [c[0] for c in ex.packs].count("rn_quant_int8_fwd") == 18
+    packs = [c[0] for c in ex.packs]
+    # the 16 non-stem convs' weight quantizers also keep the unit of their int8 codes (int8 forward)
+    assert packs.count("rn_quant_int8_fwd") + packs.count("rn_quant_int8_fwd_codes") == 18
+    assert packs.count("rn_conv_weight_pack_i8") == 16
 
 
 def test_plan_bn_apply_fusion_opt_in(monkeypatch):
