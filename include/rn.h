@@ -388,7 +388,8 @@ int rn_relu_bwd(int64_t n, int32_t dtype, const void* y, const void* dy, void* d
  * semantics from symbol/quant_ops.py:12-42 / clip_grad_quantization_int8.py:14-67.
  * ------------------------------------------------------------------------------------- */
 /* out = round(clip(x, -t, t) / (t/qmax)) * (t/qmax) with t = max|x| (weights) or the EMA
- * minmax state (activations, updated in place when is_train). ws: >= 4096 floats. */
+ * minmax state (activations, updated in place when is_train). ws: >= 4096 floats whose ws[0] is
+ * zero on entry (a zeroed buffer; every quantizer call leaves it zero, so one workspace serves all). */
 int rn_quant_int8_fwd(int32_t dtype, int64_t n, const void* x, void* out, float* minmax,
                       int32_t is_weight, int32_t is_train, float ema_decay, int32_t first_batch,
                       int32_t nbits, float* ws, rn_stream_t stream);

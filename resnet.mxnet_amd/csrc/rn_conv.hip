@@ -1725,9 +1725,10 @@ __global__ void stem_affine_absmax_kernel(const float* __restrict__ x, const flo
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(out), __float_as_uint(m));
 }
-__global__ void stem_quant_state_kernel(const float* __restrict__ curmax, float* minmax, int is_train, float decay,
+__global__ void stem_quant_state_kernel(float* __restrict__ curmax, float* minmax, int is_train, float decay,
                                         int first, float* __restrict__ thr) {
   *thr = quant_state_update(*curmax, minmax, 0, is_train, decay, first);
+  *curmax = 0.f;  // the quantizers' shared-workspace invariant (rn_quant_int8_fwd): ws[0] left zero
 }
 // The activation STE zeroes the gradient where |v| >= t (clip_grad_quantization_int8.py:56-67).
 // rn_stem_shift_grad sums the unmasked gradient; subtract the clipped elements' share:
@@ -1738,32 +1739,55 @@ __global__ void stem_clip_grad_kernel(const float* __restrict__ x, const float* 
                                       const T* __restrict__ dy, const float* __restrict__ wq,
                                       float* __restrict__ dbeta, int N, int C, int H, int W, int P, int Q, int K,
                                       int kpad, int R, int S, int sh, int sw, int ph, int pw) {
+  // A wave tests 64 consecutive input elements, then processes each clipped one (ballot) together:
+  // lanes over the output channels k (coalesced dy rows), taps in a uniform loop, one wave sum and
+  // one atomic per clipped element (no lane runs a long gather while the other 63 wait).
   const float t = *thr;
-  const int64_t total = (int64_t)N * C * H * W;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int w = (int)(i % W);
-    const int h = (int)((i / W) % H);
-    const int c = (int)((i / ((int64_t)H * W)) % C);
-    const int n = (int)(i / ((int64_t)C * H * W));
-    float v = x[i];
-    if (scale) v = fmaf(v, scale[c], shift[c]);
-    if (v > -t && v < t) continue;
-    float g = 0.f;
-    for (int r = 0; r < R; ++r) {
-      const int hp = h + ph - r;
-      if (hp < 0 || hp % sh) continue;
-      const int pp = hp / sh;
-      if (pp >= P) continue;
-      for (int s = 0; s < S; ++s) {
-        const int wp = w + pw - s;
-        if (wp < 0 || wp % sw) continue;
-        const int qq = wp / sw;
-        if (qq >= Q) continue;
-        const T* dyp = dy + (((int64_t)n * P + pp) * Q + qq) * kpad;
-        for (int k = 0; k < K; ++k) g += wq[((int64_t)(k * R + r) * S + s) * C + c] * to_f(dyp[k]);
-      }
+  const int HW = H * W, total = N * C * HW;
+  const int lane = threadIdx.x & 63;
+  // per-wave channel sums in LDS (the stem has C <= 8 channels: per-element atomics on them would
+  // serialise), one atomic per channel and block at the end
+  __shared__ float wsum[4][8];
+  if (threadIdx.x < 32) wsum[threadIdx.x >> 3][threadIdx.x & 7] = 0.f;
+  __syncthreads();
+  const int nw = gridDim.x * (blockDim.x >> 6);
+  for (int base = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; base < total; base += nw * 64) {
+    const int i = base + lane;
+    bool clipped = false;
+    if (i < total) {
+      const int c = (i / HW) % C;
+      const float v = scale ? fmaf(x[i], scale[c], shift[c]) : x[i];
+      clipped = !(v > -t && v < t);
     }
-    atomicAdd(dbeta + c, -g);
+    uint64_t m = __ballot(clipped);
+    while (m) {
+      const int e = base + __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      const int plane = e / HW, hw = e - plane * HW;
+      const int c = plane % C, n = plane / C, h = hw / W, w = hw - (hw / W) * W;
+      float g = 0.f;
+      for (int r = 0; r < R; ++r) {
+        const int hp = h + ph - r;
+        if (hp < 0 || hp % sh) continue;
+        const int pp = hp / sh;
+        if (pp >= P) continue;
+        for (int s_ = 0; s_ < S; ++s_) {
+          const int wp = w + pw - s_;
+          if (wp < 0 || wp % sw) continue;
+          const int qq = wp / sw;
+          if (qq >= Q) continue;
+          const T* dyp = dy + (((int64_t)n * P + pp) * Q + qq) * kpad;
+          for (int k = lane; k < K; k += 64) g += wq[((int64_t)(k * R + r) * S + s_) * C + c] * to_f(dyp[k]);
+        }
+      }
+      g = wave_sum(g);
+      if (lane == 0) wsum[threadIdx.x >> 6][c] -= g;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < C) {
+    const float v = wsum[0][threadIdx.x] + wsum[1][threadIdx.x] + wsum[2][threadIdx.x] + wsum[3][threadIdx.x];
+    if (v != 0.f) atomicAdd(dbeta + threadIdx.x, v);
   }
 }
 
@@ -2692,12 +2716,15 @@ int rn_stem_quant_clip_grad(const rn_conv_desc* d, const float* x, const float* 
   RN_CHECK_ARG(d && x && minmax && dy && w_q && dbeta, "null argument");
   hipStream_t st = as_stream(stream);
   const int64_t total = (int64_t)d->n * d->c_real * d->h * d->w;
+  RN_CHECK_ARG(total < (1ll << 31) - 64, "input exceeds 2^31 elements");
+  RN_CHECK_ARG(d->c_real <= 8, "the quantized stem has at most 8 input channels");
+  const int planes = grid_for(total);  // (blocks of 4 waves x 64 elements)
   if (d->dtype == RN_BF16)
-    hipLaunchKernelGGL(stem_clip_grad_kernel<bf16_t>, dim3(grid_for(total)), dim3(256), 0, st, x, scale, shift,
+    hipLaunchKernelGGL(stem_clip_grad_kernel<bf16_t>, dim3(planes), dim3(256), 0, st, x, scale, shift,
                        minmax, (const bf16_t*)dy, w_q, dbeta, d->n, d->c_real, d->h, d->w, d->p, d->q, d->k, d->k_pad,
                        d->r, d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w);
   else
-    hipLaunchKernelGGL(stem_clip_grad_kernel<float>, dim3(grid_for(total)), dim3(256), 0, st, x, scale, shift,
+    hipLaunchKernelGGL(stem_clip_grad_kernel<float>, dim3(planes), dim3(256), 0, st, x, scale, shift,
                        minmax, (const float*)dy, w_q, dbeta, d->n, d->c_real, d->h, d->w, d->p, d->q, d->k, d->k_pad,
                        d->r, d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w);
   return rn_check_launch("stem_quant_clip_grad");

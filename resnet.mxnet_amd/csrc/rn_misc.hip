@@ -419,16 +419,37 @@ __global__ void relu_bwd_kernel(int64_t nchunk, const T* __restrict__ y, const T
 // ------------------------------------------------------------------------------ int8 quant
 template <typename T>
 __global__ void absmax_kernel(int64_t n, const T* __restrict__ x, float* __restrict__ out) {
+  // 16-byte chunks (x is 16-byte aligned: device allocations / tensor offsets), then the tail
+  constexpr int CE = 16 / sizeof(T);
+  const int64_t nc = n / CE;
   float m = 0.f;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+#pragma unroll 4
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nc; i += (int64_t)gridDim.x * blockDim.x) {
+    float f[CE];
+    chunk_to_f(reinterpret_cast<const uint4*>(x)[i], f, (const T*)nullptr);
+#pragma unroll
+    for (int e = 0; e < CE; ++e) m = fmaxf(m, fabsf(f[e]));
+  }
+  for (int64_t i = nc * CE + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
     m = fmaxf(m, fabsf(to_f(x[i])));
   m = wave_max(m);
+  // one atomic per block (thousands of same-address atomics serialise in L2)
+  __shared__ float wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
   // non-negative floats order like their bit patterns
-  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(out), __float_as_uint(m));
+  if (threadIdx.x == 0)
+    atomicMax(reinterpret_cast<unsigned int*>(out), __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
 }
-__global__ void quant_state_kernel(const float* __restrict__ curmax, float* minmax, int is_weight, int is_train,
-                                   float decay, int first, float* __restrict__ thr) {
-  *thr = quant_state_update(*curmax, minmax, is_weight, is_train, decay, first);
+// curmax is consumed and re-zeroed here (the next quantizer sharing the workspace starts from 0: no
+// memset launch per call); unit (nullable) = t / qmax for the int8 codes' consumers
+__global__ void quant_state_kernel(float* __restrict__ curmax, float* minmax, int is_weight, int is_train,
+                                   float decay, int first, float* __restrict__ thr, float qmax = 1.f,
+                                   float* __restrict__ unit = nullptr) {
+  const float t = quant_state_update(*curmax, minmax, is_weight, is_train, decay, first);
+  *thr = t;
+  *curmax = 0.f;
+  if (unit) *unit = t / qmax;
 }
 template <typename T>
 __global__ void quant_apply_kernel(int64_t n, const T* __restrict__ x, T* __restrict__ out,
@@ -468,14 +489,26 @@ __global__ void quant_codes_kernel(int64_t nchunk, const T* __restrict__ x, T* _
     reinterpret_cast<uint4*>(codes)[i] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
   }
 }
-__global__ void quant_unit_kernel(const float* __restrict__ thr, float qmax, float* __restrict__ unit_out) {
-  *unit_out = *thr / qmax;
-}
 template <typename T>
 __global__ void quant_bwd_kernel(int64_t n, const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx,
                                  const float* __restrict__ minmax, int is_weight, const T* __restrict__ add) {
   const float t = (is_weight || !minmax) ? INFINITY : *minmax;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+  constexpr int CE = 16 / sizeof(T);
+  const int64_t nc = n / CE;  // 16-byte chunks, then the tail
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nc; i += (int64_t)gridDim.x * blockDim.x) {
+    float fx[CE], fd[CE], fa[CE];
+    chunk_to_f(reinterpret_cast<const uint4*>(x)[i], fx, (const T*)nullptr);
+    chunk_to_f(reinterpret_cast<const uint4*>(dy)[i], fd, (const T*)nullptr);
+    if (add) chunk_to_f(reinterpret_cast<const uint4*>(add)[i], fa, (const T*)nullptr);
+#pragma unroll
+    for (int e = 0; e < CE; ++e) {
+      float g = fd[e];
+      if (!is_weight && !(fx[e] > -t && fx[e] < t)) g = 0.f;
+      fd[e] = add ? g + fa[e] : g;
+    }
+    reinterpret_cast<uint4*>(dx)[i] = f_to_chunk(fd, (const T*)nullptr);
+  }
+  for (int64_t i = nc * CE + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const float xv = to_f(x[i]);
     float g = to_f(dy[i]);
     if (!is_weight && !(xv > -t && xv < t)) g = 0.f;
@@ -733,28 +766,30 @@ int rn_relu_bwd(int64_t n, int32_t dtype, const void* y, const void* dy, void* d
   return rn_check_launch("relu_bwd");
 }
 
-int rn_quant_int8_fwd(int32_t dtype, int64_t n, const void* x, void* out, float* minmax, int32_t is_weight,
-                      int32_t is_train, float ema_decay, int32_t first_batch, int32_t nbits, float* ws,
-                      rn_stream_t stream) {
+}  // extern "C"
+
+// rn_quant_int8_fwd; unit (nullable) also receives t / qmax
+static int quant_fwd_values(int32_t dtype, int64_t n, const void* x, void* out, float* minmax, int32_t is_weight,
+                            int32_t is_train, float ema_decay, int32_t first_batch, int32_t nbits, float* ws,
+                            float* unit, rn_stream_t stream) {
   RN_CHECK_ARG(x && out && ws && n > 0, "bad arguments");
   RN_CHECK_ARG(is_weight || minmax, "activation quantization needs the minmax state");
   RN_CHECK_ARG(nbits >= 2 && nbits <= 16, "bad nbits");
   hipStream_t st = as_stream(stream);
   const float qmax = (float)((1 << (nbits - 1)) - 1);
-  float* curmax = ws;
+  float* curmax = ws;  // zero on entry (left zero by the state kernel)
   float* thr = ws + 1;
-  hipMemsetAsync(curmax, 0, sizeof(float), st);
   const bool need_max = is_weight || is_train;
   if (need_max) {
     if (dtype == RN_BF16)
-      hipLaunchKernelGGL(absmax_kernel<bf16_t>, dim3(grid1d(n, 256, 1024)), dim3(256), 0, st, n, (const bf16_t*)x,
+      hipLaunchKernelGGL(absmax_kernel<bf16_t>, dim3(grid1d(n / 8, 256, 1024)), dim3(256), 0, st, n, (const bf16_t*)x,
                          curmax);
     else
-      hipLaunchKernelGGL(absmax_kernel<float>, dim3(grid1d(n, 256, 1024)), dim3(256), 0, st, n, (const float*)x,
+      hipLaunchKernelGGL(absmax_kernel<float>, dim3(grid1d(n / 4, 256, 1024)), dim3(256), 0, st, n, (const float*)x,
                          curmax);
   }
   hipLaunchKernelGGL(quant_state_kernel, dim3(1), dim3(1), 0, st, curmax, minmax, is_weight, is_train, ema_decay,
-                     first_batch, thr);
+                     first_batch, thr, qmax, unit);
   const int clip = is_weight ? 0 : 1;
   if (dtype == RN_BF16)
     hipLaunchKernelGGL(quant_apply_kernel<bf16_t>, dim3(grid1d(n)), dim3(256), 0, st, n, (const bf16_t*)x,
@@ -765,6 +800,15 @@ int rn_quant_int8_fwd(int32_t dtype, int64_t n, const void* x, void* out, float*
   return rn_check_launch("quant_int8_fwd");
 }
 
+extern "C" {
+
+int rn_quant_int8_fwd(int32_t dtype, int64_t n, const void* x, void* out, float* minmax, int32_t is_weight,
+                      int32_t is_train, float ema_decay, int32_t first_batch, int32_t nbits, float* ws,
+                      rn_stream_t stream) {
+  return quant_fwd_values(dtype, n, x, out, minmax, is_weight, is_train, ema_decay, first_batch, nbits, ws, nullptr,
+                          stream);
+}
+
 int rn_quant_int8_fwd_codes(int32_t dtype, int64_t n, const void* x, void* out, void* codes, float* unit,
                             float* minmax, int32_t is_weight, int32_t is_train, float ema_decay, int32_t first_batch,
                             int32_t nbits, float* ws, rn_stream_t stream) {
@@ -772,28 +816,24 @@ int rn_quant_int8_fwd_codes(int32_t dtype, int64_t n, const void* x, void* out, 
   RN_CHECK_ARG(nbits >= 2 && nbits <= 8, "int8 codes need nbits <= 8");
   RN_CHECK_ARG(!codes || n % 16 == 0, "int8 codes: n must be a multiple of 16");
   if (!codes) {  // the fake-quantized values (and the unit) only
-    if (rn_quant_int8_fwd(dtype, n, x, out, minmax, is_weight, is_train, ema_decay, first_batch, nbits, ws, stream))
-      return -1;
-    hipLaunchKernelGGL(quant_unit_kernel, dim3(1), dim3(1), 0, as_stream(stream), ws + 1,
-                       (float)((1 << (nbits - 1)) - 1), unit);
-    return rn_check_launch("quant_int8_unit");
+    return quant_fwd_values(dtype, n, x, out, minmax, is_weight, is_train, ema_decay, first_batch, nbits, ws, unit,
+                            stream);
   }
   RN_CHECK_ARG(is_weight || minmax, "activation quantization needs the minmax state");
   hipStream_t st = as_stream(stream);
   const float qmax = (float)((1 << (nbits - 1)) - 1);
-  float* curmax = ws;
+  float* curmax = ws;  // zero on entry (left zero by the state kernel)
   float* thr = ws + 1;
-  hipMemsetAsync(curmax, 0, sizeof(float), st);
   if (is_weight || is_train) {
     if (dtype == RN_BF16)
-      hipLaunchKernelGGL(absmax_kernel<bf16_t>, dim3(grid1d(n, 256, 1024)), dim3(256), 0, st, n, (const bf16_t*)x,
+      hipLaunchKernelGGL(absmax_kernel<bf16_t>, dim3(grid1d(n / 8, 256, 1024)), dim3(256), 0, st, n, (const bf16_t*)x,
                          curmax);
     else
-      hipLaunchKernelGGL(absmax_kernel<float>, dim3(grid1d(n, 256, 1024)), dim3(256), 0, st, n, (const float*)x,
+      hipLaunchKernelGGL(absmax_kernel<float>, dim3(grid1d(n / 4, 256, 1024)), dim3(256), 0, st, n, (const float*)x,
                          curmax);
   }
   hipLaunchKernelGGL(quant_state_kernel, dim3(1), dim3(1), 0, st, curmax, minmax, is_weight, is_train, ema_decay,
-                     first_batch, thr);
+                     first_batch, thr, qmax, nullptr);
   const int clip = is_weight ? 0 : 1;
   const int64_t nc = n / 16;
   if (dtype == RN_BF16)
