@@ -235,6 +235,12 @@ def main():
     if world > 1:
         rdist.init_from_env(os.environ.get("RN_DIST_BACKEND", "nccl"))
     import torch.distributed as dist
+    # RN_BENCH_ALLREDUCE=1 at N=1: an RCCL process group of one rank and the bucketed all-reduce hooks
+    # on anyway (a world-1 sum is the identity): the per-step cost of the data-parallel path itself
+    force_ar = world == 1 and os.environ.get("RN_BENCH_ALLREDUCE", "0") == "1"
+    if force_ar:
+        dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%s" % os.environ.get("MASTER_PORT", "29511"),
+                                rank=0, world_size=1, device_id=torch.device("cuda", local))
 
     sym = {"resnet50": graphs.resnet50, "resnext50": graphs.resnext50_32x4d,
            "resnet50_int8": graphs.resnet50_int8}[a.model]()
@@ -251,7 +257,7 @@ def main():
                                          "multi_precision": True})
     ex = mod.executor
     ex.bucket_bytes = int(a.bucket_mb * (1 << 20))
-    if mod._reducer is not None:
+    if mod._reducer is not None or force_ar:
         from rn.dist import BucketAllReducer
         mod._reducer = BucketAllReducer(ex.grad, ex.buckets())
     data = np.random.default_rng(0 + rank).uniform(-1, 1, shp).astype(np.float32)
@@ -412,6 +418,10 @@ def main():
                       "resident in HBM",
             "pcie_inclusive": pcie,
         }
+        if force_ar:
+            out["allreduce"] = {"backend": dist.get_backend(), "world": 1, "buckets": len(ex.buckets()),
+                                "bucket_mb": a.bucket_mb, "note": "RCCL bucket all-reduce hooks on at N=1 "
+                                                                  "(RN_BENCH_ALLREDUCE=1)"}
         if world == 1 and not a.no_cpu_baseline and a.model == "resnet50":
             try:
                 out["cpu_baseline"] = cpu_baseline(a.cpu_batch, a.cpu_steps)
@@ -419,7 +429,7 @@ def main():
             except Exception as e:  # baseline must not hide the GPU number
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if world > 1 or force_ar:
         dist.destroy_process_group()
 
 

@@ -1,0 +1,90 @@
+"""The kvstore replacement over RCCL itself (torch.distributed backend 'nccl' = RCCL on ROCm).
+
+The box has one GPU and RCCL refuses two ranks on one device, so the world-2 data-parallel tests
+(test_dist_gpu.py) use gloo as the transport. This test runs the SAME bucketed all-reduce path on
+RCCL with a world of one: the process group is initialised with backend 'nccl', the executor's
+backward plan launches every bucket's all_reduce from its hook (rn/dist.py, core/solver.py:116-121
+kvstore push), Module.update waits for them and runs the fused SGD. A world-1 sum is the identity, so
+the gradients and the updated weights must equal those of the same step without a process group
+(up to the run-to-run rounding of the fp32-atomic weight-gradient kernels: first-step gradients
+Frobenius-relative 1e-4, a torn or early-read bucket is O(1)): an ordering hazard between the RCCL
+stream and the compute / weight-gradient streams (a bucket reduced before its last writer, SGD
+reading a bucket RCCL is still writing) shows up as a difference. It also proves RCCL initialises and runs next to librn's streams.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _step(sym, data, label, reducer_bucket_bytes=None, steps=2):
+    import mxnet as mx
+    from rn.dist import BucketAllReducer
+    mod = mx.mod.Module(sym, context=[mx.gpu(0)], precision="bfloat16")
+    mod.bind(data_shapes=[("data", data.shape)], label_shapes=[("softmax_label", label.shape)], for_training=True)
+    mx.random.seed(3)
+    mod.init_params(mx.init.Xavier(rnd_type="gaussian", factor_type="in", magnitude=2))
+    mod.init_optimizer(kvstore="device", optimizer="sgd",
+                       optimizer_params={"learning_rate": 0.1, "wd": 1e-4, "momentum": 0.9})
+    ex = mod.executor
+    launched = []
+    if reducer_bucket_bytes is not None:
+        ex.bucket_bytes = reducer_bucket_bytes
+        red = BucketAllReducer(ex.grad, ex.buckets())
+        orig = red.launch
+
+        def launch(i):
+            launched.append(i)
+            orig(i)
+
+        red.launch = launch
+        mod._reducer = red
+    batch = mx.io.DataBatch(data=[mx.nd.array(data)], label=[mx.nd.array(label)])
+    grads = []
+    for _ in range(steps):
+        mod.forward(batch, is_train=True)
+        mod.backward()
+        if mod._reducer is not None:
+            mod._reducer.wait()
+        grads.append(ex.grad.float().cpu().numpy().copy())
+        mod.update()
+    arg, _ = mod.get_params()
+    return grads, {k: v.asnumpy() for k, v in arg.items()}, launched, len(ex.buckets()) if reducer_bucket_bytes else 0
+
+
+def test_bucketed_allreduce_over_rccl_world1(gpu):
+    import torch.distributed as dist
+    from oracle import net as onet
+    from rn import graphs
+    sym = graphs.resnet([3, 4, 6, 3], 4, [64, 256, 512, 1024, 2048], 16)
+    data, label = onet.synthetic_batch(8, (3, 64, 64), 16)
+    data = data.astype(np.float32)
+    ref_grads, ref_args, _, _ = _step(sym, data, label)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1,
+                            device_id=gpu)
+    try:
+        assert dist.get_backend() == "nccl"
+        grads, args, launched, nb = _step(sym, data, label, reducer_bucket_bytes=1 << 20)
+    finally:
+        dist.destroy_process_group()
+    assert nb >= 8  # 1 MB buckets over ResNet-50's 102 MB of fp32 gradients
+    assert sorted(launched) == sorted(list(range(nb)) * 2)  # every bucket, once per backward
+    fro = lambda a, b: float(np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-30))
+    # step 1 tight; step 2 starts from weights that carry step 1's run-to-run rounding through bf16
+    # storage (one flipped rounding moves an element by 2^-8), so it gets the bf16 bar
+    assert fro(grads[0], ref_grads[0]) < 1e-4, fro(grads[0], ref_grads[0])
+    assert fro(grads[1], ref_grads[1]) < 3e-2, fro(grads[1], ref_grads[1])
+    for k in ref_args:
+        assert fro(args[k], ref_args[k]) < 1e-3, k
