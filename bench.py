@@ -197,6 +197,40 @@ def cpu_baseline_c1(batch=128, steps=20):
                       % (batch, steps, dt)}
 
 
+def c1_module_cpu(batch=128, steps=10):
+    """BASELINE.json configs[0] through the drop-in itself: train.py's Module on an mx.cpu() context
+    (rn/cpu_executor.py, the product's host device), ResNet-20 CIFAR-10, batch 128, fixed synthetic
+    batch, 2 warm-up + `steps` timed forward/backward/update iterations."""
+    import numpy as np
+    import torch
+    import mxnet as mx
+    from rn import graphs
+    cores = torch.get_num_threads()
+    mod = mx.mod.Module(graphs.resnet20_cifar(), context=mx.cpu())
+    mod.bind(data_shapes=[("data", (batch, 3, 32, 32))], label_shapes=[("softmax_label", (batch,))])
+    mx.random.seed(2)
+    mod.init_params(mx.init.Xavier(rnd_type="gaussian", factor_type="in", magnitude=2))
+    mod.init_optimizer(kvstore="local", optimizer="sgd",
+                       optimizer_params={"learning_rate": 0.1, "wd": 1e-4, "momentum": 0.9})
+    rng = np.random.default_rng(0)
+    b = mx.io.DataBatch(data=[mx.nd.array(rng.uniform(-1, 1, (batch, 3, 32, 32)).astype(np.float32))],
+                        label=[mx.nd.array(rng.integers(0, 10, batch).astype(np.float32))])
+
+    def it():
+        mod.forward(b, is_train=True)
+        mod.backward()
+        mod.update()
+    for _ in range(2):
+        it()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        it()
+    dt = time.perf_counter() - t0
+    return {"value": round(batch * steps / dt, 3), "unit": "images/sec", "cores": cores,
+            "sample": "mx.mod.Module(context=mx.cpu()) ResNet-20 CIFAR-10 train step, batch %d at 32x32, "
+                      "%d timed steps (%.1f s)" % (batch, steps, dt)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -426,6 +460,7 @@ def main():
             try:
                 out["cpu_baseline"] = cpu_baseline(a.cpu_batch, a.cpu_steps)
                 out["cpu_baseline_c1"] = cpu_baseline_c1()
+                out["c1_mx_cpu_module"] = c1_module_cpu()
             except Exception as e:  # baseline must not hide the GPU number
                 out["cpu_baseline"] = {"error": repr(e)}
         print(json.dumps(out), flush=True)

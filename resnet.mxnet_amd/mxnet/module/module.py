@@ -139,11 +139,15 @@ class Module:
                    for d in (label_shapes or [])]
         self._data_shapes, self._label_shapes = dshapes, lshapes
         self.for_training = for_training
-        ctxs = self._context
-        for c in ctxs:
-            if not isinstance(c, Context) or c.device_type != "gpu":
-                raise MXNetError("the MI355X runtime executes on mx.gpu() contexts only (got %s); the CPU "
-                                 "restatement of this path lives in oracle/ (tests and baselines only)" % (c,))
+        ctxs = self._context or [cpu()]  # MXNet's default context
+        kinds = {c.device_type if isinstance(c, Context) else None for c in ctxs}
+        if kinds == {"cpu"}:
+            # mx.cpu(): the host device (BASELINE C1, rn/cpu_executor.py); one context
+            if len(ctxs) != 1:
+                raise MXNetError("Module: one mx.cpu() context per process (got %s)" % (ctxs,))
+            return self._bind_cpu(dshapes, lshapes, for_training)
+        if kinds != {"gpu"}:
+            raise MXNetError("Module: contexts must all be mx.gpu() (MI355X) or one mx.cpu(); got %s" % (ctxs,))
         d = _dist()
         world = d.get_world_size() if d else 1
         local_rank = int(os.environ.get("LOCAL_RANK", d.get_rank() if d else 0))
@@ -173,6 +177,16 @@ class Module:
             import torch
             torch.cuda.set_device(ctx.device_id)
             self._exec = Executor(plan, ctx.torch_device())
+        self.binded = True
+
+    def _bind_cpu(self, dshapes, lshapes, for_training):
+        from rn.executor import Plan
+        from rn.cpu_executor import CPUExecutor
+        self._slice = None
+        self._ctx = self._context[0] if self._context else cpu()
+        self._total_batch = dshapes[0][1][0]
+        plan = Plan(self._symbol, dshapes, lshapes, dtype="float32", for_training=for_training)
+        self._exec = CPUExecutor(plan)
         self.binded = True
 
     # ------------------------------------------------------------------ params
