@@ -10,6 +10,12 @@ the gradients and the updated weights must equal those of the same step without 
 Frobenius-relative 1e-4, a torn or early-read bucket is O(1)): an ordering hazard between the RCCL
 stream and the compute / weight-gradient streams (a bucket reduced before its last writer, SGD
 reading a bucket RCCL is still writing) shows up as a difference. It also proves RCCL initialises and runs next to librn's streams.
+
+Every later step is checked against the SAME module recomputing that step's gradient without hooks
+(same weights): comparing step 2 across two modules is not a hazard check, because this tiny-batch
+ResNet-50 (8 images, 2x2 stage-4 maps: 32 values per BN channel) is chaotic under step 1's
+run-to-run rounding -- ReLU decisions flip after the lr-0.1 update and step-2 gradients of two
+plain runs without any process group differ O(1) (seen at 0.62 Frobenius-relative).
 """
 import os
 import socket
@@ -51,16 +57,24 @@ def _step(sym, data, label, reducer_bucket_bytes=None, steps=2):
         red.launch = launch
         mod._reducer = red
     batch = mx.io.DataBatch(data=[mx.nd.array(data)], label=[mx.nd.array(label)])
-    grads = []
-    for _ in range(steps):
+    grads, plain, first_args = [], [], None
+    for step in range(steps):
         mod.forward(batch, is_train=True)
         mod.backward()
         if mod._reducer is not None:
             mod._reducer.wait()
         grads.append(ex.grad.float().cpu().numpy().copy())
+        if mod._reducer is not None:
+            # the same step's gradient again, same weights, no hooks / collective (a world-1 sum is the
+            # identity, so the buffer update() then consumes is the same gradient)
+            ex.forward(is_train=True)
+            ex.backward()
+            plain.append(ex.grad.float().cpu().numpy().copy())
         mod.update()
-    arg, _ = mod.get_params()
-    return grads, {k: v.asnumpy() for k, v in arg.items()}, launched, len(ex.buckets()) if reducer_bucket_bytes else 0
+        if step == 0:
+            first_args = {k: v.asnumpy().copy() for k, v in mod.get_params()[0].items()}
+    nb = len(ex.buckets()) if reducer_bucket_bytes else 0
+    return grads, plain, first_args, launched, nb
 
 
 def test_bucketed_allreduce_over_rccl_world1(gpu):
@@ -70,21 +84,21 @@ def test_bucketed_allreduce_over_rccl_world1(gpu):
     sym = graphs.resnet([3, 4, 6, 3], 4, [64, 256, 512, 1024, 2048], 16)
     data, label = onet.synthetic_batch(8, (3, 64, 64), 16)
     data = data.astype(np.float32)
-    ref_grads, ref_args, _, _ = _step(sym, data, label)
+    ref_grads, _, ref_args, _, _ = _step(sym, data, label, steps=1)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1,
                             device_id=gpu)
     try:
         assert dist.get_backend() == "nccl"
-        grads, args, launched, nb = _step(sym, data, label, reducer_bucket_bytes=1 << 20)
+        grads, plain, args, launched, nb = _step(sym, data, label, reducer_bucket_bytes=1 << 20, steps=2)
     finally:
         dist.destroy_process_group()
     assert nb >= 8  # 1 MB buckets over ResNet-50's 102 MB of fp32 gradients
     assert sorted(launched) == sorted(list(range(nb)) * 2)  # every bucket, once per backward
     fro = lambda a, b: float(np.linalg.norm((a - b).ravel()) / max(np.linalg.norm(b.ravel()), 1e-30))
-    # step 1 tight; step 2 starts from weights that carry step 1's run-to-run rounding through bf16
-    # storage (one flipped rounding moves an element by 2^-8), so it gets the bf16 bar
+    # step 1 against the module without a process group; every step against its own hook-free rerun
     assert fro(grads[0], ref_grads[0]) < 1e-4, fro(grads[0], ref_grads[0])
-    assert fro(grads[1], ref_grads[1]) < 3e-2, fro(grads[1], ref_grads[1])
-    for k in ref_args:
+    for g, p in zip(grads, plain):
+        assert fro(g, p) < 1e-4, fro(g, p)
+    for k in ref_args:  # weights after the first SGD step (update() waited for every bucket)
         assert fro(args[k], ref_args[k]) < 1e-3, k
