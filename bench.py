@@ -78,16 +78,18 @@ DGRAD_CALLS = ("rn_conv_bwd_data", "rn_conv_bwd_data_bnred")
 
 
 def family_of(ex, name, args):
-    if name in ("rn_conv_bwd_filter", "rn_conv_bwd_filter_ws"):  # _ws: its slab reduction pass included
+    if name in ("rn_conv_bwd_filter", "rn_conv_bwd_filter_ws", "rn_conv_bwd_filter_x"):  # slab reduction included
         return "wgrad_kernel<bf16,*>" if ex.dtype == 0 else "wgrad_kernel<f32,*>"
     if name in FWD_CALLS + DGRAD_CALLS:
         d = args[0]._obj
         dgrad = name in DGRAD_CALLS
         ncol = d.c if dgrad else d.k
         out_f32 = not dgrad and args[4] == 1 and ex.dtype == 0
-        plain = dgrad or (args[6] is None and (name != "rn_conv_fwd_x" or args[7] is None))
+        plain = dgrad or args[6] is None
         # the library's own choice (rn_conv_tile), so the family always matches the kernel that runs
         big = ex.lib.rn_conv_tile(args[0], 1 if dgrad else 0) if (ex.dtype == 0 and not out_f32 and plain) else 0
+        if name == "rn_conv_fwd_x" and args[7] is not None and big < 128:
+            big = 0  # the BN+ReLU input transform runs on the 224-row tiles only, else the 128-row kernel
         if big:  # tile rows: 256, or 224 (the BN partial blocks are half the tile rows)
             rows = 2 * ex.lib.rn_conv_bn_part_rows(args[0], 1 if dgrad else 0) if big >= 128 else 256
             return "igemm_big_kernel<%dx%d>" % (rows, big)

@@ -136,9 +136,10 @@ int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, flo
 int64_t rn_conv_wgrad_ws_bytes(const rn_conv_desc* d);
 int rn_conv_bwd_filter_ws(const rn_conv_desc* d, const void* x, const void* dy, float* dw, void* ws,
                           int64_t ws_bytes, rn_stream_t stream);
-/* rn_conv_bwd_filter over the same BN+ReLU-on-load input as rn_conv_fwd_x. */
+/* rn_conv_bwd_filter_ws over the same BN+ReLU-on-load input as rn_conv_fwd_x (x = the BatchNorm
+ * input; the 1x1 convolutions run the LDS-DMA tiles with the transform on their B fragments). */
 int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, float* dw, const float* in_scale,
-                         const float* in_shift, rn_stream_t stream);
+                         const float* in_shift, void* ws, int64_t ws_bytes, rn_stream_t stream);
 
 /* Number of fp32 elements of the master weight (K x R x S x c_real/groups, KRSC). */
 int64_t rn_conv_weight_numel(const rn_conv_desc* d);

@@ -96,6 +96,8 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, const void* l
                                            0, 0, 0);
 }
 constexpr uint32_t kOob = 0xFFFFFFF0u;
+// channels of the BatchNorm+ReLU input transform the LDS-DMA kernels keep in LDS (XF)
+constexpr int kXfMaxC = 2048;
 
 // BatchNorm-apply + ReLU of the consumer's input, applied while staging (the BN+ReLU output of
 // pre-activation units feeding 1x1 convs is never written to HBM): v = max(x*sc[c] + sh[c], 0)
@@ -688,7 +690,13 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // tap per 16-byte chunk, k = tap * 8 + c). SC 2: the padded NHWC4 image of rn_stem_prepare_p4 (zero
 // border, so no in-image test): k = (r * 8 + s) * 4 + c over r, s < 8 (tap 7 of a row and row 7
 // have zero weights), a chunk = taps (r, 2 j) and (r, 2 j + 1), K-tile t = rows 2 t, 2 t + 1.
-template <int BN, int NBUF, int EPI = 0, bool M32 = false, int BM = 256, int SC = 0, int Q8 = 0>
+// XF: the producing BatchNorm+ReLU applied on load (forward of the pre-activation units' convs,
+// symbol/resnet.py:17-31: act = relu(bn(x)) is never written). in_sc / in_sh (<= kXfMaxC channels)
+// are copied into LDS once; each thread rewrites its own landed A chunks in place, max(x*sc + sh, 0)
+// rounded to bf16 exactly as bn_apply_kernel does, between the K-tile's vmcnt wait and its barrier.
+// Chunks the DMA zero-filled (halo taps, rows past the tile) stay zero: the conv pads the BN+ReLU
+// output with zeros.
+template <int BN, int NBUF, int EPI = 0, bool M32 = false, int BM = 256, int SC = 0, int Q8 = 0, int XF = 0>
 __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_big_kernel(IgemmArgs p) {
   constexpr int ES = Q8 ? 1 : 2;                 // operand bytes per element
   constexpr int BMA = 256, CE = 16 / ES, BKE = 128 / ES;
@@ -710,12 +718,23 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   constexpr int EP_WAVE = 64 * EP_LD;            // floats per wave per epilogue half
   constexpr int kEpChunks = NW * EP_WAVE / 4;
   static_assert(BN != 64 || !SC || EPI == 0, "the stem modes have no BatchNorm epilogue");
-  __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * kStage > kEpChunks ? NBUF * kStage : kEpChunks];
+  static_assert(!XF || (!SC && !Q8 && EPI != 2 && BN >= 128), "input transform: bf16 forward, 128/256 columns");
+  constexpr int kMain = NBUF * kStage > kEpChunks ? NBUF * kStage : kEpChunks;
+  constexpr int kXfChunks = XF ? 2 * kXfMaxC / 4 : 0;  // fp32 scale[kXfMaxC], shift[kXfMaxC]
+  __shared__ __attribute__((aligned(16))) uint4 smem[kMain + kXfChunks];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WAVES_N, wn = wid % WAVES_N;
   const IgemmCls& cl = p.cls[blockIdx.z];
   const int Mc = p.N * cl.Pc * cl.Qc;
+  float* const xs = reinterpret_cast<float*>(smem + kMain);  // (XF) scale, then shift
+  if constexpr (XF) {
+    for (int i = tid; i < p.C; i += NW * 64) {
+      xs[i] = p.in_sc[i];
+      xs[kXfMaxC + i] = p.in_sh[i];
+    }
+    __syncthreads();
+  }
   // persistent mode (p.ntiles > 0, rn_set_tuning 10): each workgroup walks the tiles v = blockIdx.x +
   // k * gridDim.x (gridDim.x a multiple of 8: v stays on this XCD's contiguous tile range), so one
   // tile's output stores drain while the next tile's first K-tiles load
@@ -785,6 +804,8 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   int d_toffa = 0, d_toffb = 0, d_dh = 0, d_dw = 0;
   bool d_cok = false;
   uint32_t d_la = 0;
+  int d_buf = 0;
+  uint32_t okb = 0;  // (XF) bit buf * AR + k: A piece k of the K-tile in buffer buf holds data
   const uint32_t dmask = (p.sched & 2) ? 0xFFF0u : 0xFFFFFFFFu;  // diagnostic: L2-resident sources
   auto prep = [&](int buf) __attribute__((always_inline)) {
     if constexpr (SC == 2) {  // K-tile t: lane chunk lch is row 2 t + lch / 4, taps 2 (lch % 4) + {0, 1}
@@ -809,6 +830,10 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
       d_la = lds0 + buf * (kStage * 16);
       return;
     }
+    if constexpr (XF) {
+      d_buf = buf;
+      okb &= ~(((1u << AR) - 1u) << (buf * AR));
+    }
     const int tr = st_tr, ts = st_ts, cb = st_cb;
     const bool live = st_n++ < nstage;
     if (++st_cb == ncb) {
@@ -828,6 +853,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   auto piece = [&](int k) __attribute__((always_inline)) {
     if (k < AR) {
       const bool ok = d_cok && (unsigned)(a_h[k] + d_dh) < (unsigned)p.H && (unsigned)(a_w[k] + d_dw) < (unsigned)p.W;
+      if constexpr (XF) okb |= (uint32_t)ok << (d_buf * AR + k);
       dma16_asm(rs_x, d_la + k * (RPR * 128), ok ? ((uint32_t)((a_row[k] + d_toffa) * ES) & dmask) : kOob);
     } else {
       const int i = k - AR;
@@ -905,6 +931,27 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
     }
   };
 
+  // (XF) this thread's landed A chunks of the K-tile in buffer buf, channel block cb, rewritten in place
+  auto xform = [&](int buf, int cb) __attribute__((always_inline)) {
+    const int c0 = min(cb * BKE + lch * CE, p.C - CE);  // (clamped: a chunk past C was zero-filled)
+    float a[8], b[8];
+    *reinterpret_cast<float4*>(a) = *reinterpret_cast<const float4*>(xs + c0);
+    *reinterpret_cast<float4*>(a + 4) = *reinterpret_cast<const float4*>(xs + c0 + 4);
+    *reinterpret_cast<float4*>(b) = *reinterpret_cast<const float4*>(xs + kXfMaxC + c0);
+    *reinterpret_cast<float4*>(b + 4) = *reinterpret_cast<const float4*>(xs + kXfMaxC + c0 + 4);
+#pragma unroll
+    for (int k = 0; k < AR; ++k) {
+      uint4* cp = smem + buf * kStage + k * (RPR * 8) + tid;
+      float f[8];
+      chunk_to_f(*cp, f, (const bf16_t*)nullptr);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], a[e], b[e]), 0.f);
+      const uint4 o = f_to_chunk(f, (const bf16_t*)nullptr);
+      *cp = ((okb >> (buf * AR + k)) & 1u) ? o : make_uint4(0, 0, 0, 0);
+    }
+  };
+  int xf_cb = 0;
+
 #pragma unroll
   for (int s = 0; s < NBUF - 1; ++s) issue(s);
   for (int t = 0; t < nstage; ++t) {
@@ -912,6 +959,10 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
     if (!(p.sched & 4)) {  // (diagnostic bit 4: no wait, no barrier -- wrong results)
       if (NBUF == 3) wait_vmcnt<LPT>();
       else wait_vmcnt<0>();
+      if constexpr (XF) {
+        xform(t % NBUF, xf_cb);
+        if (++xf_cb == ncb) xf_cb = 0;
+      }
       __syncthreads();  // ... for every thread; and every wave is done reading the buffer refilled next
     }
     prep((t + NBUF - 1) % NBUF);
@@ -1389,7 +1440,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 // chunk, and read with ds_read_b64_tr_b16 as in wgrad_kernel. NBUF buffers, NBUF-1 M-tiles in flight.
 // BNC = 256: 8 waves, one workgroup per CU; BNC = 128: 4 waves (2 x 2, each 64-128 rows x 64
 // columns), two workgroups per CU.
-template <int BMK, int NBUF, int BNC = 256>
+// XF (1x1 convolutions only: no halo, so every B element is a real input pixel or a row past the
+// M range, whose dy row is zero): the producing BatchNorm+ReLU applied to the B fragments after
+// their transposed read. A lane's B fragment j holds one output column (= input channel) for the
+// whole kernel, so its scale / shift are two registers; max(x*sc + sh, 0) rounded to bf16 as
+// bn_apply_kernel does.
+template <int BMK, int NBUF, int BNC = 256, int XF = 0>
 __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(WgradArgs p) {
   constexpr int CE = 8, BKM = 64;
   constexpr int NWC = BNC / 64, NW = 2 * NWC;              // waves along the columns, waves
@@ -1482,6 +1538,15 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  float xsc[XF ? NI : 1], xsh[XF ? NI : 1];
+  if constexpr (XF) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int col = n0 + wn * 64 + j * 16 + (lane & 15);
+      xsc[j] = col < p.C ? p.in_sc[col] : 0.f;
+      xsh[j] = col < p.C ? p.in_sh[col] : 0.f;
+    }
+  }
 
   auto compute = [&](int buf, int slab) __attribute__((always_inline)) {
     const char* Ab = reinterpret_cast<const char*>(smem + buf * kStage);
@@ -1508,6 +1573,13 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
 #pragma unroll
           for (int e = 0; e < 4; ++e) af[i][4 * h + e] = v[e];
         }
+      }
+      if constexpr (XF) {
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            bfv[j][e] = (short)f2bf(fmaxf(fmaf(bf2f((bf16_t)bfv[j][e]), xsc[j], xsh[j]), 0.f));
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i)
@@ -1988,7 +2060,9 @@ int big_tile_cols(const IgemmArgs& a, int64_t xb, int64_t wb) {
   if (a.smallc)  // the stem (C = 8): the 256x64 tile in its small-C mode (rn_set_tuning 4 = 1 or 5: never)
     return (big != 1 && big != 5 && a.C == 8 && a.K <= 64 && !a.in_sc && !a.bias && !g_tune[RN_TUNE_DIAG_IGEMM_L1] &&
             xb < INT32_MAX && wb < INT32_MAX) ? 64 : 0;
-  const bool eligible = big != 1 && !a.in_sc && a.gred == 0 && !g_tune[RN_TUNE_DIAG_IGEMM_L1] &&
+  // the BN+ReLU input transform (in_sc) runs on the 224-row 128/256-column tiles only
+  const bool xf_ok = !a.in_sc || (a.C <= kXfMaxC && a.K > 64 && g_tune[RN_TUNE_IGEMM_ROWS] != 1);
+  const bool eligible = big != 1 && xf_ok && a.gred == 0 && !g_tune[RN_TUNE_DIAG_IGEMM_L1] &&
                         !a.bias && xb < INT32_MAX && wb < INT32_MAX && max_taps <= 32;
   if (!eligible) return 0;
   if (a.K <= 64) {  // 4-wave 256x64 tile where the reduction is deep (>= 8 K-tiles: the 3x3 layers);
@@ -2072,7 +2146,16 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   if (epi == 0) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 0, M, R>), grid, dim3(512), 0, st, b);        \
   else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 1, M, R>), grid, dim3(512), 0, st, b);   \
   else hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 2, M, R>), grid, dim3(512), 0, st, b);
-      if (bm == 224) {
+      if (a.in_sc) {  // (big_tile_cols: 224 rows, forward)
+        RN_CHECK_ARG(bm == 224 && epi != 2, "input transform tile");
+        if (bn == 256) {
+          if (epi == 0) hipLaunchKernelGGL((igemm_big_kernel<256, 2, 0, false, 224, 0, 0, 1>), grid, dim3(512), 0, st, b);
+          else hipLaunchKernelGGL((igemm_big_kernel<256, 2, 1, false, 224, 0, 0, 1>), grid, dim3(512), 0, st, b);
+        } else {
+          if (epi == 0) hipLaunchKernelGGL((igemm_big_kernel<128, 3, 0, false, 224, 0, 0, 1>), grid, dim3(512), 0, st, b);
+          else hipLaunchKernelGGL((igemm_big_kernel<128, 3, 1, false, 224, 0, 0, 1>), grid, dim3(512), 0, st, b);
+        }
+      } else if (bm == 224) {
         if (bn == 256) {
           RN_BIG(256, 2, false, 224)
         } else {
@@ -2381,7 +2464,9 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
   a.fdC = make_fastdiv(a.cblk); a.fdS = make_fastdiv(d->s);
   // split-M partial slabs (plain stores + wgrad_slab_reduce_kernel) instead of fp32 atomics: 2 x the
   // slab bytes at streaming rates vs the slab bytes at the chip's ~1.3 TB/s atomic rate
-  const bool slab_ok = d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c;
+  // the BN+ReLU input transform runs on the LDS-DMA tiles for 1x1 convolutions (wgrad_big_kernel XF)
+  const bool xf_big = !in_scale || (d->r == 1 && d->s == 1 && d->pad_h == 0 && d->pad_w == 0);
+  const bool slab_ok = d->dtype == RN_BF16 && !grouped && xf_big && d->c_real == d->c;
   auto finish = [&](int64_t split, const char* what) -> int {
     const int64_t need = slab_ok ? split * a.K * (int64_t)a.ldw * 4 : 0;
     if (ws_need) *ws_need = need;
@@ -2426,10 +2511,10 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
   // for >= 128 output channels and >= 256 columns: their main loop is the faster one, and the
   // 4x larger per-workgroup tile no longer costs atomics
   const bool big256 = (g_tune[RN_TUNE_WGRAD_BIG] == 1 || (g_tune[RN_TUNE_WGRAD_BIG] == 0 && slab_ok && ws)) &&
-                      d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c && a.K >= 128 &&
+                      d->dtype == RN_BF16 && !grouped && xf_big && d->c_real == d->c && a.K >= 128 &&
                       a.ncol_load >= 256 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX &&
                       (int64_t)a.M * a.ldy < INT32_MAX;
-  if (d->dtype == RN_BF16 && !grouped && !in_scale && d->c_real == d->c && !big256 &&
+  if (d->dtype == RN_BF16 && !grouped && xf_big && d->c_real == d->c && !big256 &&
       (g_tune[RN_TUNE_WGRAD_BIG] == 0 || g_tune[RN_TUNE_WGRAD_BIG] == 2 || g_tune[RN_TUNE_WGRAD_BIG] == 4) &&
       a.K > 64 && a.ncol_load > 64 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX &&
       (int64_t)a.M * a.ldy < INT32_MAX) {
@@ -2447,7 +2532,8 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     split = ceil_div(a.M, a.m_per_split);
     if (!launch) return finish(split, "wgrad_dma128");
     use_slab(split);
-    hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
+    if (in_scale) hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128, 1>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
     return finish(split, "wgrad_dma128");
   }
   if (big256) {
@@ -2462,7 +2548,10 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     if (!launch) return finish(split, "wgrad_big");
     use_slab(split);
     dim3 grid((unsigned)(tiles * split));
-    if (bmk == 256) hipLaunchKernelGGL((wgrad_big_kernel<256, 2>), grid, dim3(512), 0, st, a);
+    if (in_scale) {
+      if (bmk == 256) hipLaunchKernelGGL((wgrad_big_kernel<256, 2, 256, 1>), grid, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((wgrad_big_kernel<128, 3, 256, 1>), grid, dim3(512), 0, st, a);
+    } else if (bmk == 256) hipLaunchKernelGGL((wgrad_big_kernel<256, 2>), grid, dim3(512), 0, st, a);
     else hipLaunchKernelGGL((wgrad_big_kernel<128, 3>), grid, dim3(512), 0, st, a);
     return finish(split, "wgrad_big");
   }
@@ -2507,9 +2596,12 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
 extern "C" {
 
 int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, float* dw, const float* in_scale,
-                         const float* in_shift, rn_stream_t stream) {
+                         const float* in_shift, void* ws, int64_t ws_bytes, rn_stream_t stream) {
   RN_CHECK_ARG(d && x && dy && dw, "null argument");
-  return wgrad_dispatch(d, x, dy, dw, in_scale, in_shift, nullptr, 0, nullptr, true, as_stream(stream));
+  RN_CHECK_ARG(ws_bytes >= 0 && (ws || ws_bytes == 0), "bad workspace");
+  RN_CHECK_ARG(((uintptr_t)ws & 15) == 0, "workspace must be 16-byte aligned");
+  return wgrad_dispatch(d, x, dy, dw, in_scale, in_shift, reinterpret_cast<float*>(ws), ws_bytes, nullptr, true,
+                        as_stream(stream));
 }
 
 int64_t rn_conv_wgrad_ws_bytes(const rn_conv_desc* d) {
@@ -2531,7 +2623,7 @@ int rn_conv_bwd_filter_ws(const rn_conv_desc* d, const void* x, const void* dy, 
 }
 
 int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, float* dw, rn_stream_t stream) {
-  return rn_conv_bwd_filter_x(d, x, dy, dw, nullptr, nullptr, stream);
+  return rn_conv_bwd_filter_x(d, x, dy, dw, nullptr, nullptr, nullptr, 0, stream);
 }
 
 // ---------------------------------------------------------------- stem over the padded NHWC4 image

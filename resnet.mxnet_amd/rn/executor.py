@@ -338,7 +338,9 @@ class Plan:
             op.xf = None
             if op.kind == "bn":
                 op.apply_fused = False
-        if os.environ.get("RN_BN_APPLY_FUSION", "0") != "1":  # opt-in: measured slower
+        # default on since the LDS-DMA tiles apply it (igemm_big_kernel / wgrad_big_kernel XF): 22.82 ->
+        # 22.17 ms per step on one box; RN_BN_APPLY_FUSION=0 writes act1 / act3
+        if os.environ.get("RN_BN_APPLY_FUSION", "1") != "1":
             return
         refs = {}
         for op in self.ops:
@@ -1220,8 +1222,11 @@ class Executor:
             elif op.kind == "conv":
                 x = op.x
                 if op.xf is not None:  # input = BN+ReLU(bn input), applied on load
+                    ws = self.wgrad_ws is not None and int(self.lib.rn_conv_wgrad_ws_bytes(L.C.byref(op.desc))) > 0
                     self._bwd.append(self._call("rn_conv_bwd_filter_x", L.C.byref(op.desc), self._p(self.act(op.xf.x)),
-                                                self._p(dy), self._gp(op.weight), op.xf.sc, op.xf.sh, sp))
+                                                self._p(dy), self._gp(op.weight), op.xf.sc, op.xf.sh,
+                                                self._p(self.wgrad_ws) if ws else None,
+                                                self.wgrad_ws_bytes if ws else 0, sp))
                 else:
                     self._bwd.append(self._wgrad_call(op.desc, self._p(self.act(x)), self._p(dy), self._gp(op.weight),
                                                       sp))

@@ -46,7 +46,7 @@ SIGNATURES = {
     "rn_conv_fwd_i8": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P, _P]),
     "rn_conv_weight_pack_i8": (_i32, [_P, _P, _P, _P, _P]),
     "rn_conv_fwd_x": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P, _P, _P]),
-    "rn_conv_bwd_filter_x": (_i32, [_P, _P, _P, _P, _P, _P, _P]),
+    "rn_conv_bwd_filter_x": (_i32, [_P, _P, _P, _P, _P, _P, _P, _i64, _P]),
     "rn_conv_bwd_data_bnred": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P, _P]),
     "rn_conv_fwd_bnacc": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_data_bnacc": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P, _P]),

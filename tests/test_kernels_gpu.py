@@ -657,11 +657,64 @@ def test_conv_bnrelu_on_load(gpu, dtype, case):
     y = torch.zeros((n, P, Q, d.k_pad), dtype=tdt(dtype), device=gpu)
     L.call("rn_conv_fwd_x", C.byref(d), p(xd), p(wk), p(y), dtype, None, None, p(scd), p(shd), None, stream())
     dw = torch.zeros(k * r * r * c, dtype=torch.float32, device=gpu)
-    L.call("rn_conv_bwd_filter_x", C.byref(d), p(xd), p(to_nhwc(dy, dtype, gpu)), p(dw), p(scd), p(shd), stream())
+    L.call("rn_conv_bwd_filter_x", C.byref(d), p(xd), p(to_nhwc(dy, dtype, gpu)), p(dw), p(scd), p(shd), None, 0, stream())
     torch.cuda.synchronize()
     assert rel_err(from_nhwc(y, k), y_ref) < TOL[dtype]
     assert rel_err(dw.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2), dw_ref) < \
         (TOL[dtype] if dtype == F32 else 5e-3)
+
+
+@pytest.mark.parametrize("case", [(4, 256, 28, 28, 512, 1, 1, 0), (4, 256, 28, 28, 128, 1, 2, 0),
+                                  (2, 1024, 14, 14, 256, 1, 1, 0), (2, 2048, 7, 7, 512, 1, 1, 0),
+                                  (3, 64, 20, 20, 256, 3, 1, 1), (2, 200, 9, 11, 136, 1, 1, 0)])
+@pytest.mark.parametrize("ws", [False, True], ids=["atomic", "slab"])
+def test_conv_bnrelu_on_load_tiles(gpu, case, ws, big_tiles, tile_variant):
+    """BN+ReLU applied on load by the LDS-DMA tiles (igemm_big_kernel XF: the landed A chunks rewritten
+    in LDS, halo chunks kept zero; wgrad_big_kernel XF: the B fragments of 1x1 convolutions after their
+    transposed read) == the unfused path (rn_bn_apply, then rn_conv_fwd / rn_conv_bwd_filter_ws on its
+    output) BIT FOR BIT, and the oracle on the bf16-rounded BN+ReLU output within the bf16 bar."""
+    n, c, h, w, k, r, st, pd = case
+    x, wt = _conv_data(case, 28)
+    rng = np.random.default_rng(29)
+    sc = rng.uniform(0.5, 1.5, c)
+    sh = rng.standard_normal(c) * 0.5
+    x, wt = bf16_round(x), bf16_round(wt)
+    d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd)
+    P, Q = d.p, d.q
+    dy = bf16_round(rng.standard_normal((n, k, P, Q)))
+    f = lambda a: torch.tensor(np.pad(a, (0, d.c - c)), dtype=torch.float32, device=gpu)
+    scd, shd = f(sc), f(sh)
+    xd = to_nhwc(x, BF16, gpu)
+    dyd = to_nhwc(dy, BF16, gpu)
+    wk = torch.zeros(k * r * r * d.c, dtype=torch.bfloat16, device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), p(wk), None, stream())
+    wsb = int(L.load().rn_conv_wgrad_ws_bytes(C.byref(d))) if ws else 0
+    wsd = torch.zeros(max(wsb // 4, 4), dtype=torch.float32, device=gpu) if wsb > 0 else None
+    # fused
+    y = torch.zeros((n, P, Q, d.k_pad), dtype=torch.bfloat16, device=gpu)
+    L.call("rn_conv_fwd_x", C.byref(d), p(xd), p(wk), p(y), BF16, None, None, p(scd), p(shd), None, stream())
+    dw = torch.zeros(k * r * r * c, dtype=torch.float32, device=gpu)
+    L.call("rn_conv_bwd_filter_x", C.byref(d), p(xd), p(dyd), p(dw), p(scd), p(shd), p(wsd), wsb, stream())
+    # unfused: the BN+ReLU output written by rn_bn_apply, then the plain entry points
+    bd = L.BNDesc(dtype=BF16, m=n * h * w, c=d.c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1)
+    act = torch.zeros_like(xd)
+    L.call("rn_bn_apply", C.byref(bd), p(xd), p(act), p(scd), p(shd), stream())
+    y0 = torch.zeros_like(y)
+    L.call("rn_conv_fwd", C.byref(d), p(act), p(wk), p(y0), BF16, None, None, stream())
+    dw0 = torch.zeros_like(dw)
+    L.call("rn_conv_bwd_filter_ws", C.byref(d), p(act), p(dyd), p(dw0), p(wsd), wsb, stream())
+    torch.cuda.synchronize()
+    if tile_variant[0] == 0:  # 224-row tiles: fused and unfused run the same tile (else the transform
+        assert torch.equal(y.view(torch.int16), y0.view(torch.int16))  # falls back to the 128-row kernel)
+    if r == 1 and wsb > 0:  # the slab path is deterministic; atomics / the 3x3 fallback kernel are not
+        assert torch.equal(dw, dw0)
+    else:
+        assert rel_err(dw.cpu().numpy(), dw0.cpu().numpy()) < 1e-5
+    xa = bf16_round(np.maximum(x * sc[None, :, None, None] + sh[None, :, None, None], 0))
+    y_ref = ops.conv2d_fwd(xa, wt, (st, st), (pd, pd))
+    _, dw_ref = ops.conv2d_bwd(xa, wt, dy, (st, st), (pd, pd))
+    assert rel_err(from_nhwc(y, k), y_ref) < TOL[BF16]
+    assert rel_err(dw.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2), dw_ref) < 5e-3
 
 
 @pytest.mark.parametrize("mode", [0, 2])
