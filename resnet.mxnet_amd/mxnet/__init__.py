@@ -16,6 +16,7 @@ from . import ndarray as nd
 from . import symbol
 from . import symbol as sym
 from . import io
+from . import recordio
 from . import initializer
 from . import initializer as init
 from . import optimizer
