@@ -88,18 +88,6 @@ int rn_conv_fwd_i8(const rn_conv_desc* d, const void* x_codes, const void* w_cod
  * copy of a per-tensor quantized weight from the fp32 master (unit from rn_quant_int8_fwd_codes). */
 int rn_conv_weight_pack_i8(const rn_conv_desc* d, const float* w_master, const float* unit, void* w_codes,
                            rn_stream_t stream);
-#define RN_BN_ACC_REPLICAS 64
-/* As rn_conv_fwd_bnstats / rn_conv_bwd_data_bnred, with the BatchNorm sums accumulated straight into
- * acc = double[RN_BN_ACC_REPLICAS][2][k_pad (fwd) | c (dgrad)] by fp64 atomic adds, each workgroup
- * into one replica (spreads the same-address contention; zero on entry; the matching
- * rn_bn_*_acc call consumes and re-zeroes it) instead of per-block partials -- no partial merge
- * pass. Forward: S1, S2 of (y - pivot[c]) with pivot = the BN's moving mean; dgrad: sum dz,
- * sum dz * (x - mean). bf16 only, and only where rn_conv_tile(d, mode) >= 128. */
-int rn_conv_fwd_bnacc(const rn_conv_desc* d, const void* x, const void* w_krsc, void* y, const void* add_src,
-                      const float* pivot, double* acc, rn_stream_t stream);
-int rn_conv_bwd_data_bnacc(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx, const void* add_src,
-                           const void* bn_x, const float* bn_mean, const float* bn_scale, const float* bn_shift,
-                           int32_t relu, double* acc, rn_stream_t stream);
 
 /* rn_conv_bwd_data that also reduces the BatchNorm+ReLU backward of the BN whose output gradient
  * this call completes (dx here = d(bn output), bn_x = the BN input, bn_mean / bn_scale / bn_shift =
@@ -245,15 +233,6 @@ int rn_bn_fwd_train_part(const rn_bn_desc* d, const float* part, int64_t nblk, i
                          const void* x, void* y, const float* gamma, const float* beta, float* moving_mean,
                          float* moving_var, float* save_mean, float* save_invstd, float* scale, float* shift,
                          void* ws, rn_stream_t stream);
-/* rn_bn_fwd_train_part / rn_bn_bwd_part for sums accumulated by rn_conv_fwd_bnacc /
- * rn_conv_bwd_data_bnacc (acc re-zeroed; pivot = the array the conv read, read before the
- * moving-mean update). */
-int rn_bn_fwd_train_acc(const rn_bn_desc* d, double* acc, const float* pivot, const void* x, void* y,
-                        const float* gamma, const float* beta, float* moving_mean, float* moving_var,
-                        float* save_mean, float* save_invstd, float* scale, float* shift, rn_stream_t stream);
-int rn_bn_bwd_acc(const rn_bn_desc* d, double* acc, const void* x, const void* dy, void* dx, const void* add_src,
-                  const float* gamma, const float* save_mean, const float* save_invstd, const float* scale,
-                  const float* shift, float* dgamma, float* dbeta, void* ws, rn_stream_t stream);
 /* rn_bn_bwd with the reduction already done by the producer of dy (rn_conv_bwd_data_bnred):
  * finalize over part[nrb][c][2], then dx = BN-backward(dy) (+ add_src). ws: >= 4*c floats + 16 B. */
 int rn_bn_bwd_part(const rn_bn_desc* d, const float* part, int64_t nrb, const void* x, const void* dy, void* dx,

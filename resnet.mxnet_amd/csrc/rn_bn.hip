@@ -243,86 +243,6 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_part_kernel(const double*
   }
 }
 
-// Statistics accumulated by the producing conv (rn_conv_fwd_bnacc), summed over the replicas:
-// acc[r][0][c] = sum(y - piv), acc[r][1][c] = sum((y - piv)^2) in fp64, piv = the moving mean the conv read. Finalizes like
-// bn_fwd_finalize_part_kernel, then zeroes acc for the next step.
-__global__ __launch_bounds__(256) void bn_fwd_finalize_acc_kernel(double* __restrict__ acc, const float* pivot,
-                                                                  int64_t m, int c, int c_real, float eps,
-                                                                  float momentum, int fix_gamma,
-                                                                  const float* __restrict__ gamma,
-                                                                  const float* __restrict__ beta,
-                                                                  float* moving_mean, float* moving_var,
-                                                                  float* save_mean, float* save_invstd,
-                                                                  float* scale, float* shift) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c) return;
-  double s1 = 0.0, s2 = 0.0;
-  for (int r = 0; r < RN_BN_ACC_REPLICAS; ++r) {
-    double* a = acc + (int64_t)r * 2 * c;
-    s1 += a[ch];
-    s2 += a[c + ch];
-    a[ch] = 0.0;
-    a[c + ch] = 0.0;
-  }
-  if (ch >= c_real) {
-    scale[ch] = 0.f;
-    shift[ch] = 0.f;
-    return;
-  }
-  const double md = s1 / (double)m;
-  const double mean = (double)pivot[ch] + md;  // (pivot read before the moving-mean update below)
-  double var = s2 / (double)m - md * md;
-  if (var < 0) var = 0;
-  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
-  const float g = fix_gamma ? 1.f : gamma[ch];
-  const float sc = g * invstd;
-  scale[ch] = sc;
-  shift[ch] = beta[ch] - (float)mean * sc;
-  save_mean[ch] = (float)mean;
-  save_invstd[ch] = invstd;
-  if (moving_mean) {
-    moving_mean[ch] = moving_mean[ch] * momentum + (float)mean * (1.f - momentum);
-    moving_var[ch] = moving_var[ch] * momentum + (float)var * (1.f - momentum);
-  }
-}
-
-// Backward sums accumulated by the conv dgrad (rn_conv_bwd_data_bnacc), over the replicas:
-// acc[r][0][c] = sum dz, acc[r][1][c] = sum dz (x - mean). Same coefficients as bn_bwd_finalize_kernel; zeroes acc.
-__global__ __launch_bounds__(256) void bn_bwd_finalize_acc_kernel(double* __restrict__ acc, int64_t m, int c,
-                                                                  int c_real, int fix_gamma,
-                                                                  const float* __restrict__ gamma,
-                                                                  const float* __restrict__ save_mean,
-                                                                  const float* __restrict__ save_invstd,
-                                                                  float* dgamma, float* dbeta,
-                                                                  float* __restrict__ coef) {
-  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
-  if (ch >= c) return;
-  double s = 0.0, q0 = 0.0;
-  for (int r = 0; r < RN_BN_ACC_REPLICAS; ++r) {
-    double* a = acc + (int64_t)r * 2 * c;
-    s += a[ch];
-    q0 += a[c + ch];
-    a[ch] = 0.0;
-    a[c + ch] = 0.0;
-  }
-  if (ch >= c_real) {
-    coef[ch * 4 + 0] = 0.f;
-    coef[ch * 4 + 1] = 0.f;
-    coef[ch * 4 + 2] = 0.f;
-    coef[ch * 4 + 3] = 0.f;
-    return;
-  }
-  const double invstd = save_invstd[ch];
-  const double g = fix_gamma ? 1.0 : (double)gamma[ch];
-  const double dg_raw = q0 * invstd;  // sum dz * xhat
-  if (dbeta) dbeta[ch] = (float)s;
-  if (dgamma) dgamma[ch] = fix_gamma ? 0.f : (float)dg_raw;
-  coef[ch * 4 + 0] = (float)(g * invstd);
-  coef[ch * 4 + 1] = (float)(s / (double)m);
-  coef[ch * 4 + 2] = (float)(g * invstd * invstd * dg_raw / (double)m);
-  coef[ch * 4 + 3] = save_mean[ch];
-}
-
 // ---- stem input (bn_data over the NCHW fp32 `data`, symbol/resnet.py:90): statistics straight from
 // the NCHW planes, then one pass writing the normalised NHWC-8 compute copy for conv0.
 // part[b][c][2]: shifted sums over images [b*ipb, (b+1)*ipb) of channel c, pivot x[0][c][0][0].
@@ -838,45 +758,6 @@ int rn_bn_bwd_part(const rn_bn_desc* d, const float* part, int64_t nrb, const vo
   return rn_check_launch("bn_bwd_part");
 }
 
-int rn_bn_fwd_train_acc(const rn_bn_desc* d, double* acc, const float* pivot, const void* x, void* y,
-                        const float* gamma, const float* beta, float* moving_mean, float* moving_var,
-                        float* save_mean, float* save_invstd, float* scale, float* shift, rn_stream_t stream) {
-  if (check_bn(d)) return -1;
-  RN_CHECK_ARG(acc && pivot && beta && save_mean && save_invstd && scale && shift, "null argument");
-  RN_CHECK_ARG(d->fix_gamma || gamma, "gamma required unless fix_gamma");
-  RN_CHECK_ARG((moving_mean == nullptr) == (moving_var == nullptr), "moving stats must both be set");
-  hipStream_t st = as_stream(stream);
-  hipLaunchKernelGGL(bn_fwd_finalize_acc_kernel, dim3((d->c + 255) / 256), dim3(256), 0, st, acc, pivot, d->m, d->c,
-                     d->c_real, d->eps, d->momentum, d->fix_gamma, gamma, beta, moving_mean, moving_var, save_mean,
-                     save_invstd, scale, shift);
-  if (rn_check_launch("bn_fwd_finalize_acc")) return -1;
-  if (!y) return 0;
-  RN_CHECK_ARG(x != nullptr, "null x");
-  if (d->dtype == RN_BF16) return bn_apply_t<bf16_t>(d, x, y, scale, shift, st);
-  return bn_apply_t<float>(d, x, y, scale, shift, st);
-}
-
-int rn_bn_bwd_acc(const rn_bn_desc* d, double* acc, const void* x, const void* dy, void* dx, const void* add_src,
-                  const float* gamma, const float* save_mean, const float* save_invstd, const float* scale,
-                  const float* shift, float* dgamma, float* dbeta, void* ws, rn_stream_t stream) {
-  if (check_bn(d)) return -1;
-  RN_CHECK_ARG(acc && x && dy && save_mean && save_invstd && scale && shift && ws, "null argument");
-  RN_CHECK_ARG(d->fix_gamma || gamma, "gamma required unless fix_gamma");
-  hipStream_t st = as_stream(stream);
-  float* coef = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 15) & ~uintptr_t(15));
-  hipLaunchKernelGGL(bn_bwd_finalize_acc_kernel, dim3((d->c + 255) / 256), dim3(256), 0, st, acc, d->m, d->c,
-                     d->c_real, d->fix_gamma, gamma, save_mean, save_invstd, dgamma, dbeta, coef);
-  if (dx) {
-    if (d->dtype == RN_BF16) {
-      if (d->relu) launch_bwd_apply<bf16_t, true>(d, x, dy, dx, add_src, coef, scale, shift, st);
-      else launch_bwd_apply<bf16_t, false>(d, x, dy, dx, add_src, coef, scale, shift, st);
-    } else {
-      if (d->relu) launch_bwd_apply<float, true>(d, x, dy, dx, add_src, coef, scale, shift, st);
-      else launch_bwd_apply<float, false>(d, x, dy, dx, add_src, coef, scale, shift, st);
-    }
-  }
-  return rn_check_launch("bn_bwd_acc");
-}
 
 int rn_bn_fwd_infer(const rn_bn_desc* d, const void* x, void* y, const float* gamma, const float* beta,
                     const float* moving_mean, const float* moving_var, float* scale, float* shift,

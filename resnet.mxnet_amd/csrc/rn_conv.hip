@@ -64,11 +64,6 @@ struct IgemmArgs {
   const void* bn_x;
   const float *bn_mean, *bn_sc, *bn_sh;
   int bn_relu, mt_max;
-  // 256-row tiles, nullable: the BatchNorm sums accumulated straight into bnacc[2][ldo] (fp64
-  // atomics; zero on entry) instead of per-block partials. EPI 1: S1, S2 about bnpiv[col] (the BN's
-  // moving mean); EPI 2: sum dz, sum dz * (x - mean).
-  double* bnacc;
-  const float* bnpiv;
   // int8 forward (igemm_big_kernel Q8): per-tensor quantization units of the int8 codes in x and w
   // (Quantization_int8: value = code * unit); the int32 accumulators are scaled by their product
   const float* qunit_x;
@@ -745,7 +740,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   const int m0 = mtile * BM;
   const int n0 = (lid - mtile * p.ntn) * BN;
   if (m0 >= Mc) {  // (a dgrad parity class with fewer rows): empty BN-reduction partials
-    if (EPI == 2 && !p.bnacc)
+    if (EPI == 2)
       for (int e = tid; e < WAVES_M * BN; e += NW * 64) {
         const int hh = e / BN, col = n0 + e % BN;
         if (col < p.ldo && WAVES_M * mtile + hh < p.mt_max) {
@@ -1063,7 +1058,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
                      // (rounded) conv value of each column
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          piv[e] = p.bnacc ? (col0 + e < p.K ? p.bnpiv[col0 + e] : 0.f) : to_f(from_f<OutT>(ep[cc * 8 + e]));
+          piv[e] = to_f(from_f<OutT>(ep[cc * 8 + e]));
       }
     }
 #pragma unroll
@@ -1128,18 +1123,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
         s1[e] += __shfl_xor(s1[e], o, 64);
         s2[e] += __shfl_xor(s2[e], o, 64);
       }
-    if (p.bnacc) {  // one of RN_BN_ACC_REPLICAS copies per (workgroup, wave row): spreads the contention
-      if (lane < CPR && half_ok) {
-        const int c0 = n0 + wn * WN + lane * 8;
-        double* dst = p.bnacc + (int64_t)((2 * blockIdx.x + wm) & (RN_BN_ACC_REPLICAS - 1)) * 2 * p.ldo;
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (c0 + e < p.K) {
-            atomicAdd(dst + c0 + e, (double)s1[e]);
-            atomicAdd(dst + p.ldo + c0 + e, (double)s2[e]);
-          }
-      }
-    } else if (lane < CPR) {
+    if (lane < CPR) {
       const int c0 = n0 + wn * WN + lane * 8;
       const int blk = WAVES_M * mtile + wm;  // one partial per wave row
 #pragma unroll
@@ -2110,9 +2094,8 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   const bool dma = g_tune[RN_TUNE_IGEMM_DMA] > 0 && !a.in_sc && !b.diag_l1 && xb < INT32_MAX && wb < INT32_MAX &&
                    max_taps <= 64;
   if constexpr (std::is_same<T, bf16_t>::value && std::is_same<OutT, bf16_t>::value) {
-    const int epi = a.stats ? 1 : a.bnred ? 2 : a.bnacc ? (a.bn_x ? 2 : 1) : 0;
+    const int epi = a.stats ? 1 : a.bnred ? 2 : 0;
     const int bn = big_tile_cols(a, xb, wb);
-    RN_CHECK_ARG(!a.bnacc || bn >= 128, "accumulated BatchNorm sums need the 256-row tile (rn_conv_tile >= 128)");
     const bool m32 = g_tune[RN_TUNE_IGEMM_MFMA] != 1;
     // persistent tiles (rn_set_tuning 10 = workgroups, a multiple of 8): only where the grid is larger
     b.ntiles = 0;
@@ -2123,7 +2106,7 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
         grid.x = (unsigned)g;
       }
     };
-    if (bn == 64 && !a.bnacc && (epi == 0 || !a.smallc)) {
+    if (bn == 64 && (epi == 0 || !a.smallc)) {
       b.ntn = (int)ceil_div(a.K, 64);
       if (a.bnred) b.mt_max = (int)ceil_div(maxMc, 64);  // BN partials per 64-row wave row
       dim3 grid((unsigned)(ceil_div(maxMc, 256) * b.ntn), 1, a.ncls);
@@ -2353,28 +2336,6 @@ int rn_conv_fwd(const rn_conv_desc* d, const void* x, const void* w, void* y, in
 int rn_conv_fwd_bnstats(const rn_conv_desc* d, const void* x, const void* w, void* y, int32_t y_dtype,
                         const void* add_src, const float* bias, float* part, rn_stream_t stream) {
   return rn_conv_fwd_x(d, x, w, y, y_dtype, add_src, bias, nullptr, nullptr, part, stream);
-}
-
-int rn_conv_fwd_bnacc(const rn_conv_desc* d, const void* x, const void* w, void* y, const void* add_src,
-                      const float* pivot, double* acc, rn_stream_t stream) {
-  RN_CHECK_ARG(d && x && w && y && pivot && acc, "null argument");
-  RN_CHECK_ARG(d->dtype == RN_BF16 && d->k % 8 == 0, "accumulated BatchNorm statistics: bf16, whole 8-channel chunks");
-  IgemmArgs a = make_igemm_args(d, 0);
-  a.x = x; a.w = w; a.y = y; a.add = add_src;
-  a.bnacc = acc; a.bnpiv = pivot;
-  return launch_igemm<bf16_t, bf16_t>(a, as_stream(stream));
-}
-
-int rn_conv_bwd_data_bnacc(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx, const void* add_src,
-                           const void* bn_x, const float* bn_mean, const float* bn_scale, const float* bn_shift,
-                           int32_t relu, double* acc, rn_stream_t stream) {
-  RN_CHECK_ARG(d && dy && w_crsk && dx && bn_x && bn_mean && bn_scale && bn_shift && acc, "null argument");
-  RN_CHECK_ARG(d->dtype == RN_BF16 && d->c % 8 == 0 && d->c == d->c_real,
-               "accumulated BN reduction: bf16, whole 8-channel chunks");
-  IgemmArgs a = make_igemm_args(d, 1);
-  a.x = dy; a.w = w_crsk; a.y = dx; a.add = add_src;
-  a.bnacc = acc; a.bn_x = bn_x; a.bn_mean = bn_mean; a.bn_sc = bn_scale; a.bn_sh = bn_shift; a.bn_relu = relu;
-  return launch_igemm<bf16_t, bf16_t>(a, as_stream(stream));
 }
 
 int32_t rn_conv_tile(const rn_conv_desc* d, int32_t mode) {

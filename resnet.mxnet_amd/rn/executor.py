@@ -860,14 +860,6 @@ class Executor:
                             (stats_mode == "2" or self._big_tile(src, 0)):
                         src.bnstats = True
                         op.part_src = src
-                        # RN_BN_ACC=1: sums accumulated in fp64 atomics by the conv epilogue about the
-                        # moving mean (no partial merge pass). Off by default: measured +2 ms per step
-                        # (the device-scope fp64 atomics cost more than the merge they replace)
-                        op.bnacc = None
-                        if self.dtype == BF16 and os.environ.get("RN_BN_ACC", "0") == "1" and \
-                                self._big_tile(src, 0, 128) and getattr(src, "xf", None) is None:
-                            op.bnacc = self._zeros(L.RN_BN_ACC_REPLICAS * 2 * op.x.cp, self.torch.float64)
-                            src.stats_bn = op
         for op in plan.ops:
             if op.kind == "bn":
                 d = L.BNDesc(dtype=self.dtype, m=op.x.rows, c=op.x.cp, c_real=op.x.c, eps=op.eps,
@@ -989,10 +981,6 @@ class Executor:
                                    gamma, self._pp(op.beta), self._ap(op.mean), self._ap(op.var), op.sc, op.sh, sp)
                 if op.use_global_stats:
                     F.append(infer)
-                elif op.part_src is not None and getattr(op, "bnacc", None) is not None:
-                    F.append(self._call("rn_bn_fwd_train_acc", L.C.byref(op.desc), self._p(op.bnacc),
-                                        self._ap(op.mean), self._p(self.act(x)), yptr, gamma, self._pp(op.beta),
-                                        self._ap(op.mean), self._ap(op.var), op.sm, op.si, op.sc, op.sh, sp))
                 elif op.part_src is not None:
                     s_ = op.part_src
                     F.append(self._call("rn_bn_fwd_train_part", L.C.byref(op.desc), self._p(s_.part), s_.part_blocks,
@@ -1125,10 +1113,6 @@ class Executor:
         xf = getattr(op, "xf", None)
         sc, sh = (xf.sc, xf.sh) if xf is not None else (None, None)
         part = None
-        bn = getattr(op, "stats_bn", None)
-        if stats and op.bnstats and bn is not None:  # BN sums accumulated by the epilogue (fp64 atomics)
-            return self._call("rn_conv_fwd_bnacc", L.C.byref(d), xptr, self._p(op.wk), y, res, self._ap(bn.mean),
-                              self._p(bn.bnacc), sp)
         if stats and op.bnstats:
             if getattr(op, "part", None) is None:
                 op.part_blocks = int(self.lib.rn_conv_bnstats_blocks(L.C.byref(d)))
@@ -1271,19 +1255,6 @@ class Executor:
                     # the conv dgrad that completes this BN's output gradient also reduces its backward
                     # (sum dz, sum dz*(x - mean)); the BN then needs only finalize + apply
                     _, ci, cop, cdy, cout, cadd = w
-                    if self.dtype == BF16 and os.environ.get("RN_BN_ACC", "0") == "1" and self._big_tile(cop, 1, 128):
-                        op.bnacc2 = self._zeros(L.RN_BN_ACC_REPLICAS * 2 * op.y.cp, self.torch.float64)
-                        self._bwd[ci] = self._call("rn_conv_bwd_data_bnacc", L.C.byref(cop.desc), self._p(cdy),
-                                                   self._p(cop.wc), self._p(cout), self._p(cadd),
-                                                   self._p(self.act(x)), op.sm, op.sc, op.sh, int(op.relu),
-                                                   self._p(op.bnacc2), sp)
-                        self._bwd.append(self._call("rn_bn_bwd_acc", L.C.byref(op.desc), self._p(op.bnacc2),
-                                                    self._p(self.act(x)), self._p(dy), self._p(out), self._p(add),
-                                                    self._pp(op.gamma), op.sm, op.si, op.sc, op.sh,
-                                                    self._gp(op.gamma), self._gp(op.beta), wsp, sp))
-                        self.param_done_at[op.gamma] = len(self._bwd)
-                        self.param_done_at[op.beta] = len(self._bwd)
-                        continue
                     op.bnred_blocks = int(self.lib.rn_conv_bnred_blocks(L.C.byref(cop.desc)))
                     op.bnred = self._zeros(op.bnred_blocks * op.y.cp * 2, self.torch.float32)
                     self._bwd[ci] = self._call("rn_conv_bwd_data_bnred", L.C.byref(cop.desc), self._p(cdy),

@@ -9,7 +9,6 @@ import os
 from .build import LIB_PATH, build, needs_build
 
 RN_BF16 = 0
-RN_BN_ACC_REPLICAS = 64  # include/rn.h: fp64 BatchNorm accumulators are double[replicas][2][c]
 RN_F32 = 1
 RN_POOL_MAX = 0
 RN_POOL_AVG = 1
@@ -48,10 +47,6 @@ SIGNATURES = {
     "rn_conv_fwd_x": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_filter_x": (_i32, [_P, _P, _P, _P, _P, _P, _P, _i64, _P]),
     "rn_conv_bwd_data_bnred": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P, _P]),
-    "rn_conv_fwd_bnacc": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P]),
-    "rn_conv_bwd_data_bnacc": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P, _P]),
-    "rn_bn_fwd_train_acc": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
-    "rn_bn_bwd_acc": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bnred_blocks": (_i64, [_P]),
     "rn_bn_bwd_part": (_i32, [_P, _P, _i64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_data": (_i32, [_P, _P, _P, _P, _P, _P]),

@@ -513,11 +513,9 @@ def big_tiles(request):
 @pytest.mark.parametrize("dtype", [F32, BF16])
 @pytest.mark.parametrize("case", [(3, 32, 13, 11, 48, 3, 2, 1), (2, 64, 14, 14, 256, 1, 1, 0), (2, 16, 9, 9, 64, 1, 1, 0),
                                   (3, 128, 20, 20, 256, 3, 1, 1)])
-@pytest.mark.parametrize("acc", [False, True], ids=["partials", "fp64acc"])
-def test_conv_bnstats_epilogue(gpu, dtype, case, big_tiles, acc, tile_variant):
+def test_conv_bnstats_epilogue(gpu, dtype, case, big_tiles, tile_variant):
     """BatchNorm statistics emitted by the conv epilogue (rn_conv_fwd_bnstats, with the fused
-    residual add) and merged by rn_bn_fwd_train_part == a BatchNorm over the stored conv output.
-    acc: the fp64-accumulated variant (rn_conv_fwd_bnacc + rn_bn_fwd_train_acc, 256-row tiles)."""
+    residual add) and merged by rn_bn_fwd_train_part == a BatchNorm over the stored conv output."""
     n, c, h, w, k, r, st, pd = case
     x, wt = _conv_data(case, 13)
     if dtype == BF16:
@@ -532,24 +530,16 @@ def test_conv_bnstats_epilogue(gpu, dtype, case, big_tiles, acc, tile_variant):
     L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), p(wk), None, stream())
     y = torch.zeros((n, P, Q, d.k_pad), dtype=tdt(dtype), device=gpu)
     lib = L.load()
-    if acc and (dtype != BF16 or lib.rn_conv_tile(C.byref(d), 0) < 128):
-        pytest.skip("accumulated sums: bf16 on the 256-row tile only")
     nblk = lib.rn_conv_bnstats_blocks(C.byref(d))
     part = torch.zeros(nblk * 3 * d.k_pad, dtype=torch.float32, device=gpu)
     rd = to_nhwc(res, dtype, gpu)
-    mm0 = np.random.default_rng(17).standard_normal(k) * 0.5  # the pivot: any moving mean works
-    pivot = torch.tensor(np.pad(mm0, (0, d.k_pad - k)), dtype=torch.float32, device=gpu)
-    bacc = torch.zeros(L.RN_BN_ACC_REPLICAS * 2 * d.k_pad, dtype=torch.float64, device=gpu)
-    if acc:
-        L.call("rn_conv_fwd_bnacc", C.byref(d), p(xd), p(wk), p(y), p(rd), p(pivot), p(bacc), stream())
-    else:
-        L.call("rn_conv_fwd_bnstats", C.byref(d), p(xd), p(wk), p(y), dtype, p(rd), None, p(part), stream())
+    L.call("rn_conv_fwd_bnstats", C.byref(d), p(xd), p(wk), p(y), dtype, p(rd), None, p(part), stream())
     torch.cuda.synchronize()
     conv_out = from_nhwc(y, k)  # the stored (rounded) values the statistics must describe
     gamma = np.random.default_rng(15).uniform(0.5, 1.5, k)
     beta = np.random.default_rng(16).standard_normal(k) * 0.1
     y_ref, cache = ops.bn_train_fwd(conv_out, gamma, beta, 1e-5, False)
-    mm_start = mm0 if acc else np.zeros(k)
+    mm_start = np.zeros(k)
     mm_ref, mv_ref = ops.bn_moving_update(mm_start, np.ones(k), cache[3], cache[4], 0.9)
     bd = L.BNDesc(dtype=dtype, m=n * P * Q, c=d.k_pad, c_real=k, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1)
     f = lambda a: torch.tensor(np.pad(a, (0, d.k_pad - k)), dtype=torch.float32, device=gpu)
@@ -557,15 +547,9 @@ def test_conv_bnstats_epilogue(gpu, dtype, case, big_tiles, acc, tile_variant):
     sm, si, sc, sh = [torch.zeros(d.k_pad, dtype=torch.float32, device=gpu) for _ in range(4)]
     yb = torch.zeros_like(y)
     ws = torch.zeros(lib.rn_bn_workspace_bytes(C.byref(bd)) // 4 + 16, dtype=torch.float32, device=gpu)
-    if acc:  # the pivot is the moving mean itself, read before its update
-        L.call("rn_bn_fwd_train_acc", C.byref(bd), p(bacc), p(mm), p(y), p(yb), p(g_d), p(b_d), p(mm), p(mv),
-               p(sm), p(si), p(sc), p(sh), stream())
-    else:
-        L.call("rn_bn_fwd_train_part", C.byref(bd), p(part), nblk, lib.rn_conv_bn_part_rows(C.byref(d), 0), d.k_pad, p(y), p(yb), p(g_d), p(b_d), p(mm),
-               p(mv), p(sm), p(si), p(sc), p(sh), p(ws), stream())
+    L.call("rn_bn_fwd_train_part", C.byref(bd), p(part), nblk, lib.rn_conv_bn_part_rows(C.byref(d), 0), d.k_pad, p(y), p(yb), p(g_d), p(b_d), p(mm),
+           p(mv), p(sm), p(si), p(sc), p(sh), p(ws), stream())
     torch.cuda.synchronize()
-    if acc:
-        assert not bacc.any()  # consumed and re-zeroed for the next step
     assert rel_err(sm.cpu().numpy()[:k], cache[3]) < 1e-6
     assert rel_err(mv.cpu().numpy()[:k], mv_ref) < 1e-5
     assert rel_err(mm.cpu().numpy()[:k], mm_ref) < 1e-5
@@ -766,8 +750,7 @@ def test_stem_padded_nhwc4(gpu, mode, geom):
 @pytest.mark.parametrize("dtype", [F32, BF16])
 @pytest.mark.parametrize("case", [(2, 64, 14, 14, 128, 3, 1, 1), (2, 128, 14, 14, 256, 1, 2, 0),
                                   (3, 32, 13, 11, 48, 3, 2, 1), (3, 256, 20, 20, 128, 3, 2, 1)])
-@pytest.mark.parametrize("acc", [False, True], ids=["partials", "fp64acc"])
-def test_dgrad_bn_backward_fusion(gpu, dtype, case, big_tiles, acc, tile_variant):
+def test_dgrad_bn_backward_fusion(gpu, dtype, case, big_tiles, tile_variant):
     """rn_conv_bwd_data_bnred + rn_bn_bwd_part == conv dgrad followed by the BatchNorm+ReLU backward
     of the BN that produced the conv's input (pre-activation units)."""
     n, c, h, w, k, r, st, pd = case
@@ -802,31 +785,17 @@ def test_dgrad_bn_backward_fusion(gpu, dtype, case, big_tiles, acc, tile_variant
     xbd = to_nhwc(xb, dtype, gpu)
     L.call("rn_bn_fwd_train", C.byref(bd), p(xbd), None, p(g_d), p(b_d), p(mm), p(mv), p(sm), p(si), p(sc), p(sh),
            p(ws), stream())
-    if acc and (dtype != BF16 or lib.rn_conv_tile(C.byref(d), 1) < 128):
-        pytest.skip("accumulated sums: bf16 on the 256-row tile only")
     dact = to_nhwc(prev, dtype, gpu)                               # accumulated in place (add_src = out)
     nrb = lib.rn_conv_bnred_blocks(C.byref(d))
     part = torch.full((nrb * d.c * 2,), float("nan"), dtype=torch.float32, device=gpu)  # every slot written
-    bacc = torch.zeros(L.RN_BN_ACC_REPLICAS * 2 * d.c, dtype=torch.float64, device=gpu)
     dyd = to_nhwc(dy, dtype, gpu)
-    if acc:
-        L.call("rn_conv_bwd_data_bnacc", C.byref(d), p(dyd), p(wc), p(dact), p(dact), p(xbd), p(sm), p(sc), p(sh), 1,
-               p(bacc), stream())
-        part.zero_()
-    else:
-        L.call("rn_conv_bwd_data_bnred", C.byref(d), p(dyd), p(wc), p(dact), p(dact), p(xbd), p(sm), p(sc), p(sh), 1,
+    L.call("rn_conv_bwd_data_bnred", C.byref(d), p(dyd), p(wc), p(dact), p(dact), p(xbd), p(sm), p(sc), p(sh), 1,
                p(part), stream())
     dx = torch.zeros_like(xbd)
     dg, db = torch.zeros(d.c, dtype=torch.float32, device=gpu), torch.zeros(d.c, dtype=torch.float32, device=gpu)
-    if acc:
-        L.call("rn_bn_bwd_acc", C.byref(bd), p(bacc), p(xbd), p(dact), p(dx), None, p(g_d), p(sm), p(si), p(sc),
-               p(sh), p(dg), p(db), p(ws), stream())
-    else:
-        L.call("rn_bn_bwd_part", C.byref(bd), p(part), nrb, p(xbd), p(dact), p(dx), None, p(g_d), p(sm), p(si), p(sc),
+    L.call("rn_bn_bwd_part", C.byref(bd), p(part), nrb, p(xbd), p(dact), p(dx), None, p(g_d), p(sm), p(si), p(sc),
                p(sh), p(dg), p(db), p(ws), stream())
     torch.cuda.synchronize()
-    if acc:
-        assert not bacc.any()
     assert rel_err(from_nhwc(dact, c), dact_ref) < TOL[dtype]
     assert not torch.isnan(part).any()
     assert rel_err(db.cpu().numpy()[:c], db_ref) < (1e-4 if dtype == F32 else 2e-2)

@@ -171,13 +171,9 @@ def test_plan_bn_bwd_fusion_default(monkeypatch):
     def counts():
         ex = Executor(Plan(graphs.resnet50(), [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")
         names = [c[0] for c in ex._bwd]
-        fused = names.count("rn_conv_bwd_data_bnred") + names.count("rn_conv_bwd_data_bnacc")
-        return fused, names.count("rn_bn_bwd_part") + names.count("rn_bn_bwd_acc"), names.count("rn_bn_bwd")
+        return names.count("rn_conv_bwd_data_bnred"), names.count("rn_bn_bwd_part"), names.count("rn_bn_bwd")
     monkeypatch.delenv("RN_BN_BWD_FUSION", raising=False)
     assert counts() == (41, 41, 9)
-    monkeypatch.setenv("RN_BN_ACC", "1")  # fp64-accumulated sums instead of per-block partials
-    assert counts() == (41, 41, 9)
-    monkeypatch.delenv("RN_BN_ACC")
     monkeypatch.setenv("RN_BN_BWD_FUSION", "2")
     assert counts() == (48, 48, 2)
     monkeypatch.setenv("RN_BN_BWD_FUSION", "0")

@@ -12,8 +12,8 @@ from rn import graphs  # noqa: E402
 from rn.executor import Executor, Plan  # noqa: E402
 from bench import conv_call_bytes  # noqa: E402
 
-CONV_CALLS = ("rn_conv_fwd", "rn_conv_fwd_bnstats", "rn_conv_fwd_x", "rn_conv_fwd_bnacc", "rn_conv_bwd_data",
-              "rn_conv_bwd_data_bnred", "rn_conv_bwd_data_bnacc", "rn_conv_bwd_filter", "rn_conv_bwd_filter_x", "rn_conv_bwd_filter_ws",
+CONV_CALLS = ("rn_conv_fwd", "rn_conv_fwd_bnstats", "rn_conv_fwd_x", "rn_conv_bwd_data",
+              "rn_conv_bwd_data_bnred", "rn_conv_bwd_filter", "rn_conv_bwd_filter_x", "rn_conv_bwd_filter_ws",
               "rn_stem_conv_fwd_p4", "rn_stem_conv_wgrad_p4")
 
 
