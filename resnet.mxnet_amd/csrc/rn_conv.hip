@@ -94,25 +94,6 @@ constexpr uint32_t kOob = 0xFFFFFFF0u;
 // channels of the BatchNorm+ReLU input transform the LDS-DMA kernels keep in LDS (XF)
 constexpr int kXfMaxC = 2048;
 
-// BatchNorm-apply + ReLU of the consumer's input, applied while staging (the BN+ReLU output of
-// pre-activation units feeding 1x1 convs is never written to HBM): v = max(x*sc[c] + sh[c], 0)
-// over one 16-byte chunk of channels c..c+CE-1.
-template <typename T>
-__device__ __forceinline__ uint4 bnrelu_chunk(const uint4& u, const float* __restrict__ sc,
-                                              const float* __restrict__ sh, int c) {
-  constexpr int CE = 16 / sizeof(T);
-  float f[CE], a[CE], b[CE];
-  chunk_to_f(u, f, (const T*)nullptr);
-#pragma unroll
-  for (int e = 0; e < CE; e += 4) {  // 16-byte coefficient loads (channel chunks are 16-B aligned)
-    *reinterpret_cast<float4*>(a + e) = *reinterpret_cast<const float4*>(sc + c + e);
-    *reinterpret_cast<float4*>(b + e) = *reinterpret_cast<const float4*>(sh + c + e);
-  }
-#pragma unroll
-  for (int e = 0; e < CE; ++e) f[e] = fmaxf(fmaf(f[e], a[e], b[e]), 0.f);
-  return f_to_chunk(f, (const T*)nullptr);
-}
-
 // XCD-aware block order: the dispatcher deals consecutive workgroup ids round-robin over the 8
 // XCDs (each with a private L2). Bijective remap so that every XCD walks a contiguous range of
 // logical tiles: neighbouring tiles (which share operand panels) then share an L2.
@@ -288,6 +269,11 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
   const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.w_bytes, 0x00020000);
 
+  // BN+ReLU input transform (in_sc): the stage's channel coefficients are loaded with its chunks and
+  // applied when the chunks are written to LDS (store_stage, after the MFMA phase), so the loads stay
+  // in flight under the MFMAs; chunks outside the image stay zero (the conv pads the BN+ReLU output)
+  float xsc[CE], xsh[CE];
+  uint32_t xok = 0;
   auto load_stage = [&](uint4* ra, uint4* rb) {
     int hoff, woff, c, toff;
     int dtr = 0, dts = 0, dcb = 0;  // stage's tap / channel-block (DMA fast path)
@@ -362,9 +348,17 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
       if (ok) {
         const int off = p.diag_l1 ? (c & 63) : (a_pix[i] + hin * p.W + win) * p.C + cbase + c;  // < 2^31
         ra[i] = *reinterpret_cast<const uint4*>(xg + off);
-        if (p.in_sc) ra[i] = bnrelu_chunk<T>(ra[i], p.in_sc, p.in_sh, c);
       } else {
         ra[i] = make_uint4(0, 0, 0, 0);
+      }
+      if (i == 0) xok = 0;
+      xok |= (uint32_t)ok << i;
+    }
+    if (p.in_sc && cok) {
+#pragma unroll
+      for (int e = 0; e < CE; e += 4) {
+        *reinterpret_cast<float4*>(xsc + e) = *reinterpret_cast<const float4*>(p.in_sc + cbase + c + e);
+        *reinterpret_cast<float4*>(xsh + e) = *reinterpret_cast<const float4*>(p.in_sh + cbase + c + e);
       }
     }
 #pragma unroll
@@ -379,7 +373,15 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int row = (tid >> 3) + 32 * i;
-      As[row * 8 + swz(row, ch)] = ra[i];
+      uint4 v = ra[i];
+      if (p.in_sc) {
+        float f[CE];
+        chunk_to_f(v, f, (const T*)nullptr);
+#pragma unroll
+        for (int e = 0; e < CE; ++e) f[e] = fmaxf(fmaf(f[e], xsc[e], xsh[e]), 0.f);
+        v = ((xok >> i) & 1u) ? f_to_chunk(f, (const T*)nullptr) : make_uint4(0, 0, 0, 0);
+      }
+      As[row * 8 + swz(row, ch)] = v;
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
@@ -1241,7 +1243,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   }
 
   uint4 ra[A_CH], rb[B_CH];
+  uint32_t xok = 0;  // (XF) B chunk i holds an input pixel: transformed when stored to LDS
   auto load_stage = [&](int mb) {
+    xok = 0;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int m = mb + tid / A_CPR + A_RSTEP * i;
@@ -1264,13 +1268,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
         if ((unsigned)hin < (unsigned)p.H && (unsigned)win < (unsigned)p.W) {
           v = *reinterpret_cast<const uint4*>(
               xg + ((int64_t)(n * p.H + hin) * p.W + win) * p.C + b_ch);
-          if constexpr (XF) {
-            float f[CE];
-            chunk_to_f(v, f, (const T*)nullptr);
-#pragma unroll
-            for (int e = 0; e < CE; ++e) f[e] = fmaxf(fmaf(f[e], tsc[e], tsh[e]), 0.f);
-            v = f_to_chunk(f, (const T*)nullptr);
-          }
+          xok |= 1u << i;
         }
       }
       rb[i] = v;
@@ -1287,7 +1285,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int row = tid / B_CPR + B_RSTEP * i;
-      Bs[row * B_CPR + (b_c ^ (swz_tr(row) & (B_CPR - 1)))] = rb[i];
+      uint4 v = rb[i];
+      if constexpr (XF) {  // after the MFMA phase: the loads were in flight under it
+        float f[CE];
+        chunk_to_f(v, f, (const T*)nullptr);
+#pragma unroll
+        for (int e = 0; e < CE; ++e) f[e] = fmaxf(fmaf(f[e], tsc[e], tsh[e]), 0.f);
+        v = ((xok >> i) & 1u) ? f_to_chunk(f, (const T*)nullptr) : make_uint4(0, 0, 0, 0);
+      }
+      Bs[row * B_CPR + (b_c ^ (swz_tr(row) & (B_CPR - 1)))] = v;
     }
   };
 
