@@ -91,8 +91,8 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rsrc, const void* l
                                            0, 0, 0);
 }
 constexpr uint32_t kOob = 0xFFFFFFF0u;
-// channels of the BatchNorm+ReLU input transform the LDS-DMA kernels keep in LDS (XF)
-constexpr int kXfMaxC = 2048;
+// channels of the BatchNorm+ReLU input transform the LDS-DMA kernels keep in LDS (XF; W4 tile)
+constexpr int kXfMaxC = 2048, kXfMaxCW4 = 512;
 
 // XCD-aware block order: the dispatcher deals consecutive workgroup ids round-robin over the 8
 // XCDs (each with a private L2). Bijective remap so that every XCD walks a contiguous range of
@@ -693,13 +693,20 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // rounded to bf16 exactly as bn_apply_kernel does, between the K-tile's vmcnt wait and its barrier.
 // Chunks the DMA zero-filled (halo taps, rows past the tile) stay zero: the conv pads the BN+ReLU
 // output with zeros.
-template <int BN, int NBUF, int EPI = 0, bool M32 = false, int BM = 256, int SC = 0, int Q8 = 0, int XF = 0>
-__global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_big_kernel(IgemmArgs p) {
+// W4: the 224x128 tile on 4 waves (2 x 2, each 112 x 64, the wave tile of the 224x256 kernel) with
+// ONE K-tile buffer: 72 KB of LDS, two workgroups per CU, so one workgroup's epilogue (its output
+// stores and LDS staging) overlaps the other's loads and MFMAs. For 1x1, pad-0 convolutions with at
+// most two K-tiles (their tiles are load / store bound: the 8-wave tiles alternate a read+MFMA phase
+// and a write phase on each CU); no halo, so the DMA rows need no in-image test.
+template <int BN, int NBUF, int EPI = 0, bool M32 = false, int BM = 256, int SC = 0, int Q8 = 0, int XF = 0, int W4 = 0>
+__global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1) void igemm_big_kernel(IgemmArgs p) {
   constexpr int ES = Q8 ? 1 : 2;                 // operand bytes per element
   constexpr int BMA = 256, CE = 16 / ES, BKE = 128 / ES;
   using OutT = typename std::conditional<Q8 == 2, float, bf16_t>::type;
-  constexpr int NW = BN == 64 ? 4 : 8;           // waves
-  constexpr int WAVES_N = BN == 64 ? 1 : 4, WAVES_M = NW / WAVES_N;
+  constexpr int NW = BN == 64 || W4 ? 4 : 8;     // waves
+  constexpr int WAVES_N = BN == 64 ? 1 : W4 ? 2 : 4, WAVES_M = NW / WAVES_N;
+  static_assert(!W4 || (BN == 128 && BM == 224 && NBUF == 1 && !M32 && !SC && !Q8), "W4 tile");
+  constexpr int XFC = W4 ? kXfMaxCW4 : kXfMaxC;   // (XF) channels of the LDS scale / shift table
   constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;  // wave tile
   constexpr int RPR = NW * 8;                    // rows per DMA round (8 per wave)
   constexpr int AR = BMA / RPR, BR = BN / RPR;   // DMA rounds per K-tile
@@ -717,7 +724,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   static_assert(BN != 64 || !SC || EPI == 0, "the stem modes have no BatchNorm epilogue");
   static_assert(!XF || (!SC && !Q8 && EPI != 2 && BN >= 128), "input transform: bf16 forward, 128/256 columns");
   constexpr int kMain = NBUF * kStage > kEpChunks ? NBUF * kStage : kEpChunks;
-  constexpr int kXfChunks = XF ? 2 * kXfMaxC / 4 : 0;  // fp32 scale[kXfMaxC], shift[kXfMaxC]
+  constexpr int kXfChunks = XF ? 2 * XFC / 4 : 0;  // fp32 scale[XFC], shift[XFC]
   __shared__ __attribute__((aligned(16))) uint4 smem[kMain + kXfChunks];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -728,7 +735,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   if constexpr (XF) {
     for (int i = tid; i < p.C; i += NW * 64) {
       xs[i] = p.in_sc[i];
-      xs[kXfMaxC + i] = p.in_sh[i];
+      xs[XFC + i] = p.in_sh[i];
     }
     __syncthreads();
   }
@@ -849,7 +856,8 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
   };
   auto piece = [&](int k) __attribute__((always_inline)) {
     if (k < AR) {
-      const bool ok = d_cok && (unsigned)(a_h[k] + d_dh) < (unsigned)p.H && (unsigned)(a_w[k] + d_dw) < (unsigned)p.W;
+      const bool ok = W4 ? d_cok && a_h[k] >= 0
+                         : d_cok && (unsigned)(a_h[k] + d_dh) < (unsigned)p.H && (unsigned)(a_w[k] + d_dw) < (unsigned)p.W;
       if constexpr (XF) okb |= (uint32_t)ok << (d_buf * AR + k);
       dma16_asm(rs_x, d_la + k * (RPR * 128), ok ? ((uint32_t)((a_row[k] + d_toffa) * ES) & dmask) : kOob);
     } else {
@@ -918,7 +926,7 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
         }
         // 2 buffers: the DMAs over the first half of the K-tile's MFMA groups, so they have the
         // longest to land; 3 buffers (one more K-tile in flight): spread over all of them
-        constexpr int G = NBUF == 2 ? KS / 2 * MI : KS * MI;
+        constexpr int G = NBUF == 1 ? 0 : NBUF == 2 ? KS / 2 * MI : KS * MI;
         const int g = ks * MI + i;
         if (g < G) {
 #pragma unroll
@@ -934,8 +942,8 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
     float a[8], b[8];
     *reinterpret_cast<float4*>(a) = *reinterpret_cast<const float4*>(xs + c0);
     *reinterpret_cast<float4*>(a + 4) = *reinterpret_cast<const float4*>(xs + c0 + 4);
-    *reinterpret_cast<float4*>(b) = *reinterpret_cast<const float4*>(xs + kXfMaxC + c0);
-    *reinterpret_cast<float4*>(b + 4) = *reinterpret_cast<const float4*>(xs + kXfMaxC + c0 + 4);
+    *reinterpret_cast<float4*>(b) = *reinterpret_cast<const float4*>(xs + XFC + c0);
+    *reinterpret_cast<float4*>(b + 4) = *reinterpret_cast<const float4*>(xs + XFC + c0 + 4);
 #pragma unroll
     for (int k = 0; k < AR; ++k) {
       uint4* cp = smem + buf * kStage + k * (RPR * 8) + tid;
@@ -952,6 +960,18 @@ __global__ __launch_bounds__(BN == 64 ? 256 : 512, BN == 64 ? 2 : 1) void igemm_
 #pragma unroll
   for (int s = 0; s < NBUF - 1; ++s) issue(s);
   for (int t = 0; t < nstage; ++t) {
+    if constexpr (NBUF == 1) {  // one buffer: refilled once every wave is done reading it
+      if (t > 0) __syncthreads();
+      issue(0);
+      wait_vmcnt<0>();
+      if constexpr (XF) {
+        xform(0, xf_cb);
+        if (++xf_cb == ncb) xf_cb = 0;
+      }
+      __syncthreads();
+      compute(0);
+      continue;
+    }
     // K-tile t has landed for this thread once at most the later K-tiles' DMAs are outstanding
     if (!(p.sched & 4)) {  // (diagnostic bit 4: no wait, no barrier -- wrong results)
       if (NBUF == 3) wait_vmcnt<LPT>();
@@ -2033,6 +2053,22 @@ IgemmArgs make_igemm_args(const rn_conv_desc* d, int mode) {
   return a;
 }
 
+// The 4-wave one-buffer 224x128 tile (igemm_big_kernel W4, two workgroups per CU) for these
+// arguments? rn_set_tuning 11: 0 auto (forward 1x1, pad 0, ONE K-tile, >= 1024 tiles: the stage-1
+// conv3 / shortcut layers, 230 -> 215 us; measured no better on the 2-K-tile and dgrad layers,
+// DESIGN.md 3), 1 never, 2 every eligible 1x1 pad-0 layer, fwd and dgrad (tests).
+bool w4_tile(const IgemmArgs& a) {
+  const int mode = g_tune[RN_TUNE_IGEMM_W4];
+  if (mode == 1 || g_tune[RN_TUNE_IGEMM_ROWS] == 1 || a.ncls != 1 || a.gred > 0 || a.smallc || a.bias || a.K <= 64)
+    return false;
+  const IgemmCls& c = a.cls[0];
+  if (c.nr != 1 || c.ns != 1 || c.hoff0 != 0 || c.woff0 != 0 || c.hb0 != 0 || c.wb0 != 0) return false;
+  if (a.in_sc && a.C > kXfMaxCW4) return false;
+  if (mode == 2) return true;
+  const int64_t tiles = ceil_div((int64_t)a.N * c.Pc * c.Qc, 224) * ceil_div(a.K, 128);
+  return a.hinc > 0 && ceil_div(a.cblk, 64) == 1 && tiles >= 1024;
+}
+
 // Columns of the 256-row tile launch_igemm runs for these arguments (bf16 in and out), 0 for the
 // 128-row kernel. rn_set_tuning 4: 0 auto, 1 off, 2 force 256x256, 3 force 256x128. Auto, from
 // per-layer measurements over ResNet-50 (tools/conv_bench.py): 256x256 when the output has >= 256
@@ -2062,6 +2098,7 @@ int big_tile_cols(const IgemmArgs& a, int64_t xb, int64_t wb) {
   }
   if (big == 2) return 256;
   if (big == 3) return 128;
+  if (w4_tile(a)) return 128;
   int64_t rows = 0;  // 256-row tiles over all parity classes
   for (int z = 0; z < a.ncls; ++z) rows += ceil_div((int64_t)a.N * a.cls[z].Pc * a.cls[z].Qc, 256);
   return (a.K >= 256 && rows * ceil_div(a.K, 256) >= 192) ? 256 : 128;
@@ -2135,6 +2172,22 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   if (epi == 0) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 0, M, R>), grid, dim3(512), 0, st, b);        \
   else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 1, M, R>), grid, dim3(512), 0, st, b);   \
   else hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 2, M, R>), grid, dim3(512), 0, st, b);
+      if (bn == 128 && bm == 224 && w4_tile(a)) {  // two 4-wave workgroups per CU
+        dim3 g4((unsigned)(ceil_div(maxMc, 224) * b.ntn), 1, 1);
+        const int pw = g_tune[RN_TUNE_IGEMM_PERSIST] / 8 * 16;
+        b.ntiles = 0;
+        if (pw > 0 && (int)g4.x > pw) {
+          b.ntiles = (int)g4.x;
+          g4.x = (unsigned)pw;
+        }
+        if (a.in_sc) {
+          if (epi == 0) hipLaunchKernelGGL((igemm_big_kernel<128, 1, 0, false, 224, 0, 0, 1, 1>), g4, dim3(256), 0, st, b);
+          else hipLaunchKernelGGL((igemm_big_kernel<128, 1, 1, false, 224, 0, 0, 1, 1>), g4, dim3(256), 0, st, b);
+        } else if (epi == 0) hipLaunchKernelGGL((igemm_big_kernel<128, 1, 0, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
+        else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<128, 1, 1, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
+        else hipLaunchKernelGGL((igemm_big_kernel<128, 1, 2, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
+        return rn_check_launch("igemm_big_w4");
+      }
       if (a.in_sc) {  // (big_tile_cols: 224 rows, forward)
         RN_CHECK_ARG(bm == 224 && epi != 2, "input transform tile");
         if (bn == 256) {

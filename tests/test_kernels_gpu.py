@@ -502,12 +502,17 @@ def tile_variant(request):
     L.call("rn_set_tuning", 10, 512)
 
 
-@pytest.fixture(params=[0, 2], ids=["auto", "big256"])
+@pytest.fixture(params=[0, 2, "w4"], ids=["auto", "big256", "w4"])
 def big_tiles(request):
-    """rn_set_tuning 4 (igemm 256-row tiles): automatic choice, or 256x256 forced where eligible."""
-    L.call("rn_set_tuning", 4, request.param)
+    """rn_set_tuning 4 (igemm 256-row tiles): automatic choice, or 256x256 forced where eligible;
+    w4: rn_set_tuning 11 = 2, the 4-wave one-buffer 224x128 tile on every 1x1 pad-0 conv."""
+    if request.param == "w4":
+        L.call("rn_set_tuning", 11, 2)
+    else:
+        L.call("rn_set_tuning", 4, request.param)
     yield request.param
     L.call("rn_set_tuning", 4, 0)
+    L.call("rn_set_tuning", 11, 0)
 
 
 @pytest.mark.parametrize("dtype", [F32, BF16])
@@ -688,8 +693,8 @@ def test_conv_bnrelu_on_load_tiles(gpu, case, ws, big_tiles, tile_variant):
     dw0 = torch.zeros_like(dw)
     L.call("rn_conv_bwd_filter_ws", C.byref(d), p(act), p(dyd), p(dw0), p(wsd), wsb, stream())
     torch.cuda.synchronize()
-    if tile_variant[0] == 0:  # 224-row tiles: fused and unfused run the same tile (else the transform
-        assert torch.equal(y.view(torch.int16), y0.view(torch.int16))  # falls back to the 128-row kernel)
+    if tile_variant[0] == 0 and not (big_tiles == "w4" and c > 512):  # the same tile both ways (else the transform
+        assert torch.equal(y.view(torch.int16), y0.view(torch.int16))  # falls back to another tile)
     if r == 1 and wsb > 0:  # the slab path is deterministic; atomics / the 3x3 fallback kernel are not
         assert torch.equal(dw, dw0)
     else:
@@ -749,7 +754,8 @@ def test_stem_padded_nhwc4(gpu, mode, geom):
 
 @pytest.mark.parametrize("dtype", [F32, BF16])
 @pytest.mark.parametrize("case", [(2, 64, 14, 14, 128, 3, 1, 1), (2, 128, 14, 14, 256, 1, 2, 0),
-                                  (3, 32, 13, 11, 48, 3, 2, 1), (3, 256, 20, 20, 128, 3, 2, 1)])
+                                  (3, 32, 13, 11, 48, 3, 2, 1), (3, 256, 20, 20, 128, 3, 2, 1),
+                                  (2, 256, 14, 14, 128, 1, 1, 0), (3, 200, 9, 11, 96, 1, 1, 0)])
 def test_dgrad_bn_backward_fusion(gpu, dtype, case, big_tiles, tile_variant):
     """rn_conv_bwd_data_bnred + rn_bn_bwd_part == conv dgrad followed by the BatchNorm+ReLU backward
     of the BN that produced the conv's input (pre-activation units)."""

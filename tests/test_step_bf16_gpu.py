@@ -6,7 +6,8 @@ BatchNorm statistics / BN-backward reductions in the conv epilogues, the NHWC4 s
 weight gradients. `tiles="wide"` additionally forces the 256-column tiles (rn_set_tuning 4 = 2) and
 an 8-workgroup persistent grid (rn_set_tuning 10 = 8), so that at this small batch every eligible
 layer runs the 224x256 tile family the 256-image bench uses, with its BN epilogues, and walks
-several tiles per workgroup.
+several tiles per workgroup; `tiles="w4"` forces the 4-wave one-buffer 224x128 tile (rn_set_tuning
+11 = 2) on every 1x1 pad-0 layer, which the bench's stage-1/2 layers run.
 
 Reference: the numpy oracle in fp64 (symbol/resnet.py:77-121 restated) and its bf16-storage
 emulation (oracle.net.forward storage='bf16': weights and every stored activation rounded to
@@ -43,12 +44,15 @@ def _prio_stream():
     return torch.cuda.Stream(priority=min(lo, hi))
 
 
-@pytest.mark.parametrize("tiles", ["auto", "wide"])
+@pytest.mark.parametrize("tiles", ["auto", "wide", "w4"])
 def test_resnet50_bf16_step_gradients(gpu, tiles):
     from rn import lib as L
     lib = L.load()
     if tiles == "wide":
         L.check(lib.rn_set_tuning(4, 2), "tune")
+        L.check(lib.rn_set_tuning(10, 8), "tune")
+    if tiles == "w4":  # every 1x1 pad-0 layer on the 4-wave one-buffer tile, persistent over 16 workgroups
+        L.check(lib.rn_set_tuning(11, 2), "tune")
         L.check(lib.rn_set_tuning(10, 8), "tune")
     try:
         g = onet.resnet50_imagenet(num_classes=16)
@@ -60,6 +64,7 @@ def test_resnet50_bf16_step_gradients(gpu, tiles):
     finally:
         L.check(lib.rn_set_tuning(4, 0), "tune")
         L.check(lib.rn_set_tuning(10, 512), "tune")
+        L.check(lib.rn_set_tuning(11, 0), "tune")
     masks = res["relu_masks"][0]
     # (1) unreplayed: at 2 images of 112x112 a random-init ResNet-50 is chaotic under ANY rounding
     # (thousands of ReLU decisions flip; measured: the bf16 emulation's own gradients have cosine
