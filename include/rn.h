@@ -243,6 +243,14 @@ int rn_bn_fwd_infer(const rn_bn_desc* d, const void* x, void* y, const float* ga
                     const float* beta, const float* moving_mean, const float* moving_var,
                     float* scale, float* shift, rn_stream_t stream);
 
+/* The post-activation unit tail (symbol/resnext.py:40-47, symbol/resnet.py:63-74):
+ * y = act(bf16(xa*scale_a + shift_a) + b), b = bf16(xb*scale_b + shift_b) (the shortcut's
+ * BatchNorm) or, with scale_b = shift_b = NULL, xb itself; each BatchNorm output rounded to the
+ * storage type as rn_bn_apply stores it, so the result equals rn_bn_apply + rn_eltwise_add bit for
+ * bit while the BatchNorm outputs are never written. act = ReLU when relu != 0. */
+int rn_bn_apply_add(const rn_bn_desc* d, const void* xa, const float* scale_a, const float* shift_a,
+                    const void* xb, const float* scale_b, const float* shift_b, void* y, int32_t relu,
+                    rn_stream_t stream);
 /* Apply y = act(x*scale + shift) with precomputed per-channel scale/shift. */
 int rn_bn_apply(const rn_bn_desc* d, const void* x, void* y, const float* scale,
                 const float* shift, rn_stream_t stream);

@@ -370,6 +370,46 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x, 
   }
 }
 
+// ---- post-activation unit tail (symbol/resnext.py:40-47, symbol/resnet.py:63-74): y = act(bn_a(xa) +
+// b) with b = bn_b(xb) (the shortcut's BatchNorm) or xb itself. Each BatchNorm output is rounded to
+// the storage type before the add, exactly as the unfused bn_apply + eltwise_add pair stores and
+// re-reads it, so the result is bit-identical and the BatchNorm outputs are never written.
+template <typename T, bool RELU, bool BNB>
+__global__ __launch_bounds__(256) void bn_add_kernel(const T* __restrict__ xa, const float* __restrict__ sca,
+                                                     const float* __restrict__ sha, const T* __restrict__ xb,
+                                                     const float* __restrict__ scb, const float* __restrict__ shb,
+                                                     T* __restrict__ y, int64_t m, int c, int ct,
+                                                     int64_t rows_per_block) {
+  constexpr int CE = 16 / sizeof(T);
+  const int tc = threadIdx.x % ct, tr = threadIdx.x / ct, rl = blockDim.x / ct;
+  const int cbase = (blockIdx.x * ct + tc) * CE;
+  const int64_t r0 = blockIdx.y * rows_per_block;
+  const int64_t r1 = min(m, r0 + rows_per_block);
+  float a_sc[CE], a_sh[CE], b_sc[BNB ? CE : 1], b_sh[BNB ? CE : 1];
+#pragma unroll
+  for (int e = 0; e < CE; ++e) {
+    a_sc[e] = sca[cbase + e];
+    a_sh[e] = sha[cbase + e];
+    if constexpr (BNB) {
+      b_sc[e] = scb[cbase + e];
+      b_sh[e] = shb[cbase + e];
+    }
+  }
+  for (int64_t r = r0 + tr; r < r1; r += rl) {
+    float fa[CE], fb[CE];
+    chunk_to_f(*reinterpret_cast<const uint4*>(xa + r * c + cbase), fa, (const T*)nullptr);
+    chunk_to_f(*reinterpret_cast<const uint4*>(xb + r * c + cbase), fb, (const T*)nullptr);
+#pragma unroll
+    for (int e = 0; e < CE; ++e) {
+      const float va = to_f(from_f<T>(fmaf(fa[e], a_sc[e], a_sh[e])));
+      const float vb = BNB ? to_f(from_f<T>(fmaf(fb[e], b_sc[e], b_sh[e]))) : fb[e];
+      const float v = va + vb;
+      fa[e] = RELU ? fmaxf(v, 0.f) : v;
+    }
+    *reinterpret_cast<uint4*>(y + r * c + cbase) = f_to_chunk(fa, (const T*)nullptr);
+  }
+}
+
 // ---- backward reduce: sum dz, sum dz*(x - mean)
 template <typename T, bool RELU>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict__ x, const T* __restrict__ dy,
@@ -772,6 +812,36 @@ int rn_bn_fwd_infer(const rn_bn_desc* d, const void* x, void* y, const float* ga
   RN_CHECK_ARG(x != nullptr, "null x");
   if (d->dtype == RN_BF16) return bn_apply_t<bf16_t>(d, x, y, scale, shift, st);
   return bn_apply_t<float>(d, x, y, scale, shift, st);
+}
+
+int rn_bn_apply_add(const rn_bn_desc* d, const void* xa, const float* scale_a, const float* shift_a,
+                    const void* xb, const float* scale_b, const float* shift_b, void* y, int32_t relu,
+                    rn_stream_t stream) {
+  if (check_bn(d)) return -1;
+  RN_CHECK_ARG(xa && scale_a && shift_a && xb && y, "null argument");
+  RN_CHECK_ARG((scale_b == nullptr) == (shift_b == nullptr), "scale_b / shift_b must both be set or both null");
+  hipStream_t st = as_stream(stream);
+  const bool bnb = scale_b != nullptr;
+#define RN_BN_ADD(T)                                                                                           \
+  {                                                                                                            \
+    Geo g = make_apply_geo<T>(d->m, d->c);                                                                     \
+    dim3 gr(g.gx, g.nrb), bl(kThreads);                                                                        \
+    if (relu && bnb) hipLaunchKernelGGL((bn_add_kernel<T, true, true>), gr, bl, 0, st, (const T*)xa, scale_a,  \
+                                        shift_a, (const T*)xb, scale_b, shift_b, (T*)y, d->m, d->c, g.ct,      \
+                                        g.rows_per_block);                                                     \
+    else if (relu) hipLaunchKernelGGL((bn_add_kernel<T, true, false>), gr, bl, 0, st, (const T*)xa, scale_a,   \
+                                      shift_a, (const T*)xb, scale_b, shift_b, (T*)y, d->m, d->c, g.ct,        \
+                                      g.rows_per_block);                                                       \
+    else if (bnb) hipLaunchKernelGGL((bn_add_kernel<T, false, true>), gr, bl, 0, st, (const T*)xa, scale_a,    \
+                                     shift_a, (const T*)xb, scale_b, shift_b, (T*)y, d->m, d->c, g.ct,         \
+                                     g.rows_per_block);                                                        \
+    else hipLaunchKernelGGL((bn_add_kernel<T, false, false>), gr, bl, 0, st, (const T*)xa, scale_a, shift_a,   \
+                            (const T*)xb, scale_b, shift_b, (T*)y, d->m, d->c, g.ct, g.rows_per_block);        \
+  }
+  if (d->dtype == RN_BF16) RN_BN_ADD(bf16_t)
+  else RN_BN_ADD(float)
+#undef RN_BN_ADD
+  return rn_check_launch("bn_apply_add");
 }
 
 int rn_bn_apply(const rn_bn_desc* d, const void* x, void* y, const float* scale, const float* shift,

@@ -338,10 +338,8 @@ class Plan:
             op.xf = None
             if op.kind == "bn":
                 op.apply_fused = False
-        # default on since the LDS-DMA tiles apply it (igemm_big_kernel / wgrad_big_kernel XF): 22.82 ->
-        # 22.17 ms per step on one box (DESIGN.md section 3); RN_BN_APPLY_FUSION=0 writes act1 / act3
-        if os.environ.get("RN_BN_APPLY_FUSION", "1") != "1":
-            return
+            if op.kind == "add":
+                op.bn_a = op.bn_b = op.bn_a_key = None
         refs = {}
         for op in self.ops:
             for key in ("x", "res", "a", "b"):
@@ -349,6 +347,11 @@ class Plan:
                 if isinstance(t, TensorSpec):
                     refs.setdefault(id(t), []).append((op, key))
         out_ids = {id(t) for t in self.outputs}
+        self._fuse_bn_add(refs, out_ids)
+        # default on since the LDS-DMA tiles apply it (igemm_big_kernel / wgrad_big_kernel XF): 22.82 ->
+        # 22.17 ms per step on one box (DESIGN.md section 3); RN_BN_APPLY_FUSION=0 writes act1 / act3
+        if os.environ.get("RN_BN_APPLY_FUSION", "1") != "1":
+            return
         for bn in self.ops:
             if bn.kind != "bn" or not bn.relu or id(bn.y) in out_ids:
                 continue
@@ -361,6 +364,30 @@ class Plan:
             bn.y.virtual = True
             for u, _ in users:
                 u.xf = bn
+
+    def _fuse_bn_add(self, refs, out_ids):
+        """The post-activation unit tail (symbol/resnext.py:40-47, symbol/resnet.py:63-74: bn3 (+ the
+        shortcut's BN) -> add -> relu): a BatchNorm without ReLU whose output only this add reads is
+        applied inside the add (rn_bn_apply_add); its output is never written. RN_BN_ADD_FUSION=0 off."""
+        if os.environ.get("RN_BN_ADD_FUSION", "1") != "1":
+            return
+        producer = {id(op.y): op for op in self.ops if op.kind == "bn"}
+        for op in self.ops:
+            if op.kind != "add" or op.a is op.b:
+                continue
+            fused = []
+            for key in ("a", "b"):
+                t = getattr(op, key)
+                bn = producer.get(id(t))
+                if bn is not None and not bn.relu and id(t) not in out_ids and len(refs.get(id(t), [])) == 1:
+                    fused.append((key, bn))
+            if not fused:
+                continue
+            op.bn_a_key, op.bn_a = fused[0]
+            op.bn_b = fused[1][1] if len(fused) == 2 else None
+            for _, bn in fused:
+                bn.apply_fused = True
+                bn.y.virtual = True
 
     def _is_stem(self, conv_node):
         src = conv_node.inputs[0][0]
@@ -1033,6 +1060,15 @@ class Executor:
                         lst.append(self._call("rn_quant_int8_fwd", self.dtype, op.x.numel, self._p(self.act(op.x)),
                                               self._p(self.act(op.y)), self._ap(q["minmax"]), 0, tr, q["ema"],
                                               self._qfirst, q["nbits"], qwsp, sp))
+            elif op.kind == "add" and getattr(op, "bn_a", None) is not None:
+                bna, bnb = op.bn_a, op.bn_b
+                other = op.b if op.bn_a_key == "a" else op.a
+                c = self._call("rn_bn_apply_add", L.C.byref(bna.desc), self._p(self.act(bna.x)), bna.sc, bna.sh,
+                               self._p(self.act(bnb.x if bnb is not None else other)),
+                               bnb.sc if bnb is not None else None, bnb.sh if bnb is not None else None,
+                               self._p(self.act(op.y)), int(op.relu), sp)
+                F.append(c)
+                I.append(c)
             elif op.kind == "add":
                 c = self._call("rn_eltwise_add", op.y.numel, self.dtype, self._p(self.act(op.a)),
                                self._p(self.act(op.b)), self._p(self.act(op.y)), int(op.relu), sp)

@@ -46,6 +46,7 @@ SIGNATURES = {
     "rn_conv_weight_pack_i8": (_i32, [_P, _P, _P, _P, _P]),
     "rn_conv_fwd_x": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_filter_x": (_i32, [_P, _P, _P, _P, _P, _P, _P, _i64, _P]),
+    "rn_bn_apply_add": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _i32, _P]),
     "rn_conv_bwd_data_bnred": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P, _P]),
     "rn_conv_bnred_blocks": (_i64, [_P]),
     "rn_bn_bwd_part": (_i32, [_P, _P, _i64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -872,3 +872,36 @@ def test_conv_big_tiles(gpu, mode, case, tile_variant):
     dw3 -= 0.5
     for g in (dw, dw2, dw3, dw4):
         assert rel_err(g.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2), dw_ref) < 5e-3
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("bnb", [False, True], ids=["identity_shortcut", "bn_shortcut"])
+@pytest.mark.parametrize("relu", [1, 0])
+def test_bn_apply_add(gpu, dtype, bnb, relu):
+    """rn_bn_apply_add (the post-activation unit tail, symbol/resnext.py:40-47: bn3 [+ shortcut BN] ->
+    add -> relu) == rn_bn_apply of each BatchNorm, then rn_eltwise_add, bit for bit."""
+    n, c, h, w = 3, 72, 9, 7
+    rng = np.random.default_rng(31)
+    m = n * h * w
+    xa = torch.tensor(rng.standard_normal((m, c)) * 2, dtype=tdt(dtype), device=gpu)
+    xb = torch.tensor(rng.standard_normal((m, c)) * 2, dtype=tdt(dtype), device=gpu)
+    f = lambda a: torch.tensor(a, dtype=torch.float32, device=gpu)
+    sca, sha, scb, shb = f(rng.uniform(0.3, 1.7, c)), f(rng.standard_normal(c)), f(rng.uniform(0.3, 1.7, c)), \
+        f(rng.standard_normal(c))
+    bd = L.BNDesc(dtype=dtype, m=m, c=c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=0)
+    y = torch.zeros_like(xa)
+    L.call("rn_bn_apply_add", C.byref(bd), p(xa), p(sca), p(sha), p(xb), p(scb) if bnb else None,
+           p(shb) if bnb else None, p(y), relu, stream())
+    ya, yb, y0 = torch.zeros_like(xa), torch.zeros_like(xa), torch.zeros_like(xa)
+    L.call("rn_bn_apply", C.byref(bd), p(xa), p(ya), p(sca), p(sha), stream())
+    if bnb:
+        L.call("rn_bn_apply", C.byref(bd), p(xb), p(yb), p(scb), p(shb), stream())
+    L.call("rn_eltwise_add", m * c, dtype, p(ya), p(yb if bnb else xb), p(y0), relu, stream())
+    torch.cuda.synchronize()
+    iv = torch.int16 if dtype == BF16 else torch.int32
+    assert torch.equal(y.view(iv), y0.view(iv))
+    ref = xa.double().cpu().numpy() * sca.cpu().numpy() + sha.cpu().numpy()
+    ref = ref + ((xb.double().cpu().numpy() * scb.cpu().numpy() + shb.cpu().numpy()) if bnb else xb.double().cpu().numpy())
+    if relu:
+        ref = np.maximum(ref, 0)
+    assert rel_err(y.double().cpu().numpy(), ref) < TOL[dtype]
