@@ -251,6 +251,14 @@ int rn_bn_fwd_infer(const rn_bn_desc* d, const void* x, void* y, const float* ga
 int rn_bn_apply_add(const rn_bn_desc* d, const void* xa, const float* scale_a, const float* shift_a,
                     const void* xb, const float* scale_b, const float* shift_b, void* y, int32_t relu,
                     rn_stream_t stream);
+/* Its backward: g = dy * [y > 0] (the ReLU after the add) written once, and in the same pass the
+ * backward reductions of the BatchNorm(s) feeding the add: part_a[nrb][c][2] = {sum g,
+ * sum g*(xa - mean_a)} per row block (and part_b for xb / mean_b, the shortcut's BN; or all three
+ * NULL), nrb = rn_bn_reduce_blocks(d); rn_bn_bwd_part(d, part, nrb, x, g, ...) finalizes and applies. */
+int64_t rn_bn_reduce_blocks(const rn_bn_desc* d);
+int rn_relu_bwd_bnred(const rn_bn_desc* d, const void* y, const void* dy, void* g, const void* xa,
+                      const float* mean_a, float* part_a, const void* xb, const float* mean_b, float* part_b,
+                      rn_stream_t stream);
 /* Apply y = act(x*scale + shift) with precomputed per-channel scale/shift. */
 int rn_bn_apply(const rn_bn_desc* d, const void* x, void* y, const float* scale,
                 const float* shift, rn_stream_t stream);

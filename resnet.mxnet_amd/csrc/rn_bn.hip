@@ -460,6 +460,70 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
   }
 }
 
+// ---- backward of the post-activation unit tail (bn_add_kernel): g = dy * [y > 0] (the ReLU after the
+// residual add) written once, and in the same pass the backward reductions of the BatchNorm(s) that
+// feed the add (sum g, sum g*(x - mean); rn_bn_bwd_part finalizes and applies them): the gradient
+// and the BN inputs are not read a second time by separate reduction passes.
+template <typename T, bool BNB>
+__global__ __launch_bounds__(256) void relu_bwd_bnred_kernel(const T* __restrict__ y, const T* __restrict__ dy,
+                                                             T* __restrict__ g, const T* __restrict__ xa,
+                                                             const float* __restrict__ mean_a, float* __restrict__ part_a,
+                                                             const T* __restrict__ xb,
+                                                             const float* __restrict__ mean_b, float* __restrict__ part_b,
+                                                             int64_t m, int c, int ct, int64_t rows_per_block) {
+  constexpr int CE = 16 / sizeof(T);
+  constexpr int NB = BNB ? 2 : 1;
+  const int tc = threadIdx.x % ct, tr = threadIdx.x / ct, rl = blockDim.x / ct;
+  const int cbase = (blockIdx.x * ct + tc) * CE;
+  const int64_t r0 = blockIdx.y * rows_per_block;
+  const int64_t r1 = min(m, r0 + rows_per_block);
+  float mu[NB][CE], s[NB][CE], q[NB][CE];
+#pragma unroll
+  for (int e = 0; e < CE; ++e) {
+    mu[0][e] = mean_a[cbase + e];
+    if constexpr (BNB) mu[NB - 1][e] = mean_b[cbase + e];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) s[b][e] = q[b][e] = 0.f;
+  }
+  for (int64_t r = r0 + tr; r < r1; r += rl) {
+    const int64_t off = r * c + cbase;
+    float fy[CE], fd[CE], fx[NB][CE];
+    chunk_to_f(*reinterpret_cast<const uint4*>(y + off), fy, (const T*)nullptr);
+    chunk_to_f(*reinterpret_cast<const uint4*>(dy + off), fd, (const T*)nullptr);
+    chunk_to_f(*reinterpret_cast<const uint4*>(xa + off), fx[0], (const T*)nullptr);
+    if constexpr (BNB) chunk_to_f(*reinterpret_cast<const uint4*>(xb + off), fx[NB - 1], (const T*)nullptr);
+#pragma unroll
+    for (int e = 0; e < CE; ++e) {
+      fd[e] = fy[e] > 0.f ? fd[e] : 0.f;  // (exact in the storage type: dy or 0)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        s[b][e] += fd[e];
+        q[b][e] = fmaf(fd[e], fx[b][e] - mu[b][e], q[b][e]);
+      }
+    }
+    *reinterpret_cast<uint4*>(g + off) = f_to_chunk(fd, (const T*)nullptr);
+  }
+  __shared__ float red[kThreads * 8 * 2];
+  const int ncol = ct * CE * 2;
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    if (b > 0) __syncthreads();
+#pragma unroll
+    for (int e = 0; e < CE; ++e) {
+      red[(tr * ct + tc) * CE * 2 + 2 * e] = s[b][e];
+      red[(tr * ct + tc) * CE * 2 + 2 * e + 1] = q[b][e];
+    }
+    __syncthreads();
+    float* part = b == 0 ? part_a : part_b;
+    for (int col = threadIdx.x; col < ncol; col += blockDim.x) {
+      float acc = 0.f;
+      for (int r = 0; r < rl; ++r) acc += red[r * ncol + col];
+      const int cc = blockIdx.x * ct * CE + col / 2;
+      part[((int64_t)blockIdx.y * c + cc) * 2 + (col & 1)] = acc;
+    }
+  }
+}
+
 // coef[c] = {A = g*invstd, mean(dz), A2 = g*invstd^2*sum(dz*xhat)/m, mean}; block per channel.
 __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __restrict__ part, int nrb, int64_t m,
                                                               int c, int c_real, int fix_gamma,
@@ -842,6 +906,35 @@ int rn_bn_apply_add(const rn_bn_desc* d, const void* xa, const float* scale_a, c
   else RN_BN_ADD(float)
 #undef RN_BN_ADD
   return rn_check_launch("bn_apply_add");
+}
+
+int64_t rn_bn_reduce_blocks(const rn_bn_desc* d) {
+  if (check_bn(d)) return -1;
+  return d->dtype == RN_BF16 ? make_geo<bf16_t>(d->m, d->c).nrb : make_geo<float>(d->m, d->c).nrb;
+}
+
+int rn_relu_bwd_bnred(const rn_bn_desc* d, const void* y, const void* dy, void* g, const void* xa,
+                      const float* mean_a, float* part_a, const void* xb, const float* mean_b, float* part_b,
+                      rn_stream_t stream) {
+  if (check_bn(d)) return -1;
+  RN_CHECK_ARG(y && dy && g && xa && mean_a && part_a, "null argument");
+  RN_CHECK_ARG((xb == nullptr) == (mean_b == nullptr) && (xb == nullptr) == (part_b == nullptr),
+               "xb / mean_b / part_b must all be set or all null");
+  hipStream_t st = as_stream(stream);
+#define RN_RBR(T)                                                                                              \
+  {                                                                                                            \
+    Geo gm = make_geo<T>(d->m, d->c);                                                                          \
+    if (xb) hipLaunchKernelGGL((relu_bwd_bnred_kernel<T, true>), dim3(gm.gx, gm.nrb), dim3(kThreads), 0, st,   \
+                               (const T*)y, (const T*)dy, (T*)g, (const T*)xa, mean_a, part_a, (const T*)xb,   \
+                               mean_b, part_b, d->m, d->c, gm.ct, gm.rows_per_block);                          \
+    else hipLaunchKernelGGL((relu_bwd_bnred_kernel<T, false>), dim3(gm.gx, gm.nrb), dim3(kThreads), 0, st,     \
+                            (const T*)y, (const T*)dy, (T*)g, (const T*)xa, mean_a, part_a, (const T*)nullptr, \
+                            (const float*)nullptr, (float*)nullptr, d->m, d->c, gm.ct, gm.rows_per_block);      \
+  }
+  if (d->dtype == RN_BF16) RN_RBR(bf16_t)
+  else RN_RBR(float)
+#undef RN_RBR
+  return rn_check_launch("relu_bwd_bnred");
 }
 
 int rn_bn_apply(const rn_bn_desc* d, const void* x, void* y, const float* scale, const float* shift,

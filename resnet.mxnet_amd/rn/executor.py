@@ -1207,6 +1207,9 @@ class Executor:
         self.param_done_at = {}  # param -> index in self._bwd after which its grad is final
         self._gw = {}  # id(tensor) -> last writer of its gradient buffer: ("dgrad", call index, conv op)
         # default on where the dgrad runs the 256-row tile (see RN_BN_EPILOGUE_STATS; =2: every dgrad)
+        for op in plan.ops:
+            if op.kind == "bn":
+                op.pre_part = None  # set by the residual add's fused ReLU backward (this build)
         bwd_fusion = os.environ.get("RN_BN_BWD_FUSION", "1") in ("1", "2")
         bwd_all = os.environ.get("RN_BN_BWD_FUSION", "1") == "2"
         # one workspace for the weight gradients' split-M partial tiles (rn_conv_bwd_filter_ws),
@@ -1300,6 +1303,12 @@ class Executor:
                                                 op.bnred_blocks, self._p(self.act(x)), self._p(dy), self._p(out),
                                                 self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc, op.sh,
                                                 self._gp(op.gamma), self._gp(op.beta), wsp, sp))
+                elif getattr(op, "pre_part", None) is not None:
+                    # the reduction was done by the residual add's ReLU backward (rn_relu_bwd_bnred)
+                    self._bwd.append(self._call("rn_bn_bwd_part", L.C.byref(op.desc), self._p(op.pre_part),
+                                                op.pre_nrb, self._p(self.act(x)), self._p(dy), self._p(out),
+                                                self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc, op.sh,
+                                                self._gp(op.gamma), self._gp(op.beta), wsp, sp))
                 else:
                     self._bwd.append(self._call("rn_bn_bwd", L.C.byref(op.desc), self._p(self.act(x)), self._p(dy),
                                                 self._p(out), self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc,
@@ -1339,8 +1348,23 @@ class Executor:
                     # tensor would be recycled by the caching allocator while the plan writes it)
                     gbuf = self._zeros(op.y.numel, self.tdtype)
                     self._grads[("relu_add", id(op))] = gbuf
-                    self._bwd.append(self._call("rn_relu_bwd", op.y.numel, self.dtype, self._p(self.act(op.y)),
-                                                self._p(dy), self._p(gbuf), None, sp))
+                    # the BatchNorms applied inside this add (rn_bn_apply_add) get their backward
+                    # reductions from the same pass (rn_relu_bwd_bnred)
+                    bns = [b for b in (getattr(op, "bn_a", None), getattr(op, "bn_b", None))
+                           if b is not None and not b.use_global_stats and dy is not None]
+                    if bns and len(bns) == len([b for b in (op.bn_a, op.bn_b) if b is not None]):
+                        for b in bns:
+                            b.pre_nrb = int(self.lib.rn_bn_reduce_blocks(L.C.byref(b.desc)))
+                            b.pre_part = self._zeros(b.pre_nrb * b.x.cp * 2, self.torch.float32)
+                        b2 = bns[1] if len(bns) == 2 else None
+                        self._bwd.append(self._call(
+                            "rn_relu_bwd_bnred", L.C.byref(bns[0].desc), self._p(self.act(op.y)), self._p(dy),
+                            self._p(gbuf), self._p(self.act(bns[0].x)), bns[0].sm, self._p(bns[0].pre_part),
+                            self._p(self.act(b2.x)) if b2 else None, b2.sm if b2 else None,
+                            self._p(b2.pre_part) if b2 else None, sp))
+                    else:
+                        self._bwd.append(self._call("rn_relu_bwd", op.y.numel, self.dtype, self._p(self.act(op.y)),
+                                                    self._p(dy), self._p(gbuf), None, sp))
                     g = gbuf
                 for t in (op.a, op.b):
                     if t.needs_grad:

@@ -47,6 +47,8 @@ SIGNATURES = {
     "rn_conv_fwd_x": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_filter_x": (_i32, [_P, _P, _P, _P, _P, _P, _P, _i64, _P]),
     "rn_bn_apply_add": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _i32, _P]),
+    "rn_bn_reduce_blocks": (_i64, [_P]),
+    "rn_relu_bwd_bnred": (_i32, [_P] * 11),
     "rn_conv_bwd_data_bnred": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P, _P]),
     "rn_conv_bnred_blocks": (_i64, [_P]),
     "rn_bn_bwd_part": (_i32, [_P, _P, _i64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),

@@ -905,3 +905,57 @@ def test_bn_apply_add(gpu, dtype, bnb, relu):
     if relu:
         ref = np.maximum(ref, 0)
     assert rel_err(y.double().cpu().numpy(), ref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("bnb", [False, True], ids=["identity_shortcut", "bn_shortcut"])
+def test_relu_bwd_bnred(gpu, dtype, bnb):
+    """rn_relu_bwd_bnred + rn_bn_bwd_part (the backward of the post-activation unit tail) == rn_relu_bwd
+    then rn_bn_bwd on each BatchNorm feeding the add: the ReLU gradient bit for bit, the BN gradients
+    (dx, dgamma, dbeta) within fp32 reduction-order error, and the oracle's BN backward."""
+    n, c, h, w = 4, 80, 11, 9
+    m = n * h * w
+    rng = np.random.default_rng(37)
+    t = lambda a: torch.tensor(a, dtype=tdt(dtype), device=gpu)
+    f = lambda a: torch.tensor(a, dtype=torch.float32, device=gpu)
+    y = t(np.maximum(rng.standard_normal((m, c)), 0) * (rng.random((m, c)) < 0.7))
+    dy = t(rng.standard_normal((m, c)))
+    xs = [t(rng.standard_normal((m, c)) * 1.5 + 0.4) for _ in range(2)]
+    bd = L.BNDesc(dtype=dtype, m=m, c=c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=0)
+    lib = L.load()
+    ws = torch.zeros(lib.rn_bn_workspace_bytes(C.byref(bd)) // 4 + 16, dtype=torch.float32, device=gpu)
+    stats = []
+    for x in xs:  # save_mean / save_invstd / scale / shift of each BN from its forward
+        g_, b_ = f(rng.uniform(0.5, 1.5, c)), f(rng.standard_normal(c) * 0.1)
+        sm, si, sc, sh = [torch.zeros(c, dtype=torch.float32, device=gpu) for _ in range(4)]
+        L.call("rn_bn_fwd_train", C.byref(bd), p(x), None, p(g_), p(b_), None, None, p(sm), p(si), p(sc), p(sh), p(ws),
+               stream())
+        stats.append((g_, sm, si, sc, sh))
+    nrb = lib.rn_bn_reduce_blocks(C.byref(bd))
+    parts = [torch.full((nrb * c * 2,), float("nan"), dtype=torch.float32, device=gpu) for _ in range(2)]
+    g = torch.zeros_like(dy)
+    L.call("rn_relu_bwd_bnred", C.byref(bd), p(y), p(dy), p(g), p(xs[0]), p(stats[0][1]), p(parts[0]),
+           p(xs[1]) if bnb else None, p(stats[1][1]) if bnb else None, p(parts[1]) if bnb else None, stream())
+    g0 = torch.zeros_like(dy)
+    L.call("rn_relu_bwd", m * c, dtype, p(y), p(dy), p(g0), None, stream())
+    torch.cuda.synchronize()
+    iv = torch.int16 if dtype == BF16 else torch.int32
+    assert torch.equal(g.view(iv), g0.view(iv))
+    for k in range(2 if bnb else 1):
+        gam, sm, si, sc, sh = stats[k]
+        dx, dx0 = torch.zeros_like(dy), torch.zeros_like(dy)
+        dg, db, dg0, db0 = [torch.zeros(c, dtype=torch.float32, device=gpu) for _ in range(4)]
+        L.call("rn_bn_bwd_part", C.byref(bd), p(parts[k]), nrb, p(xs[k]), p(g), p(dx), None, p(gam), p(sm), p(si),
+               p(sc), p(sh), p(dg), p(db), p(ws), stream())
+        L.call("rn_bn_bwd", C.byref(bd), p(xs[k]), p(g0), p(dx0), None, p(gam), p(sm), p(si), p(sc), p(sh), p(dg0),
+               p(db0), p(ws), stream())
+        torch.cuda.synchronize()
+        assert rel_err(dg.cpu().numpy(), dg0.cpu().numpy()) < 1e-5
+        assert rel_err(db.cpu().numpy(), db0.cpu().numpy()) < 1e-5
+        assert rel_err(dx.double().cpu().numpy(), dx0.double().cpu().numpy()) < (1e-5 if dtype == F32 else 1e-2)
+        xd = xs[k].double().cpu().numpy().reshape(n, h, w, c).transpose(0, 3, 1, 2)
+        gd = g.double().cpu().numpy().reshape(n, h, w, c).transpose(0, 3, 1, 2)
+        _, cache = ops.bn_train_fwd(xd, gam.double().cpu().numpy(), np.zeros(c), 1e-5, False)
+        dx_ref, dg_ref, db_ref = ops.bn_train_bwd(gd, cache, False)
+        assert rel_err(db.cpu().numpy(), db_ref) < 1e-4 and rel_err(dg.cpu().numpy(), dg_ref) < 1e-4
+        assert rel_err(dx.double().cpu().numpy().reshape(n, h, w, c).transpose(0, 3, 1, 2), dx_ref) < TOL[dtype]
