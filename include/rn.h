@@ -417,7 +417,9 @@ const char* rn_last_error(void);
  * 9 = igemm 224-row tiles for the 256/128-column tiles (0 = on, 1 = 256 rows),
  * 10 = igemm 256-row-family persistent grid: workgroups (a multiple of 8) that walk the tiles of a
  *      larger grid, so one tile's output stores drain while the next tile loads (default 512; 0 = one
- *      tile per workgroup). */
+ *      tile per workgroup),
+ * 11 = the 4-wave one-buffer 224x128 conv tile, two workgroups per CU (0 auto: one-K-tile forward
+ *      1x1 layers of >= 1024 tiles; 1 off; 2 every 1x1 pad-0 conv). */
 int rn_set_tuning(int32_t key, int32_t value);
 int32_t rn_version(void);
 /* Number of compute units of the current device (for split heuristics / reporting). */

@@ -959,3 +959,4 @@ def test_relu_bwd_bnred(gpu, dtype, bnb):
         dx_ref, dg_ref, db_ref = ops.bn_train_bwd(gd, cache, False)
         assert rel_err(db.cpu().numpy(), db_ref) < 1e-4 and rel_err(dg.cpu().numpy(), dg_ref) < 1e-4
         assert rel_err(dx.double().cpu().numpy().reshape(n, h, w, c).transpose(0, 3, 1, 2), dx_ref) < TOL[dtype]
+
