@@ -1,7 +1,7 @@
 """Map the conv dispatch durations (igemm*/wgrad* kernels) of the LAST training step in a rocprofv3
 kernel trace onto the ResNet-50 layers (plan call order) and print per-layer TFLOP/s and the
 fraction of each layer's own roofline max(FLOP/2.5 PF, algorithmic bytes/8 TB/s). CPU-only tool.
-usage: python tools/trace_layers.py <run_kernel_trace.csv> [batch]"""
+usage: python tools/trace_layers.py <run_kernel_trace.csv> [batch] [resnet50|resnext50|resnet50_int8]"""
 import csv
 import os
 import sys
@@ -29,7 +29,9 @@ def kernel_short(name):
 def main():
     trace = sys.argv[1]
     batch = int(sys.argv[2]) if len(sys.argv) > 2 else 256
-    plan = Plan(graphs.resnet50(), [("data", (batch, 3, 224, 224))], [("softmax_label", (batch,))])
+    gname = sys.argv[3] if len(sys.argv) > 3 else "resnet50"
+    sym = {"resnet50": graphs.resnet50, "resnext50": graphs.resnext50_32x4d, "resnet50_int8": graphs.resnet50_int8}[gname]()
+    plan = Plan(sym, [("data", (batch, 3, 224, 224))], [("softmax_label", (batch,))])
     ex = Executor(plan, "cpu")
     names = {}
     for op in plan.ops:
