@@ -70,6 +70,8 @@ struct IgemmArgs {
   const float* qunit_w;
   FastDiv fdS;
   int ncls;
+  int ksplit;          // igemm_kernel, fp32 output, one-tap 1x1 reductions: split-K over blockIdx.y, fp32
+                       // atomic adds into the zeroed output (the FC forward's 16-tile grids)
   IgemmCls cls[4];
 };
 
@@ -259,12 +261,18 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
   }
 
   const int ncb = (p.cblk + BKE - 1) / BKE;
-  const int nstage = p.smallc ? (p.rs * p.C + BKE - 1) / BKE : cl.nr * cl.ns * ncb;
+  int nstage = p.smallc ? (p.rs * p.C + BKE - 1) / BKE : cl.nr * cl.ns * ncb;
+  int kbeg = 0;  // split-K (host: one tap, no smallc): this split's channel-block range
+  if (p.ksplit > 1) {
+    const int per = (nstage + p.ksplit - 1) / p.ksplit;
+    kbeg = blockIdx.y * per;
+    nstage = max(0, min(nstage, kbeg + per) - kbeg);
+  }
 
   // register-staged loads: stage t+1 is loaded while stage t is computed, then written to
   // the other LDS buffer (async-STAGE split: write after the MFMA phase).
   uint4 ra0[A_CH], rb0[B_CH];
-  int st_tr = 0, st_ts = 0, st_cb = 0;  // next stage to load
+  int st_tr = 0, st_ts = 0, st_cb = kbeg;  // next stage to load
   int st_buf = 0;                       // LDS buffer the next DMA stage lands in
   const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, p.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc((void*)p.w, (short)0, p.w_bytes, 0x00020000);
@@ -528,9 +536,15 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
     float v[OE];
 #pragma unroll
     for (int e = 0; e < OE; ++e) v[e] = tile[row * LDT + cc * OE + e];
-    if (p.bias) {
+    if (p.bias && blockIdx.y == 0) {
 #pragma unroll
       for (int e = 0; e < OE; ++e) v[e] += (col0 + e < p.K) ? p.bias[col0 + e] : 0.f;
+    }
+    if constexpr (std::is_same<OutT, float>::value) {
+      if (p.ksplit > 1) {  // split-K: partial sums added into the zeroed fp32 output
+        for (int e = 0; e < OE && col0 + e < p.K; ++e) atomicAdd(yg + ep_off[k] + e, v[e]);
+        continue;
+      }
     }
     if (col0 + OE <= p.K) {  // full chunk: vector path
       if (ag) {
@@ -2214,6 +2228,21 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
       }
 #undef RN_BIG
       return rn_check_launch("igemm_big");
+    }
+  }
+  if (std::is_same<T, bf16_t>::value && std::is_same<OutT, float>::value && a.ncls == 1 && !a.smallc && !a.add &&
+      !a.stats && !a.bnred && !a.in_sc && a.gred == 0 && a.cls[0].nr * a.cls[0].ns == 1 && a.K > 64) {
+    // split-K for small grids (the FC forward: 256 x 1000 over 2048 = 16 tiles of 32 stages)
+    const int64_t tiles = ceil_div(maxMc, 128) * ceil_div(a.K, 128);
+    const int nst = (int)ceil_div(a.cblk, 64);
+    if (tiles < 128 && nst >= 8) {
+      b.ksplit = (int)std::min<int64_t>(nst / 4, std::max<int64_t>(1, 256 / tiles));
+      b.ntn = (int)ceil_div(a.K, 128);
+      if (hipMemsetAsync(b.y, 0, (size_t)maxMc * a.ldo * sizeof(float), st) != hipSuccess)
+        return rn_check_launch("igemm_splitk_zero");
+      dim3 grid((unsigned)(ceil_div(maxMc, 128) * b.ntn), (unsigned)b.ksplit, 1);
+      hipLaunchKernelGGL((igemm_kernel<T, OutT, 128, 128, false>), grid, dim3(256), 0, st, b);
+      return rn_check_launch("igemm_splitk");
     }
   }
   if (a.K <= 64 || a.gred > 0) {  // grouped: the block width is RN_GROUP_BLOCK
