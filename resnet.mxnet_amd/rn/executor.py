@@ -883,7 +883,7 @@ class Executor:
             for op in plan.ops:
                 if op.kind == "bn" and not op.use_global_stats:
                     src = producer.get(id(op.x))
-                    if src is not None and src.y.c % 8 == 0 and src.y.cp == op.x.cp and \
+                    if src is not None and src.kind == "conv" and src.y.c % 8 == 0 and src.y.cp == op.x.cp and \
                             (stats_mode == "2" or self._big_tile(src, 0)):
                         src.bnstats = True
                         op.part_src = src

@@ -229,3 +229,12 @@ def test_bound_pointers_are_owned(graph):
                     assert i >= 0 and a.value < spans[i][1], (name, hex(a.value))
                     n += 1
     assert n > 100
+
+
+def test_plan_bn_epilogue_stats_every_conv(monkeypatch):
+    """RN_BN_EPILOGUE_STATS=2 (statistics in every producing conv's epilogue) binds: producers that are
+    not convolutions (the stem, pooling, residual adds) keep the separate statistics pass."""
+    monkeypatch.setenv("RN_BN_EPILOGUE_STATS", "2")
+    ex = Executor(Plan(graphs.resnet50(), [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")
+    names = [c[0] for c in ex._fwd_train]
+    assert names.count("rn_bn_fwd_train_part") > 0 and names.count("rn_bn_fwd_train") > 0
