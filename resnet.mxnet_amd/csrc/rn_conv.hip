@@ -728,6 +728,11 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
   constexpr int FM = M32 ? 32 : 16;              // MFMA tile edge
   constexpr int MI = WM / FM, NI = WN / FM;      // accumulators per wave
   constexpr int NCH = (WM + 63) / 64;            // 64-row epilogue chunks per wave
+  // BatchNorm partials (EPI 1 / 2): the two wave rows of the 8-wave and W4 tiles share one partial
+  // per tile (one pivot, sums combined through LDS), halving what the merge / finalize passes read;
+  // the 64-column tile keeps one per 64-row wave row
+  constexpr bool PAIR = WAVES_M == 2;
+  constexpr int PR = PAIR ? 1 : WAVES_M;         // BatchNorm partials per tile
   static_assert(WM % FM == 0 && (BM == 256 || !M32) && (BM == 256 || BN != 64) && (!SC || BN == 64), "tile shape");
   static_assert(!Q8 || (!M32 && !SC && EPI != 2), "int8: 16x16x64 MFMAs, forward only");
   using AccT = typename std::conditional<Q8 != 0, v4i, typename std::conditional<M32, v16f, v4f>::type>::type;
@@ -764,10 +769,10 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
   const int n0 = (lid - mtile * p.ntn) * BN;
   if (m0 >= Mc) {  // (a dgrad parity class with fewer rows): empty BN-reduction partials
     if (EPI == 2)
-      for (int e = tid; e < WAVES_M * BN; e += NW * 64) {
+      for (int e = tid; e < PR * BN; e += NW * 64) {
         const int hh = e / BN, col = n0 + e % BN;
-        if (col < p.ldo && WAVES_M * mtile + hh < p.mt_max) {
-          float* dst = p.bnred + ((int64_t)(blockIdx.z * p.mt_max + WAVES_M * mtile + hh) * p.ldo + col) * 2;
+        if (col < p.ldo && PR * mtile + hh < p.mt_max) {
+          float* dst = p.bnred + ((int64_t)(blockIdx.z * p.mt_max + PR * mtile + hh) * p.ldo + col) * 2;
           dst[0] = 0.f;
           dst[1] = 0.f;
         }
@@ -1090,11 +1095,12 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
     }
     __syncthreads();
     if constexpr (EPI == 1) {
-      if (h == 0) {  // pivot: the BN's moving mean (accumulated sums), else the wave row's first
-                     // (rounded) conv value of each column
+      if (h == 0) {  // pivot: the first (rounded) conv value of each column in the tile's first wave
+                     // row (PAIR: both wave rows use it, so their sums add), else in this wave row
+        const float* ep0 = PAIR ? reinterpret_cast<const float*>(smem) + wn * EP_WAVE : ep;
 #pragma unroll
         for (int e = 0; e < 8; ++e)
-          piv[e] = to_f(from_f<OutT>(ep[cc * 8 + e]));
+          piv[e] = to_f(from_f<OutT>(ep0[cc * 8 + e]));
       }
     }
 #pragma unroll
@@ -1159,16 +1165,34 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
         s1[e] += __shfl_xor(s1[e], o, 64);
         s2[e] += __shfl_xor(s2[e], o, 64);
       }
-    if (lane < CPR) {
+    if constexpr (PAIR) {  // wave row 1 hands its sums to wave row 0 (same columns)
+      float* xch = reinterpret_cast<float*>(smem) + wn * (CPR * 16);
+      __syncthreads();  // every wave is done reading the epilogue staging
+      if (wm == 1 && lane < CPR)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          xch[lane * 16 + e] = s1[e];
+          xch[lane * 16 + 8 + e] = s2[e];
+        }
+      __syncthreads();
+      if (wm == 0 && lane < CPR)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s1[e] += xch[lane * 16 + e];
+          s2[e] += xch[lane * 16 + 8 + e];
+        }
+    }
+    if (lane < CPR && (!PAIR || wm == 0)) {
       const int c0 = n0 + wn * WN + lane * 8;
-      const int blk = WAVES_M * mtile + wm;  // one partial per wave row
+      const int blk = PR * mtile + (PAIR ? 0 : wm);  // one partial per tile (PAIR) or wave row
+      const bool rows_ok = PAIR || half_ok;         // (PAIR: wave row 0 always holds rows)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int col = c0 + e;
         if (col >= p.ldo) continue;
         const bool okc = col < p.K;
         if constexpr (EPI == 1) {
-          if (half_ok) {
+          if (rows_ok) {
             float* dst = p.stats + (int64_t)blk * 3 * p.ldo + col;
             dst[0] = okc ? s1[e] : 0.f;
             dst[p.ldo] = okc ? s2[e] : 0.f;
@@ -1176,8 +1200,8 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
           }
         } else if (blk < p.mt_max) {  // (a half past the class's rows may lie past its partial slots)
           float* dst = p.bnred + ((int64_t)(blockIdx.z * p.mt_max + blk) * p.ldo + col) * 2;
-          dst[0] = (half_ok && okc) ? s1[e] : 0.f;
-          dst[1] = (half_ok && okc) ? s2[e] : 0.f;
+          dst[0] = (rows_ok && okc) ? s1[e] : 0.f;
+          dst[1] = (rows_ok && okc) ? s2[e] : 0.f;
         }
       }
     }
@@ -2127,7 +2151,7 @@ int bn_part_rows(const IgemmArgs& a, bool bf16) {
   if (!bf16) return 128;
   const int64_t xb = (int64_t)a.N * a.H * a.W * a.C * 2, wb = (int64_t)a.K * a.wrow * 2;
   const int bn = big_tile_cols(a, xb, wb);
-  return bn >= 128 ? big_tile_rows(bn) / 2 : bn == 64 ? 64 : 128;  // one wave row: 2 x 2 / 4 x 1 waves
+  return bn >= 128 ? big_tile_rows(bn) : bn == 64 ? 64 : 128;  // one per tile / 64-row wave row / 128-row tile
 }
 
 template <typename T, typename OutT>
@@ -2177,8 +2201,8 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
     }
     if (bn >= 128) {
       const int bm = big_tile_rows(bn);
-      RN_CHECK_ARG(!(a.stats || a.bnred) || bm / 2 == bn_part_rows(a, true), "BN partial rows mismatch");
-      if (a.bnred) b.mt_max = (int)ceil_div(maxMc, bm / 2);
+      RN_CHECK_ARG(!(a.stats || a.bnred) || bm == bn_part_rows(a, true), "BN partial rows mismatch");
+      if (a.bnred) b.mt_max = (int)ceil_div(maxMc, bm);
       b.ntn = (int)ceil_div(a.K, bn);
       dim3 grid((unsigned)(ceil_div(maxMc, bm) * b.ntn), 1, a.ncls);
       persist(grid);
@@ -2435,7 +2459,7 @@ int32_t rn_conv_tile(const rn_conv_desc* d, int32_t mode) {
 }
 
 int32_t rn_conv_bn_part_rows(const rn_conv_desc* d, int32_t mode) {
-  if (d && mode == 2) return rn_conv_tile(d, 2) == 64 ? 64 : 112;  // int8 forward: one wave row
+  if (d && mode == 2) return rn_conv_tile(d, 2) == 64 ? 64 : 224;  // int8 forward: per wave row / tile
   if (!d || (mode != 0 && mode != 1)) return 0;
   return bn_part_rows(make_igemm_args(d, mode), d->dtype == RN_BF16);
 }
