@@ -90,8 +90,8 @@ def family_of(ex, name, args):
         big = ex.lib.rn_conv_tile(args[0], 1 if dgrad else 0) if (ex.dtype == 0 and not out_f32 and plain) else 0
         if name == "rn_conv_fwd_x" and args[7] is not None and big < 128:
             big = 0  # the BN+ReLU input transform runs on the 224-row tiles only, else the 128-row kernel
-        if big:  # tile rows: 256, or 224 (the BN partial blocks are half the tile rows)
-            rows = 2 * ex.lib.rn_conv_bn_part_rows(args[0], 1 if dgrad else 0) if big >= 128 else 256
+        if big:  # tile rows: 256, or 224 (one BN partial block per 128/256-column tile)
+            rows = ex.lib.rn_conv_bn_part_rows(args[0], 1 if dgrad else 0) if big >= 128 else 256
             return "igemm_big_kernel<%dx%d>" % (rows, big)
         tile = "128x64" if ncol <= 64 else "128x128"
         return "igemm_kernel<bf16,%s,%s>" % ("f32" if out_f32 else "bf16", tile)

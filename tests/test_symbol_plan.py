@@ -238,3 +238,13 @@ def test_plan_bn_epilogue_stats_every_conv(monkeypatch):
     ex = Executor(Plan(graphs.resnet50(), [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")
     names = [c[0] for c in ex._fwd_train]
     assert names.count("rn_bn_fwd_train_part") > 0 and names.count("rn_bn_fwd_train") > 0
+
+
+def test_bench_family_names():
+    """bench.py names the conv kernel family of each call from the library's own tile choice: the
+    ResNet-50 bench step uses the 224-row 256 / 128-column families and the 256x64 tile."""
+    import bench
+    ex = Executor(Plan(graphs.resnet50(), [("data", (256, 3, 224, 224))], [("softmax_label", (256,))]), "cpu")
+    fams = {bench.family_of(ex, n, a) for n, f, a in ex._fwd_train + ex._bwd} - {None}
+    assert "igemm_big_kernel<224x256>" in fams and "igemm_big_kernel<224x128>" in fams
+    assert all(not f.startswith("igemm_big_kernel<448") for f in fams), fams
