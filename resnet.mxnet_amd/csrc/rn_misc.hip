@@ -519,7 +519,7 @@ __global__ void quant_bwd_kernel(int64_t n, const T* __restrict__ x, const T* __
 
 }  // namespace
 
-int g_tune[RN_TUNE_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512, 0};
+int g_tune[RN_TUNE_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512, 0, 0};
 
 extern "C" {
 
@@ -573,6 +573,66 @@ int rn_pool_fwd(const rn_pool_desc* d, const void* x, void* y, uint8_t* argmax, 
   return rn_check_launch("pool_fwd");
 }
 
+}  // extern "C" (reopened below, after the 2x2-block max-pool backward)
+
+namespace {
+// Max pool 3x3 / stride 2 / pad 1 with H = 2P, W = 2Q (the ResNet stem pool, symbol/resnet.py:97),
+// backward: thread per (image, 2x2 input block (2i.., 2j..), channel chunk). The block's pixels take
+// gradient only from the outputs (i | i+1) x (j | j+1) -- input row 2i from output row i, row 2i+1
+// from rows i and i+1 -- so each dy / tap-index chunk is read once per block instead of once per
+// covered input pixel (up to 4x). Sums in the generic kernel's order (outputs row-major): bit-identical.
+template <typename T>
+__global__ void maxpool3s2_bwd_kernel(PoolArgs a, const T* __restrict__ dy, const uint8_t* __restrict__ argmax,
+                                      T* __restrict__ dx, const T* __restrict__ add) {
+  constexpr int CE = 16 / sizeof(T);
+  const int cpr = a.c / CE;
+  const uint32_t total = (uint32_t)a.n * a.p * a.q * cpr;  // blocks x chunks (P = H/2, Q = W/2)
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const uint32_t blk = fdiv(i, a.fd_cpr);
+    const int cc = (int)(i - blk * cpr);
+    const uint32_t t = fdiv(blk, a.fd_a);  // fd_a: q
+    const int bj = (int)(blk - t * a.q);
+    const uint32_t n = fdiv(t, a.fd_b);    // fd_b: p
+    const int bi = (int)(t - n * a.p);
+    uint4 g4[4];
+    uint64_t am4[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {  // outputs (bi + u/2, bj + u%2)
+      const int pp = bi + (u >> 1), qq = bj + (u & 1);
+      const bool ok = pp < a.p && qq < a.q;
+      const int64_t ob = (((int64_t)n * a.p + (ok ? pp : bi)) * a.q + (ok ? qq : bj)) * a.c + cc * CE;
+      g4[u] = ok ? *reinterpret_cast<const uint4*>(dy + ob) : make_uint4(0, 0, 0, 0);
+      am4[u] = !ok ? ~0ull : CE == 8 ? *reinterpret_cast<const uint64_t*>(argmax + ob)
+                                     : (uint64_t)*reinterpret_cast<const uint32_t*>(argmax + ob);
+    }
+    float g[4][CE];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) chunk_to_f(g4[u], g[u], (const T*)nullptr);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {  // input pixel (2 bi + dh, 2 bj + dw)
+      const int dh = v >> 1, dw = v & 1;
+      const int64_t xi = (((int64_t)n * a.h + 2 * bi + dh) * a.w + 2 * bj + dw) * cpr + cc;
+      float acc[CE];
+      if (add) chunk_to_f(reinterpret_cast<const uint4*>(add)[xi], acc, (const T*)nullptr);
+      else
+#pragma unroll
+        for (int e = 0; e < CE; ++e) acc[e] = 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int du = u >> 1, dv = u & 1;  // output (bi + du, bj + dv)
+        if ((du && !dh) || (dv && !dw)) continue;  // row 2 bi is only in output row bi (same for columns)
+        const int tap = (dh + 1 - 2 * du) * 3 + (dw + 1 - 2 * dv);
+#pragma unroll
+        for (int e = 0; e < CE; ++e)
+          if ((int)((am4[u] >> (8 * e)) & 0xFF) == tap) acc[e] += g[u][e];
+      }
+      reinterpret_cast<uint4*>(dx)[xi] = f_to_chunk(acc, (const T*)nullptr);
+    }
+  }
+}
+}  // namespace
+
+extern "C" {
 int rn_pool_bwd(const rn_pool_desc* d, const void* dy, const uint8_t* argmax, void* dx, const void* add_src,
                 rn_stream_t stream) {
   RN_CHECK_ARG(d && dy && dx, "null argument");
@@ -584,6 +644,20 @@ int rn_pool_bwd(const rn_pool_desc* d, const void* dy, const uint8_t* argmax, vo
   RN_CHECK_ARG((int64_t)d->n * d->h * d->w * d->c < INT32_MAX, "pooling tensor exceeds 2^31 elements");
   hipStream_t st = as_stream(stream);
   const int64_t total = (int64_t)d->n * d->h * d->w * d->c / 8;
+  if (d->type == RN_POOL_MAX && d->r == 3 && d->s == 3 && d->stride_h == 2 && d->stride_w == 2 && d->pad_h == 1 &&
+      d->pad_w == 1 && d->h == 2 * d->p && d->w == 2 * d->q && g_tune[RN_TUNE_POOL_BLOCK_BWD] != 1) {
+    PoolArgs b = a;
+    b.fd_a = make_fastdiv(d->q);
+    b.fd_b = make_fastdiv(d->p);
+    const int64_t nb = (int64_t)d->n * d->p * d->q * d->c / (d->dtype == RN_BF16 ? 8 : 4);
+    if (d->dtype == RN_BF16)
+      hipLaunchKernelGGL(maxpool3s2_bwd_kernel<bf16_t>, dim3(grid1d(nb)), dim3(256), 0, st, b, (const bf16_t*)dy,
+                         argmax, (bf16_t*)dx, (const bf16_t*)add_src);
+    else
+      hipLaunchKernelGGL(maxpool3s2_bwd_kernel<float>, dim3(grid1d(nb)), dim3(256), 0, st, b, (const float*)dy,
+                         argmax, (float*)dx, (const float*)add_src);
+    return rn_check_launch("maxpool3s2_bwd");
+  }
   if (d->dtype == RN_BF16)
     hipLaunchKernelGGL(pool_bwd_kernel<bf16_t>, dim3(grid1d(total)), dim3(256), 0, st, a, (const bf16_t*)dy,
                        argmax, (bf16_t*)dx, (const bf16_t*)add_src);

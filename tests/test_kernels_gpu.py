@@ -960,3 +960,40 @@ def test_relu_bwd_bnred(gpu, dtype, bnb):
         assert rel_err(db.cpu().numpy(), db_ref) < 1e-4 and rel_err(dg.cpu().numpy(), dg_ref) < 1e-4
         assert rel_err(dx.double().cpu().numpy().reshape(n, h, w, c).transpose(0, 3, 1, 2), dx_ref) < TOL[dtype]
 
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("with_add", [False, True])
+def test_maxpool_block_bwd(gpu, dtype, with_add):
+    """3x3 / stride-2 max-pool backward over 2x2 input blocks (H = 2P, W = 2Q: the stem pool,
+    symbol/resnet.py:97) == the per-pixel gather (rn_set_tuning 12 = 1) bit for bit, and the oracle's
+    first-max rule; ties from post-ReLU zeros, an accumulated add_src."""
+    rng = np.random.default_rng(43)
+    n, c, h, w = 3, 24, 14, 12
+    x = np.round(np.maximum(rng.standard_normal((n, c, h, w)), 0) * 4) / 4
+    y_ref, arg = ops.maxpool_fwd(x, (3, 3), (2, 2), (1, 1))
+    dy = rng.standard_normal(y_ref.shape)
+    prev = rng.standard_normal(x.shape)
+    if dtype == BF16:
+        dy, prev = bf16_round(dy), bf16_round(prev)
+    dx_ref = ops.maxpool_bwd(dy, arg, x.shape, (3, 3), (2, 2), (1, 1)) + (prev if with_add else 0)
+    d = L.PoolDesc(dtype=dtype, n=n, h=h, w=w, c=pad8(c), r=3, s=3, stride_h=2, stride_w=2, pad_h=1, pad_w=1,
+                   type=L.RN_POOL_MAX, global_pool=0)
+    L.call("rn_pool_desc_init", C.byref(d))
+    assert (d.p, d.q) == (h // 2, w // 2)
+    xd = to_nhwc(x, dtype, gpu)
+    yd = torch.zeros((n, d.p, d.q, pad8(c)), dtype=tdt(dtype), device=gpu)
+    am = torch.zeros(yd.numel(), dtype=torch.uint8, device=gpu)
+    L.call("rn_pool_fwd", C.byref(d), p(xd), p(yd), p(am), stream())
+    dyd, addd = to_nhwc(dy, dtype, gpu), to_nhwc(prev, dtype, gpu)
+    out = []
+    for mode in (0, 1):
+        L.call("rn_set_tuning", 12, mode)
+        dxd = torch.zeros_like(xd)
+        L.call("rn_pool_bwd", C.byref(d), p(dyd), p(am), p(dxd), p(addd) if with_add else None, stream())
+        torch.cuda.synchronize()
+        out.append(dxd)
+    L.call("rn_set_tuning", 12, 0)
+    iv = torch.int16 if dtype == BF16 else torch.int32
+    assert torch.equal(out[0].view(iv), out[1].view(iv))
+    assert rel_err(from_nhwc(out[0], c), dx_ref) < TOL[dtype]
