@@ -71,18 +71,19 @@ __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, 
       q[e] = fmaf(d, d, q[e]);
     }
   }
-  __shared__ float red[kThreads * 8 * 2];
+  __shared__ float red[kThreads * (8 * 2 + 1)];  // odd row stride: conflict-free LDS writes
 #pragma unroll
   for (int e = 0; e < CE; ++e) {
-    red[(tr * ct + tc) * CE * 2 + 2 * e] = s[e];
-    red[(tr * ct + tc) * CE * 2 + 2 * e + 1] = q[e];
+    red[(tr * ct + tc) * (CE * 2 + 1) + 2 * e] = s[e];
+    red[(tr * ct + tc) * (CE * 2 + 1) + 2 * e + 1] = q[e];
   }
   __syncthreads();
   // reduce over row lanes: thread t < ct*CE*2 sums column t
   const int ncol = ct * CE * 2;
   for (int col = threadIdx.x; col < ncol; col += blockDim.x) {
     float acc = 0.f;
-    for (int r = 0; r < rl; ++r) acc += red[r * ncol + col];
+    const int tcv = col / (CE * 2), v = col - tcv * (CE * 2);
+    for (int r = 0; r < rl; ++r) acc += red[(r * ct + tcv) * (CE * 2 + 1) + v];
     const int cc = blockIdx.x * ct * CE + col / 2;
     part[((int64_t)blockIdx.y * c + cc) * 2 + (col & 1)] = acc;
   }
@@ -444,17 +445,18 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
       q[e] = fmaf(dz, fx[e] - mu[e], q[e]);
     }
   }
-  __shared__ float red[kThreads * 8 * 2];
+  __shared__ float red[kThreads * (8 * 2 + 1)];  // odd row stride: conflict-free LDS writes
 #pragma unroll
   for (int e = 0; e < CE; ++e) {
-    red[(tr * ct + tc) * CE * 2 + 2 * e] = s[e];
-    red[(tr * ct + tc) * CE * 2 + 2 * e + 1] = q[e];
+    red[(tr * ct + tc) * (CE * 2 + 1) + 2 * e] = s[e];
+    red[(tr * ct + tc) * (CE * 2 + 1) + 2 * e + 1] = q[e];
   }
   __syncthreads();
   const int ncol = ct * CE * 2;
   for (int col = threadIdx.x; col < ncol; col += blockDim.x) {
     float acc = 0.f;
-    for (int r = 0; r < rl; ++r) acc += red[r * ncol + col];
+    const int tcv = col / (CE * 2), v = col - tcv * (CE * 2);
+    for (int r = 0; r < rl; ++r) acc += red[(r * ct + tcv) * (CE * 2 + 1) + v];
     const int cc = blockIdx.x * ct * CE + col / 2;
     part[((int64_t)blockIdx.y * c + cc) * 2 + (col & 1)] = acc;
   }
@@ -503,21 +505,22 @@ __global__ __launch_bounds__(256) void relu_bwd_bnred_kernel(const T* __restrict
     }
     *reinterpret_cast<uint4*>(g + off) = f_to_chunk(fd, (const T*)nullptr);
   }
-  __shared__ float red[kThreads * 8 * 2];
+  __shared__ float red[kThreads * (8 * 2 + 1)];  // odd row stride: conflict-free LDS writes
   const int ncol = ct * CE * 2;
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
     if (b > 0) __syncthreads();
 #pragma unroll
     for (int e = 0; e < CE; ++e) {
-      red[(tr * ct + tc) * CE * 2 + 2 * e] = s[b][e];
-      red[(tr * ct + tc) * CE * 2 + 2 * e + 1] = q[b][e];
+      red[(tr * ct + tc) * (CE * 2 + 1) + 2 * e] = s[b][e];
+      red[(tr * ct + tc) * (CE * 2 + 1) + 2 * e + 1] = q[b][e];
     }
     __syncthreads();
     float* part = b == 0 ? part_a : part_b;
     for (int col = threadIdx.x; col < ncol; col += blockDim.x) {
       float acc = 0.f;
-      for (int r = 0; r < rl; ++r) acc += red[r * ncol + col];
+      const int tcv = col / (CE * 2), v = col - tcv * (CE * 2);
+    for (int r = 0; r < rl; ++r) acc += red[(r * ct + tcv) * (CE * 2 + 1) + v];
       const int cc = blockIdx.x * ct * CE + col / 2;
       part[((int64_t)blockIdx.y * c + cc) * 2 + (col & 1)] = acc;
     }
