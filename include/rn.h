@@ -421,7 +421,9 @@ const char* rn_last_error(void);
  * 11 = the 4-wave one-buffer 224x128 conv tile, two workgroups per CU (0 auto: one-K-tile forward
  *      1x1 layers of >= 1024 tiles; 1 off; 2 every 1x1 pad-0 conv),
  * 12 = 3x3 / stride-2 max-pool backward over 2x2 input blocks (0 = on where H = 2P, W = 2Q; 1 = the
- *      per-pixel gather). */
+ *      per-pixel gather),
+ * 13 = grouped convolutions with equal channels in and out per group (<= 32): skip the MFMAs of the
+ *      block-diagonal tile's zero blocks (0 = on, 1 = off). */
 int rn_set_tuning(int32_t key, int32_t value);
 int32_t rn_version(void);
 /* Number of compute units of the current device (for split heuristics / reporting). */

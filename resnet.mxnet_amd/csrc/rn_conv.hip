@@ -712,7 +712,13 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // stores and LDS staging) overlaps the other's loads and MFMAs. For 1x1, pad-0 convolutions with at
 // most two K-tiles (their tiles are load / store bound: the 8-wave tiles alternate a read+MFMA phase
 // and a write phase on each CU); no halo, so the DMA rows need no in-image test.
-template <int BN, int NBUF, int EPI = 0, bool M32 = false, int BM = 256, int SC = 0, int Q8 = 0, int XF = 0, int W4 = 0>
+// GD: grouped convolutions with as many output columns as input channels per group (ResNeXt's 3x3,
+// symbol/resnext.py:23-25), <= 32 per group, on the 64-column tile: block column c and block channel c
+// belong to the same group, so an MFMA of k-step ks and column sub-block j multiplies zeros unless the
+// channel range of ks lies in the column range of j (32x32x16: ks >> 1 == j; 16x16x32: j >> 1 == ks).
+// Those MFMAs and their B-fragment reads are skipped: half the MFMA work of the block-diagonal tile.
+template <int BN, int NBUF, int EPI = 0, bool M32 = false, int BM = 256, int SC = 0, int Q8 = 0, int XF = 0, int W4 = 0,
+          int GD = 0>
 __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1) void igemm_big_kernel(IgemmArgs p) {
   constexpr int ES = Q8 ? 1 : 2;                 // operand bytes per element
   constexpr int BMA = 256, CE = 16 / ES, BKE = 128 / ES;
@@ -912,10 +918,15 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
     // double-buffered in registers: k-step ks + 1 is read while ks multiplies.
     constexpr int KS = M32 ? 4 : 2;
     uint4 af[2][MI], bfr[2][NI];
+    // (GD) does k-step ks meet column sub-block j?
+    auto live = [](int ks, int j) __attribute__((always_inline)) {
+      return !GD || (M32 ? (ks >> 1) == j : (j >> 1) == ks);
+    };
     auto ldf = [&](int ks) __attribute__((always_inline)) {
       const int kc = M32 ? 2 * ks + (lane >> 5) : 4 * ks + (lane >> 4);
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
+        if (!live(ks, j)) continue;
         const int row = wn * WN + j * FM + (lane & (FM - 1));
         bfr[ks & 1][j] = Bs[row * 8 + (M32 ? swz32(row, kc) : swz(row, kc))];
       }
@@ -933,6 +944,7 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
       for (int i = 0; i < MI; ++i) {
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
+          if (!live(ks, j)) continue;
           if constexpr (Q8) {
             const uint4 a8 = af[ks & 1][i], b8 = bfr[ks & 1][j];
             acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(*reinterpret_cast<const v4i*>(&a8),
@@ -2195,6 +2207,8 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
       if (a.smallc) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, 1>), grid, dim3(256), 0, st, b);
       else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 1, true>), grid, dim3(256), 0, st, b);
       else if (epi == 2) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 2, true>), grid, dim3(256), 0, st, b);
+      else if (m32 && a.gred > 0 && a.gcol == a.gred && a.gcol <= 32 && a.cblk == 64 && g_tune[RN_TUNE_IGEMM_GD] != 1)
+        hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, 0, 0, 0, 0, 1>), grid, dim3(256), 0, st, b);
       else if (m32) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true>), grid, dim3(256), 0, st, b);
       else hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, false>), grid, dim3(256), 0, st, b);
       return rn_check_launch("igemm_big64");

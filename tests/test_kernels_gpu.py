@@ -997,3 +997,37 @@ def test_maxpool_block_bwd(gpu, dtype, with_add):
     iv = torch.int16 if dtype == BF16 else torch.int32
     assert torch.equal(out[0].view(iv), out[1].view(iv))
     assert rel_err(from_nhwc(out[0], c), dx_ref) < TOL[dtype]
+
+
+@pytest.mark.parametrize("case", GCONV_CASES[:4])
+def test_grouped_conv_zero_block_skip(gpu, case):
+    """rn_set_tuning 13: the grouped 64-column tile skips the MFMAs of its block-diagonal zero blocks
+    (equal channels in and out per group, <= 32: every ResNeXt-50 3x3) -- the skipped products are
+    exact zeros, so forward and data gradient equal the unskipped tile's values exactly."""
+    n, c, h, w, k, r, st, pd, g = case
+    rng = np.random.default_rng(12)
+    x = bf16_round(rng.standard_normal((n, c, h, w)))
+    wt = bf16_round(rng.standard_normal((k, c // g, r, r)) / np.sqrt(c // g * r * r))
+    P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+    dy = bf16_round(rng.standard_normal((n, k, P, Q)))
+    d = L.ConvDesc(dtype=BF16, n=n, h=h, w=w, c=c, c_real=c, k=k, k_pad=k, r=r, s=r, stride_h=st, stride_w=st,
+                   pad_h=pd, pad_w=pd, groups=g)
+    L.call("rn_conv_desc_init", C.byref(d))
+    lib = L.load()
+    assert lib.rn_conv_tile(C.byref(d), 0) == 64
+    wk = torch.zeros(lib.rn_conv_pack_numel(C.byref(d), 0), dtype=torch.bfloat16, device=gpu)
+    wc = torch.zeros(lib.rn_conv_pack_numel(C.byref(d), 1), dtype=torch.bfloat16, device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), p(wk), p(wc), stream())
+    xd, dyd = to_nhwc(x, BF16, gpu), to_nhwc(dy, BF16, gpu)
+    outs = []
+    for mode in (0, 1):
+        L.call("rn_set_tuning", 13, mode)
+        y = torch.zeros((n, P, Q, k), dtype=torch.bfloat16, device=gpu)
+        dx = torch.zeros((n, h, w, c), dtype=torch.bfloat16, device=gpu)
+        L.call("rn_conv_fwd", C.byref(d), p(xd), p(wk), p(y), BF16, None, None, stream())
+        L.call("rn_conv_bwd_data", C.byref(d), p(dyd), p(wc), p(dx), None, stream())
+        torch.cuda.synchronize()
+        outs.append((y.float().cpu().numpy(), dx.float().cpu().numpy()))
+    L.call("rn_set_tuning", 13, 0)  # (the library default)
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    assert rel_err(from_nhwc(torch.tensor(outs[0][0]), k), ops.conv2d_fwd(x, wt, (st, st), (pd, pd), g)) < TOL[BF16]
