@@ -120,5 +120,5 @@ __device__ __forceinline__ float quant_value(float v, float t, float qmax, int c
 }
 
 // ------------------------------------------------------------------ tuning knobs (rn_set_tuning)
-enum { RN_TUNE_WGRAD_DMA = 0, RN_TUNE_IGEMM_DMA = 1, RN_TUNE_WGRAD_BLOCKS_PER_CU = 2, RN_TUNE_DIAG_IGEMM_L1 = 3, RN_TUNE_IGEMM_BIG = 4, RN_TUNE_WGRAD_BIG = 5, RN_TUNE_DIAG_WGRAD_NOEPI = 6, RN_TUNE_IGEMM_SCHED = 7, RN_TUNE_IGEMM_MFMA = 8, RN_TUNE_IGEMM_ROWS = 9, RN_TUNE_IGEMM_PERSIST = 10, RN_TUNE_IGEMM_W4 = 11, RN_TUNE_POOL_BLOCK_BWD = 12, RN_TUNE_IGEMM_GD = 13, RN_TUNE_COUNT = 14 };
+enum { RN_TUNE_WGRAD_DMA = 0, RN_TUNE_IGEMM_DMA = 1, RN_TUNE_WGRAD_BLOCKS_PER_CU = 2, RN_TUNE_DIAG_IGEMM_L1 = 3, RN_TUNE_IGEMM_BIG = 4, RN_TUNE_WGRAD_BIG = 5, RN_TUNE_DIAG_WGRAD_NOEPI = 6, RN_TUNE_IGEMM_SCHED = 7, RN_TUNE_IGEMM_MFMA = 8, RN_TUNE_IGEMM_ROWS = 9, RN_TUNE_IGEMM_PERSIST = 10, RN_TUNE_IGEMM_W4 = 11, RN_TUNE_POOL_BLOCK_BWD = 12, RN_TUNE_IGEMM_GD = 13, RN_TUNE_WGRAD_GD = 14, RN_TUNE_COUNT = 15 };
 extern int g_tune[RN_TUNE_COUNT];

@@ -1239,6 +1239,8 @@ struct WgradArgs {
   int diag_noepi;             // diagnostic (rn_set_tuning 6): skip the dW epilogue (wrong results)
   int p4;                     // the stem's padded NHWC4 image (rn_stem_prepare_p4): column = (r*8 + s)*4 + c,
                               // r, s < 8; dW keeps r < R, s < S, c < creal ([K][R][S][creal])
+  int gdiag;                  // grouped zero-block skip (bf16, rn_set_tuning 14): 16-row blocks per group
+                              // span (1: <= 16 channels per group, 2: 32); 0 = off
   float* slab;                // nullable (LDS-DMA kernels): the split's tile stored into slab[split][K][ldw]
                               // (no atomics; wgrad_slab_reduce_kernel sums the splits into dw)
   const float* in_sc;         // nullable: BN+ReLU applied to the gathered x while staging
@@ -1372,6 +1374,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  // grouped, equal rows and channels per group (<= 32, the 64 x 64 tile = one RN_GROUP_BLOCK): the
+  // 16 x 16 block (16-row block rb of k, 16-column block cb of c) is nonzero only when both lie in
+  // the same group span, so a wave whose k half and c half differ multiplies zeros only (skips its
+  // LDS reads and MFMAs; still loads and syncs), and the other waves skip their off-diagonal blocks
+  const int gd = sizeof(T) == 2 ? p.gdiag : 0;
+  const bool wave_live = !gd || wm == wn;
+  auto live = [&](int i, int j) __attribute__((always_inline)) {
+    return !gd || (wm * MI + i) / gd == (wn * NI + j) / gd;
+  };
 
   const int nstage = (mend - mbeg + BKM - 1) / BKM;
   load_stage(mbeg);
@@ -1383,6 +1394,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
     const uint4* As = smem + (t & 1) * (A_SZ + B_SZ);
     const uint4* Bs = As + A_SZ;
     if constexpr (sizeof(T) == 2) {
+      if (wave_live) {
       // 2 slabs of 32 m per stage; per slab each lane needs rows 8g+j (j=0..7) at its column.
       const char* Ab = reinterpret_cast<const char*>(As);
       const char* Bb = reinterpret_cast<const char*>(Bs);
@@ -1422,7 +1434,8 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
         for (int i = 0; i < MI; ++i)
 #pragma unroll
           for (int j = 0; j < NI; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+            if (live(i, j)) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+      }
       }
     } else {
       // f32: 16x16x4 steps; lane holds A[k=col l&15][m = 4s + (l>>4)].
@@ -2544,6 +2557,9 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     a.ncol_load = d->r * d->s * a.cblk;
     a.ncol = d->r * d->s * a.gc;
     a.ldw = a.ncol;
+    if (d->dtype == RN_BF16 && a.gk == a.gc && a.gk <= 32 && a.cblk == 64 && RN_GROUP_BLOCK == 64 &&
+        g_tune[RN_TUNE_WGRAD_GD] != 1)
+      a.gdiag = a.gk > 16 ? 2 : 1;
   }
   a.M = d->n * d->p * d->q;
   a.diag_noepi = g_tune[RN_TUNE_DIAG_WGRAD_NOEPI];

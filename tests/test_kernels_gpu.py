@@ -1001,9 +1001,10 @@ def test_maxpool_block_bwd(gpu, dtype, with_add):
 
 @pytest.mark.parametrize("case", GCONV_CASES[:4])
 def test_grouped_conv_zero_block_skip(gpu, case):
-    """rn_set_tuning 13: the grouped 64-column tile skips the MFMAs of its block-diagonal zero blocks
-    (equal channels in and out per group, <= 32: every ResNeXt-50 3x3) -- the skipped products are
-    exact zeros, so forward and data gradient equal the unskipped tile's values exactly."""
+    """rn_set_tuning 13 / 14: the grouped 64-column tiles skip the MFMAs of their block-diagonal zero
+    blocks (equal channels in and out per group, <= 32: every ResNeXt-50 3x3) -- the skipped products
+    are exact zeros, so forward and data gradient equal the unskipped tile's values exactly; the weight
+    gradient (fp32 atomics over the M splits: summation order varies) to fp32 rounding."""
     n, c, h, w, k, r, st, pd, g = case
     rng = np.random.default_rng(12)
     x = bf16_round(rng.standard_normal((n, c, h, w)))
@@ -1022,12 +1023,19 @@ def test_grouped_conv_zero_block_skip(gpu, case):
     outs = []
     for mode in (0, 1):
         L.call("rn_set_tuning", 13, mode)
+        L.call("rn_set_tuning", 14, mode)
         y = torch.zeros((n, P, Q, k), dtype=torch.bfloat16, device=gpu)
         dx = torch.zeros((n, h, w, c), dtype=torch.bfloat16, device=gpu)
+        dw = torch.zeros(lib.rn_conv_weight_numel(C.byref(d)), dtype=torch.float32, device=gpu)
         L.call("rn_conv_fwd", C.byref(d), p(xd), p(wk), p(y), BF16, None, None, stream())
         L.call("rn_conv_bwd_data", C.byref(d), p(dyd), p(wc), p(dx), None, stream())
+        L.call("rn_conv_bwd_filter", C.byref(d), p(xd), p(dyd), p(dw), stream())
         torch.cuda.synchronize()
-        outs.append((y.float().cpu().numpy(), dx.float().cpu().numpy()))
-    L.call("rn_set_tuning", 13, 0)  # (the library default)
+        outs.append((y.float().cpu().numpy(), dx.float().cpu().numpy(), dw.cpu().numpy()))
+    L.call("rn_set_tuning", 13, 0)  # (the library defaults)
+    L.call("rn_set_tuning", 14, 0)
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
     assert rel_err(from_nhwc(torch.tensor(outs[0][0]), k), ops.conv2d_fwd(x, wt, (st, st), (pd, pd), g)) < TOL[BF16]
+    assert rel_err(outs[0][2], outs[1][2]) < 1e-5
+    _, dw_ref = ops.conv2d_bwd(x, wt, dy, (st, st), (pd, pd), g)
+    assert rel_err(outs[0][2].reshape(k, r, r, c // g).transpose(0, 3, 1, 2), dw_ref) < 5e-3
