@@ -1252,7 +1252,7 @@ struct WgradArgs {
 // ds_read_b64_tr_b16 (rows 8g+4h+q): keeps the 8 rows of a 32-lane half on distinct slots.
 __device__ __forceinline__ int swz_tr(int row) { return 2 * ((row & 3) | (((row >> 3) & 1) << 2)); }
 
-template <typename T, int BMK, int BNC, bool XF = false>
+template <typename T, int BMK, int BNC, bool XF = false, bool GW = false>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   constexpr int CE = 16 / sizeof(T);
   constexpr int BKM = 128 / sizeof(T);        // m rows per stage
@@ -1378,7 +1378,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   // 16 x 16 block (16-row block rb of k, 16-column block cb of c) is nonzero only when both lie in
   // the same group span, so a wave whose k half and c half differ multiplies zeros only (skips its
   // LDS reads and MFMAs; still loads and syncs), and the other waves skip their off-diagonal blocks
-  const int gd = sizeof(T) == 2 ? p.gdiag : 0;
+  const int gd = GW && sizeof(T) == 2 ? p.gdiag : 0;  // (GW: the grouped instantiation only)
   const bool wave_live = !gd || wm == wn;
   auto live = [&](int i, int j) __attribute__((always_inline)) {
     return !gd || (wm * MI + i) / gd == (wn * NI + j) / gd;
@@ -2681,7 +2681,9 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
   dim3 grid((unsigned)(a.nct * a.nkt * split));
   if (!launch) return 0;
   if (grouped) {
-    if (d->dtype == RN_BF16)
+    if (d->dtype == RN_BF16 && a.gdiag)
+      hipLaunchKernelGGL((wgrad_kernel<bf16_t, RN_GROUP_BLOCK, RN_GROUP_BLOCK, false, true>), grid, dim3(256), 0, st, a);
+    else if (d->dtype == RN_BF16)
       hipLaunchKernelGGL((wgrad_kernel<bf16_t, RN_GROUP_BLOCK, RN_GROUP_BLOCK>), grid, dim3(256), 0, st, a);
     else
       hipLaunchKernelGGL((wgrad_kernel<float, RN_GROUP_BLOCK, RN_GROUP_BLOCK>), grid, dim3(256), 0, st, a);
