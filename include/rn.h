@@ -424,8 +424,9 @@ const char* rn_last_error(void);
  *      per-pixel gather),
  * 13 = grouped convolutions with equal channels in and out per group (<= 32): skip the MFMAs of the
  *      block-diagonal tile's zero blocks (0 = on, 1 = off),
- * 14 = the same for their bf16 weight gradients (64 x 64 tile: off-diagonal waves and 16 x 16 blocks
- *      skip their MFMAs; 0 = on, 1 = off). */
+ * 14 = the same for their bf16 weight gradients (64 x 64 tile: only the two diagonal 32 x 32 blocks,
+ *      each wave one of them over half of each M stage; 0 = on, 1 = off, 2 = on, the
+ *      diagonal blocks on two of the four waves). */
 int rn_set_tuning(int32_t key, int32_t value);
 int32_t rn_version(void);
 /* Number of compute units of the current device (for split heuristics / reporting). */

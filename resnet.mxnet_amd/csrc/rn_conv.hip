@@ -1239,6 +1239,7 @@ struct WgradArgs {
   int diag_noepi;             // diagnostic (rn_set_tuning 6): skip the dW epilogue (wrong results)
   int p4;                     // the stem's padded NHWC4 image (rn_stem_prepare_p4): column = (r*8 + s)*4 + c,
                               // r, s < 8; dW keeps r < R, s < S, c < creal ([K][R][S][creal])
+  int gspread;                // (gdiag) the diagonal blocks spread over all four waves
   int gdiag;                  // grouped zero-block skip (bf16, rn_set_tuning 14): 16-row blocks per group
                               // span (1: <= 16 channels per group, 2: 32); 0 = off
   float* slab;                // nullable (LDS-DMA kernels): the split's tile stored into slab[split][K][ldw]
@@ -1376,12 +1377,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
     for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
   // grouped, equal rows and channels per group (<= 32, the 64 x 64 tile = one RN_GROUP_BLOCK): the
   // 16 x 16 block (16-row block rb of k, 16-column block cb of c) is nonzero only when both lie in
-  // the same group span, so a wave whose k half and c half differ multiplies zeros only (skips its
-  // LDS reads and MFMAs; still loads and syncs), and the other waves skip their off-diagonal blocks
+  // the same group span: only the two diagonal 32 x 32 blocks are computed, wave (wm, wn) taking
+  // diagonal block wm over the stage's 32-row slab wn (the two partials of a block meet in the
+  // epilogue's atomic adds), and inside it the off-diagonal 16 x 16 blocks are skipped
   const int gd = GW && sizeof(T) == 2 ? p.gdiag : 0;  // (GW: the grouped instantiation only)
-  const bool wave_live = !gd || wm == wn;
+  const bool spread = gd && p.gspread;                 // rn_set_tuning 14 = 2: two waves idle instead
+  const int wnE = spread ? wm : wn;                    // the wave's column half
+  const bool wave_live = !gd || spread || wm == wn;
   auto live = [&](int i, int j) __attribute__((always_inline)) {
-    return !gd || (wm * MI + i) / gd == (wn * NI + j) / gd;
+    return !gd || (wm * MI + i) / gd == (wnE * NI + j) / gd;
   };
 
   const int nstage = (mend - mbeg + BKM - 1) / BKM;
@@ -1401,6 +1405,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
       const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
 #pragma unroll
       for (int slab = 0; slab < 2; ++slab) {
+        if (spread && slab != wn) continue;  // (grouped: one slab per wave)
         v8s af[MI], bfv[NI];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -1419,7 +1424,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
           }
 #pragma unroll
           for (int j = 0; j < NI; ++j) {
-            const int col = wn * (BNC / 2) + j * 16 + 4 * pp;
+            const int col = wnE * (BNC / 2) + j * 16 + 4 * pp;
             const int cch = (col * 2) >> 4;
             const int byte = row * (B_CPR * 16) + ((cch ^ (swz_tr(row) & (B_CPR - 1))) << 4) + ((col * 2) & 15);
             v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -1486,7 +1491,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
       if (k >= p.K) continue;
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const int col = n0 + wn * (BNC / 2) + j * 16 + (lane & 15);
+        const int col = n0 + wnE * (BNC / 2) + j * 16 + (lane & 15);
         if (!p.grouped && p.creal == p.C) {
           if (col < p.ncol) atomicAdd(p.dw + (int64_t)k * p.ldw + col, acc[i][j][e]);
         } else if (!p.grouped) {  // padded channels (the stem's 3 of 8): keep c < c_real
@@ -2559,7 +2564,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     a.ldw = a.ncol;
     if (d->dtype == RN_BF16 && a.gk == a.gc && a.gk <= 32 && a.cblk == 64 && RN_GROUP_BLOCK == 64 &&
         g_tune[RN_TUNE_WGRAD_GD] != 1)
-      a.gdiag = a.gk > 16 ? 2 : 1;
+      a.gdiag = a.gk > 16 ? 2 : 1, a.gspread = g_tune[RN_TUNE_WGRAD_GD] != 2;
   }
   a.M = d->n * d->p * d->q;
   a.diag_noepi = g_tune[RN_TUNE_DIAG_WGRAD_NOEPI];

@@ -1021,8 +1021,8 @@ def test_grouped_conv_zero_block_skip(gpu, case):
     L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), p(wk), p(wc), stream())
     xd, dyd = to_nhwc(x, BF16, gpu), to_nhwc(dy, BF16, gpu)
     outs = []
-    for mode in (0, 1):
-        L.call("rn_set_tuning", 13, mode)
+    for mode in (0, 1, 2):  # (14 = 2: the diagonal blocks on two of the four waves)
+        L.call("rn_set_tuning", 13, min(mode, 1))
         L.call("rn_set_tuning", 14, mode)
         y = torch.zeros((n, P, Q, k), dtype=torch.bfloat16, device=gpu)
         dx = torch.zeros((n, h, w, c), dtype=torch.bfloat16, device=gpu)
@@ -1036,6 +1036,6 @@ def test_grouped_conv_zero_block_skip(gpu, case):
     L.call("rn_set_tuning", 14, 0)
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
     assert rel_err(from_nhwc(torch.tensor(outs[0][0]), k), ops.conv2d_fwd(x, wt, (st, st), (pd, pd), g)) < TOL[BF16]
-    assert rel_err(outs[0][2], outs[1][2]) < 1e-5
+    assert rel_err(outs[0][2], outs[1][2]) < 1e-5 and rel_err(outs[2][2], outs[1][2]) < 1e-5
     _, dw_ref = ops.conv2d_bwd(x, wt, dy, (st, st), (pd, pd), g)
     assert rel_err(outs[0][2].reshape(k, r, r, c // g).transpose(0, 3, 1, 2), dw_ref) < 5e-3
