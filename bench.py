@@ -1,7 +1,8 @@
 """Headline benchmark: ResNet-50 v2 training throughput on MI355X (BASELINE.json configs[1..2]).
 
-`python bench.py --gpus N --steps K --warmup W` (N>1 under torch.distributed.run, one rank per
-GPU, RCCL all-reduce). One step = forward(is_train) + backward + bucketed all-reduce + SGD
+`python bench.py --gpus N --steps K --warmup W`: for N > 1 bench.py starts one rank process per
+GPU itself (or runs as one rank of `python -m torch.distributed.run --nproc-per-node N`), RCCL
+all-reduce between them. One step = forward(is_train) + backward + bucketed all-reduce + SGD
 update over one synthetic 224x224 batch of 256 images per GPU (data/imagenet.py:9-41 restated:
 seeded U(-1,1) data, random labels), bf16 activations/weights with fp32 master weights,
 gradients and BN statistics. Inputs are resident in HBM before the timed region.
@@ -233,9 +234,63 @@ def c1_module_cpu(batch=128, steps=10):
                       "%d timed steps (%.1f s)" % (batch, steps, dt)}
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv):
+    """`python bench.py --gpus N` without a torch.distributed launcher (how the driver runs it):
+    start N fresh rank processes of this script -- one per GPU, RANK / LOCAL_RANK / WORLD_SIZE /
+    MASTER_* set as torch.distributed.run would -- before this process touches the GPU, wait for
+    them and return the exit status. The reference drives its GPUs from one `python train.py`
+    (train.py:34-35, core/solver.py:58-61,121); here each GPU gets its own process and RCCL sums the
+    gradients. A rank that fails takes the others down (they would block in a collective)."""
+    import signal
+    import subprocess
+    import torch
+    backend = os.environ.get("RN_DIST_BACKEND", "nccl")
+    ngpu = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if backend == "nccl" and ngpu < n:
+        print("bench.py: --gpus %d but %d GPU(s) visible (RN_DIST_BACKEND=gloo rehearses N ranks on "
+              "fewer GPUs)" % (n, ngpu), file=sys.stderr)
+        return 2
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port, RN_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      start_new_session=True))
+    rc = 0
+    live = list(range(n))
+    while live:
+        time.sleep(0.2)
+        for r in list(live):
+            c = procs[r].poll()
+            if c is None:
+                continue
+            live.remove(r)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print("bench.py: rank %d exited with %d; stopping the other ranks" % (r, c), file=sys.stderr)
+                for q in live:
+                    try:
+                        os.killpg(procs[q].pid, signal.SIGKILL)
+                    except OSError:
+                        pass
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node (one rank each). Without a torch.distributed launcher bench.py "
+                         "starts the ranks itself; under one it must equal WORLD_SIZE. Default: WORLD_SIZE or 1")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256)
@@ -256,6 +311,13 @@ def main():
     ap.add_argument("--graph", default="auto", choices=["auto", "0", "1"],
                     help="replay the captured step as one HIP graph (auto: on for a single GPU)")
     a = ap.parse_args()
+
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and (a.gpus or 1) > 1:
+        sys.exit(launch_ranks(a.gpus, sys.argv[1:]))
+    if env_world is not None and a.gpus is not None and a.gpus != int(env_world):
+        print("bench.py: --gpus %d disagrees with WORLD_SIZE=%s" % (a.gpus, env_world), file=sys.stderr)
+        sys.exit(2)
 
     import numpy as np
     import torch
@@ -454,10 +516,15 @@ def main():
                       "resident in HBM",
             "pcie_inclusive": pcie,
         }
-        if force_ar:
-            out["allreduce"] = {"backend": dist.get_backend(), "world": 1, "buckets": len(ex.buckets()),
-                                "bucket_mb": a.bucket_mb, "note": "RCCL bucket all-reduce hooks on at N=1 "
-                                                                  "(RN_BENCH_ALLREDUCE=1)"}
+        if force_ar or world > 1:
+            nbytes = int(ex.grad.numel()) * ex.grad.element_size()
+            out["allreduce"] = {"backend": dist.get_backend(), "world": world, "buckets": len(ex.buckets()),
+                                "bucket_mb": a.bucket_mb, "grad_mb_per_step": round(nbytes / 2 ** 20, 2),
+                                "launch": "one process per GPU (%s)" % (
+                                    "bench.py --gpus" if os.environ.get("RN_BENCH_LAUNCHED") else "torch.distributed.run"),
+                                "overlap": "buckets launched from the backward plan on the weight-gradient stream"}
+            if force_ar:
+                out["allreduce"]["note"] = "RCCL bucket all-reduce hooks on at N=1 (RN_BENCH_ALLREDUCE=1)"
         if world == 1 and not a.no_cpu_baseline and a.model == "resnet50":
             try:
                 out["cpu_baseline"] = cpu_baseline(a.cpu_batch, a.cpu_steps)

@@ -339,14 +339,6 @@ int rn_sgd_mom_update_pack(int32_t ntensors, const int64_t* offsets, const int64
                            const rn_wpack* packs, const int32_t* work, int32_t nwork,
                            int32_t lowp_dtype, float lr, const float* lr_dev, float momentum,
                            float rescale_grad, float clip, rn_stream_t stream);
-/* Diagnostic twin of rn_sgd_mom_update_pack: every global index is checked against
- * lim = {nparam, then per tensor the KRSC and CRSK copy sizes}; out-of-range accesses are
- * skipped and flagged (bit mask) in *flag (device int). */
-int rn_sgd_mom_update_pack_checked(int32_t ntensors, const int64_t* offsets, const int64_t* numels,
-                                   const float* wds, float* w, const float* g, float* mom,
-                                   const rn_wpack* packs, const int32_t* work, int32_t nwork,
-                                   int32_t lowp_dtype, float lr, float momentum, float rescale_grad,
-                                   const int64_t* lim, int32_t* flag, rn_stream_t stream);
 /* Host helper: fills `work` (host memory, capacity max_items x 4) for the tensors described by
  * numels / packs (host copies); returns the item count, or -1 if max_items is too small. */
 int32_t rn_sgd_pack_work(int32_t ntensors, const int64_t* numels, const rn_wpack* packs, int32_t* work,
@@ -406,13 +398,14 @@ int rn_quant_int8_bwd(int32_t dtype, int64_t n, const void* x, const void* dy, v
 const char* rn_last_error(void);
 /* Kernel-variant switches (A/B measurements): 0 = wgrad LDS-DMA staging (default off),
  * 1 = igemm LDS-DMA staging (default off: measured slower), 2 = wgrad split-M target blocks per CU
- * (default: occupancy), 3 = diagnostic only:
+ * (default: occupancy), 3 = diagnostic build only (RN_DIAG=1; refused by librn.so):
  * igemm A operand from one L1-resident chunk (wrong results; isolates memory latency),
  * 4 = igemm 256-row tiles (0 auto, 1 off, 2 force 256x256, 3 force 256x128, 5 no 256x64),
  * 5 = wgrad variant (0 auto: 128x128 LDS-DMA tiles where K and the column count exceed 64; 1 = 256-column
  *     LDS-DMA tiles, measured slower; 3 = the register-staged kernel only),
- * 6 = diagnostic only: wgrad skips its dW epilogue (wrong results; isolates the atomic adds),
- * 7 = igemm 256-row tile schedule experiments (bit mask; 0 = default),
+ * 6 = diagnostic build only: wgrad skips its dW epilogue (wrong results; isolates the atomic adds),
+ * 7 = diagnostic build only: igemm 256-row tile schedule experiments (bit mask; 0 = default; bits 4,
+ *     8, 16, 32 drop waits / DMAs / the epilogue / the stores: wrong results),
  * 8 = igemm 256-row tile MFMA shape (0 = 32x32x16, 1 = 16x16x32),
  * 9 = igemm 224-row tiles for the 256/128-column tiles (0 = on, 1 = 256 rows),
  * 10 = igemm 256-row-family persistent grid: workgroups (a multiple of 8) that walk the tiles of a
@@ -431,6 +424,20 @@ int rn_set_tuning(int32_t key, int32_t value);
 int32_t rn_version(void);
 /* Number of compute units of the current device (for split heuristics / reporting). */
 int32_t rn_device_cu_count(void);
+
+/* ---------------------------------------------------------------------------------------
+ * Diagnostic build only (RN_DIAG=1 at build time: librn_diag.so, never the shipped librn.so).
+ * ------------------------------------------------------------------------------------- */
+#ifdef RN_DIAG
+/* Diagnostic twin of rn_sgd_mom_update_pack: every global index is checked against
+ * lim = {nparam, then per tensor the KRSC and CRSK copy sizes}; out-of-range accesses are
+ * skipped and flagged (bit mask) in *flag (device int). */
+int rn_sgd_mom_update_pack_checked(int32_t ntensors, const int64_t* offsets, const int64_t* numels,
+                                   const float* wds, float* w, const float* g, float* mom,
+                                   const rn_wpack* packs, const int32_t* work, int32_t nwork,
+                                   int32_t lowp_dtype, float lr, float momentum, float rescale_grad,
+                                   const int64_t* lim, int32_t* flag, rn_stream_t stream);
+#endif /* RN_DIAG */
 
 #ifdef __cplusplus
 }

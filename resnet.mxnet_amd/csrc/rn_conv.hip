@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
       const int win = a_wb[i] + woff;
       const bool ok = cok && (unsigned)hin < (unsigned)p.H && (unsigned)win < (unsigned)p.W;
       if (ok) {
-        const int off = p.diag_l1 ? (c & 63) : (a_pix[i] + hin * p.W + win) * p.C + cbase + c;  // < 2^31
+        const int off = (kRnDiag && p.diag_l1) ? (c & 63) : (a_pix[i] + hin * p.W + win) * p.C + cbase + c;  // < 2^31
         ra[i] = *reinterpret_cast<const uint4*>(xg + off);
       } else {
         ra[i] = make_uint4(0, 0, 0, 0);
@@ -835,7 +835,7 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
   uint32_t d_la = 0;
   int d_buf = 0;
   uint32_t okb = 0;  // (XF) bit buf * AR + k: A piece k of the K-tile in buffer buf holds data
-  const uint32_t dmask = (p.sched & 2) ? 0xFFF0u : 0xFFFFFFFFu;  // diagnostic: L2-resident sources
+  const uint32_t dmask = (kRnDiag && (p.sched & 2)) ? 0xFFF0u : 0xFFFFFFFFu;  // diagnostic: L2-resident sources
   auto prep = [&](int buf) __attribute__((always_inline)) {
     if constexpr (SC == 2) {  // K-tile t: lane chunk lch is row 2 t + lch / 4, taps 2 (lch % 4) + {0, 1}
       const int t = st_n++;
@@ -892,7 +892,7 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
     }
   };
   // diagnostic (rn_set_tuning 7 bit 8): no DMAs inside the main loop (wrong results; isolates their cost)
-  const bool loop_dma = !(p.sched & 8);
+  const bool loop_dma = !(kRnDiag && (p.sched & 8));
   auto lpiece = [&](int k) __attribute__((always_inline)) {
     if (loop_dma) piece(k);
   };
@@ -1004,7 +1004,7 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
       continue;
     }
     // K-tile t has landed for this thread once at most the later K-tiles' DMAs are outstanding
-    if (!(p.sched & 4)) {  // (diagnostic bit 4: no wait, no barrier -- wrong results)
+    if (!(kRnDiag && (p.sched & 4))) {  // (diagnostic bit 4: no wait, no barrier -- wrong results)
       if (NBUF == 3) wait_vmcnt<LPT>();
       else wait_vmcnt<0>();
       if constexpr (XF) {
@@ -1014,13 +1014,13 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
       __syncthreads();  // ... for every thread; and every wave is done reading the buffer refilled next
     }
     prep((t + NBUF - 1) % NBUF);
-    if (p.sched & 1) __builtin_amdgcn_s_setprio(1);
+    if (kRnDiag && (p.sched & 1)) __builtin_amdgcn_s_setprio(1);
     compute(t % NBUF);
-    if (p.sched & 1) __builtin_amdgcn_s_setprio(0);
+    if (kRnDiag && (p.sched & 1)) __builtin_amdgcn_s_setprio(0);
   }
   wait_vmcnt<0>();  // the zero-fill DMAs past the range land before the epilogue reuses the buffers
   __syncthreads();  // the epilogue reuses the staging buffers
-  if (p.sched & 16) {  // diagnostic (rn_set_tuning 7 bit 16): no epilogue, one store per wave keeps
+  if (kRnDiag && (p.sched & 16)) {  // diagnostic (rn_set_tuning 7 bit 16): no epilogue, one store per wave keeps
                        // the accumulators live (wrong results; isolates the epilogue's cost)
     float t = 0.f;
 #pragma unroll
@@ -1133,7 +1133,7 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
         uint4 out[AW];
 #pragma unroll
         for (int u = 0; u < AW; ++u) out[u] = f_to_chunk(v + u * (8 / AW), (const OutT*)nullptr);
-        if (!(p.sched & 32) || (out[0].x & 0xFFFF) == 0x7FC1)  // diagnostic bit 32: no output stores
+        if (!(kRnDiag && (p.sched & 32)) || (out[0].x & 0xFFFF) == 0x7FC1)  // diagnostic bit 32: no output stores
 #pragma unroll
           for (int u = 0; u < AW; ++u) reinterpret_cast<uint4*>(yg + off[k])[u] = out[u];
         if constexpr (EPI != 0) {  // on the stored (rounded) values, as a separate pass would read them
@@ -1474,7 +1474,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   }
 
   // epilogue: D[row = k][col] -> atomic add into dw
-  if (p.diag_noepi) {  // keep the accumulators live without touching memory
+  if (kRnDiag && p.diag_noepi) {  // keep the accumulators live without touching memory
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -1684,7 +1684,7 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
 
   // D[row = k][col] -> fp32 atomic add into dw (dense, unpadded: ldw = ncol); padded channels (the
   // stem's 3 of 8) keep c < creal
-  if (p.diag_noepi) return;  // diagnostic (rn_set_tuning 6): no dW epilogue (wrong results)
+  if (kRnDiag && p.diag_noepi) return;  // diagnostic (rn_set_tuning 6): no dW epilogue (wrong results)
   if (p.slab) {  // plain stores of this split's partial tile (rows of 16 columns: 64-byte segments)
     float* dst = p.slab + (int64_t)zs * p.K * p.ldw;
 #pragma unroll

@@ -527,6 +527,9 @@ const char* rn_last_error(void) { return g_last_error.c_str(); }
 
 int rn_set_tuning(int32_t key, int32_t value) {
   RN_CHECK_ARG(key >= 0 && key < RN_TUNE_COUNT, "bad tuning key");
+  RN_CHECK_ARG(kRnDiag || (key != RN_TUNE_DIAG_IGEMM_L1 && key != RN_TUNE_DIAG_WGRAD_NOEPI && key != RN_TUNE_IGEMM_SCHED) ||
+                   value == 0,
+               "diagnostic tuning key (3, 6, 7): only in the diagnostic build (RN_DIAG=1, librn_diag.so)");
   g_tune[key] = value;
   return 0;
 }
@@ -727,6 +730,7 @@ int rn_sgd_mom_update_pack(int32_t ntensors, const int64_t* offsets, const int64
   return rn_check_launch("sgd_mom_update_pack");
 }
 
+#if RN_DIAG
 // Diagnostic: the same kernel with every global index checked against lim = {nparam, then per
 // tensor KRSC and CRSK copy sizes}; out-of-range accesses are skipped and flagged in *flag.
 int rn_sgd_mom_update_pack_checked(int32_t ntensors, const int64_t* offsets, const int64_t* numels, const float* wds,
@@ -744,6 +748,7 @@ int rn_sgd_mom_update_pack_checked(int32_t ntensors, const int64_t* offsets, con
                        packs, wk, numels, lr, nullptr, momentum, rescale_grad, -1.f, lim, flag);
   return rn_check_launch("sgd_mom_update_pack_checked");
 }
+#endif  // RN_DIAG
 
 int32_t rn_sgd_pack_work(int32_t ntensors, const int64_t* numels, const rn_wpack* packs, int32_t* work,
                          int32_t max_items) {

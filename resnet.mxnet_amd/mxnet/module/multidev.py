@@ -21,6 +21,7 @@ exists so that the reference's single-process entry point runs unchanged.
 import atexit
 import os
 import socket
+import time
 import traceback
 
 import numpy as np
@@ -140,6 +141,9 @@ def _worker_main(rank, world, port, device_ids, sym_json, names, precision, back
             conn.send(("ok", None))
             break
         try:
+            # fault injection for the failure-path tests: RN_FAULT_INJECT="<command>:<rank>"
+            if os.environ.get("RN_FAULT_INJECT") == "%s:%d" % (cmd, rank):
+                raise RuntimeError("injected fault in %s on worker %d" % (cmd, rank))
             conn.send(("ok", getattr(w, cmd)(*args)))
         except Exception:
             conn.send(("error", traceback.format_exc()))
@@ -174,22 +178,72 @@ class DeviceGroup:
         self._collect()  # every worker initialised its process group
         atexit.register(self.close)
 
-    def _collect(self):
-        out, errs = [], []
-        for r, c in enumerate(self.conns):
-            status, val = c.recv()
-            if status != "ok":
-                errs.append("worker %d:\n%s" % (r, val))
-            out.append(val)
+    def _collect(self, timeout=None):
+        """Every worker's reply to the last command, in rank order. Replies are taken in whatever
+        order they arrive: the first error (or a worker that dies, or no reply within `timeout`
+        seconds: RN_WORKER_TIMEOUT, default 1800) ends the wait at once and kills every worker --
+        its peers may be blocked in a collective it will never join, so they are not asked to close."""
+        from multiprocessing.connection import wait
+        if timeout is None:
+            timeout = float(os.environ.get("RN_WORKER_TIMEOUT", "1800"))
+        deadline = time.monotonic() + timeout
+        out = [None] * len(self.conns)
+        pending = dict(enumerate(self.conns))
+        errs = []
+        while pending and not errs:
+            left = deadline - time.monotonic()
+            if left <= 0:
+                errs.append("no reply from worker(s) %s within %.0f s" % (sorted(pending), timeout))
+                break
+            sentinels = {self.procs[r].sentinel: r for r in pending}
+            ready = wait(list(pending.values()) + list(sentinels), timeout=min(left, 5.0))
+            for r, c in list(pending.items()):
+                if c.poll():
+                    try:
+                        status, val = c.recv()
+                    except (EOFError, OSError):
+                        errs.append("worker %d exited (code %s)" % (r, self.procs[r].exitcode))
+                        del pending[r]
+                        continue
+                    del pending[r]
+                    out[r] = val
+                    if status != "ok":
+                        errs.append("worker %d:\n%s" % (r, val))
+                elif self.procs[r].sentinel in ready:
+                    self.procs[r].join(timeout=1)
+                    errs.append("worker %d exited (code %s) without replying" % (r, self.procs[r].exitcode))
+                    del pending[r]
         if errs:
-            self.close()
+            self.kill()
             raise MXNetError("\n".join(errs))
         return out
 
+    def kill(self):
+        """Stop every worker without asking (used after a failure)."""
+        for p in self.procs:
+            if p.is_alive():
+                p.kill()
+        for p in self.procs:
+            p.join(timeout=10)
+        for c in self.conns:
+            try:
+                c.close()
+            except OSError:
+                pass
+        self.conns, self.procs = [], []
+
     def call(self, cmd, *args, per_rank=None):
         """Run `cmd` on every worker (per_rank: one argument tuple per worker); results by rank."""
+        if not self.conns:
+            raise MXNetError("the device workers are gone (an earlier command failed)")
         for r, c in enumerate(self.conns):
-            c.send((cmd, per_rank[r] if per_rank is not None else args))
+            try:
+                c.send((cmd, per_rank[r] if per_rank is not None else args))
+            except OSError:
+                self.procs[r].join(timeout=1)
+                code = self.procs[r].exitcode
+                self.kill()
+                raise MXNetError("worker %d exited (code %s)" % (r, code))
         return self._collect()
 
     def close(self):

@@ -14,13 +14,18 @@ ROOT = os.path.dirname(PKG_DIR)                      # resnet.mxnet_amd/
 REPO = os.path.dirname(ROOT)
 CSRC = os.path.join(ROOT, "csrc")
 INCLUDE = os.path.join(REPO, "include")
-BUILD_DIR = os.path.join(ROOT, "build")
-LIB_PATH = os.path.join(PKG_DIR, "librn.so")
+# RN_DIAG=1: the diagnostic build (wrong-result isolation modes of rn_set_tuning 3 / 6 / 7 and
+# rn_sgd_mom_update_pack_checked compiled in) as a separate library; the product loads librn.so
+DIAG = os.environ.get("RN_DIAG", "0") == "1"
+BUILD_DIR = os.path.join(ROOT, "build_diag" if DIAG else "build")
+LIB_PATH = os.path.join(PKG_DIR, "librn_diag.so" if DIAG else "librn.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 CXXFLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
             "-Wno-unused-result", "-munsafe-fp-atomics",
             "-mllvm", "-disable-promote-alloca-to-lds"]  # keep per-thread arrays out of the staging LDS
+if DIAG:
+    CXXFLAGS.append("-DRN_DIAG=1")
 
 
 def _sources():

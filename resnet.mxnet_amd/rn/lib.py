@@ -85,8 +85,6 @@ SIGNATURES = {
     "rn_sgd_mom_update": (_i32, [_i32, _P, _P, _P, _P, _P, _P, _P, _i32, _f32, _P, _f32, _f32, _f32, _P]),
     "rn_sgd_mom_update_pack": (_i32, [_i32, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _i32, _f32, _P, _f32, _f32, _f32,
                                       _P]),
-    "rn_sgd_mom_update_pack_checked": (_i32, [_i32, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _i32, _f32, _f32, _f32, _P,
-                                              _P, _P]),
     "rn_sgd_pack_work": (_i32, [_i32, _P, _P, _P, _i32]),
     "rn_nchw_to_nhwc": (_i32, [_i32, _i32, _i32, _i32, _i32, _P, _P, _i32, _P]),
     "rn_cast": (_i32, [_i64, _P, _i32, _P, _i32, _P]),
@@ -99,6 +97,12 @@ SIGNATURES = {
     "rn_last_error": (C.c_char_p, []),
     "rn_version": (_i32, []),
     "rn_device_cu_count": (_i32, []),
+}
+
+# include/rn.h's `#ifdef RN_DIAG` section: exported by the diagnostic build (librn_diag.so) only
+DIAG_SIGNATURES = {
+    "rn_sgd_mom_update_pack_checked": (_i32, [_i32, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _i32, _f32, _f32, _f32, _P,
+                                              _P, _P]),
 }
 
 _lib = None
@@ -124,7 +128,9 @@ def load(auto_build=True):
     # device ("no ROCm-capable device is detected"). Importing torch does not initialise the GPU.
     import torch  # noqa: F401
     lib = C.CDLL(LIB_PATH)
-    for name, (res, args) in SIGNATURES.items():
+    for name, (res, args) in list(SIGNATURES.items()) + list(DIAG_SIGNATURES.items()):
+        if name in DIAG_SIGNATURES and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

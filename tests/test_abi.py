@@ -11,6 +11,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared():
     src = open(os.path.join(REPO, "include", "rn.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    src = re.sub(r"#ifdef RN_DIAG.*?#endif", "", src, flags=re.S)  # diagnostic build only
     return sorted(set(re.findall(r"\b(rn_[a-z0-9_]+)\s*\(", src)))
 
 
@@ -67,3 +68,15 @@ def test_sgd_pack_work_table():
     assert lib.rn_sgd_pack_work(3, P(nums), P(tab), P(work), 4) == -1
     tab[1]["k"] = 99  # size mismatch is refused
     assert lib.rn_sgd_pack_work(3, P(nums), P(tab), P(work), 64) == -1
+
+
+def test_diagnostic_modes_are_not_in_the_product_library():
+    """the wrong-result diagnostics (rn_set_tuning 3 / 6 / 7, the checked SGD
+    twin) exist only in the RN_DIAG build; librn.so refuses the keys and does not export the twin."""
+    lib = L.load()
+    assert not hasattr(lib, "rn_sgd_mom_update_pack_checked")
+    for key in (3, 6, 7):
+        assert lib.rn_set_tuning(key, 1) == -1
+        assert b"diagnostic" in lib.rn_last_error()
+        assert lib.rn_set_tuning(key, 0) == 0
+    assert lib.rn_set_tuning(12, 0) == 0  # ordinary variant keys stay available

@@ -57,6 +57,37 @@ def test_two_contexts_split_the_batch(dry):
         mod.close()
 
 
+def test_worker_failure_in_a_collective_raises_instead_of_hanging(dry, monkeypatch):
+    """worker 1 raises inside get_params (the aux all-reduce of core/solver.py:170) while
+    worker 0 blocks in that collective; the parent must report the error promptly and kill both."""
+    import time
+    monkeypatch.setenv("RN_FAULT_INJECT", "get_params:1")
+    mod = mx.mod.Module(graphs.resnet20_cifar(), context=[mx.gpu(0), mx.gpu(1)])
+    try:
+        mod.bind(data_shapes=[("data", (4, 3, 32, 32))], label_shapes=[("softmax_label", (4,))])
+        mx.random.seed(1)
+        mod.init_params(mx.init.Xavier(rnd_type="gaussian", factor_type="in", magnitude=2))
+        procs = list(mod._group.procs)
+        t0 = time.monotonic()
+        with pytest.raises(mx.MXNetError, match="injected fault in get_params on worker 1"):
+            mod.get_params()
+        assert time.monotonic() - t0 < 60
+        assert not any(p.is_alive() for p in procs)  # worker 0 was stuck in the all-reduce: killed
+    finally:
+        mod.close()
+
+
+def test_worker_death_is_reported(dry):
+    mod = mx.mod.Module(graphs.resnet20_cifar(), context=[mx.gpu(0), mx.gpu(1)])
+    try:
+        mod.bind(data_shapes=[("data", (4, 3, 32, 32))], label_shapes=[("softmax_label", (4,))])
+        mod._group.procs[0].kill()
+        with pytest.raises(mx.MXNetError, match="worker 0 exited"):
+            mod._group.call("stats")
+    finally:
+        mod.close()
+
+
 def test_multi_context_under_mismatched_launch_raises(dry, monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "3")
     mod = mx.mod.Module(graphs.resnet20_cifar(), context=[mx.gpu(0), mx.gpu(1)])
