@@ -97,8 +97,12 @@ def test_resnet50_bf16_step_gradients(gpu, tiles):
 def test_resnet50_bf16_full_size_gradients(gpu):
     """The exact bench configuration -- 256 images at 224x224, no tuning override -- against the
     torch-CPU fp32 restatement of the same step (oracle/torch_cpu.py, itself pinned to the numpy
-    oracle): at this size BatchNorm averages over >= 12,544 elements per channel, the network is
-    well conditioned and bf16 storage costs ~1 % per gradient tensor, so absolute bars apply."""
+    oracle) and its bf16-storage emulation. At this Xavier init the network is chaotic under ANY
+    bf16 rounding (the emulation's own forward error grows ~1.17x per
+    BatchNorm+ReLU layer, 0.2 % at the stem to 25 % at stage 4; measured r03, profiles/r03/
+    bf16_full_size_gradients.log: emulation vs fp32 cosine 0.297, device vs fp32 cosine 0.298), so
+    end to end the bar is relative: the device no further from fp32 than ideal bf16 storage (+10 %).
+    The absolute per-layer bars are test_resnet50_bf16_full_size_layerwise below."""
     from oracle import torch_cpu
     g = onet.resnet50_imagenet()
     args, aux = onet.init_params(g, dtype=np.float32)
@@ -113,16 +117,94 @@ def test_resnet50_bf16_full_size_gradients(gpu):
     egrads, eprob = torch_cpu.TorchStep(g, args, aux, storage="bf16").grads(data, label)
     s = grad_summary(res["grads"][0], grads)
     se = grad_summary(egrads, grads)
+    sde = grad_summary(res["grads"][0], egrads)
     p, pe = max_rel(res["prob"][0], prob), max_rel(eprob, prob)
     print("bench config vs torch-CPU fp32:", s, "prob", p)
     print("torch-CPU bf16-storage emulation vs fp32:", se, "prob", pe)
-    # the random-init network is chaotic under bf16 rounding even at this size: the device must be
-    # no further from fp32 than ideal bf16 storage is
-    assert 1 - s["cos"] < 1.5 * (1 - se["cos"]) + 0.01, (s, se)
+    print("bench config vs the bf16-storage emulation:", sde, "prob", max_rel(res["prob"][0], eprob))
+    assert 1 - s["cos"] < 1.1 * (1 - se["cos"]) + 0.01, (s, se)
     for k in ("fro", "median", "p95"):
-        assert s[k] < 1.5 * se[k] + 0.02, (k, s, se)
-    assert p < 2 * pe + 0.02, (p, pe)
+        assert s[k] < 1.1 * se[k] + 0.01, (k, s, se)
+    assert p < 1.25 * pe + 0.01, (p, pe)
     assert abs(ce_loss(res["prob"][0], label) - ce_loss(prob, label)) < 0.01 * ce_loss(prob, label)
+
+
+def _layerwise(sym, n, image, precision, tune=None):
+    """One training step (forward + backward, serialised on one stream) with every kernel checked
+    against its fp32 torch restatement from the device's own inputs (tests/layerwise.py)."""
+    import json
+    import os
+    import mxnet as mx
+    from layerwise import Checker
+    from rn import lib as L
+    lib = L.load()
+    for k, v in (tune or {}).items():
+        L.check(lib.rn_set_tuning(k, v), "tune")
+    try:
+        rng = np.random.default_rng(0)
+        data = rng.uniform(-1, 1, (n, 3, image, image)).astype(np.float32)
+        label = np.random.default_rng(1).integers(0, 1000, n).astype(np.float32)
+        mod = mx.mod.Module(sym, context=[mx.gpu(0)], precision=precision)
+        mod.bind(data_shapes=[("data", data.shape)], label_shapes=[("softmax_label", (n,))])
+        mx.random.seed(2)
+        mod.init_params(mx.init.Xavier(rnd_type="gaussian", factor_type="in", magnitude=2))
+        mod.init_optimizer(kvstore="device", optimizer="sgd",
+                           optimizer_params={"learning_rate": 0.1, "wd": 1e-4, "momentum": 0.9})
+        ex = mod.executor
+        ex.side_enabled = False  # the checks read buffers between calls: one stream, in plan order
+        batch = mx.io.DataBatch(data=[mx.nd.array(data)], label=[mx.nd.array(label)])
+        mod.forward(batch, is_train=True)
+        torch.cuda.synchronize()
+        ck = Checker(ex)
+        with torch.no_grad():
+            ck.check_forward()
+            ex.backward(hooks=ck.backward_hooks())
+        torch.cuda.synchronize()
+    finally:
+        for k in (tune or {}):
+            L.check(lib.rn_set_tuning(k, 512 if k == 10 else 0), "tune")
+    tab = ck.table()
+    for kind, e in sorted(tab.items()):
+        print("%-16s %4d checked, worst: %s" % (kind, e["n"], ", ".join(
+            "%s %.2e (%s)" % (k, v[0], v[1]) for k, v in sorted(e.items()) if k != "n")))
+    print("backward calls checked:", ck.covered, "not checked:", ck.skipped)
+    out = os.environ.get("RN_LAYERWISE_OUT")
+    if out:
+        with open(out, "w") as f:
+            json.dump({"config": [n, image, precision], "records": ck.rec, "covered": ck.covered,
+                       "skipped": ck.skipped}, f)
+    return ck
+
+
+def test_resnet50_bf16_full_size_layerwise(gpu):
+    """The bench configuration (ResNet-50 v2, 256 x 224 x 224, bf16, default knobs) with ABSOLUTE
+    bars per kernel: every one of the step's 53 convolutions forward / data gradient / weight gradient,
+    51 BatchNorms forward (statistics, coefficients, stored outputs) and backward (dx, dgamma, dbeta),
+    the stem's bn_data transform, pooling, FullyConnected, SoftmaxOutput and the gradient fan-in adds,
+    each recomputed in fp32 from the device's own inputs: bf16 outputs within one bf16 rounding (Frobenius
+    4e-3, max 8e-3 of the tensor's max), fp32 weight gradients within 2e-6 of the magnitude sum of their
+    terms per element (layerwise.WGRAD_BAR), BatchNorm statistics within 1e-5. Every call of the backward
+    plan is checked. Measured numbers: profiles/r03/layerwise_bf16.log."""
+    from rn import graphs
+    ck = _layerwise(graphs.resnet50(), 256, 224, "bfloat16")
+    assert not ck.skipped, ck.skipped
+    kinds = {r[0] for r in ck.rec}
+    assert {"conv_fwd", "dgrad", "dgrad_bnred", "wgrad", "bn_fwd", "bn_bwd_dx", "bn_bwd_params", "stem_prepare",
+            "pool_fwd", "pool_bwd", "fc_fwd", "softmax", "softmax_grad", "bn_apply", "fc_bias_grad", "stem_dbeta"} <= kinds, kinds
+    assert sum(1 for r in ck.rec if r[0] == "wgrad") == 54  # 53 convs + fc1
+    assert sum(1 for r in ck.rec if r[0] == "conv_fwd") == 53
+    bad = ck.failures()
+    assert not bad, bad[:10]
+
+
+def test_resnet50_fp32_layerwise(gpu):
+    """The same per-kernel checks on the fp32 parity path (exact fp32 MFMA), small batch: validates
+    the checker itself at fp32 bars and covers the fp32 kernels layer by layer."""
+    from rn import graphs
+    ck = _layerwise(graphs.resnet50(), 4, 64, "float32")
+    assert not ck.skipped, ck.skipped
+    bad = ck.failures()
+    assert not bad, bad[:10]
 
 
 def test_resnet50_bf16_full_size_properties(gpu):
