@@ -93,10 +93,24 @@ int rn_conv_weight_pack_i8(const rn_conv_desc* d, const float* w_master, const f
  * this call completes (dx here = d(bn output), bn_x = the BN input, bn_mean / bn_scale / bn_shift =
  * its saved mean and the scale/shift of its forward): part[rn_conv_bnred_blocks(d)][c][2] receives
  * per-output-block (sum dz, sum dz*(x - mean)), dz = dx * [bn_x*scale + shift > 0] (relu != 0);
- * rn_bn_bwd_part then finishes the BN backward without its own reduction pass over x and dy. */
+ * rn_bn_bwd_part then finishes the BN backward without its own reduction pass over x and dy.
+ * dx = NULL (no add_src; the 224/256-row tile): the reduction only, nothing is stored (the first
+ * pass of rn_conv_bwd_data_bnapply's recompute). */
 int rn_conv_bwd_data_bnred(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx, const void* add_src,
                            const void* bn_x, const float* bn_mean, const float* bn_scale, const float* bn_shift,
                            int32_t relu, float* part, rn_stream_t stream);
+/* The BatchNorm(+ReLU) backward of the BN whose output gradient this convolution's data gradient is,
+ * APPLIED in the epilogue to the recomputed gradient: dx = A (dz - mean(dz)) - A2 (x - mean)
+ * (+ add_src), dz = g relu'(x scale + shift) (relu != 0), g = conv_transpose(dy, w) rounded as
+ * rn_conv_bwd_data would store it, coef from rn_bn_bwd_finalize over the partials of a
+ * reduction-only rn_conv_bwd_data_bnred (dx = NULL) of the same convolution. Bit-identical to
+ * rn_conv_bwd_data + rn_bn_bwd_part. For cheap data gradients (a 1x1 convolution whose input has
+ * more channels than its output, the pre-activation units' conv1, symbol/resnet.py:17-20): the
+ * BN-width gradient is never written nor read back. bf16, the 224/256-row tile (rn_conv_tile(d, 1)
+ * >= 128). */
+int rn_conv_bwd_data_bnapply(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
+                             const void* add_src, const void* bn_x, const float* coef, const float* bn_scale,
+                             const float* bn_shift, int32_t relu, rn_stream_t stream);
 int64_t rn_conv_bnred_blocks(const rn_conv_desc* d);
 
 /* rn_conv_fwd whose input is the PRE-BatchNorm tensor of a BatchNorm+ReLU (pre-activation
@@ -239,6 +253,12 @@ int rn_bn_bwd_part(const rn_bn_desc* d, const float* part, int64_t nrb, const vo
                    const void* add_src, const float* gamma, const float* save_mean, const float* save_invstd,
                    const float* scale, const float* shift, float* dgamma, float* dbeta, void* ws,
                    rn_stream_t stream);
+/* The finalize half of rn_bn_bwd_part: dgamma / dbeta and coef[c][4] = {A = gamma*invstd, mean(dz),
+ * A2 = gamma*invstd^2*sum(dz*xhat)/m, mean} (16-byte aligned), from which dx = A (dz - mean(dz)) -
+ * A2 (x - mean) (+ add). For rn_conv_bwd_data_bnapply. */
+int rn_bn_bwd_finalize(const rn_bn_desc* d, const float* part, int64_t nrb, const float* gamma,
+                       const float* save_mean, const float* save_invstd, float* dgamma, float* dbeta, float* coef,
+                       rn_stream_t stream);
 int rn_bn_fwd_infer(const rn_bn_desc* d, const void* x, void* y, const float* gamma,
                     const float* beta, const float* moving_mean, const float* moving_var,
                     float* scale, float* shift, rn_stream_t stream);
@@ -419,7 +439,13 @@ const char* rn_last_error(void);
  *      block-diagonal tile's zero blocks (0 = on, 1 = off),
  * 14 = the same for their bf16 weight gradients (64 x 64 tile: only the two diagonal 32 x 32 blocks,
  *      each wave one of them over half of each M stage; 0 = on, 1 = off, 2 = on, the
- *      diagonal blocks on two of the four waves). */
+ *      diagonal blocks on two of the four waves),
+ * 15, 16 = (reserved: round-3 conv-tile experiments, measured and removed -- DESIGN.md §3),
+ * 17 = deterministic weight gradients (1 = on): every M-split of every weight gradient stores its
+ *      partial tile into the workspace slab (rn_conv_bwd_filter_ws / _x; rn_conv_wgrad_ws_bytes is
+ *      > 0 for every layer then, fp32 included) and one pass sums the splits in a fixed order, instead
+ *      of fp32 atomic adds; the FullyConnected forward's split-K atomics are off. Bitwise
+ *      run-to-run reproducible steps (the parity tests' mode). */
 int rn_set_tuning(int32_t key, int32_t value);
 int32_t rn_version(void);
 /* Number of compute units of the current device (for split heuristics / reporting). */

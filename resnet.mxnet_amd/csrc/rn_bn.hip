@@ -866,6 +866,18 @@ int rn_bn_bwd_part(const rn_bn_desc* d, const float* part, int64_t nrb, const vo
 }
 
 
+int rn_bn_bwd_finalize(const rn_bn_desc* d, const float* part, int64_t nrb, const float* gamma,
+                       const float* save_mean, const float* save_invstd, float* dgamma, float* dbeta, float* coef,
+                       rn_stream_t stream) {
+  if (check_bn(d)) return -1;
+  RN_CHECK_ARG(part && nrb > 0 && save_mean && save_invstd && coef, "null argument");
+  RN_CHECK_ARG(((uintptr_t)coef & 15) == 0, "coef must be 16-byte aligned");
+  RN_CHECK_ARG(d->fix_gamma || gamma, "gamma required unless fix_gamma");
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(d->c), dim3(256), 0, as_stream(stream), part, (int)nrb, d->m, d->c,
+                     d->c_real, d->fix_gamma, gamma, save_mean, save_invstd, dgamma, dbeta, coef);
+  return rn_check_launch("bn_bwd_finalize");
+}
+
 int rn_bn_fwd_infer(const rn_bn_desc* d, const void* x, void* y, const float* gamma, const float* beta,
                     const float* moving_mean, const float* moving_var, float* scale, float* shift,
                     rn_stream_t stream) {

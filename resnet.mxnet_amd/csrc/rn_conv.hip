@@ -64,6 +64,10 @@ struct IgemmArgs {
   const void* bn_x;
   const float *bn_mean, *bn_sc, *bn_sh;
   int bn_relu, mt_max;
+  // dgrad only, nullable (igemm_big_kernel EPI 3): the BatchNorm backward APPLIED to the recomputed
+  // gradient g (rounded as stored): dx = A (dz - mean dz) - A2 (x - mean) (+ add), coefficients
+  // {A, mean dz, A2, mean} per channel from rn_bn_bwd_finalize, x = bn_x, dz = g relu'(x sc + sh)
+  const float* bn_coef;
   // int8 forward (igemm_big_kernel Q8): per-tensor quantization units of the int8 codes in x and w
   // (Quantization_int8: value = code * unit); the int32 accumulators are scaled by their product
   const float* qunit_x;
@@ -1042,17 +1046,26 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
   const int col0 = n0 + wn * WN + cc * 8;
   const bool half_ok = m0 + wm * WM < Mc;  // this wave row holds at least one output row
   // BatchNorm partials of this lane's 8 columns (EPI 1: S1, S2 about the pivot; EPI 2: sum dz,
-  // sum dz * (x - mean)), over its rows; the lanes sharing a column chunk are summed at the end
+  // sum dz * (x - mean)), over its rows; the lanes sharing a column chunk are summed at the end.
+  // EPI 3 keeps its coefficients in the same registers: s1 = A, s2 = mean(dz), piv = A2, r_mu = mean.
   constexpr int NS = EPI ? 8 : 1;
   float s1[NS], s2[NS], piv[NS], r_mu[NS], r_sc[NS], r_sh[NS];
 #pragma unroll
   for (int e = 0; e < NS; ++e) {
     s1[e] = s2[e] = piv[e] = r_mu[e] = r_sc[e] = r_sh[e] = 0.f;
-    if constexpr (EPI == 2) {
+    if constexpr (EPI == 2 || EPI == 3) {
       const bool okc = col0 + e < p.K;
-      r_mu[e] = okc ? p.bn_mean[col0 + e] : 0.f;
       r_sc[e] = okc ? p.bn_sc[col0 + e] : 0.f;
       r_sh[e] = okc ? p.bn_sh[col0 + e] : 0.f;
+      if constexpr (EPI == 2) {
+        r_mu[e] = okc ? p.bn_mean[col0 + e] : 0.f;
+      } else if (okc) {
+        const float4 cf = reinterpret_cast<const float4*>(p.bn_coef)[col0 + e];
+        s1[e] = cf.x;
+        s2[e] = cf.y;
+        piv[e] = cf.z;
+        r_mu[e] = cf.w;
+      }
     }
   }
   const bf16_t* __restrict__ bxg = reinterpret_cast<const bf16_t*>(p.bn_x);
@@ -1062,7 +1075,8 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
     const int rows_h = h + 1 < NCH ? 64 : kLast;
     int64_t off[CPR];  // this lane's rows: lane / CPR + (64 / CPR) k
     uint4 addv[CPR][AW];
-    uint4 xpre[EPI == 2 ? CPR : 1];  // BN input at the same positions (EPI 2), loaded with the residual
+    constexpr bool XP = EPI == 2 || EPI == 3;
+    uint4 xpre[XP ? CPR : 1];  // BN input at the same positions (EPI 2 / 3), loaded with the residual
 #pragma unroll
     for (int k = 0; k < CPR; ++k) {
       const int r = lane / CPR + (64 / CPR) * k;
@@ -1070,7 +1084,7 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
       off[k] = -1;
 #pragma unroll
       for (int u = 0; u < AW; ++u) addv[k][u] = make_uint4(0, 0, 0, 0);
-      if constexpr (EPI == 2) xpre[k] = make_uint4(0, 0, 0, 0);
+      if constexpr (XP) xpre[k] = make_uint4(0, 0, 0, 0);
       if (m < Mc && col0 < p.K && r < rows_h) {
         const int n = fdiv(m, cl.fdPQ);
         const int rem = m - n * cl.Pc * cl.Qc;
@@ -1080,7 +1094,7 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
         if (ag && col0 + 8 <= p.K)
 #pragma unroll
           for (int u = 0; u < AW; ++u) addv[k][u] = reinterpret_cast<const uint4*>(ag + off[k])[u];
-        if constexpr (EPI == 2)
+        if constexpr (XP)
           if (col0 + 8 <= p.K) xpre[k] = *reinterpret_cast<const uint4*>(bxg + off[k]);
       }
     }
@@ -1123,7 +1137,21 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
       *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(ep + r * EP_LD + cc * 8);
       *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(ep + r * EP_LD + cc * 8 + 4);
       if (col0 + 8 <= p.K) {
-        if (ag) {
+        if constexpr (EPI == 3) {
+          // the BatchNorm(+ReLU) backward applied to the gradient as rn_conv_bwd_data would store it,
+          // exactly as bn_bwd_apply_kernel (rn_bn.hip) computes it from the stored gradient
+          float g[8], xv[8], a[8];
+          chunk_to_f(f_to_chunk(v, (const bf16_t*)nullptr), g, (const bf16_t*)nullptr);
+          chunk_to_f(xpre[XP ? k : 0], xv, (const bf16_t*)nullptr);
+          if (ag) chunk_to_f(addv[k][0], a, (const bf16_t*)nullptr);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float dz = p.bn_relu ? g[e] * (fmaf(xv[e], r_sc[e], r_sh[e]) > 0.f ? 1.f : 0.f) : g[e];
+            float w = s1[e] * (dz - s2[e]) - piv[e] * (xv[e] - r_mu[e]);
+            if (ag) w += a[e];
+            v[e] = w;
+          }
+        } else if (ag) {
           float a[8];
 #pragma unroll
           for (int u = 0; u < AW; ++u) chunk_to_f(addv[k][u], a + u * (8 / AW), (const OutT*)nullptr);
@@ -1133,10 +1161,11 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
         uint4 out[AW];
 #pragma unroll
         for (int u = 0; u < AW; ++u) out[u] = f_to_chunk(v + u * (8 / AW), (const OutT*)nullptr);
-        if (!(kRnDiag && (p.sched & 32)) || (out[0].x & 0xFFFF) == 0x7FC1)  // diagnostic bit 32: no output stores
+        if (yg && (!(kRnDiag && (p.sched & 32)) || (out[0].x & 0xFFFF) == 0x7FC1))  // (EPI 2 may only reduce;
+                                                                                  // diagnostic bit 32: no stores)
 #pragma unroll
           for (int u = 0; u < AW; ++u) reinterpret_cast<uint4*>(yg + off[k])[u] = out[u];
-        if constexpr (EPI != 0) {  // on the stored (rounded) values, as a separate pass would read them
+        if constexpr (EPI == 1 || EPI == 2) {  // on the stored (rounded) values, as a separate pass would read them
           float g[8];
 #pragma unroll
           for (int u = 0; u < AW; ++u) chunk_to_f(out[u], g + u * (8 / AW), (const OutT*)nullptr);
@@ -1149,7 +1178,7 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
             }
           } else {
             float xv[8];
-            chunk_to_f(xpre[EPI == 2 ? k : 0], xv, (const bf16_t*)nullptr);
+            chunk_to_f(xpre[XP ? k : 0], xv, (const bf16_t*)nullptr);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const float dz = (!p.bn_relu || fmaf(xv[e], r_sc[e], r_sh[e]) > 0.f) ? g[e] : 0.f;
@@ -1158,7 +1187,7 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
             }
           }
         }
-      } else {
+      } else if (yg) {  // (ragged columns: never with EPI 3, whose channels come in whole chunks)
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (col0 + e < p.K) {
@@ -1169,7 +1198,7 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
       }
     }
   }
-  if constexpr (EPI != 0) {
+  if constexpr (EPI == 1 || EPI == 2) {
 #pragma unroll
     for (int o = CPR; o < 64; o <<= 1)
 #pragma unroll
@@ -1483,6 +1512,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
     if (s == 12345.678f) p.dw[0] = s;
     return;
   }
+  // (deterministic mode, p.slab: this split's partial into slab[zs][K][ldw] -- every element of a
+  // split is produced by exactly one wave of one block -- and wgrad_slab_reduce_kernel sums the splits
+  // in order)
+  float* const dst = p.slab ? p.slab + (int64_t)zs * p.K * p.ldw : p.dw;
+  auto put = [&](int64_t i, float v) __attribute__((always_inline)) {
+    if (p.slab) dst[i] = v;
+    else atomicAdd(dst + i, v);
+  };
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
 #pragma unroll
@@ -1493,18 +1530,18 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
       for (int j = 0; j < NI; ++j) {
         const int col = n0 + wnE * (BNC / 2) + j * 16 + (lane & 15);
         if (!p.grouped && p.creal == p.C) {
-          if (col < p.ncol) atomicAdd(p.dw + (int64_t)k * p.ldw + col, acc[i][j][e]);
+          if (col < p.ncol) put((int64_t)k * p.ldw + col, acc[i][j][e]);
         } else if (!p.grouped) {  // padded channels (the stem's 3 of 8): keep c < c_real
           if (col < p.ncol_load) {
             const int tap = fdiv(col, p.fdC);
             const int c = col - tap * p.C;
-            if (c < p.creal) atomicAdd(p.dw + (int64_t)k * p.ldw + tap * p.creal + c, acc[i][j][e]);
+            if (c < p.creal) put((int64_t)k * p.ldw + tap * p.creal + c, acc[i][j][e]);
           }
         } else if (col < p.ncol_load) {  // keep the block-diagonal part: channel in k's group
           const int tap = fdiv(col, p.fdC);
           const int c = cbase + col - tap * p.cblk;
           const int g = k / p.gk;
-          if (c / p.gc == g) atomicAdd(p.dw + (int64_t)k * p.ldw + tap * p.gc + (c - g * p.gc), acc[i][j][e]);
+          if (c / p.gc == g) put((int64_t)k * p.ldw + tap * p.gc + (c - g * p.gc), acc[i][j][e]);
         }
       }
     }
@@ -1685,7 +1722,8 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
   // D[row = k][col] -> fp32 atomic add into dw (dense, unpadded: ldw = ncol); padded channels (the
   // stem's 3 of 8) keep c < creal
   if (kRnDiag && p.diag_noepi) return;  // diagnostic (rn_set_tuning 6): no dW epilogue (wrong results)
-  if (p.slab) {  // plain stores of this split's partial tile (rows of 16 columns: 64-byte segments)
+  const bool padded = p.creal != p.C;
+  if (p.slab && !padded) {  // plain stores of this split's partial tile (rows of 16 columns: 64-byte segments)
     float* dst = p.slab + (int64_t)zs * p.K * p.ldw;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -1701,7 +1739,12 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
       }
     return;
   }
-  const bool padded = p.creal != p.C;
+  // (padded channels: the slab, in the deterministic mode, takes the same compacted indices)
+  float* const pdst = p.slab ? p.slab + (int64_t)zs * p.K * p.ldw : p.dw;
+  auto put = [&](int64_t i, float v) __attribute__((always_inline)) {
+    if (p.slab) pdst[i] = v;
+    else atomicAdd(pdst + i, v);
+  };
 #pragma unroll
   for (int i = 0; i < MI; ++i)
 #pragma unroll
@@ -1715,12 +1758,11 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
           if (col < p.ncol) atomicAdd(p.dw + (int64_t)k * p.ldw + col, acc[i][j][e]);
         } else if (p.p4) {  // column (r*8 + s)*4 + c of the padded NHWC4 image
           const int c = col & 3, s = (col >> 2) & 7, r = col >> 5;
-          if (c < p.creal && s < p.S && r < p.R)
-            atomicAdd(p.dw + (int64_t)k * p.ldw + (r * p.S + s) * p.creal + c, acc[i][j][e]);
+          if (c < p.creal && s < p.S && r < p.R) put((int64_t)k * p.ldw + (r * p.S + s) * p.creal + c, acc[i][j][e]);
         } else if (col < p.ncol_load) {
           const int tap = fdiv(col, p.fdC);
           const int c = col - tap * p.C;
-          if (c < p.creal) atomicAdd(p.dw + (int64_t)k * p.ldw + tap * p.creal + c, acc[i][j][e]);
+          if (c < p.creal) put((int64_t)k * p.ldw + tap * p.creal + c, acc[i][j][e]);
         }
       }
     }
@@ -1729,6 +1771,14 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
 // dw[i] += sum_z slab[z][i] (the split-M partial tiles of wgrad_big_kernel), float4 per thread
 __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __restrict__ slab, int nsplit,
                                                                 int64_t n, float* __restrict__ dw) {
+  if (n & 3) {  // (a split's slab not a whole number of 16-byte chunks: scalar, same summation order)
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+      float a = dw[i];
+      for (int z = 0; z < nsplit; ++z) a += slab[(int64_t)z * n + i];
+      dw[i] = a;
+    }
+    return;
+  }
   const int64_t n4 = n / 4;
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     float4 a = reinterpret_cast<const float4*>(dw)[i];
@@ -2205,8 +2255,9 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   const bool dma = g_tune[RN_TUNE_IGEMM_DMA] > 0 && !a.in_sc && !b.diag_l1 && xb < INT32_MAX && wb < INT32_MAX &&
                    max_taps <= 64;
   if constexpr (std::is_same<T, bf16_t>::value && std::is_same<OutT, bf16_t>::value) {
-    const int epi = a.stats ? 1 : a.bnred ? 2 : 0;
+    const int epi = a.stats ? 1 : a.bnred ? 2 : a.bn_coef ? 3 : 0;
     const int bn = big_tile_cols(a, xb, wb);
+    RN_CHECK_ARG(epi != 3 || bn >= 128, "BatchNorm-backward-apply dgrad needs the 224/256-row tile");
     const bool m32 = g_tune[RN_TUNE_IGEMM_MFMA] != 1;
     // persistent tiles (rn_set_tuning 10 = workgroups, a multiple of 8): only where the grid is larger
     b.ntiles = 0;
@@ -2241,7 +2292,8 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
 #define RN_BIG(BNV, NB, M, R)                                                                                 \
   if (epi == 0) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 0, M, R>), grid, dim3(512), 0, st, b);        \
   else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 1, M, R>), grid, dim3(512), 0, st, b);   \
-  else hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 2, M, R>), grid, dim3(512), 0, st, b);
+  else if (epi == 2) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 2, M, R>), grid, dim3(512), 0, st, b);   \
+  else hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 3, M, R>), grid, dim3(512), 0, st, b);
       if (bn == 128 && bm == 224 && w4_tile(a)) {  // two 4-wave workgroups per CU
         dim3 g4((unsigned)(ceil_div(maxMc, 224) * b.ntn), 1, 1);
         const int pw = g_tune[RN_TUNE_IGEMM_PERSIST] / 8 * 16;
@@ -2255,7 +2307,8 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
           else hipLaunchKernelGGL((igemm_big_kernel<128, 1, 1, false, 224, 0, 0, 1, 1>), g4, dim3(256), 0, st, b);
         } else if (epi == 0) hipLaunchKernelGGL((igemm_big_kernel<128, 1, 0, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
         else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<128, 1, 1, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
-        else hipLaunchKernelGGL((igemm_big_kernel<128, 1, 2, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
+        else if (epi == 2) hipLaunchKernelGGL((igemm_big_kernel<128, 1, 2, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
+        else hipLaunchKernelGGL((igemm_big_kernel<128, 1, 3, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
         return rn_check_launch("igemm_big_w4");
       }
       if (a.in_sc) {  // (big_tile_cols: 224 rows, forward)
@@ -2286,7 +2339,8 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
       return rn_check_launch("igemm_big");
     }
   }
-  if (std::is_same<T, bf16_t>::value && std::is_same<OutT, float>::value && a.ncls == 1 && !a.smallc && !a.add &&
+  if (std::is_same<T, bf16_t>::value && std::is_same<OutT, float>::value && g_tune[RN_TUNE_DETERMINISTIC] != 1 &&
+      a.ncls == 1 && !a.smallc && !a.add &&
       !a.stats && !a.bnred && !a.in_sc && a.gred == 0 && a.cls[0].nr * a.cls[0].ns == 1 && a.K > 64) {
     // split-K for small grids (the FC forward: 256 x 1000 over 2048 = 16 tiles of 32 stages)
     const int64_t tiles = ceil_div(maxMc, 128) * ceil_div(a.K, 128);
@@ -2510,7 +2564,8 @@ int64_t rn_conv_bnred_blocks(const rn_conv_desc* d) {
 int rn_conv_bwd_data_bnred(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx, const void* add_src,
                            const void* bn_x, const float* bn_mean, const float* bn_scale, const float* bn_shift,
                            int32_t relu, float* part, rn_stream_t stream) {
-  RN_CHECK_ARG(d && dy && w_crsk && dx, "null argument");
+  RN_CHECK_ARG(d && dy && w_crsk && (dx || (part && !add_src)), "null argument");
+  RN_CHECK_ARG(dx || rn_conv_tile(d, 1) >= 128, "a reduction-only dgrad (dx = NULL) needs the 224/256-row tile");
   IgemmArgs a = make_igemm_args(d, 1);
   a.x = dy; a.w = w_crsk; a.y = dx; a.add = add_src; a.bias = nullptr;
   if (part) {
@@ -2524,6 +2579,18 @@ int rn_conv_bwd_data_bnred(const rn_conv_desc* d, const void* dy, const void* w_
   hipStream_t st = as_stream(stream);
   if (d->dtype == RN_BF16) return launch_igemm<bf16_t, bf16_t>(a, st);
   return launch_igemm<float, float>(a, st);
+}
+
+int rn_conv_bwd_data_bnapply(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
+                             const void* add_src, const void* bn_x, const float* coef, const float* bn_scale,
+                             const float* bn_shift, int32_t relu, rn_stream_t stream) {
+  RN_CHECK_ARG(d && dy && w_crsk && dx && bn_x && coef && bn_scale && bn_shift, "null argument");
+  RN_CHECK_ARG(d->dtype == RN_BF16 && d->c % 8 == 0 && d->c == d->c_real, "bf16, whole 8-channel chunks");
+  RN_CHECK_ARG(rn_conv_tile(d, 1) >= 128, "BatchNorm-backward-apply dgrad needs the 224/256-row tile");
+  IgemmArgs a = make_igemm_args(d, 1);
+  a.x = dy; a.w = w_crsk; a.y = dx; a.add = add_src; a.bias = nullptr;
+  a.bn_x = bn_x; a.bn_coef = coef; a.bn_sc = bn_scale; a.bn_sh = bn_shift; a.bn_relu = relu;
+  return launch_igemm<bf16_t, bf16_t>(a, as_stream(stream));
 }
 
 int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx, const void* add_src,
@@ -2574,7 +2641,10 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
   // slab bytes at streaming rates vs the slab bytes at the chip's ~1.3 TB/s atomic rate
   // the BN+ReLU input transform runs on the LDS-DMA tiles for 1x1 convolutions (wgrad_big_kernel XF)
   const bool xf_big = !in_scale || (d->r == 1 && d->s == 1 && d->pad_h == 0 && d->pad_w == 0);
-  const bool slab_ok = d->dtype == RN_BF16 && !grouped && xf_big && d->c_real == d->c;
+  // deterministic mode (rn_set_tuning 17): slabs for every kernel and dtype, never atomics
+  const bool det = g_tune[RN_TUNE_DETERMINISTIC] == 1;
+  const bool slab_ok = det || (d->dtype == RN_BF16 && !grouped && xf_big && d->c_real == d->c);
+  if (det) a.gspread = 0;  // (grouped: each diagonal block on one wave, so one writer per element)
   auto finish = [&](int64_t split, const char* what) -> int {
     const int64_t need = slab_ok ? split * a.K * (int64_t)a.ldw * 4 : 0;
     if (ws_need) *ws_need = need;
@@ -2582,14 +2652,19 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     if (rn_check_launch(what)) return -1;
     if (a.slab) {
       const int64_t n = (int64_t)a.K * a.ldw;
-      hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3(grid_for(n / 4)), dim3(256), 0, st, a.slab, (int)split, n, dw);
+      hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, a.slab, (int)split, n, dw);
       return rn_check_launch("wgrad_slab_reduce");
     }
     return 0;
   };
-  auto use_slab = [&](int64_t split) {
+  auto use_slab = [&](int64_t split) -> bool {
     const int64_t need = split * a.K * (int64_t)a.ldw * 4;
     a.slab = (slab_ok && ws && ws_bytes >= need) ? ws : nullptr;
+    if (det && !a.slab) {
+      rn_set_error("deterministic weight gradients need the split-M workspace (rn_conv_wgrad_ws_bytes)");
+      return false;
+    }
+    return true;
   };
   // 256-column, 8-wave LDS-DMA tiles (rn_set_tuning 5: 1 = on, default off) for dense bf16 layers
   // with >= 128 output channels and >= 256 columns; the M range is split so that the grid is one
@@ -2611,7 +2686,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
     split = ceil_div(a.M, a.m_per_split);
     if (!launch) return finish(split, "wgrad_dma64");
-    use_slab(split);
+    if (!use_slab(split)) return -1;
     hipLaunchKernelGGL((wgrad_big_kernel<64, 3, 128>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
     return finish(split, "wgrad_dma64");
   }
@@ -2639,7 +2714,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
     split = ceil_div(a.M, a.m_per_split);
     if (!launch) return finish(split, "wgrad_dma128");
-    use_slab(split);
+    if (!use_slab(split)) return -1;
     if (in_scale) hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128, 1>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
     return finish(split, "wgrad_dma128");
@@ -2654,7 +2729,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
     split = ceil_div(a.M, a.m_per_split);
     if (!launch) return finish(split, "wgrad_big");
-    use_slab(split);
+    if (!use_slab(split)) return -1;
     dim3 grid((unsigned)(tiles * split));
     if (in_scale) {
       if (bmk == 256) hipLaunchKernelGGL((wgrad_big_kernel<256, 2, 256, 1>), grid, dim3(512), 0, st, a);
@@ -2673,11 +2748,15 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
   // split M so that the whole grid is ONE round of resident blocks (floor: a partly filled second
   // round of long blocks is the worst tail), with >= 8 stages per block. Resident blocks per CU
   // of each tile variant (VGPR / LDS bound): 128x128 -> 2, 64x128 / 128x64 -> 3, 64x64 -> 5.
-  // (grouped: 8, measured on the ResNeXt-50 3x3 layers -- 2.08 vs 2.39 ms per step at 5, 2.23 at 3,
-  // 2.20 at 12; tools/runs/gsplit.sh)
-  int per_cu = grouped ? 8 : (bmk == 128 && bnc == 128) ? 2 : (bmk == 64 && bnc == 64) ? (in_scale ? 4 : 5) : 3;
+  // (the bf16 grouped block-diagonal-skip kernel (gdiag): 8, measured on the ResNeXt-50 3x3 layers --
+  // 2.08 vs 2.39 ms per step at 5, 2.23 at 3, 2.20 at 12; tools/runs/gsplit.sh. Other grouped
+  // variants keep the 64x64 tile's 5.) The chip size is the gfx950 constant kSplitCus, not a device
+  // query: rn_conv_wgrad_ws_bytes sizes the slab workspace from this same split at plan time, possibly
+  // on a host without a GPU, and the launch must agree with it.
+  constexpr int kSplitCus = 256;
+  int per_cu = (grouped && a.gdiag) ? 8 : (bmk == 128 && bnc == 128) ? 2 : (bmk == 64 && bnc == 64) ? (in_scale ? 4 : 5) : 3;
   if (g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU] > 0) per_cu = g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU];
-  int64_t want = std::max<int64_t>(1, (int64_t)per_cu * 256 / tiles);
+  int64_t want = std::max<int64_t>(1, (int64_t)per_cu * kSplitCus / tiles);
   int64_t maxsplit = std::max<int64_t>(1, mstages / 8);
   int64_t split = std::min(want, maxsplit);
   int64_t stages_per = ceil_div(mstages, split);
@@ -2686,7 +2765,14 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
   a.nct = (int)ceil_div(a.ncol_load, bnc);
   a.nkt = (int)ceil_div(a.K, bmk);
   dim3 grid((unsigned)(a.nct * a.nkt * split));
-  if (!launch) return 0;
+  if (det) {  // this register-staged kernel stores slabs only in the deterministic mode
+    if (!launch) return finish(split, "wgrad");
+    if (!use_slab(split)) return -1;
+  } else {
+    if (ws_need) *ws_need = 0;
+    if (!launch) return 0;
+    a.slab = nullptr;
+  }
   if (grouped) {
     if (d->dtype == RN_BF16 && a.gdiag)
       hipLaunchKernelGGL((wgrad_kernel<bf16_t, RN_GROUP_BLOCK, RN_GROUP_BLOCK, false, true>), grid, dim3(256), 0, st, a);
@@ -2701,6 +2787,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     if (in_scale) launch_wgrad_tiles<float, true>(bmk, bnc, grid, st, a);
     else launch_wgrad_tiles<float, false>(bmk, bnc, grid, st, a);
   }
+  if (det) return finish(split, "wgrad");
   return rn_check_launch("wgrad");
 }
 }  // namespace

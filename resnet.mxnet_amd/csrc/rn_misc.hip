@@ -519,7 +519,7 @@ __global__ void quant_bwd_kernel(int64_t n, const T* __restrict__ x, const T* __
 
 }  // namespace
 
-int g_tune[RN_TUNE_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512, 0, 0, 0, 0};
+int g_tune[RN_TUNE_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512, 0, 0, 0, 0, 0, 0, 0};
 
 extern "C" {
 

@@ -93,7 +93,9 @@ class ImageRecordIter(DataIter):
             offs = rec.scan_offsets()
         rec.close()
         self.path = path_imgrec
-        # MXNet splits the input into num_parts contiguous parts (InputSplit); part_index reads one
+        # MXNet splits the input into num_parts contiguous parts (InputSplit); part_index reads one.
+        # The split here is by record count; MXNet's InputSplit cuts by bytes and moves each cut to the
+        # next record boundary, so parts can differ by a few records (sharding parity unpinned)
         n = len(offs)
         a, b = n * int(part_index) // int(num_parts), n * (int(part_index) + 1) // int(num_parts)
         self.offsets = offs[a:b]
@@ -134,8 +136,10 @@ class ImageRecordIter(DataIter):
         while len(self._pending) < self.prefetch and self._cursor < len(self._order):
             idx = self._order[self._cursor:self._cursor + self.batch_size]
             pad = self.batch_size - len(idx)
-            if pad:  # the last batch is filled from the first records; `pad` counts them
+            if pad and self.round_batch:  # the last batch is filled from the first records; `pad` counts them
                 idx = np.concatenate([idx, np.resize(self._order, pad)])
+            # round_batch=False: the last batch keeps only its own records, the `pad` slots are zeros
+            # (MXNet's BatchLoader leaves them unfilled and reports the same pad)
             self._cursor += self.batch_size
             self._pending.append(self._prefetcher.submit(self._make_batch, idx, pad, self._batch_no))
             self._batch_no += 1
@@ -156,8 +160,8 @@ class ImageRecordIter(DataIter):
 
     def _make_batch(self, idx, pad, batch_no):
         c, h, w = self.data_shape
-        data = np.empty((self.batch_size, c, h, w), dtype=np.float32)
-        label = np.empty((self.batch_size, self.label_width), dtype=np.float32)
+        data = np.zeros((self.batch_size, c, h, w), dtype=np.float32)
+        label = np.zeros((self.batch_size, self.label_width), dtype=np.float32)
 
         def one(i):
             r = self._reader()

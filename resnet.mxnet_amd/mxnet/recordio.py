@@ -206,19 +206,25 @@ def unpack(s):
 
 
 def pack_img(header, img, quality=95, img_fmt=".jpg"):
-    """IRHeader + HWC uint8 image (RGB, or 2-D gray) -> record bytes, encoded by PIL."""
+    """IRHeader + HWC uint8 image -> record bytes, encoded by PIL. As MXNet's (cv2.imencode), a
+    3-channel image is taken in BGR order (2-D: gray); the file stores it as a normal RGB image."""
     from PIL import Image
     buf = io.BytesIO()
     fmt = {".jpg": "JPEG", ".jpeg": "JPEG", ".png": "PNG"}[img_fmt.lower()]
     kw = {"quality": int(quality)} if fmt == "JPEG" else {"compress_level": 1}
-    Image.fromarray(np.asarray(img, dtype=np.uint8)).save(buf, format=fmt, **kw)
+    a = np.asarray(img, dtype=np.uint8)
+    if a.ndim == 3 and a.shape[2] == 3:
+        a = np.ascontiguousarray(a[:, :, ::-1])  # BGR -> RGB for the encoder
+    Image.fromarray(a).save(buf, format=fmt, **kw)
     return pack(header, buf.getvalue())
 
 
 def unpack_img(s, iscolor=-1):
-    """record bytes -> (IRHeader, HWC uint8 RGB image; 2-D for iscolor=0)."""
+    """record bytes -> (IRHeader, HWC uint8 image in BGR order as MXNet's cv2.imdecode; 2-D gray for
+    iscolor=0). (ImageRecordIter decodes to RGB itself, as MXNet's iterator does.)"""
     from PIL import Image
     header, s = unpack(s)
     im = Image.open(io.BytesIO(s))
-    im = im.convert("L" if iscolor == 0 else "RGB")
-    return header, np.asarray(im)
+    if iscolor == 0:
+        return header, np.asarray(im.convert("L"))
+    return header, np.ascontiguousarray(np.asarray(im.convert("RGB"))[:, :, ::-1])

@@ -925,7 +925,9 @@ class Executor:
                 hp = max(x.h + 2 * op.pad[0], (dfull.p - 1) * op.stride[0] + 8)
                 wp = max(x.w + 2 * op.pad[1], (dfull.q - 1) * op.stride[1] + 8)
                 op.p4 = None
+                # (the NHWC4 stem's weight gradient adds with atomics: not in the deterministic mode)
                 if self.dtype == BF16 and not op.quant and os.environ.get("RN_STEM_P4", "1") == "1" and \
+                        os.environ.get("RN_DETERMINISTIC", "0") != "1" and \
                         self.lib.rn_stem_p4_supported(L.C.byref(dfull), hp, wp):
                     op.p4 = (hp, wp)
                     op.x8 = self._zeros(x.n * hp * wp * 4, self.tdtype)
@@ -1199,6 +1201,18 @@ class Executor:
                               self.wgrad_ws_bytes, sp)
         return self._call("rn_conv_bwd_filter", L.C.byref(d), x, dy, dw, sp)
 
+    def _bn_recompute_ok(self, op, cop, cadd):
+        """May the BatchNorm `op`, whose output gradient the data gradient of conv `cop` completes, take
+        its backward from a recomputed dgrad (rn_conv_bwd_data_bnapply)? Where that dgrad is cheap: bf16,
+        a dense 1x1 stride-1 convolution reducing over at most half the BN's channels (the
+        pre-activation units' conv1, symbol/resnet.py:17-20), the only writer of the gradient (no fan-in
+        add), on the 224/256-row tile."""
+        d = cop.desc
+        return (self.dtype == L.RN_BF16 and cadd is None and d.groups <= 1 and d.r == 1 and d.s == 1
+                and d.stride_h == 1 and d.stride_w == 1 and d.pad_h == 0 and d.pad_w == 0 and 2 * d.k <= d.c
+                and d.c == d.c_real and d.c % 8 == 0 and op.y.c == d.c
+                and int(self.lib.rn_conv_tile(L.C.byref(d), 1)) >= 128)
+
     def _build_backward(self):
         plan = self.plan
         sp = self._sp()
@@ -1212,6 +1226,9 @@ class Executor:
                 op.pre_part = None  # set by the residual add's fused ReLU backward (this build)
         bwd_fusion = os.environ.get("RN_BN_BWD_FUSION", "1") in ("1", "2")
         bwd_all = os.environ.get("RN_BN_BWD_FUSION", "1") == "2"
+        # BN backward applied by a recomputed cheap dgrad (rn_conv_bwd_data_bnapply), opt-in
+        # (RN_BN_BWD_RECOMPUTE=1): bit-identical, but measured 22.18 vs 21.45 ms per step
+        recompute = os.environ.get("RN_BN_BWD_RECOMPUTE", "0") == "1"
         # one workspace for the weight gradients' split-M partial tiles (rn_conv_bwd_filter_ws),
         # sized for the largest layer. Shared safely because every call using it is a weight-gradient
         # call, and those all run in plan order on ONE stream (the side stream when it is on:
@@ -1220,6 +1237,9 @@ class Executor:
         if os.environ.get("RN_WGRAD_SLAB", "1") == "1":
             need = [int(self.lib.rn_conv_wgrad_ws_bytes(L.C.byref(op.desc))) for op in plan.ops
                     if op.kind in ("conv", "fc") and getattr(op, "desc", None) is not None]
+            # (the stem's weight gradient; it needs a slab only in the deterministic mode)
+            need += [int(self.lib.rn_conv_wgrad_ws_bytes(L.C.byref(op.dfull))) for op in plan.ops
+                     if op.kind == "stem" and not op.p4]
             self.wgrad_ws_bytes = max(need + [0])
             if self.wgrad_ws_bytes > 0:
                 self.wgrad_ws = self._zeros(self.wgrad_ws_bytes // 4, self.torch.float32)
@@ -1266,8 +1286,7 @@ class Executor:
                     self._bwd.append(self._call("rn_stem_conv_wgrad_p4", L.C.byref(op.dfull), self._p(op.x8),
                                                 self._p(dy), self._gp(op.weight), op.p4[0], op.p4[1], sp))
                 else:
-                    self._bwd.append(self._call("rn_conv_bwd_filter", L.C.byref(op.dfull), self._p(op.x8),
-                                                self._p(dy), self._gp(op.weight), sp))
+                    self._bwd.append(self._wgrad_call(op.dfull, self._p(op.x8), self._p(dy), self._gp(op.weight), sp))
                 self.param_done_at[op.weight] = len(self._bwd)
                 if op.bn:
                     self._bwd.append(self._call("rn_stem_shift_grad", L.C.byref(op.dfull), self._p(dy),
@@ -1296,13 +1315,30 @@ class Executor:
                     _, ci, cop, cdy, cout, cadd = w
                     op.bnred_blocks = int(self.lib.rn_conv_bnred_blocks(L.C.byref(cop.desc)))
                     op.bnred = self._zeros(op.bnred_blocks * op.y.cp * 2, self.torch.float32)
-                    self._bwd[ci] = self._call("rn_conv_bwd_data_bnred", L.C.byref(cop.desc), self._p(cdy),
-                                               self._p(cop.wc), self._p(cout), self._p(cadd), self._p(self.act(x)),
-                                               op.sm, op.sc, op.sh, int(op.relu), self._p(op.bnred), sp)
-                    self._bwd.append(self._call("rn_bn_bwd_part", L.C.byref(op.desc), self._p(op.bnred),
-                                                op.bnred_blocks, self._p(self.act(x)), self._p(dy), self._p(out),
-                                                self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc, op.sh,
-                                                self._gp(op.gamma), self._gp(op.beta), wsp, sp))
+                    if recompute and self._bn_recompute_ok(op, cop, cadd):
+                        # the dgrad is cheap (1x1, reduction over fewer channels than the BN has): pass 1
+                        # only reduces (its BN-width output is never written), finalize, then the same
+                        # dgrad recomputed with the BN backward applied in its epilogue (bit-identical)
+                        op.coef = self._zeros(4 * op.y.cp, self.torch.float32)
+                        self._bwd[ci] = self._call("rn_conv_bwd_data_bnred", L.C.byref(cop.desc), self._p(cdy),
+                                                   self._p(cop.wc), None, None, self._p(self.act(x)), op.sm, op.sc,
+                                                   op.sh, int(op.relu), self._p(op.bnred), sp)
+                        self._bwd.append(self._call("rn_bn_bwd_finalize", L.C.byref(op.desc), self._p(op.bnred),
+                                                    op.bnred_blocks, self._pp(op.gamma), op.sm, op.si,
+                                                    self._gp(op.gamma), self._gp(op.beta), self._p(op.coef), sp))
+                        self._bwd.append(self._call("rn_conv_bwd_data_bnapply", L.C.byref(cop.desc), self._p(cdy),
+                                                    self._p(cop.wc), self._p(out), self._p(add), self._p(self.act(x)),
+                                                    self._p(op.coef), op.sc, op.sh, int(op.relu), sp))
+                        op.recomputed = True
+                    else:
+                        self._bwd[ci] = self._call("rn_conv_bwd_data_bnred", L.C.byref(cop.desc), self._p(cdy),
+                                                   self._p(cop.wc), self._p(cout), self._p(cadd),
+                                                   self._p(self.act(x)), op.sm, op.sc, op.sh, int(op.relu),
+                                                   self._p(op.bnred), sp)
+                        self._bwd.append(self._call("rn_bn_bwd_part", L.C.byref(op.desc), self._p(op.bnred),
+                                                    op.bnred_blocks, self._p(self.act(x)), self._p(dy), self._p(out),
+                                                    self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc, op.sh,
+                                                    self._gp(op.gamma), self._gp(op.beta), wsp, sp))
                 elif getattr(op, "pre_part", None) is not None:
                     # the reduction was done by the residual add's ReLU backward (rn_relu_bwd_bnred)
                     self._bwd.append(self._call("rn_bn_bwd_part", L.C.byref(op.desc), self._p(op.pre_part),

@@ -52,6 +52,8 @@ SIGNATURES = {
     "rn_conv_bwd_data_bnred": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P, _P]),
     "rn_conv_bnred_blocks": (_i64, [_P]),
     "rn_bn_bwd_part": (_i32, [_P, _P, _i64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "rn_bn_bwd_finalize": (_i32, [_P, _P, _i64, _P, _P, _P, _P, _P, _P, _P]),
+    "rn_conv_bwd_data_bnapply": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P]),
     "rn_conv_bwd_data": (_i32, [_P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_filter": (_i32, [_P, _P, _P, _P, _P]),
     "rn_conv_wgrad_ws_bytes": (_i64, [_P]),
@@ -135,6 +137,9 @@ def load(auto_build=True):
         fn.restype = res
         fn.argtypes = args
     _lib = lib
+    # RN_DETERMINISTIC=1: bitwise reproducible weight gradients (rn_set_tuning 17)
+    if os.environ.get("RN_DETERMINISTIC", "0") == "1":
+        check(lib.rn_set_tuning(17, 1), "rn_set_tuning")
     # RN_TUNE="key=value,..." selects kernel variants (rn_set_tuning; A/B measurements)
     for kv in filter(None, os.environ.get("RN_TUNE", "").split(",")):
         k, v = kv.split("=")

@@ -44,9 +44,9 @@ def p(t):
     return None if t is None else C.c_void_p(t.data_ptr())
 
 
-def conv_desc(dtype, n, c, h, w, k, r, s, stride, pad, c_real=None):
+def conv_desc(dtype, n, c, h, w, k, r, s, stride, pad, c_real=None, groups=1):
     d = L.ConvDesc(dtype=dtype, n=n, h=h, w=w, c=pad8(c) if c_real is None else c, c_real=c if c_real is None else c_real,
-                   k=k, k_pad=pad8(k), r=r, s=s, stride_h=stride, stride_w=stride, pad_h=pad, pad_w=pad, groups=1)
+                   k=k, k_pad=pad8(k), r=r, s=s, stride_h=stride, stride_w=stride, pad_h=pad, pad_w=pad, groups=groups)
     L.call("rn_conv_desc_init", C.byref(d))
     return d
 

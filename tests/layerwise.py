@@ -320,7 +320,28 @@ class Checker:
         return self._dgrad(args, state)
 
     def _h_rn_conv_bwd_data_bnred(self, args, state):
+        if args[3] is None:  # reduction only (the first pass of the recompute): nothing stored; its partials
+            return None, (lambda: None)  # are checked through dgamma / dbeta / dx of the apply below
         return self._dgrad(args, state, bnred=True)
+
+    def _h_rn_bn_bwd_finalize(self, args, state):
+        return None, (lambda: None)  # (dgamma / dbeta: checked after rn_conv_bwd_data_bnapply)
+
+    def _h_rn_conv_bwd_data_bnapply(self, args, state):
+        """the dgrad recomputed with the BN backward applied: dx vs the fp32 dgrad of the device's dy,
+        rounded to bf16 as rn_conv_bwd_data would store it, through the BN(+ReLU) backward (+ add)."""
+        if not hasattr(self, "bn_by_sm_x"):
+            self.bn_by_sm_x = {self.ex.act(op.x).data_ptr(): op for op in self.ex.plan.ops if op.kind == "bn"}
+        d = args[0]._obj
+        dyp, wcp, dxp, addp, xp = args[1], args[2], args[3], args[4], args[5]
+        cop, op = self.wc_op[wcp.value], self.bn_by_sm_x[xp.value]
+
+        def post():
+            dy = self.nchw(self.t(dyp), d.n, d.p, d.q, d.k_pad, d.k)
+            w = self.w_from_crsk(cop.wc, d)
+            g = ref_dgrad(dy, w, (d.h, d.w), (d.stride_h, d.stride_w), (d.pad_h, d.pad_w))
+            self._bn_bwd_check(op, _bf16(g).double(), state.get("add"), dxp)
+        return (self._snap(addp, state, "add") if addp is not None else None), post
 
     def _wgrad(self, args, state, xf=False, p4=False):
         d = args[0]._obj
@@ -378,38 +399,43 @@ class Checker:
 
         def post():
             t = op.x
-            c = t.c
-            sm, si, sc, sh = self.bn_coefs(op)
-            x = self.act_nchw(t).double()
-            dy = self.nchw(self.t(dyp), t.n, t.h, t.w, t.cp, c).double()
-            mu, inv = sm[:c].double().view(1, c, 1, 1), si[:c].double().view(1, c, 1, 1)
-            dz = dy
-            if op.relu:
-                dz = dy * ((x * sc[:c].double().view(1, c, 1, 1) + sh[:c].double().view(1, c, 1, 1)) > 0)
-            xc = x - mu
-            m = t.n * t.h * t.w
-            s = dz.sum(dim=(0, 2, 3))
-            q = (dz * xc).sum(dim=(0, 2, 3))
-            g = torch.ones(c, device=x.device, dtype=torch.float64) if op.fix_gamma else \
-                self.param(op.gamma).double()
-            gi = (g.view(1, c, 1, 1) * inv)
-            # dx = g*invstd*(dz - mean(dz) - xhat*mean(dz*xhat)), xhat = (x - mean)*invstd
-            dx = gi * (dz - (s / m).view(1, c, 1, 1)) - gi * inv * inv * (q / m).view(1, c, 1, 1) * xc
-            if state.get("add") is not None:
-                dx = dx + self.nchw(state["add"], t.n, t.h, t.w, t.cp, c).double()
-            if dxp is not None:
-                dev = self.nchw(self.t(dxp), t.n, t.h, t.w, t.cp, c)
-                self.add("bn_bwd_dx", op.name, dev, dx, BF16_BAR if self.ex.dtype == 0 else F32_BAR)
-            # fp32 sums: bounded by the sum of the magnitudes of their terms
-            sa = dz.abs().sum(dim=(0, 2, 3))
-            qa = (dz * xc).abs().sum(dim=(0, 2, 3)) * inv.view(-1)
-            db = self.ex.gview(op.beta)[:c].double()
-            mb = {"dbeta": float(((db - s).abs() / (sa + 1e-30)).max())}
-            if not op.fix_gamma:
-                dgv = self.ex.gview(op.gamma)[:c].double()
-                mb["dgamma"] = float(((dgv - q * inv.view(-1)).abs() / (qa + 1e-30)).max())
-            self.add_metric("bn_bwd_params", op.name, mb, {k: 1e-5 for k in mb})
+            self._bn_bwd_check(op, self.nchw(self.t(dyp), t.n, t.h, t.w, t.cp, t.c).double(), state.get("add"), dxp)
         return (self._snap(addp, state, "add") if addp is not None else None), post
+
+    def _bn_bwd_check(self, op, dy, add, dxp):
+        """BN(+ReLU) backward of `op` from its output gradient dy (fp64, NCHW): dx (+ add) vs the device's
+        dxp, dgamma / dbeta vs the gradient buffers."""
+        t = op.x
+        c = t.c
+        sm, si, sc, sh = self.bn_coefs(op)
+        x = self.act_nchw(t).double()
+        mu, inv = sm[:c].double().view(1, c, 1, 1), si[:c].double().view(1, c, 1, 1)
+        dz = dy
+        if op.relu:
+            dz = dy * ((x * sc[:c].double().view(1, c, 1, 1) + sh[:c].double().view(1, c, 1, 1)) > 0)
+        xc = x - mu
+        m = t.n * t.h * t.w
+        s = dz.sum(dim=(0, 2, 3))
+        q = (dz * xc).sum(dim=(0, 2, 3))
+        g = torch.ones(c, device=x.device, dtype=torch.float64) if op.fix_gamma else \
+            self.param(op.gamma).double()
+        gi = (g.view(1, c, 1, 1) * inv)
+        # dx = g*invstd*(dz - mean(dz) - xhat*mean(dz*xhat)), xhat = (x - mean)*invstd
+        dx = gi * (dz - (s / m).view(1, c, 1, 1)) - gi * inv * inv * (q / m).view(1, c, 1, 1) * xc
+        if add is not None:
+            dx = dx + self.nchw(add, t.n, t.h, t.w, t.cp, c).double()
+        if dxp is not None:
+            dev = self.nchw(self.t(dxp), t.n, t.h, t.w, t.cp, c)
+            self.add("bn_bwd_dx", op.name, dev, dx, BF16_BAR if self.ex.dtype == 0 else F32_BAR)
+        # fp32 sums: bounded by the sum of the magnitudes of their terms
+        sa = dz.abs().sum(dim=(0, 2, 3))
+        qa = (dz * xc).abs().sum(dim=(0, 2, 3)) * inv.view(-1)
+        db = self.ex.gview(op.beta)[:c].double()
+        mb = {"dbeta": float(((db - s).abs() / (sa + 1e-30)).max())}
+        if not op.fix_gamma:
+            dgv = self.ex.gview(op.gamma)[:c].double()
+            mb["dgamma"] = float(((dgv - q * inv.view(-1)).abs() / (qa + 1e-30)).max())
+        self.add_metric("bn_bwd_params", op.name, mb, {k: 1e-5 for k in mb})
 
     def _h_rn_bn_bwd_part(self, args, state):
         return self._bn_bwd(args, state, True)

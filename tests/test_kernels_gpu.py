@@ -809,6 +809,89 @@ def test_dgrad_bn_backward_fusion(gpu, dtype, case, big_tiles, tile_variant):
     assert rel_err(from_nhwc(dx, c), dx_ref) < (TOL[dtype] * 5 if dtype == F32 else 3e-2)
 
 
+@pytest.mark.parametrize("relu,fix_gamma,with_add", [(1, 0, 0), (1, 0, 1), (0, 1, 1)])
+@pytest.mark.parametrize("case", [(2, 256, 14, 14, 64, 1, 1, 0), (3, 512, 9, 11, 128, 1, 1, 0),
+                                  (2, 1024, 7, 7, 256, 1, 1, 0), (4, 256, 28, 28, 64, 1, 1, 0)])
+def test_dgrad_bn_backward_recompute(gpu, case, relu, fix_gamma, with_add, big_tiles, tile_variant):
+    """rn_conv_bwd_data_bnred (dx = NULL: reduction only) + rn_bn_bwd_finalize + rn_conv_bwd_data_bnapply
+    (the dgrad recomputed with the BatchNorm backward applied in its epilogue) == rn_conv_bwd_data_bnred +
+    rn_bn_bwd_part, bit for bit (dx, dgamma, dbeta), and == the oracle's conv dgrad + BN(+ReLU) backward
+    within bf16 tolerance. The pre-activation units' conv1 (1x1, the BN has 4x the conv's channels)."""
+    n, c, h, w, k, r, st, pd = case
+    rng = np.random.default_rng(21)
+    xb = bf16_round(rng.standard_normal((n, c, h, w)) * 1.5 + 0.3)  # BN input
+    gamma, beta = rng.uniform(0.5, 1.5, c), rng.standard_normal(c) * 0.2
+    a_ref, cache = ops.bn_train_fwd(xb, gamma, beta, 1e-5, bool(fix_gamma))
+    act = ops.relu_fwd(a_ref) if relu else a_ref
+    wt = bf16_round(rng.standard_normal((k, c, r, r)) / np.sqrt(c * r * r))
+    dy = bf16_round(rng.standard_normal((n, k, h, w)))
+    res = bf16_round(rng.standard_normal((n, c, h, w)) * 0.5)      # the gradient fan-in (add_src of the apply)
+    dact_ref, _ = ops.conv2d_bwd(act, wt, dy, (1, 1), (0, 0))
+    dz = ops.relu_bwd(bf16_round(dact_ref), act) if relu else bf16_round(dact_ref)
+    dx_ref, dg_ref, db_ref = ops.bn_train_bwd(dz, cache, bool(fix_gamma))
+    if with_add:
+        dx_ref = dx_ref + res
+
+    d = conv_desc(BF16, n, c, h, w, k, 1, 1, 1, 0)
+    lib = L.load()
+    if lib.rn_conv_tile(C.byref(d), 1) < 128:
+        pytest.skip("not a 224/256-row dgrad tile under this variant")
+    wc = torch.zeros(d.c * d.k_pad, dtype=torch.bfloat16, device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), None, p(wc), stream())
+    bd = L.BNDesc(dtype=BF16, m=n * h * w, c=d.c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=fix_gamma, relu=relu)
+    f = lambda a: torch.tensor(np.asarray(a, np.float64), dtype=torch.float32, device=gpu)
+    g_d, b_d, mm, mv = f(gamma), f(beta), f(np.zeros(c)), f(np.ones(c))
+    sm, si, sc, sh = [torch.zeros(d.c, dtype=torch.float32, device=gpu) for _ in range(4)]
+    ws = torch.zeros(lib.rn_bn_workspace_bytes(C.byref(bd)) // 4 + 16, dtype=torch.float32, device=gpu)
+    xbd = to_nhwc(xb, BF16, gpu)
+    L.call("rn_bn_fwd_train", C.byref(bd), p(xbd), None, p(g_d), p(b_d), p(mm), p(mv), p(sm), p(si), p(sc), p(sh),
+           p(ws), stream())
+    dyd, resd = to_nhwc(dy, BF16, gpu), to_nhwc(res, BF16, gpu)
+    add = resd if with_add else None
+    nrb = lib.rn_conv_bnred_blocks(C.byref(d))
+    zf = lambda: torch.zeros(d.c, dtype=torch.float32, device=gpu)
+    # reference path: the dgrad stores its gradient, rn_bn_bwd_part reads it back
+    part0 = torch.full((nrb * d.c * 2,), float("nan"), dtype=torch.float32, device=gpu)
+    dact = torch.zeros_like(xbd)
+    L.call("rn_conv_bwd_data_bnred", C.byref(d), p(dyd), p(wc), p(dact), None, p(xbd), p(sm), p(sc), p(sh), relu,
+           p(part0), stream())
+    dx0, dg0, db0 = torch.zeros_like(xbd), zf(), zf()
+    L.call("rn_bn_bwd_part", C.byref(bd), p(part0), nrb, p(xbd), p(dact), p(dx0), p(add), p(g_d), p(sm), p(si),
+           p(sc), p(sh), p(dg0), p(db0), p(ws), stream())
+    # recompute path
+    part1 = torch.full((nrb * d.c * 2,), float("nan"), dtype=torch.float32, device=gpu)
+    L.call("rn_conv_bwd_data_bnred", C.byref(d), p(dyd), p(wc), None, None, p(xbd), p(sm), p(sc), p(sh), relu,
+           p(part1), stream())
+    coef = torch.zeros(4 * d.c, dtype=torch.float32, device=gpu)
+    dg1, db1 = zf(), zf()
+    L.call("rn_bn_bwd_finalize", C.byref(bd), p(part1), nrb, p(g_d), p(sm), p(si), p(dg1), p(db1), p(coef), stream())
+    dx1 = torch.full_like(xbd, float("nan"))
+    L.call("rn_conv_bwd_data_bnapply", C.byref(d), p(dyd), p(wc), p(dx1), p(add), p(xbd), p(coef), p(sc), p(sh),
+           relu, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(part0, part1)
+    assert torch.equal(dg0, dg1) and torch.equal(db0, db1)
+    assert torch.equal(dx0.view(torch.int16), dx1.view(torch.int16))
+    assert rel_err(from_nhwc(dx1, c), dx_ref) < 3e-2
+    assert rel_err(db1.cpu().numpy()[:c], db_ref) < 2e-2
+    if not fix_gamma:
+        assert rel_err(dg1.cpu().numpy()[:c], dg_ref) < 2e-2
+
+
+def test_dgrad_bn_backward_recompute_args(gpu):
+    """The reduction-only dgrad and the apply dgrad need the 224/256-row tile (bf16): the fp32 path
+    and a missing output are refused with an error, not run."""
+    d32 = conv_desc(F32, 2, 256, 14, 14, 64, 1, 1, 1, 0)
+    lib = L.load()
+    x = torch.zeros(8, device=gpu)
+    assert lib.rn_conv_bwd_data_bnapply(C.byref(d32), p(x), p(x), p(x), None, p(x), p(x), p(x), p(x), 1,
+                                        stream()) != 0
+    assert lib.rn_conv_bwd_data_bnred(C.byref(d32), p(x), p(x), None, None, p(x), p(x), p(x), p(x), 1, p(x),
+                                      stream()) != 0
+    assert lib.rn_conv_bwd_data_bnred(C.byref(d32), p(x), p(x), None, None, None, None, None, None, 1, None,
+                                      stream()) != 0
+
+
 BIG_CASES = [
     # n, c, h, w, k, r, stride, pad: 256-row tiles (fwd when k >= 128, dgrad when c >= 128)
     (2, 128, 14, 14, 256, 3, 1, 1),

@@ -22,6 +22,7 @@ import socket
 
 import numpy as np
 import pytest
+import torch
 
 pytestmark = pytest.mark.gpu
 
@@ -70,6 +71,9 @@ def _step(sym, data, label, reducer_bucket_bytes=None, steps=2):
             ex.forward(is_train=True)
             ex.backward()
             plain.append(ex.grad.float().cpu().numpy().copy())
+            # the update must consume the ALL-REDUCED buffer (the rerun overwrote ex.grad): put it back,
+            # so the post-update weights checked below come from the hooked path
+            ex.grad.copy_(torch.from_numpy(grads[-1]).to(ex.grad.device, ex.grad.dtype))
         mod.update()
         if step == 0:
             first_args = {k: v.asnumpy().copy() for k, v in mod.get_params()[0].items()}

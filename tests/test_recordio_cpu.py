@@ -30,7 +30,8 @@ def _write_rec(path, imgs, fmt=".png", labels=None):
     w = recordio.MXIndexedRecordIO(str(path) + ".idx", str(path), "w")
     for i, im in enumerate(imgs):
         lab = float(i) if labels is None else labels[i]
-        w.write_idx(i, recordio.pack_img(recordio.IRHeader(0, lab, i, 0), im, img_fmt=fmt))
+        # pack_img takes BGR (MXNet's cv2 convention): the file then holds `im` as RGB
+        w.write_idx(i, recordio.pack_img(recordio.IRHeader(0, lab, i, 0), im[:, :, ::-1], img_fmt=fmt))
     w.close()
 
 
@@ -96,6 +97,31 @@ def test_pack_img_png_exact():
     img = _images(1, 3)[0]
     h, out = recordio.unpack_img(recordio.pack_img(recordio.IRHeader(0, 5.0, 1, 0), img, img_fmt=".png"))
     assert h.label == 5.0 and np.array_equal(out, img)
+
+
+def test_pack_img_channel_order_bgr():
+    """pack_img / unpack_img use MXNet's (OpenCV's) BGR order: a BGR blue pixel (255, 0, 0) is stored
+    as RGB (0, 0, 255), and the iterator (RGB, as MXNet's ImageRecordIter) reads it as blue."""
+    bgr = np.zeros((4, 4, 3), np.uint8)
+    bgr[..., 0] = 255
+    rec = recordio.pack_img(recordio.IRHeader(0, 0.0, 0, 0), bgr, img_fmt=".png")
+    _, payload = recordio.unpack(rec)
+    rgb = np.asarray(Image.open(io.BytesIO(payload)).convert("RGB"))
+    assert (rgb[..., 2] == 255).all() and (rgb[..., :2] == 0).all()
+    assert np.array_equal(recordio.unpack_img(rec)[1], bgr)
+    assert recordio.unpack_img(rec, iscolor=0)[1].ndim == 2
+
+
+def test_round_batch_false_pads_with_zeros(tmp_path):
+    """round_batch=False: the last batch holds only its own records; its pad slots are zeros."""
+    path = tmp_path / "rb.rec"
+    _write_rec(path, _images(5, 4))
+    it = mx.io.ImageRecordIter(path_imgrec=str(path), data_shape=(3, 24, 24), batch_size=4, resize=24,
+                               round_batch=False)
+    b = list(it)
+    assert [x.pad for x in b] == [0, 3]
+    last = b[1].data[0].asnumpy()
+    assert b[1].label[0].asnumpy()[0] == 4.0 and not last[1:].any() and last[0].any()
 
 
 MEAN = np.array([123.68, 116.28, 103.53])
