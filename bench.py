@@ -31,6 +31,10 @@ for _p in (REPO, os.path.join(REPO, "resnet.mxnet_amd")):
         sys.path.insert(0, _p)
 
 METRIC = "images/sec/GPU ResNet-50 224px bf16 bs256; 1→8 GPU scaling"
+# the other BASELINE configs (C4, C5) are reported under their own names, never as the headline metric
+MODEL_METRIC = {"resnet50": METRIC,
+                "resnext50": "images/sec/GPU ResNeXt-50 32x4d 224px bf16 bs256 (BASELINE C4)",
+                "resnet50_int8": "images/sec/GPU ResNet-50 int8 QAT 224px (int8 fwd, bf16 bwd) bs256 (BASELINE C5)"}
 PEAK_BF16_TFLOPS = 2500.0
 PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md: 8 TB/s spec (6.3 TB/s achievable)
 RIDGE = PEAK_BF16_TFLOPS * 1e12 / (PEAK_HBM_GBS * 1e9)  # 312.5 FLOP/B: below it a kernel is HBM-bound
@@ -482,9 +486,12 @@ def main():
         solo_tf = per_launch_flops / (solo_ms * 1e-3) / 1e12
         solo_gbs = alg_bytes / (solo_ms * 1e-3) / 1e9
         out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "images/sec", "n_gpus": world,
+            "metric": MODEL_METRIC[a.model], "value": round(value, 2), "unit": "images/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if a.precision.startswith("bf") else "fp32",
+            "scaling": "weak", "vs_baseline": None,
+            # the int8 graph multiplies int8 codes on int8 MFMAs forward; its backward (STE) runs in bf16
+            "dtype": ("int8 fwd / bf16 bwd" if a.model == "resnet50_int8" else "bf16") if a.precision.startswith("bf")
+            else "fp32",
             "data": "synthetic (seeded U(-1,1) %dx%d images, random labels; Xavier-init %s)" % (
                 a.image, a.image, workload.split(" (")[0]),
             "config": {"workload": "%s train step, batch %d/GPU, %dx%d" % (

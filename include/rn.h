@@ -99,6 +99,12 @@ int rn_conv_weight_pack_i8(const rn_conv_desc* d, const float* w_master, const f
 int rn_conv_bwd_data_bnred(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx, const void* add_src,
                            const void* bn_x, const float* bn_mean, const float* bn_scale, const float* bn_shift,
                            int32_t relu, float* part, rn_stream_t stream);
+/* rn_conv_bwd_data_bnred whose BN output feeds a Quantization_int8 (rn_bn_desc.clip): the reduction's
+ * dz also carries the quantizer's straight-through clip, dz = dx * [y > 0] * [y < *clip]. */
+int rn_conv_bwd_data_bnred_clip(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
+                                const void* add_src, const void* bn_x, const float* bn_mean, const float* bn_scale,
+                                const float* bn_shift, int32_t relu, const float* clip, float* part,
+                                rn_stream_t stream);
 /* The BatchNorm(+ReLU) backward of the BN whose output gradient this convolution's data gradient is,
  * APPLIED in the epilogue to the recomputed gradient: dx = A (dz - mean(dz)) - A2 (x - mean)
  * (+ add_src), dz = g relu'(x scale + shift) (relu != 0), g = conv_transpose(dy, w) rounded as
@@ -199,6 +205,11 @@ typedef struct rn_bn_desc {
   float momentum;    /* moving = moving*momentum + batch*(1-momentum)         */
   int32_t fix_gamma; /* gamma := 1, dgamma := 0                                */
   int32_t relu;      /* fuse Activation(relu) on the output                   */
+  /* nullable (backward only, with relu): device pointer to the threshold t of the Quantization_int8
+   * that alone consumes this BN's output (the int8 graph, symbol/resnet_int8.py via int8_api.py:
+   * 133-136). Its straight-through backward (clip_grad_quantization_int8.py: zero where |y| >= t) is
+   * folded into this BN's backward: dz = dy * [y > 0] * [y < t], y = the output as stored. */
+  const float* clip;
 } rn_bn_desc;
 
 /* Workspace (bytes) needed by rn_bn_fwd_train / rn_bn_bwd. */

@@ -43,6 +43,13 @@ Geo make_geo(int64_t m, int c) {
 }
 
 __device__ __forceinline__ float relu_mask(float x, float sc, float sh) { return fmaf(x, sc, sh) > 0.f ? 1.f : 0.f; }
+// the backward's dz mask with a folded Quantization_int8 straight-through clip (rn_bn_desc.clip): the
+// ReLU, and zero where the output as stored (rounded to T, as bn_apply_kernel writes it) is >= t
+template <typename T>
+__device__ __forceinline__ float relu_clip_mask(float x, float sc, float sh, bool clip, float t) {
+  const float z = fmaf(x, sc, sh);
+  return (z > 0.f && (!clip || to_f(from_f<T>(z)) < t)) ? 1.f : 0.f;
+}
 
 // ---- forward stats: partial shifted sums; pivot = x[0][c]
 template <typename T>
@@ -418,8 +425,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ scale,
                                                             const float* __restrict__ shift,
-                                                            float* __restrict__ part) {
+                                                            float* __restrict__ part,
+                                                            const float* __restrict__ clip = nullptr) {
   constexpr int CE = 16 / sizeof(T);
+  const bool hc = clip != nullptr;
+  const float t = hc ? *clip : 0.f;
   const int tc = threadIdx.x % ct, tr = threadIdx.x / ct, rl = blockDim.x / ct;
   const int cbase = (blockIdx.x * ct + tc) * CE;
   const int64_t r0 = blockIdx.y * rows_per_block;
@@ -440,7 +450,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
     chunk_to_f(ud, fd, (const T*)nullptr);
 #pragma unroll
     for (int e = 0; e < CE; ++e) {
-      const float dz = RELU ? fd[e] * relu_mask(fx[e], sc[e], sh[e]) : fd[e];
+      const float dz = RELU ? fd[e] * relu_clip_mask<T>(fx[e], sc[e], sh[e], hc, t) : fd[e];
       s[e] += dz;
       q[e] = fmaf(dz, fx[e] - mu[e], q[e]);
     }
@@ -573,8 +583,11 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
                                                            const float* __restrict__ coef,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ shift, int64_t m, int c, int ct,
-                                                           int64_t rows_per_block) {
+                                                           int64_t rows_per_block,
+                                                           const float* __restrict__ clip = nullptr) {
   constexpr int CE = 16 / sizeof(T);
+  const bool hc = clip != nullptr;
+  const float t = hc ? *clip : 0.f;
   const int tc = threadIdx.x % ct, tr = threadIdx.x / ct, rl = blockDim.x / ct;
   const int cbase = (blockIdx.x * ct + tc) * CE;
   const int64_t r0 = blockIdx.y * rows_per_block;
@@ -598,7 +611,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
     if (add) chunk_to_f(*reinterpret_cast<const uint4*>(add + off), fa, (const T*)nullptr);
 #pragma unroll
     for (int e = 0; e < CE; ++e) {
-      const float dz = RELU ? fd[e] * relu_mask(fx[e], sc[e], sh[e]) : fd[e];
+      const float dz = RELU ? fd[e] * relu_clip_mask<T>(fx[e], sc[e], sh[e], hc, t) : fd[e];
       float v = A[e] * (dz - mdz[e]) - A2[e] * (fx[e] - mu[e]);
       if (add) v += fa[e];
       fd[e] = v;
@@ -632,7 +645,8 @@ void launch_bwd_apply(const rn_bn_desc* d, const void* x, const void* dy, void* 
                       const float* coef, const float* scale, const float* shift, hipStream_t st) {
   Geo a = make_apply_geo<T>(d->m, d->c);
   hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RELU>), dim3(a.gx, a.nrb), dim3(kThreads), 0, st, (const T*)x,
-                     (const T*)dy, (T*)dx, (const T*)add, coef, scale, shift, d->m, d->c, a.ct, a.rows_per_block);
+                     (const T*)dy, (T*)dx, (const T*)add, coef, scale, shift, d->m, d->c, a.ct, a.rows_per_block,
+                     d->clip);
 }
 
 template <typename T>
@@ -671,7 +685,7 @@ int bn_bwd_t(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const
   coef = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(coef) + 15) & ~uintptr_t(15));
   if (d->relu)
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(g.gx, g.nrb), dim3(kThreads), 0, st, (const T*)x,
-                       (const T*)dy, d->m, d->c, g.ct, g.rows_per_block, smean, scale, shift, part);
+                       (const T*)dy, d->m, d->c, g.ct, g.rows_per_block, smean, scale, shift, part, d->clip);
   else
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(g.gx, g.nrb), dim3(kThreads), 0, st, (const T*)x,
                        (const T*)dy, d->m, d->c, g.ct, g.rows_per_block, smean, scale, shift, part);

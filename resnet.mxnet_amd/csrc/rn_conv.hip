@@ -68,6 +68,8 @@ struct IgemmArgs {
   // gradient g (rounded as stored): dx = A (dz - mean dz) - A2 (x - mean) (+ add), coefficients
   // {A, mean dz, A2, mean} per channel from rn_bn_bwd_finalize, x = bn_x, dz = g relu'(x sc + sh)
   const float* bn_coef;
+  // dgrad only, nullable: a folded Quantization_int8 straight-through clip on the BN output (rn_bn_desc.clip)
+  const float* bn_clip;
   // int8 forward (igemm_big_kernel Q8): per-tensor quantization units of the int8 codes in x and w
   // (Quantization_int8: value = code * unit); the int32 accumulators are scaled by their product
   const float* qunit_x;
@@ -721,9 +723,14 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // belong to the same group, so an MFMA of k-step ks and column sub-block j multiplies zeros unless the
 // channel range of ks lies in the column range of j (32x32x16: ks >> 1 == j; 16x16x32: j >> 1 == ks).
 // Those MFMAs and their B-fragment reads are skipped: half the MFMA work of the block-diagonal tile.
-template <int BN, int NBUF, int EPI = 0, bool M32 = false, int BM = 256, int SC = 0, int Q8 = 0, int XF = 0, int W4 = 0,
+// EPIX 4: EPI 2 whose BatchNorm output feeds a Quantization_int8 (rn_conv_bwd_data_bnred_clip): dz also
+// carries the quantizer's straight-through clip (a compile-time variant: the other epilogues keep
+// their code)
+template <int BN, int NBUF, int EPIX = 0, bool M32 = false, int BM = 256, int SC = 0, int Q8 = 0, int XF = 0, int W4 = 0,
           int GD = 0>
 __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1) void igemm_big_kernel(IgemmArgs p) {
+  constexpr int EPI = EPIX == 4 ? 2 : EPIX;
+  constexpr bool CLIP = EPIX == 4;
   constexpr int ES = Q8 ? 1 : 2;                 // operand bytes per element
   constexpr int BMA = 256, CE = 16 / ES, BKE = 128 / ES;
   using OutT = typename std::conditional<Q8 == 2, float, bf16_t>::type;
@@ -1069,6 +1076,7 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
     }
   }
   const bf16_t* __restrict__ bxg = reinterpret_cast<const bf16_t*>(p.bn_x);
+  const float clipt = CLIP ? *p.bn_clip : 0.f;  // (EPI 4: a folded quantizer clip)
 #pragma unroll
   for (int h = 0; h < NCH; ++h) {
     constexpr int kLast = WM - 64 * (NCH - 1);  // rows of the last chunk (48 for 112-row waves)
@@ -1181,7 +1189,9 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
             chunk_to_f(xpre[XP ? k : 0], xv, (const bf16_t*)nullptr);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
-              const float dz = (!p.bn_relu || fmaf(xv[e], r_sc[e], r_sh[e]) > 0.f) ? g[e] : 0.f;
+              float dz = (!p.bn_relu || fmaf(xv[e], r_sc[e], r_sh[e]) > 0.f) ? g[e] : 0.f;
+              if constexpr (CLIP)  // the quantizer's straight-through clip on the stored BN output
+                if (!(to_f(from_f<bf16_t>(fmaf(xv[e], r_sc[e], r_sh[e]))) < clipt)) dz = 0.f;
               s1[e] += dz;
               s2[e] = fmaf(dz, xv[e] - r_mu[e], s2[e]);
             }
@@ -2255,9 +2265,9 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   const bool dma = g_tune[RN_TUNE_IGEMM_DMA] > 0 && !a.in_sc && !b.diag_l1 && xb < INT32_MAX && wb < INT32_MAX &&
                    max_taps <= 64;
   if constexpr (std::is_same<T, bf16_t>::value && std::is_same<OutT, bf16_t>::value) {
-    const int epi = a.stats ? 1 : a.bnred ? 2 : a.bn_coef ? 3 : 0;
+    const int epi = a.stats ? 1 : a.bnred ? (a.bn_clip ? 4 : 2) : a.bn_coef ? 3 : 0;
     const int bn = big_tile_cols(a, xb, wb);
-    RN_CHECK_ARG(epi != 3 || bn >= 128, "BatchNorm-backward-apply dgrad needs the 224/256-row tile");
+    RN_CHECK_ARG((epi != 3 || bn >= 128) && (epi != 4 || bn >= 64), "this dgrad epilogue needs an LDS-DMA tile");
     const bool m32 = g_tune[RN_TUNE_IGEMM_MFMA] != 1;
     // persistent tiles (rn_set_tuning 10 = workgroups, a multiple of 8): only where the grid is larger
     b.ntiles = 0;
@@ -2276,6 +2286,7 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
       if (a.smallc) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, 1>), grid, dim3(256), 0, st, b);
       else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 1, true>), grid, dim3(256), 0, st, b);
       else if (epi == 2) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 2, true>), grid, dim3(256), 0, st, b);
+      else if (epi == 4) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 4, true>), grid, dim3(256), 0, st, b);
       else if (m32 && a.gred > 0 && a.gcol == a.gred && a.gcol <= 32 && a.cblk == 64 && g_tune[RN_TUNE_IGEMM_GD] != 1)
         hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, 0, 0, 0, 0, 1>), grid, dim3(256), 0, st, b);
       else if (m32) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true>), grid, dim3(256), 0, st, b);
@@ -2293,7 +2304,8 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   if (epi == 0) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 0, M, R>), grid, dim3(512), 0, st, b);        \
   else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 1, M, R>), grid, dim3(512), 0, st, b);   \
   else if (epi == 2) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 2, M, R>), grid, dim3(512), 0, st, b);   \
-  else hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 3, M, R>), grid, dim3(512), 0, st, b);
+  else if (epi == 3) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 3, M, R>), grid, dim3(512), 0, st, b);   \
+  else hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 4, M, R>), grid, dim3(512), 0, st, b);
       if (bn == 128 && bm == 224 && w4_tile(a)) {  // two 4-wave workgroups per CU
         dim3 g4((unsigned)(ceil_div(maxMc, 224) * b.ntn), 1, 1);
         const int pw = g_tune[RN_TUNE_IGEMM_PERSIST] / 8 * 16;
@@ -2308,7 +2320,8 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
         } else if (epi == 0) hipLaunchKernelGGL((igemm_big_kernel<128, 1, 0, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
         else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<128, 1, 1, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
         else if (epi == 2) hipLaunchKernelGGL((igemm_big_kernel<128, 1, 2, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
-        else hipLaunchKernelGGL((igemm_big_kernel<128, 1, 3, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
+        else if (epi == 3) hipLaunchKernelGGL((igemm_big_kernel<128, 1, 3, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
+        else hipLaunchKernelGGL((igemm_big_kernel<128, 1, 4, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
         return rn_check_launch("igemm_big_w4");
       }
       if (a.in_sc) {  // (big_tile_cols: 224 rows, forward)
@@ -2564,6 +2577,16 @@ int64_t rn_conv_bnred_blocks(const rn_conv_desc* d) {
 int rn_conv_bwd_data_bnred(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx, const void* add_src,
                            const void* bn_x, const float* bn_mean, const float* bn_scale, const float* bn_shift,
                            int32_t relu, float* part, rn_stream_t stream) {
+  return rn_conv_bwd_data_bnred_clip(d, dy, w_crsk, dx, add_src, bn_x, bn_mean, bn_scale, bn_shift, relu, nullptr,
+                                     part, stream);
+}
+
+int rn_conv_bwd_data_bnred_clip(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
+                                const void* add_src, const void* bn_x, const float* bn_mean, const float* bn_scale,
+                                const float* bn_shift, int32_t relu, const float* clip, float* part,
+                                rn_stream_t stream) {
+  RN_CHECK_ARG(!clip || (part && relu && d && d->dtype == RN_BF16 && rn_conv_tile(d, 1) >= 64),
+               "the quantizer clip is folded into a bf16 BN+ReLU reduction on an LDS-DMA tile");
   RN_CHECK_ARG(d && dy && w_crsk && (dx || (part && !add_src)), "null argument");
   RN_CHECK_ARG(dx || rn_conv_tile(d, 1) >= 128, "a reduction-only dgrad (dx = NULL) needs the 224/256-row tile");
   IgemmArgs a = make_igemm_args(d, 1);
@@ -2574,7 +2597,7 @@ int rn_conv_bwd_data_bnred(const rn_conv_desc* d, const void* dy, const void* w_
     int maxMc = 0;
     for (int z = 0; z < a.ncls; ++z) maxMc = std::max(maxMc, a.N * a.cls[z].Pc * a.cls[z].Qc);
     a.bnred = part; a.bn_x = bn_x; a.bn_mean = bn_mean; a.bn_sc = bn_scale; a.bn_sh = bn_shift;
-    a.bn_relu = relu; a.mt_max = (int)ceil_div(maxMc, 128);
+    a.bn_relu = relu; a.bn_clip = clip; a.mt_max = (int)ceil_div(maxMc, 128);
   }
   hipStream_t st = as_stream(stream);
   if (d->dtype == RN_BF16) return launch_igemm<bf16_t, bf16_t>(a, st);

@@ -1123,11 +1123,11 @@ class Executor:
         variant on the 128/256-column tiles only)?"""
         if op.kind != "conv" or self.lib is None:
             return False
-        if getattr(op, "int8", False):  # the int8 forward's tile (mode 0 only)
+        if getattr(op, "int8", False) and mode == 0:  # the int8 forward's tile (its dgrad is the bf16 one)
             x, y = op.x, op.y
             d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad, op.groups)
             mc = min_cols if min_cols is not None else int(os.environ.get("RN_BN_FUSION_MIN_COLS", "128"))
-            return mode == 0 and int(self.lib.rn_conv_tile(L.C.byref(d), 2)) >= mc
+            return int(self.lib.rn_conv_tile(L.C.byref(d), 2)) >= mc
         if min_cols is None:  # RN_BN_FUSION_MIN_COLS=64: also on the 64-column tile (opt-in: measured
             min_cols = int(os.environ.get("RN_BN_FUSION_MIN_COLS", "128"))  # 0.6 % slower per step)
         x, y = op.x, op.y
@@ -1208,15 +1208,49 @@ class Executor:
         pre-activation units' conv1, symbol/resnet.py:17-20), the only writer of the gradient (no fan-in
         add), on the 224/256-row tile."""
         d = cop.desc
-        return (self.dtype == L.RN_BF16 and cadd is None and d.groups <= 1 and d.r == 1 and d.s == 1
+        return (self.dtype == L.RN_BF16 and cadd is None and not op.desc.clip and d.groups <= 1 and d.r == 1 and d.s == 1
                 and d.stride_h == 1 and d.stride_w == 1 and d.pad_h == 0 and d.pad_w == 0 and 2 * d.k <= d.c
                 and d.c == d.c_real and d.c % 8 == 0 and op.y.c == d.c
                 and int(self.lib.rn_conv_tile(L.C.byref(d), 1)) >= 128)
+
+    def _quant_folds(self):
+        """{id(quant op): bn op} for the activation quantizers (Quantization_int8 of data, the int8 graph)
+        whose input is the output of a BatchNorm+ReLU that nothing else reads: their straight-through
+        backward (zero where the input is >= the moving threshold, clip_grad_quantization_int8.py) folds
+        into that BN's backward (rn_bn_desc.clip), so the quantizer costs no backward pass and the BN's
+        output gradient is the consumer conv's data gradient itself (which then reduces the BN backward
+        in its epilogue). RN_QUANT_BWD_FOLD=0: separate rn_quant_int8_bwd passes."""
+        if os.environ.get("RN_QUANT_BWD_FOLD", "1") != "1":
+            return {}
+        ops = self.plan.ops
+        readers = {}
+        for o in ops:
+            for k in ("x", "a", "b", "res", "label"):
+                t = getattr(o, k, None)
+                if isinstance(t, TensorSpec):
+                    readers[id(t)] = readers.get(id(t), 0) + 1
+        bn_of = {id(o.y): o for o in ops if o.kind == "bn"}
+        outs = {id(t) for t in self.plan.outputs}
+        folds = {}
+        for o in ops:
+            if o.kind != "quant" or o.q.get("is_weight"):
+                continue
+            bn = bn_of.get(id(o.x))
+            if bn is None or not bn.relu or readers.get(id(o.x)) != 1 or id(o.x) in outs or \
+                    getattr(bn, "apply_fused", False):
+                continue
+            folds[id(o)] = bn
+        return folds
 
     def _build_backward(self):
         plan = self.plan
         sp = self._sp()
         gs = _GradState(self)
+        folds = self._quant_folds()
+        for qop in plan.ops:
+            bn = folds.get(id(qop))
+            if bn is not None:
+                bn.desc.clip = self._ap(qop.q["minmax"]).value  # (the threshold the forward just updated)
         wsp = self._p(self.ws)
         self.param_done_at = {}  # param -> index in self._bwd after which its grad is final
         self._gw = {}  # id(tensor) -> last writer of its gradient buffer: ("dgrad", call index, conv op)
@@ -1308,8 +1342,9 @@ class Executor:
                                                 self._p(dy), self._p(out), self._p(add), self._pp(op.gamma),
                                                 self._ap(op.mean), self._ap(op.var), op.sc, op.sh,
                                                 self._gp(op.gamma), self._gp(op.beta), wsp, sp))
-                elif bwd_fusion and w and w[0] == "dgrad" and dy is self._grads.get(id(op.y)) and \
-                        op.y.c % 8 == 0 and op.y.c == op.y.cp and (bwd_all or self._big_tile(w[2], 1)):
+                elif bwd_fusion and w and w[0] == "dgrad" and dy is w[4] and \
+                        op.y.c % 8 == 0 and op.y.c == op.y.cp and (bwd_all or self._big_tile(w[2], 1)) and \
+                        (not op.desc.clip or self._big_tile(w[2], 1)):  # (the clip: bf16 LDS-DMA tiles)
                     # the conv dgrad that completes this BN's output gradient also reduces its backward
                     # (sum dz, sum dz*(x - mean)); the BN then needs only finalize + apply
                     _, ci, cop, cdy, cout, cadd = w
@@ -1331,10 +1366,16 @@ class Executor:
                                                     self._p(op.coef), op.sc, op.sh, int(op.relu), sp))
                         op.recomputed = True
                     else:
-                        self._bwd[ci] = self._call("rn_conv_bwd_data_bnred", L.C.byref(cop.desc), self._p(cdy),
-                                                   self._p(cop.wc), self._p(cout), self._p(cadd),
-                                                   self._p(self.act(x)), op.sm, op.sc, op.sh, int(op.relu),
-                                                   self._p(op.bnred), sp)
+                        if op.desc.clip:  # (a folded quantizer straight-through clip)
+                            self._bwd[ci] = self._call("rn_conv_bwd_data_bnred_clip", L.C.byref(cop.desc),
+                                                       self._p(cdy), self._p(cop.wc), self._p(cout), self._p(cadd),
+                                                       self._p(self.act(x)), op.sm, op.sc, op.sh, int(op.relu),
+                                                       L.C.c_void_p(op.desc.clip), self._p(op.bnred), sp)
+                        else:
+                            self._bwd[ci] = self._call("rn_conv_bwd_data_bnred", L.C.byref(cop.desc), self._p(cdy),
+                                                       self._p(cop.wc), self._p(cout), self._p(cadd),
+                                                       self._p(self.act(x)), op.sm, op.sc, op.sh, int(op.relu),
+                                                       self._p(op.bnred), sp)
                         self._bwd.append(self._call("rn_bn_bwd_part", L.C.byref(op.desc), self._p(op.bnred),
                                                     op.bnred_blocks, self._p(self.act(x)), self._p(dy), self._p(out),
                                                     self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc, op.sh,
@@ -1367,7 +1408,13 @@ class Executor:
                     if nm is not None:
                         self.param_done_at[nm] = len(self._bwd)
             elif op.kind == "quant":
-                if op.x.needs_grad:
+                if op.x.needs_grad and id(op) in folds:
+                    # straight-through: the gradient passes unchanged to the BN output, whose backward
+                    # applies the clip; the conv that wrote dy stays its last writer (BN reduction fusion)
+                    gs.alias(op.x, dy)
+                    if id(op.y) in self._gw:
+                        self._gw[id(op.x)] = self._gw[id(op.y)]
+                elif op.x.needs_grad:
                     out, add = gs.contribute(op.x)
                     self._bwd.append(self._call("rn_quant_int8_bwd", self.dtype, op.x.numel, self._p(self.act(op.x)),
                                                 self._p(dy), self._p(out), self._ap(op.q["minmax"]), 0, self._p(add),

@@ -6,7 +6,10 @@ PyTorch fallback for any op of the training path.
 import ctypes as C
 import os
 
-from .build import LIB_PATH, build, needs_build
+from .build import LIB_PATH as _BUILT_LIB, build, needs_build
+
+# RN_LIB_PATH: load another build of the library (A/B of two builds in one GPU call); default the in-tree one
+LIB_PATH = os.environ.get("RN_LIB_PATH", _BUILT_LIB)
 
 RN_BF16 = 0
 RN_F32 = 1
@@ -26,7 +29,7 @@ class ConvDesc(C.Structure):
 
 class BNDesc(C.Structure):
     _fields_ = [("dtype", _i32), ("m", _i64), ("c", _i32), ("c_real", _i32), ("eps", _f32), ("momentum", _f32),
-                ("fix_gamma", _i32), ("relu", _i32)]
+                ("fix_gamma", _i32), ("relu", _i32), ("clip", _P)]
 
 
 class PoolDesc(C.Structure):
@@ -50,6 +53,7 @@ SIGNATURES = {
     "rn_bn_reduce_blocks": (_i64, [_P]),
     "rn_relu_bwd_bnred": (_i32, [_P] * 11),
     "rn_conv_bwd_data_bnred": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P, _P]),
+    "rn_conv_bwd_data_bnred_clip": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P, _P, _P]),
     "rn_conv_bnred_blocks": (_i64, [_P]),
     "rn_bn_bwd_part": (_i32, [_P, _P, _i64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rn_bn_bwd_finalize": (_i32, [_P, _P, _i64, _P, _P, _P, _P, _P, _P, _P]),
@@ -119,7 +123,7 @@ def load(auto_build=True):
     global _lib
     if _lib is not None:
         return _lib
-    if auto_build and os.path.exists("/opt/rocm/bin/hipcc") and needs_build():
+    if auto_build and LIB_PATH == _BUILT_LIB and os.path.exists("/opt/rocm/bin/hipcc") and needs_build():
         build()
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"librn.so not found at {LIB_PATH}: build it with "
@@ -131,8 +135,8 @@ def load(auto_build=True):
     import torch  # noqa: F401
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in list(SIGNATURES.items()) + list(DIAG_SIGNATURES.items()):
-        if name in DIAG_SIGNATURES and not hasattr(lib, name):
-            continue
+        if (name in DIAG_SIGNATURES or LIB_PATH != _BUILT_LIB) and not hasattr(lib, name):
+            continue  # (diagnostic-only symbols; an older build loaded for an A/B may lack new entries)
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

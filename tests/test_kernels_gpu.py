@@ -892,6 +892,83 @@ def test_dgrad_bn_backward_recompute_args(gpu):
                                       stream()) != 0
 
 
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("case", [(2, 256, 14, 14, 64, 1, 1, 0), (3, 128, 13, 11, 96, 3, 1, 1), (2, 64, 16, 16, 128, 3, 2, 1)])
+def test_bn_backward_quant_clip_fold(gpu, dtype, case):
+    """The int8 graph's activation quantizer (Quantization_int8 after BN+ReLU, symbol/resnet_int8.py)
+    folded into the BN backward (rn_bn_desc.clip): (a) rn_bn_bwd with the clip == rn_quant_int8_bwd
+    followed by rn_bn_bwd without it, bit for bit; (b, bf16) the conv dgrad reducing the clipped BN
+    backward in its epilogue (rn_conv_bwd_data_bnred_clip + rn_bn_bwd_part) == the oracle's dgrad ->
+    STE clip (zero where the stored BN output >= t) -> BN+ReLU backward."""
+    n, c, h, w, k, r, st, pd = case
+    rng = np.random.default_rng(31)
+    xb = rng.standard_normal((n, c, h, w)) * 1.5 + 0.3
+    if dtype == BF16:
+        xb = bf16_round(xb)
+    gamma, beta = rng.uniform(0.5, 1.5, c), rng.standard_normal(c) * 0.2
+    d = conv_desc(dtype, n, c, h, w, k, r, r, st, pd)
+    lib = L.load()
+    f = lambda a: torch.tensor(np.pad(np.asarray(a, np.float64), (0, d.c - c)), dtype=torch.float32, device=gpu)
+    g_d, b_d, mm, mv = f(gamma), f(beta), f(np.zeros(c)), f(np.ones(c))
+    sm, si, sc, sh = [torch.zeros(d.c, dtype=torch.float32, device=gpu) for _ in range(4)]
+    bd = L.BNDesc(dtype=dtype, m=n * h * w, c=d.c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1)
+    ws = torch.zeros(lib.rn_bn_workspace_bytes(C.byref(bd)) // 4 + 16, dtype=torch.float32, device=gpu)
+    xbd = to_nhwc(xb, dtype, gpu)
+    act = torch.zeros_like(xbd)
+    L.call("rn_bn_fwd_train", C.byref(bd), p(xbd), p(act), p(g_d), p(b_d), p(mm), p(mv), p(sm), p(si), p(sc), p(sh),
+           p(ws), stream())
+    torch.cuda.synchronize()
+    a_np = from_nhwc(act, c)
+    t = float(np.quantile(a_np[a_np > 0], 0.7))  # a threshold that clips ~30 % of the positive outputs
+    tq = torch.tensor([t], dtype=torch.float32, device=gpu)
+    # (a) the BN backward with the folded clip vs the quantizer's backward pass followed by it
+    dyb = to_nhwc(rng.standard_normal((n, c, h, w)), dtype, gpu)
+    zf = lambda: torch.zeros(d.c, dtype=torch.float32, device=gpu)
+    dq = torch.zeros_like(xbd)
+    L.call("rn_quant_int8_bwd", dtype, act.numel(), p(act), p(dyb), p(dq), p(tq), 0, None, stream())
+    dx0, dg0, db0 = torch.zeros_like(xbd), zf(), zf()
+    L.call("rn_bn_bwd", C.byref(bd), p(xbd), p(dq), p(dx0), None, p(g_d), p(sm), p(si), p(sc), p(sh), p(dg0), p(db0),
+           p(ws), stream())
+    bdc = L.BNDesc(dtype=dtype, m=n * h * w, c=d.c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1,
+                   clip=tq.data_ptr())
+    dx1, dg1, db1 = torch.zeros_like(xbd), zf(), zf()
+    L.call("rn_bn_bwd", C.byref(bdc), p(xbd), p(dyb), p(dx1), None, p(g_d), p(sm), p(si), p(sc), p(sh), p(dg1), p(db1),
+           p(ws), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1) and torch.equal(dg0, dg1) and torch.equal(db0, db1)
+    assert (dq == 0).float().mean().item() > 0.05  # the clip zeroed the gradient of the outputs >= t
+    if dtype != BF16:
+        return  # (b) runs on the bf16 LDS-DMA tiles only
+    # (b) the dgrad's epilogue reduces the clipped BN backward
+    wt = rng.standard_normal((k, c, r, r)) / np.sqrt(c * r * r)
+    P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+    dy = rng.standard_normal((n, k, P, Q))
+    if dtype == BF16:
+        wt, dy = bf16_round(wt), bf16_round(dy)
+    wc = torch.zeros(d.c * r * r * d.k_pad, dtype=tdt(dtype), device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), None, p(wc), stream())
+    nrb = lib.rn_conv_bnred_blocks(C.byref(d))
+    part = torch.full((nrb * d.c * 2,), float("nan"), dtype=torch.float32, device=gpu)
+    dact = torch.zeros_like(xbd)
+    dyd = to_nhwc(dy, dtype, gpu)
+    L.call("rn_conv_bwd_data_bnred_clip", C.byref(d), p(dyd), p(wc), p(dact), None, p(xbd), p(sm), p(sc), p(sh), 1,
+           p(tq), p(part), stream())
+    dx2, dg2, db2 = torch.zeros_like(xbd), zf(), zf()
+    L.call("rn_bn_bwd_part", C.byref(bdc), p(part), nrb, p(xbd), p(dact), p(dx2), None, p(g_d), p(sm), p(si),
+           p(sc), p(sh), p(dg2), p(db2), p(ws), stream())
+    torch.cuda.synchronize()
+    a_ref, cache = ops.bn_train_fwd(xb, gamma, beta, 1e-5, False)
+    act_ref = ops.relu_fwd(a_ref)
+    dact_ref, _ = ops.conv2d_bwd(act_ref, wt, dy, (st, st), (pd, pd))
+    g_st = from_nhwc(dact, c)                                 # the stored gradient (what the STE reads)
+    keep = (a_np > 0) & (a_np < t)                            # relu' x clip on the stored BN output
+    dx_ref, dg_ref, db_ref = ops.bn_train_bwd(g_st * keep, cache, False)
+    assert rel_err(g_st, dact_ref) < TOL[dtype]
+    assert rel_err(from_nhwc(dx2, c), dx_ref) < (TOL[dtype] * 5 if dtype == F32 else 3e-2)
+    assert rel_err(db2.cpu().numpy()[:c], db_ref) < (1e-4 if dtype == F32 else 2e-2)
+    assert rel_err(dg2.cpu().numpy()[:c], dg_ref) < (1e-4 if dtype == F32 else 2e-2)
+
+
 BIG_CASES = [
     # n, c, h, w, k, r, stride, pad: 256-row tiles (fwd when k >= 128, dgrad when c >= 128)
     (2, 128, 14, 14, 256, 3, 1, 1),
