@@ -130,7 +130,7 @@ def test_executor_dry_run(dtype):
     np.testing.assert_array_equal(ex.get_param("stage2_unit1_conv2_weight"), w3)
 
 
-def test_plan_int8_quantization():
+def test_plan_int8_quantization(monkeypatch):
     """resnet_int8 (symbol/resnet_int8.py): 108 Quantization_int8 nodes -> 54 weight
     quantizations folded into the weight packs, 53 activation quant ops, 1 folded into the stem."""
     sym = graphs.resnet50_int8()
@@ -144,7 +144,14 @@ def test_plan_int8_quantization():
     ex = Executor(Plan(graphs.resnet_int8([1, 1, 1, 1], 4, [64, 256, 512, 1024, 2048], 16),
                        [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")
     names = [c[0] for c in ex._bwd]
-    assert names.count("rn_quant_int8_bwd") == 17 and names.count("rn_stem_quant_clip_grad") == 1
+    # 8 of the 17 activation quantizers read a BN+ReLU output nothing else reads: their straight-through
+    # backward is folded into that BN's backward (rn_bn_desc.clip); RN_QUANT_BWD_FOLD=0 keeps all 17
+    assert names.count("rn_quant_int8_bwd") == 9 and names.count("rn_stem_quant_clip_grad") == 1
+    assert sum(1 for op in ex.plan.ops if op.kind == "bn" and op.desc.clip) == 8
+    monkeypatch.setenv("RN_QUANT_BWD_FOLD", "0")
+    ex = Executor(Plan(graphs.resnet_int8([1, 1, 1, 1], 4, [64, 256, 512, 1024, 2048], 16),
+                       [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")
+    assert [c[0] for c in ex._bwd].count("rn_quant_int8_bwd") == 17
     packs = [c[0] for c in ex.packs]
     # the 16 non-stem convs' weight quantizers also keep the unit of their int8 codes (int8 forward)
     assert packs.count("rn_quant_int8_fwd") + packs.count("rn_quant_int8_fwd_codes") == 18
