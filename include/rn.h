@@ -418,6 +418,16 @@ int rn_quant_int8_fwd(int32_t dtype, int64_t n, const void* x, void* out, float*
 int rn_quant_int8_fwd_codes(int32_t dtype, int64_t n, const void* x, void* out, void* codes, float* unit,
                             float* minmax, int32_t is_weight, int32_t is_train, float ema_decay,
                             int32_t first_batch, int32_t nbits, float* ws, rn_stream_t stream);
+/* The activation Quantization_int8 of a BatchNorm(+ReLU) output that only the quantizer reads
+ * (symbol/resnet_int8.py's bn -> relu -> Quantization_int8 -> conv), the BatchNorm applied on load:
+ * y = [relu](x*scale + shift) (d->relu) rounded to d->dtype as rn_bn_apply stores it, then
+ * rn_quant_int8_fwd_codes(y) with is_weight = 0 -- bit-identical to that pair, but y is never
+ * written nor re-read. scale / shift from rn_bn_fwd_train[_part] / rn_bn_fwd_infer with y = NULL;
+ * d->c a multiple of 16; out and codes required. */
+int rn_quant_int8_fwd_codes_bn(const rn_bn_desc* d, const void* x, const float* scale, const float* shift,
+                               void* out, void* codes, float* unit, float* minmax, int32_t is_train,
+                               float ema_decay, int32_t first_batch, int32_t nbits, float* ws,
+                               rn_stream_t stream);
 /* STE backward: dx = dy (weights) or dy * (|x| <= t) (activations). */
 int rn_quant_int8_bwd(int32_t dtype, int64_t n, const void* x, const void* dy, void* dx,
                       const float* minmax, int32_t is_weight, const void* add_src,

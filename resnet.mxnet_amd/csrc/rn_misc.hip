@@ -517,6 +517,93 @@ __global__ void quant_bwd_kernel(int64_t n, const T* __restrict__ x, const T* __
   }
 }
 
+// ---- Quantization_int8 of a BatchNorm(+ReLU) output, the BatchNorm applied on load
+// (rn_quant_int8_fwd_codes_bn). Thread = one 16-channel group (one 16-byte code chunk) of the rows
+// r0 + tr, r0 + tr + rl, ...; y = [relu](fmaf(x, scale, shift)) rounded to T exactly as bn_apply_kernel
+// stores it, so max|y|, the codes and the fake-quantized values equal rn_bn_apply followed by
+// rn_quant_int8_fwd_codes bit for bit, without the BatchNorm output's write and two re-reads.
+template <typename T, bool RELU>
+__device__ __forceinline__ void bnq_load(const T* __restrict__ x, const float* sc, const float* sh, float* f) {
+  constexpr int CE = 16 / sizeof(T);
+#pragma unroll
+  for (int h = 0; h < 16 / CE; ++h) chunk_to_f(reinterpret_cast<const uint4*>(x)[h], f + h * CE, (const T*)nullptr);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const float v = fmaf(f[e], sc[e], sh[e]);
+    f[e] = to_f(from_f<T>(RELU ? fmaxf(v, 0.f) : v));
+  }
+}
+template <typename T, bool RELU>
+__global__ __launch_bounds__(256) void bnq_absmax_kernel(const T* __restrict__ x, const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, int64_t m, int c, int ct,
+                                                         int64_t rows_per_block, float* __restrict__ out) {
+  const int tc = threadIdx.x % ct, tr = threadIdx.x / ct, rl = blockDim.x / ct;
+  const int cb = (blockIdx.x * ct + tc) * 16;
+  const int64_t r0 = blockIdx.y * rows_per_block;
+  const int64_t r1 = min(m, r0 + rows_per_block);
+  float mx = 0.f;
+  if (tr < rl) {  // (256 % ct threads idle)
+    float sc[16], sh[16];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      sc[e] = scale[cb + e];
+      sh[e] = shift[cb + e];
+    }
+    for (int64_t r = r0 + tr; r < r1; r += rl) {
+      float f[16];
+      bnq_load<T, RELU>(x + r * c + cb, sc, sh, f);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) mx = fmaxf(mx, fabsf(f[e]));
+    }
+  }
+  mx = wave_max(mx);
+  __shared__ float wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(reinterpret_cast<unsigned int*>(out), __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
+}
+template <typename T, bool RELU>
+__global__ __launch_bounds__(256) void bnq_codes_kernel(const T* __restrict__ x, const float* __restrict__ scale,
+                                                        const float* __restrict__ shift, int64_t m, int c, int ct,
+                                                        int64_t rows_per_block, T* __restrict__ out,
+                                                        int8_t* __restrict__ codes, const float* __restrict__ thr,
+                                                        float qmax, float* __restrict__ unit_out) {
+  const float t = *thr;
+  const float unit = t / qmax;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && unit_out) *unit_out = unit;
+  const int tc = threadIdx.x % ct, tr = threadIdx.x / ct, rl = blockDim.x / ct;
+  if (tr >= rl) return;
+  const int cb = (blockIdx.x * ct + tc) * 16;
+  const int64_t r0 = blockIdx.y * rows_per_block;
+  const int64_t r1 = min(m, r0 + rows_per_block);
+  constexpr int CE = 16 / sizeof(T);
+  float sc[16], sh[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    sc[e] = scale[cb + e];
+    sh[e] = shift[cb + e];
+  }
+  for (int64_t r = r0 + tr; r < r1; r += rl) {
+    float f[16];
+    bnq_load<T, RELU>(x + r * c + cb, sc, sh, f);
+    uint32_t cw[4];
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {  // quant_codes_kernel's clip / round / dequantize
+      const float v = fminf(fmaxf(f[e], -t), t);
+      const float q = unit > 0.f ? roundf(v / unit) : 0.f;
+      f[e] = q * unit;
+      const uint32_t b = (uint32_t)(uint8_t)(int8_t)(int)q;
+      if ((e & 3) == 0) cw[e >> 2] = b;
+      else cw[e >> 2] |= b << (8 * (e & 3));
+    }
+    const int64_t off = r * c + cb;
+#pragma unroll
+    for (int h = 0; h < 16 / CE; ++h) reinterpret_cast<uint4*>(out + off)[h] = f_to_chunk(f + h * CE, (const T*)nullptr);
+    reinterpret_cast<uint4*>(codes + off)[0] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+  }
+}
+
 }  // namespace
 
 int g_tune[RN_TUNE_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512, 0, 0, 0, 0, 0, 0, 0};
@@ -922,6 +1009,61 @@ int rn_quant_int8_fwd_codes(int32_t dtype, int64_t n, const void* x, void* out, 
     hipLaunchKernelGGL(quant_codes_kernel<float>, dim3(grid1d(nc)), dim3(256), 0, st, nc, (const float*)x,
                        (float*)out, (int8_t*)codes, thr, qmax, clip, unit);
   return rn_check_launch("quant_int8_fwd_codes");
+}
+
+extern "C++" {
+template <typename T, bool RELU>
+static void launch_quant_codes_bn(const rn_bn_desc* d, const void* x, const float* scale, const float* shift,
+                                  void* out, void* codes, float* unit, float* curmax, float* thr, float* minmax,
+                                  int32_t is_train, float ema_decay, int32_t first_batch, float qmax,
+                                  hipStream_t st) {
+  const int cpr = d->c / 16;  // 16-channel groups per row
+  int ct = std::min(cpr, 64);
+  while (cpr % ct) --ct;
+  const int rl = 256 / ct, gx = cpr / ct;
+  auto geo = [&](int rows_each) {
+    const int64_t want = std::max<int64_t>(1, 4096 / gx);
+    const int64_t maxrb = std::max<int64_t>(1, d->m / ((int64_t)rl * rows_each));
+    const int nrb = (int)std::min(want, maxrb);
+    return std::make_pair(nrb, (d->m + nrb - 1) / nrb);
+  };
+  if (is_train) {
+    const auto g = geo(16);
+    hipLaunchKernelGGL((bnq_absmax_kernel<T, RELU>), dim3(gx, g.first), dim3(256), 0, st, (const T*)x, scale, shift,
+                       d->m, d->c, ct, g.second, curmax);
+  }
+  hipLaunchKernelGGL(quant_state_kernel, dim3(1), dim3(1), 0, st, curmax, minmax, 0, is_train, ema_decay, first_batch,
+                     thr, qmax, nullptr);
+  const auto g = geo(8);
+  hipLaunchKernelGGL((bnq_codes_kernel<T, RELU>), dim3(gx, g.first), dim3(256), 0, st, (const T*)x, scale, shift, d->m,
+                     d->c, ct, g.second, (T*)out, (int8_t*)codes, thr, qmax, unit);
+}
+}  // extern "C++"
+
+int rn_quant_int8_fwd_codes_bn(const rn_bn_desc* d, const void* x, const float* scale, const float* shift, void* out,
+                               void* codes, float* unit, float* minmax, int32_t is_train, float ema_decay,
+                               int32_t first_batch, int32_t nbits, float* ws, rn_stream_t stream) {
+  RN_CHECK_ARG(d && x && scale && shift && out && codes && unit && minmax && ws, "null argument");
+  RN_CHECK_ARG(d->dtype == RN_BF16 || d->dtype == RN_F32, "bad dtype");
+  RN_CHECK_ARG(d->m > 0 && d->c > 0 && d->c % 16 == 0, "bad shape (c must be a multiple of 16)");
+  RN_CHECK_ARG(nbits >= 2 && nbits <= 8, "int8 codes need nbits <= 8");
+  hipStream_t st = as_stream(stream);
+  const float qmax = (float)((1 << (nbits - 1)) - 1);
+  float* curmax = ws;  // zero on entry (left zero by the state kernel)
+  float* thr = ws + 1;
+  const bool bf = d->dtype == RN_BF16;
+  if (d->relu) {
+    if (bf) launch_quant_codes_bn<bf16_t, true>(d, x, scale, shift, out, codes, unit, curmax, thr, minmax, is_train,
+                                                ema_decay, first_batch, qmax, st);
+    else launch_quant_codes_bn<float, true>(d, x, scale, shift, out, codes, unit, curmax, thr, minmax, is_train,
+                                            ema_decay, first_batch, qmax, st);
+  } else {
+    if (bf) launch_quant_codes_bn<bf16_t, false>(d, x, scale, shift, out, codes, unit, curmax, thr, minmax, is_train,
+                                                 ema_decay, first_batch, qmax, st);
+    else launch_quant_codes_bn<float, false>(d, x, scale, shift, out, codes, unit, curmax, thr, minmax, is_train,
+                                             ema_decay, first_batch, qmax, st);
+  }
+  return rn_check_launch("quant_int8_fwd_codes_bn");
 }
 
 int rn_quant_int8_bwd(int32_t dtype, int64_t n, const void* x, const void* dy, void* dx, const float* minmax,

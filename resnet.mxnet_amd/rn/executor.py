@@ -907,6 +907,20 @@ class Executor:
         wsp = self._p(self.ws)
         self.qws = self._zeros(4096, self.torch.float32)
         qwsp = self._p(self.qws)
+        # activation quantizers whose BatchNorm(+ReLU) input nothing else reads (the int8 graph): the
+        # quantizer applies the BN on load (rn_quant_int8_fwd_codes_bn, bit-identical) and the BN's
+        # output is never written -- with the folded straight-through backward nothing reads it
+        # (RN_QUANT_BN_FUSE=0: rn_bn_apply + rn_quant_int8_fwd_codes)
+        qbn = self._quant_folds() if os.environ.get("RN_QUANT_BN_FUSE", "1") == "1" else {}
+        for op in plan.ops:
+            op.bn_src = None
+            if op.kind == "bn":
+                op.apply_in_quant = False
+        for op in plan.ops:
+            bn = qbn.get(id(op))
+            if bn is not None and op.emit_codes and bn.x.cp % 16 == 0:
+                op.bn_src = bn
+                bn.apply_in_quant = True
         for op in plan.ops:
             F, I = [], []  # train-mode, infer-mode call lists
             op.wsrc = self._weight_source(op, qwsp, sp) if getattr(op, "qweight", None) else \
@@ -1005,7 +1019,8 @@ class Executor:
                 op.buf = self._zeros(4 * c, self.torch.float32)
                 op.sm, op.si, op.sc, op.sh = [L.C.c_void_p(op.buf.data_ptr() + 4 * c * i) for i in range(4)]
                 gamma = self._pp(op.gamma)
-                yptr = None if op.apply_fused else self._p(self.act(y))  # fused: coefficients only
+                # fused into the 1x1 consumers' loads or the quantizer's: coefficients only
+                yptr = None if op.apply_fused or op.apply_in_quant else self._p(self.act(y))
                 infer = self._call("rn_bn_fwd_infer", L.C.byref(op.desc), self._p(self.act(x)), yptr,
                                    gamma, self._pp(op.beta), self._ap(op.mean), self._ap(op.var), op.sc, op.sh, sp)
                 if op.use_global_stats:
@@ -1053,7 +1068,13 @@ class Executor:
                     op.codes = self.torch.zeros(op.x.numel, dtype=self.torch.int8, device=self.device)
                     op.unit = self._zeros(1, self.torch.float32)
                 for lst, tr in ((F, 1), (I, 0)):
-                    if op.emit_codes:
+                    if op.bn_src is not None:
+                        bn = op.bn_src
+                        lst.append(self._call("rn_quant_int8_fwd_codes_bn", L.C.byref(bn.desc),
+                                              self._p(self.act(bn.x)), bn.sc, bn.sh, self._p(self.act(op.y)),
+                                              self._p(op.codes), self._p(op.unit), self._ap(q["minmax"]), tr,
+                                              q["ema"], self._qfirst, q["nbits"], qwsp, sp))
+                    elif op.emit_codes:
                         lst.append(self._call("rn_quant_int8_fwd_codes", self.dtype, op.x.numel,
                                               self._p(self.act(op.x)), self._p(self.act(op.y)), self._p(op.codes),
                                               self._p(op.unit), self._ap(q["minmax"]), 0, tr, q["ema"],

@@ -98,6 +98,7 @@ SIGNATURES = {
     "rn_relu_bwd": (_i32, [_i64, _i32, _P, _P, _P, _P, _P]),
     "rn_quant_int8_fwd": (_i32, [_i32, _i64, _P, _P, _P, _i32, _i32, _f32, _i32, _i32, _P, _P]),
     "rn_quant_int8_fwd_codes": (_i32, [_i32, _i64, _P, _P, _P, _P, _P, _i32, _i32, _f32, _i32, _i32, _P, _P]),
+    "rn_quant_int8_fwd_codes_bn": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _i32, _f32, _i32, _i32, _P, _P]),
     "rn_quant_int8_bwd": (_i32, [_i32, _i64, _P, _P, _P, _P, _i32, _P, _P]),
     "rn_set_tuning": (_i32, [_i32, _i32]),
     "rn_last_error": (C.c_char_p, []),

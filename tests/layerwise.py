@@ -236,7 +236,7 @@ class Checker:
                                     max(1.0, float((beta - mean * g * inv).abs().max())))}
                 self.add_metric("bn_fwd", op.name, m, {"mean": 1e-5, "invstd": 1e-5, "scale": 1e-5,
                                                        "shift": 1e-5})
-                if not getattr(op, "apply_fused", False):
+                if not (getattr(op, "apply_fused", False) or getattr(op, "apply_in_quant", False)):
                     v = _fma(x.float(), sc[:c].view(1, c, 1, 1), sh[:c].view(1, c, 1, 1))
                     if op.relu:
                         v = torch.relu(v)

@@ -47,8 +47,8 @@ def gpu_relu_masks(ex):
         if not name:
             continue
         t = op.y
-        if op.kind == "bn" and getattr(op, "apply_fused", False):
-            # BN+ReLU applied on load by its 1x1 consumers: the decision is fmaf(x, sc, sh) > 0 (exact
+        if op.kind == "bn" and (getattr(op, "apply_fused", False) or getattr(op, "apply_in_quant", False)):
+            # BN+ReLU applied on load by its 1x1 consumers or its quantizer: the decision is fmaf(x, sc, sh) > 0 (exact
             # in fp64 for fp32 operands, same sign as the device's fused multiply-add)
             x = op.x
             xv = ex.act(x).float().cpu().numpy().reshape(x.n, x.h, x.w, x.cp).astype(np.float64)

@@ -166,7 +166,11 @@ def test_int8_forward_plan(dry, monkeypatch):
             assert _call_names(ex._fwd_infer).count("rn_conv_fwd_i8") == nconv
             qops = [op for op in ex.plan.ops if op.kind == "quant"]
             # every conv's data quantizer emits codes (fc1's, in resnet_int8, does not)
-            assert names.count("rn_quant_int8_fwd_codes") == sum(op.emit_codes for op in qops) >= len(qops) - 1
+            nbn = names.count("rn_quant_int8_fwd_codes_bn")
+            assert names.count("rn_quant_int8_fwd_codes") + nbn == sum(op.emit_codes for op in qops) >= len(qops) - 1
+            # quantizers of a BN+ReLU output nothing else reads apply that BN on load; its output is not written
+            assert nbn == sum(op.bn_src is not None for op in qops) > 0
+            assert all(op.bn_src.apply_in_quant and op.bn_src.y is op.x for op in qops if op.bn_src is not None)
             assert _call_names(ex.packs).count("rn_conv_weight_pack_i8") == nconv
     monkeypatch.setenv("RN_INT8_MFMA", "0")
     ex = _bind(graphs.resnet_int8(*R50_SMALL.values()), shape).executor

@@ -1,5 +1,5 @@
 """Int8 MFMA forward of quantized convolutions (rn_conv_fwd_i8, v_mfma_i32_16x16x64_i8) and the int8
-codes of Quantization_int8 (rn_quant_int8_fwd_codes, rn_conv_weight_pack_i8).
+codes of Quantization_int8 (rn_quant_int8_fwd_codes[_bn], rn_conv_weight_pack_i8).
 
 The reference computes a quantized conv in fp32 on fake-quantized values (symbol/int8_api.py:120-151,
 values code * unit, symbol/quant_ops.py:17-31, clip_grad_quantization_int8.py:37-54). On the integer
@@ -160,3 +160,42 @@ def test_weight_pack_i8(gpu):
     u = np.float32(unit.item())
     qv = qw.cpu().numpy().reshape(k, r, r, c)
     np.testing.assert_array_equal(codes[..., :c].astype(np.float32) * u, qv)
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("relu", [1, 0])
+@pytest.mark.parametrize("m,c", [(3136, 64), (1001, 48), (98, 2048), (7, 16)])
+def test_quant_codes_bn_fused(gpu, dtype, relu, m, c):
+    """rn_quant_int8_fwd_codes_bn (the BatchNorm applied on load) == rn_bn_apply followed by
+    rn_quant_int8_fwd_codes, bit for bit: values, codes, unit and the EMA state, training (max|y| and
+    the EMA update) and inference (the moving threshold); c = 48 leaves threads of each block idle."""
+    rng = np.random.default_rng(m + c)
+    x = torch.tensor(rng.standard_normal((m, c)) * 3.0, dtype=tdt(dtype), device=gpu)
+    sc = torch.tensor(rng.standard_normal(c) * 0.7, dtype=torch.float32, device=gpu)
+    sh = torch.tensor(rng.standard_normal(c) * 0.5, dtype=torch.float32, device=gpu)
+    d = L.BNDesc(dtype=dtype, m=m, c=c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=relu)
+    n = m * c
+    y = torch.zeros_like(x)
+    ws = torch.zeros(4096, dtype=torch.float32, device=gpu)
+    for train in (1, 0):
+        outs = []
+        for fused in (False, True):
+            out = torch.full_like(x, float("nan"))
+            codes = torch.zeros(n, dtype=torch.int8, device=gpu)
+            unit = torch.zeros(1, dtype=torch.float32, device=gpu)
+            mm = torch.tensor([2.5], dtype=torch.float32, device=gpu)
+            if fused:
+                L.call("rn_quant_int8_fwd_codes_bn", C.byref(d), p(x), p(sc), p(sh), p(out), p(codes), p(unit), p(mm),
+                       train, 0.99, 0, 8, p(ws), stream())
+            else:
+                L.call("rn_bn_apply", C.byref(d), p(x), p(y), p(sc), p(sh), stream())
+                L.call("rn_quant_int8_fwd_codes", dtype, n, p(y), p(out), p(codes), p(unit), p(mm), 0, train, 0.99,
+                       0, 8, p(ws), stream())
+            outs.append((out, codes, unit, mm))
+        torch.cuda.synchronize()
+        for a, b in zip(*outs):
+            assert torch.equal(a, b)
+        assert ws[0].item() == 0.0  # the shared workspace's running max is left zero
+        if train:
+            yv = y.float()
+            assert outs[1][3].item() != 2.5 and yv.abs().max().item() > 0
