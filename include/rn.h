@@ -210,6 +210,13 @@ typedef struct rn_bn_desc {
    * 133-136). Its straight-through backward (clip_grad_quantization_int8.py: zero where |y| >= t) is
    * folded into this BN's backward: dz = dy * [y > 0] * [y < t], y = the output as stored. */
   const float* clip;
+  /* nullable (rn_bn_bwd / rn_bn_bwd_global only, with relu and clip): a SECOND Quantization_int8 of
+   * this BN's output (symbol/resnet_int8.py: a stage's first unit quantizes act1 for conv1 and for
+   * the shortcut conv, each with its own threshold), its threshold and its output gradient. Both
+   * straight-through backwards fold in: dz = [y > 0] * round(dy * [y < *clip] + dy2 * [y < *clip2]),
+   * round = to the storage type, as two rn_quant_int8_bwd calls summing into one buffer store it. */
+  const float* clip2;
+  const void* dy2;
 } rn_bn_desc;
 
 /* Workspace (bytes) needed by rn_bn_fwd_train / rn_bn_bwd. */
@@ -428,6 +435,13 @@ int rn_quant_int8_fwd_codes_bn(const rn_bn_desc* d, const void* x, const float* 
                                void* out, void* codes, float* unit, float* minmax, int32_t is_train,
                                float ema_decay, int32_t first_batch, int32_t nbits, float* ws,
                                rn_stream_t stream);
+/* The same for the two quantizers of one BatchNorm output (rn_bn_desc.dy2): one max|y| pass, both
+ * threshold states updated from it, one pass writing both quantizers' values and codes. */
+int rn_quant_int8_fwd_codes_bn2(const rn_bn_desc* d, const void* x, const float* scale, const float* shift,
+                                void* out, void* codes, float* unit, float* minmax, float ema_decay,
+                                int32_t nbits, void* out2, void* codes2, float* unit2, float* minmax2,
+                                float ema_decay2, int32_t nbits2, int32_t is_train, int32_t first_batch,
+                                float* ws, rn_stream_t stream);
 /* STE backward: dx = dy (weights) or dy * (|x| <= t) (activations). */
 int rn_quant_int8_bwd(int32_t dtype, int64_t n, const void* x, const void* dy, void* dx,
                       const float* minmax, int32_t is_weight, const void* add_src,

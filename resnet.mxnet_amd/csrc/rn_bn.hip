@@ -51,6 +51,16 @@ __device__ __forceinline__ float relu_clip_mask(float x, float sc, float sh, boo
   return (z > 0.f && (!clip || to_f(from_f<T>(z)) < t)) ? 1.f : 0.f;
 }
 
+// the dz of a BatchNorm+ReLU whose output two Quantization_int8 read (rn_bn_desc.dy2): both
+// straight-through backwards summed and rounded to T, as two rn_quant_int8_bwd calls store them
+template <typename T>
+__device__ __forceinline__ float relu_clip2_dz(float x, float sc, float sh, float g1, float t1, float g2, float t2) {
+  const float z = fmaf(x, sc, sh);
+  if (!(z > 0.f)) return 0.f;
+  const float y = to_f(from_f<T>(z));
+  return to_f(from_f<T>((y < t1 ? g1 : 0.f) + (y < t2 ? g2 : 0.f)));
+}
+
 // ---- forward stats: partial shifted sums; pivot = x[0][c]
 template <typename T>
 __global__ __launch_bounds__(256) void bn_stats_kernel(const T* __restrict__ x, int64_t m, int c, int ct,
@@ -419,17 +429,20 @@ __global__ __launch_bounds__(256) void bn_add_kernel(const T* __restrict__ xa, c
 }
 
 // ---- backward reduce: sum dz, sum dz*(x - mean)
-template <typename T, bool RELU>
+template <typename T, bool RELU, bool PAIR = false>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                                             int64_t m, int c, int ct, int64_t rows_per_block,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ scale,
                                                             const float* __restrict__ shift,
                                                             float* __restrict__ part,
-                                                            const float* __restrict__ clip = nullptr) {
+                                                            const float* __restrict__ clip = nullptr,
+                                                            const T* __restrict__ dy2 = nullptr,
+                                                            const float* __restrict__ clip2 = nullptr) {
   constexpr int CE = 16 / sizeof(T);
   const bool hc = clip != nullptr;
   const float t = hc ? *clip : 0.f;
+  const float t2 = PAIR ? *clip2 : 0.f;
   const int tc = threadIdx.x % ct, tr = threadIdx.x / ct, rl = blockDim.x / ct;
   const int cbase = (blockIdx.x * ct + tc) * CE;
   const int64_t r0 = blockIdx.y * rows_per_block;
@@ -445,12 +458,14 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
   for (int64_t r = r0 + tr; r < r1; r += rl) {
     uint4 ux = *reinterpret_cast<const uint4*>(x + r * c + cbase);
     uint4 ud = *reinterpret_cast<const uint4*>(dy + r * c + cbase);
-    float fx[CE], fd[CE];
+    float fx[CE], fd[CE], f2[CE];
     chunk_to_f(ux, fx, (const T*)nullptr);
     chunk_to_f(ud, fd, (const T*)nullptr);
+    if constexpr (PAIR) chunk_to_f(*reinterpret_cast<const uint4*>(dy2 + r * c + cbase), f2, (const T*)nullptr);
 #pragma unroll
     for (int e = 0; e < CE; ++e) {
-      const float dz = RELU ? fd[e] * relu_clip_mask<T>(fx[e], sc[e], sh[e], hc, t) : fd[e];
+      const float dz = PAIR ? relu_clip2_dz<T>(fx[e], sc[e], sh[e], fd[e], t, f2[e], t2)
+                            : RELU ? fd[e] * relu_clip_mask<T>(fx[e], sc[e], sh[e], hc, t) : fd[e];
       s[e] += dz;
       q[e] = fmaf(dz, fx[e] - mu[e], q[e]);
     }
@@ -577,17 +592,20 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   coef[ch * 4 + 3] = save_mean[ch];
 }
 
-template <typename T, bool RELU>
+template <typename T, bool RELU, bool PAIR = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                                            T* __restrict__ dx, const T* __restrict__ add,
                                                            const float* __restrict__ coef,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ shift, int64_t m, int c, int ct,
                                                            int64_t rows_per_block,
-                                                           const float* __restrict__ clip = nullptr) {
+                                                           const float* __restrict__ clip = nullptr,
+                                                           const T* __restrict__ dy2 = nullptr,
+                                                           const float* __restrict__ clip2 = nullptr) {
   constexpr int CE = 16 / sizeof(T);
   const bool hc = clip != nullptr;
   const float t = hc ? *clip : 0.f;
+  const float t2 = PAIR ? *clip2 : 0.f;
   const int tc = threadIdx.x % ct, tr = threadIdx.x / ct, rl = blockDim.x / ct;
   const int cbase = (blockIdx.x * ct + tc) * CE;
   const int64_t r0 = blockIdx.y * rows_per_block;
@@ -605,13 +623,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
   }
   for (int64_t r = r0 + tr; r < r1; r += rl) {
     const int64_t off = r * c + cbase;
-    float fx[CE], fd[CE], fa[CE];
+    float fx[CE], fd[CE], fa[CE], f2[CE];
     chunk_to_f(*reinterpret_cast<const uint4*>(x + off), fx, (const T*)nullptr);
     chunk_to_f(*reinterpret_cast<const uint4*>(dy + off), fd, (const T*)nullptr);
+    if constexpr (PAIR) chunk_to_f(*reinterpret_cast<const uint4*>(dy2 + off), f2, (const T*)nullptr);
     if (add) chunk_to_f(*reinterpret_cast<const uint4*>(add + off), fa, (const T*)nullptr);
 #pragma unroll
     for (int e = 0; e < CE; ++e) {
-      const float dz = RELU ? fd[e] * relu_clip_mask<T>(fx[e], sc[e], sh[e], hc, t) : fd[e];
+      const float dz = PAIR ? relu_clip2_dz<T>(fx[e], sc[e], sh[e], fd[e], t, f2[e], t2)
+                            : RELU ? fd[e] * relu_clip_mask<T>(fx[e], sc[e], sh[e], hc, t) : fd[e];
       float v = A[e] * (dz - mdz[e]) - A2[e] * (fx[e] - mu[e]);
       if (add) v += fa[e];
       fd[e] = v;
@@ -644,9 +664,14 @@ template <typename T, bool RELU>
 void launch_bwd_apply(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const void* add,
                       const float* coef, const float* scale, const float* shift, hipStream_t st) {
   Geo a = make_apply_geo<T>(d->m, d->c);
-  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RELU>), dim3(a.gx, a.nrb), dim3(kThreads), 0, st, (const T*)x,
-                     (const T*)dy, (T*)dx, (const T*)add, coef, scale, shift, d->m, d->c, a.ct, a.rows_per_block,
-                     d->clip);
+  if (RELU && d->dy2)
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true>), dim3(a.gx, a.nrb), dim3(kThreads), 0, st, (const T*)x,
+                       (const T*)dy, (T*)dx, (const T*)add, coef, scale, shift, d->m, d->c, a.ct, a.rows_per_block,
+                       d->clip, (const T*)d->dy2, d->clip2);
+  else
+    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RELU>), dim3(a.gx, a.nrb), dim3(kThreads), 0, st, (const T*)x,
+                       (const T*)dy, (T*)dx, (const T*)add, coef, scale, shift, d->m, d->c, a.ct, a.rows_per_block,
+                       d->clip);
 }
 
 template <typename T>
@@ -683,7 +708,11 @@ int bn_bwd_t(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const
   float* part = reinterpret_cast<float*>(ws);
   float* coef = part + (int64_t)g.nrb * d->c * 2;
   coef = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(coef) + 15) & ~uintptr_t(15));
-  if (d->relu)
+  if (d->relu && d->dy2)
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true, true>), dim3(g.gx, g.nrb), dim3(kThreads), 0, st, (const T*)x,
+                       (const T*)dy, d->m, d->c, g.ct, g.rows_per_block, smean, scale, shift, part, d->clip,
+                       (const T*)d->dy2, d->clip2);
+  else if (d->relu)
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(g.gx, g.nrb), dim3(kThreads), 0, st, (const T*)x,
                        (const T*)dy, d->m, d->c, g.ct, g.rows_per_block, smean, scale, shift, part, d->clip);
   else
@@ -715,6 +744,7 @@ static int check_bn(const rn_bn_desc* d) {
   RN_CHECK_ARG(d->dtype == RN_BF16 || d->dtype == RN_F32, "bad dtype");
   RN_CHECK_ARG(d->m > 0 && d->c > 0 && d->c % 8 == 0, "bad shape (c must be a multiple of 8)");
   RN_CHECK_ARG(d->c_real > 0 && d->c_real <= d->c, "bad c_real");
+  RN_CHECK_ARG(!d->dy2 || (d->relu && d->clip && d->clip2), "dy2 needs relu, clip and clip2");
   return 0;
 }
 
@@ -863,6 +893,7 @@ int rn_bn_bwd_part(const rn_bn_desc* d, const float* part, int64_t nrb, const vo
   if (check_bn(d)) return -1;
   RN_CHECK_ARG(part && nrb > 0 && x && dy && save_mean && save_invstd && scale && shift && ws, "null argument");
   RN_CHECK_ARG(d->fix_gamma || gamma, "gamma required unless fix_gamma");
+  RN_CHECK_ARG(!d->dy2, "dy2: rn_bn_bwd only (the partials hold one gradient)");
   hipStream_t st = as_stream(stream);
   float* coef = reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(ws) + 15) & ~uintptr_t(15));
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(d->c), dim3(256), 0, st, part, (int)nrb, d->m, d->c, d->c_real,

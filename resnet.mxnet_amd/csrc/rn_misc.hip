@@ -563,15 +563,26 @@ __global__ __launch_bounds__(256) void bnq_absmax_kernel(const T* __restrict__ x
   if (threadIdx.x == 0)
     atomicMax(reinterpret_cast<unsigned int*>(out), __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
 }
-template <typename T, bool RELU>
+// up to two activation quantizers of the same BatchNorm output (symbol/resnet_int8.py: a stage's first
+// unit quantizes act1 once for conv1 and once for the shortcut conv, each with its own threshold state)
+struct BnqTargets {
+  void* out[2];
+  int8_t* codes[2];
+  float* unit[2];
+  float qmax[2];
+};
+template <typename T, bool RELU, int NQ>
 __global__ __launch_bounds__(256) void bnq_codes_kernel(const T* __restrict__ x, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, int64_t m, int c, int ct,
-                                                        int64_t rows_per_block, T* __restrict__ out,
-                                                        int8_t* __restrict__ codes, const float* __restrict__ thr,
-                                                        float qmax, float* __restrict__ unit_out) {
-  const float t = *thr;
-  const float unit = t / qmax;
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0 && unit_out) *unit_out = unit;
+                                                        int64_t rows_per_block, BnqTargets tg,
+                                                        const float* __restrict__ thr) {
+  float t[NQ], unit[NQ];
+#pragma unroll
+  for (int k = 0; k < NQ; ++k) {
+    t[k] = thr[k];
+    unit[k] = t[k] / tg.qmax[k];
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *tg.unit[k] = unit[k];
+  }
   const int tc = threadIdx.x % ct, tr = threadIdx.x / ct, rl = blockDim.x / ct;
   if (tr >= rl) return;
   const int cb = (blockIdx.x * ct + tc) * 16;
@@ -587,21 +598,33 @@ __global__ __launch_bounds__(256) void bnq_codes_kernel(const T* __restrict__ x,
   for (int64_t r = r0 + tr; r < r1; r += rl) {
     float f[16];
     bnq_load<T, RELU>(x + r * c + cb, sc, sh, f);
-    uint32_t cw[4];
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {  // quant_codes_kernel's clip / round / dequantize
-      const float v = fminf(fmaxf(f[e], -t), t);
-      const float q = unit > 0.f ? roundf(v / unit) : 0.f;
-      f[e] = q * unit;
-      const uint32_t b = (uint32_t)(uint8_t)(int8_t)(int)q;
-      if ((e & 3) == 0) cw[e >> 2] = b;
-      else cw[e >> 2] |= b << (8 * (e & 3));
-    }
     const int64_t off = r * c + cb;
 #pragma unroll
-    for (int h = 0; h < 16 / CE; ++h) reinterpret_cast<uint4*>(out + off)[h] = f_to_chunk(f + h * CE, (const T*)nullptr);
-    reinterpret_cast<uint4*>(codes + off)[0] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+    for (int k = 0; k < NQ; ++k) {
+      float g[16];
+      uint32_t cw[4];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {  // quant_codes_kernel's clip / round / dequantize
+        const float v = fminf(fmaxf(f[e], -t[k]), t[k]);
+        const float q = unit[k] > 0.f ? roundf(v / unit[k]) : 0.f;
+        g[e] = q * unit[k];
+        const uint32_t b = (uint32_t)(uint8_t)(int8_t)(int)q;
+        if ((e & 3) == 0) cw[e >> 2] = b;
+        else cw[e >> 2] |= b << (8 * (e & 3));
+      }
+#pragma unroll
+      for (int h = 0; h < 16 / CE; ++h)
+        reinterpret_cast<uint4*>(reinterpret_cast<T*>(tg.out[k]) + off)[h] = f_to_chunk(g + h * CE, (const T*)nullptr);
+      reinterpret_cast<uint4*>(tg.codes[k] + off)[0] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+    }
   }
+}
+// the threshold states of NQ quantizers of one tensor from its max (consumed and re-zeroed)
+__global__ void quant_state_multi_kernel(float* __restrict__ curmax, float* minmax0, float* minmax1, int nq,
+                                         int is_train, float decay0, float decay1, int first, float* __restrict__ thr) {
+  thr[0] = quant_state_update(*curmax, minmax0, 0, is_train, decay0, first);
+  if (nq > 1) thr[1] = quant_state_update(*curmax, minmax1, 0, is_train, decay1, first);
+  *curmax = 0.f;
 }
 
 }  // namespace
@@ -1012,11 +1035,12 @@ int rn_quant_int8_fwd_codes(int32_t dtype, int64_t n, const void* x, void* out, 
 }
 
 extern "C++" {
-template <typename T, bool RELU>
+template <typename T, bool RELU, int NQ>
 static void launch_quant_codes_bn(const rn_bn_desc* d, const void* x, const float* scale, const float* shift,
-                                  void* out, void* codes, float* unit, float* curmax, float* thr, float* minmax,
-                                  int32_t is_train, float ema_decay, int32_t first_batch, float qmax,
-                                  hipStream_t st) {
+                                  const BnqTargets& tg, float* const* minmax, const float* decay, float* ws,
+                                  int32_t is_train, int32_t first_batch, hipStream_t st) {
+  float* curmax = ws;  // zero on entry (left zero by the state kernel)
+  float* thr = ws + 1;
   const int cpr = d->c / 16;  // 16-channel groups per row
   int ct = std::min(cpr, 64);
   while (cpr % ct) --ct;
@@ -1027,43 +1051,57 @@ static void launch_quant_codes_bn(const rn_bn_desc* d, const void* x, const floa
     const int nrb = (int)std::min(want, maxrb);
     return std::make_pair(nrb, (d->m + nrb - 1) / nrb);
   };
-  if (is_train) {
+  if (is_train) {  // one max for all the quantizers of the tensor
     const auto g = geo(16);
     hipLaunchKernelGGL((bnq_absmax_kernel<T, RELU>), dim3(gx, g.first), dim3(256), 0, st, (const T*)x, scale, shift,
                        d->m, d->c, ct, g.second, curmax);
   }
-  hipLaunchKernelGGL(quant_state_kernel, dim3(1), dim3(1), 0, st, curmax, minmax, 0, is_train, ema_decay, first_batch,
-                     thr, qmax, nullptr);
+  hipLaunchKernelGGL(quant_state_multi_kernel, dim3(1), dim3(1), 0, st, curmax, minmax[0], minmax[NQ - 1], NQ,
+                     is_train, decay[0], decay[NQ - 1], first_batch, thr);
   const auto g = geo(8);
-  hipLaunchKernelGGL((bnq_codes_kernel<T, RELU>), dim3(gx, g.first), dim3(256), 0, st, (const T*)x, scale, shift, d->m,
-                     d->c, ct, g.second, (T*)out, (int8_t*)codes, thr, qmax, unit);
+  hipLaunchKernelGGL((bnq_codes_kernel<T, RELU, NQ>), dim3(gx, g.first), dim3(256), 0, st, (const T*)x, scale, shift,
+                     d->m, d->c, ct, g.second, tg, thr);
+}
+template <int NQ>
+static int quant_codes_bn(const rn_bn_desc* d, const void* x, const float* scale, const float* shift,
+                          const BnqTargets& tg, float* const* minmax, const float* decay, float* ws, int32_t is_train,
+                          int32_t first_batch, hipStream_t st) {
+  RN_CHECK_ARG(d && x && scale && shift && ws, "null argument");
+  RN_CHECK_ARG(d->dtype == RN_BF16 || d->dtype == RN_F32, "bad dtype");
+  RN_CHECK_ARG(d->m > 0 && d->c > 0 && d->c % 16 == 0, "bad shape (c must be a multiple of 16)");
+  for (int k = 0; k < NQ; ++k) RN_CHECK_ARG(tg.out[k] && tg.codes[k] && tg.unit[k] && minmax[k], "null argument");
+  const bool bf = d->dtype == RN_BF16;
+  if (d->relu) {
+    if (bf) launch_quant_codes_bn<bf16_t, true, NQ>(d, x, scale, shift, tg, minmax, decay, ws, is_train, first_batch, st);
+    else launch_quant_codes_bn<float, true, NQ>(d, x, scale, shift, tg, minmax, decay, ws, is_train, first_batch, st);
+  } else {
+    if (bf) launch_quant_codes_bn<bf16_t, false, NQ>(d, x, scale, shift, tg, minmax, decay, ws, is_train, first_batch, st);
+    else launch_quant_codes_bn<float, false, NQ>(d, x, scale, shift, tg, minmax, decay, ws, is_train, first_batch, st);
+  }
+  return rn_check_launch("quant_int8_fwd_codes_bn");
 }
 }  // extern "C++"
 
 int rn_quant_int8_fwd_codes_bn(const rn_bn_desc* d, const void* x, const float* scale, const float* shift, void* out,
                                void* codes, float* unit, float* minmax, int32_t is_train, float ema_decay,
                                int32_t first_batch, int32_t nbits, float* ws, rn_stream_t stream) {
-  RN_CHECK_ARG(d && x && scale && shift && out && codes && unit && minmax && ws, "null argument");
-  RN_CHECK_ARG(d->dtype == RN_BF16 || d->dtype == RN_F32, "bad dtype");
-  RN_CHECK_ARG(d->m > 0 && d->c > 0 && d->c % 16 == 0, "bad shape (c must be a multiple of 16)");
   RN_CHECK_ARG(nbits >= 2 && nbits <= 8, "int8 codes need nbits <= 8");
-  hipStream_t st = as_stream(stream);
-  const float qmax = (float)((1 << (nbits - 1)) - 1);
-  float* curmax = ws;  // zero on entry (left zero by the state kernel)
-  float* thr = ws + 1;
-  const bool bf = d->dtype == RN_BF16;
-  if (d->relu) {
-    if (bf) launch_quant_codes_bn<bf16_t, true>(d, x, scale, shift, out, codes, unit, curmax, thr, minmax, is_train,
-                                                ema_decay, first_batch, qmax, st);
-    else launch_quant_codes_bn<float, true>(d, x, scale, shift, out, codes, unit, curmax, thr, minmax, is_train,
-                                            ema_decay, first_batch, qmax, st);
-  } else {
-    if (bf) launch_quant_codes_bn<bf16_t, false>(d, x, scale, shift, out, codes, unit, curmax, thr, minmax, is_train,
-                                                 ema_decay, first_batch, qmax, st);
-    else launch_quant_codes_bn<float, false>(d, x, scale, shift, out, codes, unit, curmax, thr, minmax, is_train,
-                                             ema_decay, first_batch, qmax, st);
-  }
-  return rn_check_launch("quant_int8_fwd_codes_bn");
+  BnqTargets tg{{out, nullptr}, {(int8_t*)codes, nullptr}, {unit, nullptr}, {(float)((1 << (nbits - 1)) - 1), 1.f}};
+  float* mm[2] = {minmax, nullptr};
+  const float decay[2] = {ema_decay, 0.f};
+  return quant_codes_bn<1>(d, x, scale, shift, tg, mm, decay, ws, is_train, first_batch, as_stream(stream));
+}
+
+int rn_quant_int8_fwd_codes_bn2(const rn_bn_desc* d, const void* x, const float* scale, const float* shift,
+                                void* out, void* codes, float* unit, float* minmax, float ema_decay, int32_t nbits,
+                                void* out2, void* codes2, float* unit2, float* minmax2, float ema_decay2,
+                                int32_t nbits2, int32_t is_train, int32_t first_batch, float* ws, rn_stream_t stream) {
+  RN_CHECK_ARG(nbits >= 2 && nbits <= 8 && nbits2 >= 2 && nbits2 <= 8, "int8 codes need nbits <= 8");
+  BnqTargets tg{{out, out2}, {(int8_t*)codes, (int8_t*)codes2}, {unit, unit2},
+                {(float)((1 << (nbits - 1)) - 1), (float)((1 << (nbits2 - 1)) - 1)}};
+  float* mm[2] = {minmax, minmax2};
+  const float decay[2] = {ema_decay, ema_decay2};
+  return quant_codes_bn<2>(d, x, scale, shift, tg, mm, decay, ws, is_train, first_batch, as_stream(stream));
 }
 
 int rn_quant_int8_bwd(int32_t dtype, int64_t n, const void* x, const void* dy, void* dx, const float* minmax,

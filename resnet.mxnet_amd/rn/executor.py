@@ -911,16 +911,19 @@ class Executor:
         # quantizer applies the BN on load (rn_quant_int8_fwd_codes_bn, bit-identical) and the BN's
         # output is never written -- with the folded straight-through backward nothing reads it
         # (RN_QUANT_BN_FUSE=0: rn_bn_apply + rn_quant_int8_fwd_codes)
-        qbn = self._quant_folds() if os.environ.get("RN_QUANT_BN_FUSE", "1") == "1" else {}
+        groups = self._quant_groups() if os.environ.get("RN_QUANT_BN_FUSE", "1") == "1" else {}
         for op in plan.ops:
             op.bn_src = None
+            op.bn_peer = None  # the second quantizer of the same BN output (written by this op's call)
+            op.bn_lead = None  # (the quantizer whose call writes this one)
             if op.kind == "bn":
                 op.apply_in_quant = False
-        for op in plan.ops:
-            bn = qbn.get(id(op))
-            if bn is not None and op.emit_codes and bn.x.cp % 16 == 0:
-                op.bn_src = bn
+        for bn, qs in groups.values():
+            if all(q.emit_codes for q in qs) and bn.x.cp % 16 == 0:
                 bn.apply_in_quant = True
+                qs[0].bn_src = bn
+                if len(qs) == 2:
+                    qs[0].bn_peer, qs[1].bn_lead = qs[1], qs[0]
         for op in plan.ops:
             F, I = [], []  # train-mode, infer-mode call lists
             op.wsrc = self._weight_source(op, qwsp, sp) if getattr(op, "qweight", None) else \
@@ -1064,11 +1067,23 @@ class Executor:
                 I.append(c)
             elif op.kind == "quant":
                 q = op.q
-                if op.emit_codes:  # + the int8 codes and unit the consumers' int8 forward reads
-                    op.codes = self.torch.zeros(op.x.numel, dtype=self.torch.int8, device=self.device)
-                    op.unit = self._zeros(1, self.torch.float32)
+                for o in (op, op.bn_peer):
+                    if o is not None and o.emit_codes and getattr(o, "codes", None) is None:
+                        # + the int8 codes and unit the consumers' int8 forward reads
+                        o.codes = self.torch.zeros(o.x.numel, dtype=self.torch.int8, device=self.device)
+                        o.unit = self._zeros(1, self.torch.float32)
                 for lst, tr in ((F, 1), (I, 0)):
-                    if op.bn_src is not None:
+                    if op.bn_lead is not None:
+                        pass  # written by its peer's call
+                    elif op.bn_peer is not None:
+                        bn, o2 = op.bn_src, op.bn_peer
+                        lst.append(self._call("rn_quant_int8_fwd_codes_bn2", L.C.byref(bn.desc),
+                                              self._p(self.act(bn.x)), bn.sc, bn.sh, self._p(self.act(op.y)),
+                                              self._p(op.codes), self._p(op.unit), self._ap(q["minmax"]), q["ema"],
+                                              q["nbits"], self._p(self.act(o2.y)), self._p(o2.codes),
+                                              self._p(o2.unit), self._ap(o2.q["minmax"]), o2.q["ema"],
+                                              o2.q["nbits"], tr, self._qfirst, qwsp, sp))
+                    elif op.bn_src is not None:
                         bn = op.bn_src
                         lst.append(self._call("rn_quant_int8_fwd_codes_bn", L.C.byref(bn.desc),
                                               self._p(self.act(bn.x)), bn.sc, bn.sh, self._p(self.act(op.y)),
@@ -1234,44 +1249,54 @@ class Executor:
                 and d.c == d.c_real and d.c % 8 == 0 and op.y.c == d.c
                 and int(self.lib.rn_conv_tile(L.C.byref(d), 1)) >= 128)
 
-    def _quant_folds(self):
-        """{id(quant op): bn op} for the activation quantizers (Quantization_int8 of data, the int8 graph)
-        whose input is the output of a BatchNorm+ReLU that nothing else reads: their straight-through
-        backward (zero where the input is >= the moving threshold, clip_grad_quantization_int8.py) folds
-        into that BN's backward (rn_bn_desc.clip), so the quantizer costs no backward pass and the BN's
-        output gradient is the consumer conv's data gradient itself (which then reduces the BN backward
-        in its epilogue). RN_QUANT_BWD_FOLD=0: separate rn_quant_int8_bwd passes."""
+    def _quant_groups(self):
+        """{id(bn): (bn, [quant ops])} for the BatchNorm+ReLU outputs that only activation quantizers
+        (Quantization_int8 of data, the int8 graph) read -- one, or two (symbol/resnet_int8.py: a stage's
+        first unit quantizes act1 for conv1 and for the shortcut conv). Their straight-through backwards
+        (zero where the input is >= the moving threshold, clip_grad_quantization_int8.py) fold into that
+        BN's backward (rn_bn_desc.clip, and clip2 / dy2 for the second), so the quantizers cost no
+        backward pass, and their forwards apply the BN on load (rn_quant_int8_fwd_codes_bn[2]): the BN
+        output is never written. RN_QUANT_BWD_FOLD=0: separate rn_quant_int8_bwd passes."""
         if os.environ.get("RN_QUANT_BWD_FOLD", "1") != "1":
             return {}
         ops = self.plan.ops
-        readers = {}
+        readers, qreaders = {}, {}
         for o in ops:
             for k in ("x", "a", "b", "res", "label"):
                 t = getattr(o, k, None)
                 if isinstance(t, TensorSpec):
                     readers[id(t)] = readers.get(id(t), 0) + 1
-        bn_of = {id(o.y): o for o in ops if o.kind == "bn"}
+                    if o.kind == "quant" and k == "x" and not o.q.get("is_weight"):
+                        qreaders.setdefault(id(t), []).append(o)
         outs = {id(t) for t in self.plan.outputs}
-        folds = {}
-        for o in ops:
-            if o.kind != "quant" or o.q.get("is_weight"):
+        groups = {}
+        for bn in ops:
+            if bn.kind != "bn" or not bn.relu or id(bn.y) in outs or getattr(bn, "apply_fused", False):
                 continue
-            bn = bn_of.get(id(o.x))
-            if bn is None or not bn.relu or readers.get(id(o.x)) != 1 or id(o.x) in outs or \
-                    getattr(bn, "apply_fused", False):
-                continue
-            folds[id(o)] = bn
-        return folds
+            qs = qreaders.get(id(bn.y), [])
+            if qs and len(qs) == readers.get(id(bn.y)) and len(qs) <= 2:
+                groups[id(bn)] = (bn, qs)
+        return groups
+
+    def _quant_folds(self):
+        """{id(quant op): bn op} over _quant_groups (the quantizers whose backward folds into a BN's)."""
+        return {id(q): bn for bn, qs in self._quant_groups().values() for q in qs}
 
     def _build_backward(self):
         plan = self.plan
         sp = self._sp()
         gs = _GradState(self)
-        folds = self._quant_folds()
-        for qop in plan.ops:
-            bn = folds.get(id(qop))
-            if bn is not None:
-                bn.desc.clip = self._ap(qop.q["minmax"]).value  # (the threshold the forward just updated)
+        groups = self._quant_groups()
+        folds = {id(q): bn for bn, qs in groups.values() for q in qs}
+        for op in plan.ops:
+            if op.kind == "bn":
+                op.qpair = False
+                op.qorder = []  # the folded quantizers in backward order (their gradients' pending order)
+        for bn, qs in groups.values():
+            if len(qs) == 1:
+                bn.desc.clip = self._ap(qs[0].q["minmax"]).value  # (the threshold the forward just updated)
+            else:
+                bn.qpair = True  # clip / clip2 / dy2 set where its backward is bound
         wsp = self._p(self.ws)
         self.param_done_at = {}  # param -> index in self._bwd after which its grad is final
         self._gw = {}  # id(tensor) -> last writer of its gradient buffer: ("dgrad", call index, conv op)
@@ -1302,7 +1327,19 @@ class Executor:
             if op.kind == "softmax":
                 gs.has_value.add(id(op.x))  # dlogits written by the forward softmax call
                 continue
-            dy = gs.read(op.y) if op.kind != "softmax" else None
+            if op.kind == "bn" and op.qpair:
+                # two folded quantizers: their output gradients stay separate (dy, rn_bn_desc.dy2)
+                assert id(op.y) not in gs.has_value
+                pend = gs.pending.pop(id(op.y), [])
+                if not pend:
+                    continue
+                dy = pend[0]
+                op.desc.clip = self._ap(op.qorder[0].q["minmax"]).value
+                if len(pend) == 2:
+                    op.desc.clip2 = self._ap(op.qorder[1].q["minmax"]).value
+                    op.desc.dy2 = self._p(pend[1]).value
+            else:
+                dy = gs.read(op.y) if op.kind != "softmax" else None
             if dy is None:
                 continue
             if op.kind == "fc":
@@ -1363,7 +1400,7 @@ class Executor:
                                                 self._p(dy), self._p(out), self._p(add), self._pp(op.gamma),
                                                 self._ap(op.mean), self._ap(op.var), op.sc, op.sh,
                                                 self._gp(op.gamma), self._gp(op.beta), wsp, sp))
-                elif bwd_fusion and w and w[0] == "dgrad" and dy is w[4] and \
+                elif bwd_fusion and not op.desc.dy2 and w and w[0] == "dgrad" and dy is w[4] and \
                         op.y.c % 8 == 0 and op.y.c == op.y.cp and (bwd_all or self._big_tile(w[2], 1)) and \
                         (not op.desc.clip or self._big_tile(w[2], 1)):  # (the clip: bf16 LDS-DMA tiles)
                     # the conv dgrad that completes this BN's output gradient also reduces its backward
@@ -1401,7 +1438,7 @@ class Executor:
                                                     op.bnred_blocks, self._p(self.act(x)), self._p(dy), self._p(out),
                                                     self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc, op.sh,
                                                     self._gp(op.gamma), self._gp(op.beta), wsp, sp))
-                elif getattr(op, "pre_part", None) is not None:
+                elif getattr(op, "pre_part", None) is not None and not op.desc.dy2:
                     # the reduction was done by the residual add's ReLU backward (rn_relu_bwd_bnred)
                     self._bwd.append(self._call("rn_bn_bwd_part", L.C.byref(op.desc), self._p(op.pre_part),
                                                 op.pre_nrb, self._p(self.act(x)), self._p(dy), self._p(out),
@@ -1433,7 +1470,11 @@ class Executor:
                     # straight-through: the gradient passes unchanged to the BN output, whose backward
                     # applies the clip; the conv that wrote dy stays its last writer (BN reduction fusion)
                     gs.alias(op.x, dy)
-                    if id(op.y) in self._gw:
+                    bn = folds[id(op)]
+                    bn.qorder.append(op)
+                    if bn.qpair:
+                        self._gw[id(op.x)] = ("other",)
+                    elif id(op.y) in self._gw:
                         self._gw[id(op.x)] = self._gw[id(op.y)]
                 elif op.x.needs_grad:
                     out, add = gs.contribute(op.x)

@@ -29,7 +29,8 @@ class ConvDesc(C.Structure):
 
 class BNDesc(C.Structure):
     _fields_ = [("dtype", _i32), ("m", _i64), ("c", _i32), ("c_real", _i32), ("eps", _f32), ("momentum", _f32),
-                ("fix_gamma", _i32), ("relu", _i32), ("clip", _P)]
+                ("fix_gamma", _i32), ("relu", _i32), ("clip", _P),
+                ("clip2", _P), ("dy2", _P)]
 
 
 class PoolDesc(C.Structure):
@@ -99,6 +100,8 @@ SIGNATURES = {
     "rn_quant_int8_fwd": (_i32, [_i32, _i64, _P, _P, _P, _i32, _i32, _f32, _i32, _i32, _P, _P]),
     "rn_quant_int8_fwd_codes": (_i32, [_i32, _i64, _P, _P, _P, _P, _P, _i32, _i32, _f32, _i32, _i32, _P, _P]),
     "rn_quant_int8_fwd_codes_bn": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _i32, _f32, _i32, _i32, _P, _P]),
+    "rn_quant_int8_fwd_codes_bn2": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _f32, _i32, _P, _P, _P, _P, _f32, _i32,
+                                           _i32, _i32, _P, _P]),
     "rn_quant_int8_bwd": (_i32, [_i32, _i64, _P, _P, _P, _P, _i32, _P, _P]),
     "rn_set_tuning": (_i32, [_i32, _i32]),
     "rn_last_error": (C.c_char_p, []),

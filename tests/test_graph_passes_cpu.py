@@ -150,11 +150,13 @@ def test_int8_forward_plan(dry, monkeypatch):
     fed by the quantizer's codes (rn_quant_int8_fwd_codes); the stem (quantizer folded into its
     im2col) and fc1 stay on the fake-quant path; RN_INT8_MFMA=0 turns it off."""
     shape = (2, 3, 64, 64)
-    for sym, nconv in ((graphs.resnet_int8(*R50_SMALL.values()), 52),
+    # npair: BNs whose output two quantizers read (resnet_int8's first units: conv1 and the shortcut
+    # each quantize act1; attach_quantize_node shares one quantizer per tensor)
+    for sym, nconv, npair in ((graphs.resnet_int8(*R50_SMALL.values()), 52, 4),
                        (attach_quantize_node(graphs.resnet(**R50_SMALL), shape_dict(graphs.resnet(**R50_SMALL), shape,
                                                                                      (2,)),
                                              QSET["weight"], QSET["act"], ("Convolution", "FullyConnected"),
-                                             {"Convolution": 1, "FullyConnected": 1}), 52)):
+                                             {"Convolution": 1, "FullyConnected": 1}), 52, 0)):
         for prec in ("float32", "bfloat16"):
             ex = _bind(sym, shape, precision=prec).executor
             convs = [op for op in ex.plan.ops if op.kind == "conv"]
@@ -166,10 +168,13 @@ def test_int8_forward_plan(dry, monkeypatch):
             assert _call_names(ex._fwd_infer).count("rn_conv_fwd_i8") == nconv
             qops = [op for op in ex.plan.ops if op.kind == "quant"]
             # every conv's data quantizer emits codes (fc1's, in resnet_int8, does not)
-            nbn = names.count("rn_quant_int8_fwd_codes_bn")
-            assert names.count("rn_quant_int8_fwd_codes") + nbn == sum(op.emit_codes for op in qops) >= len(qops) - 1
-            # quantizers of a BN+ReLU output nothing else reads apply that BN on load; its output is not written
-            assert nbn == sum(op.bn_src is not None for op in qops) > 0
+            nbn, nbn2 = names.count("rn_quant_int8_fwd_codes_bn"), names.count("rn_quant_int8_fwd_codes_bn2")
+            assert names.count("rn_quant_int8_fwd_codes") + nbn + 2 * nbn2 == sum(op.emit_codes for op in qops) \
+                >= len(qops) - 1
+            # quantizers of a BN+ReLU output nothing else reads apply that BN on load (one call for the
+            # two quantizers of a stage's first unit); the BN output is not written
+            assert nbn + nbn2 == sum(op.bn_src is not None for op in qops) > 0
+            assert nbn2 == sum(op.bn_peer is not None for op in qops) == npair
             assert all(op.bn_src.apply_in_quant and op.bn_src.y is op.x for op in qops if op.bn_src is not None)
             assert _call_names(ex.packs).count("rn_conv_weight_pack_i8") == nconv
     monkeypatch.setenv("RN_INT8_MFMA", "0")

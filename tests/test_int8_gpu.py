@@ -199,3 +199,92 @@ def test_quant_codes_bn_fused(gpu, dtype, relu, m, c):
         if train:
             yv = y.float()
             assert outs[1][3].item() != 2.5 and yv.abs().max().item() > 0
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("m,c", [(3136, 64), (1001, 48)])
+def test_quant_codes_bn_pair(gpu, dtype, m, c):
+    """rn_quant_int8_fwd_codes_bn2 (the two quantizers of one BN output, symbol/resnet_int8.py's first
+    units: conv1 and the shortcut) == rn_bn_apply + rn_quant_int8_fwd_codes twice, bit for bit: both
+    quantizers' values, codes, units and EMA states (different states, decays and nbits)."""
+    rng = np.random.default_rng(m + c + 1)
+    x = torch.tensor(rng.standard_normal((m, c)) * 3.0, dtype=tdt(dtype), device=gpu)
+    sc = torch.tensor(rng.standard_normal(c) * 0.7, dtype=torch.float32, device=gpu)
+    sh = torch.tensor(rng.standard_normal(c) * 0.5, dtype=torch.float32, device=gpu)
+    d = L.BNDesc(dtype=dtype, m=m, c=c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1)
+    n = m * c
+    y = torch.zeros_like(x)
+    ws = torch.zeros(4096, dtype=torch.float32, device=gpu)
+    qs = [(2.5, 0.99, 8), (1.25, 0.9, 4)]  # (minmax state, ema decay, nbits) of the two quantizers
+    for train in (1, 0):
+        res = []
+        for fused in (False, True):
+            bufs = [(torch.full_like(x, float("nan")), torch.zeros(n, dtype=torch.int8, device=gpu),
+                     torch.zeros(1, dtype=torch.float32, device=gpu),
+                     torch.tensor([mm0], dtype=torch.float32, device=gpu)) for mm0, _, _ in qs]
+            if fused:
+                (o1, c1, u1, m1), (o2, c2, u2, m2) = bufs
+                L.call("rn_quant_int8_fwd_codes_bn2", C.byref(d), p(x), p(sc), p(sh), p(o1), p(c1), p(u1), p(m1),
+                       qs[0][1], qs[0][2], p(o2), p(c2), p(u2), p(m2), qs[1][1], qs[1][2], train, 0, p(ws), stream())
+            else:
+                L.call("rn_bn_apply", C.byref(d), p(x), p(y), p(sc), p(sh), stream())
+                for (o, cd, u, mm), (_, dec, nb) in zip(bufs, qs):
+                    L.call("rn_quant_int8_fwd_codes", dtype, n, p(y), p(o), p(cd), p(u), p(mm), 0, train, dec, 0, nb,
+                           p(ws), stream())
+            res.append(bufs)
+        torch.cuda.synchronize()
+        for b0, b1 in zip(*res):
+            for a, b in zip(b0, b1):
+                assert torch.equal(a, b)
+        assert ws[0].item() == 0.0
+        assert not torch.equal(res[1][0][1], res[1][1][1])  # (8 and 4 bits: different codes)
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("use_global", [False, True])
+def test_bn_backward_quant_pair_fold(gpu, dtype, use_global):
+    """The two quantizers of one BN+ReLU output folded into its backward (rn_bn_desc.clip / clip2 / dy2):
+    rn_bn_bwd[_global] == two rn_quant_int8_bwd summing into one buffer followed by rn_bn_bwd[_global]
+    without clips, bit for bit (dx, dgamma, dbeta); rn_bn_bwd_part refuses dy2."""
+    n, c, h, w = 3, 96, 13, 11
+    rng = np.random.default_rng(41)
+    xb = rng.standard_normal((n, c, h, w)) * 1.5 + 0.3
+    lib = L.load()
+    f = lambda a: torch.tensor(np.asarray(a, np.float64), dtype=torch.float32, device=gpu)
+    g_d, b_d = f(rng.uniform(0.5, 1.5, c)), f(rng.standard_normal(c) * 0.2)
+    mm, mv = f(rng.standard_normal(c) * 0.1), f(rng.uniform(0.8, 1.2, c))
+    sm, si, sc, sh = [torch.zeros(c, dtype=torch.float32, device=gpu) for _ in range(4)]
+    bd = L.BNDesc(dtype=dtype, m=n * h * w, c=c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1)
+    ws = torch.zeros(lib.rn_bn_workspace_bytes(C.byref(bd)) // 4 + 16, dtype=torch.float32, device=gpu)
+    xbd = to_nhwc(xb, dtype, gpu)
+    act = torch.zeros_like(xbd)
+    if use_global:
+        L.call("rn_bn_fwd_infer", C.byref(bd), p(xbd), p(act), p(g_d), p(b_d), p(mm), p(mv), p(sc), p(sh), stream())
+    else:
+        L.call("rn_bn_fwd_train", C.byref(bd), p(xbd), p(act), p(g_d), p(b_d), p(mm), p(mv), p(sm), p(si), p(sc),
+               p(sh), p(ws), stream())
+    torch.cuda.synchronize()
+    a_np = from_nhwc(act, c)
+    t1, t2 = (float(np.quantile(a_np[a_np > 0], qq)) for qq in (0.6, 0.85))
+    tq1, tq2 = (torch.tensor([t], dtype=torch.float32, device=gpu) for t in (t1, t2))
+    dy1, dy2 = (to_nhwc(rng.standard_normal((n, c, h, w)), dtype, gpu) for _ in range(2))
+    zf = lambda: torch.zeros(c, dtype=torch.float32, device=gpu)
+    bwd = "rn_bn_bwd_global" if use_global else "rn_bn_bwd"
+    stats = (p(mm), p(mv)) if use_global else (p(sm), p(si))
+    g = torch.zeros_like(xbd)
+    L.call("rn_quant_int8_bwd", dtype, act.numel(), p(act), p(dy2), p(g), p(tq2), 0, None, stream())
+    L.call("rn_quant_int8_bwd", dtype, act.numel(), p(act), p(dy1), p(g), p(tq1), 0, p(g), stream())
+    dx0, dg0, db0 = torch.zeros_like(xbd), zf(), zf()
+    L.call(bwd, C.byref(bd), p(xbd), p(g), p(dx0), None, p(g_d), *stats, p(sc), p(sh), p(dg0), p(db0), p(ws), stream())
+    bdp = L.BNDesc(dtype=dtype, m=n * h * w, c=c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1,
+                   clip=tq1.data_ptr(), clip2=tq2.data_ptr(), dy2=dy2.data_ptr())
+    dx1, dg1, db1 = torch.zeros_like(xbd), zf(), zf()
+    L.call(bwd, C.byref(bdp), p(xbd), p(dy1), p(dx1), None, p(g_d), *stats, p(sc), p(sh), p(dg1), p(db1), p(ws),
+           stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1) and torch.equal(dg0, dg1) and torch.equal(db0, db1)
+    pos = act > 0
+    assert ((g == 0) & pos).float().sum().item() > 0.05 * pos.float().sum().item()  # the clips bit
+    part = torch.zeros(64, dtype=torch.float32, device=gpu)
+    assert lib.rn_bn_bwd_part(C.byref(bdp), p(part), 1, p(xbd), p(dy1), p(dx1), None, p(g_d), p(sm), p(si), p(sc),
+                              p(sh), p(dg1), p(db1), p(ws), stream()) != 0

@@ -144,10 +144,12 @@ def test_plan_int8_quantization(monkeypatch):
     ex = Executor(Plan(graphs.resnet_int8([1, 1, 1, 1], 4, [64, 256, 512, 1024, 2048], 16),
                        [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")
     names = [c[0] for c in ex._bwd]
-    # 8 of the 17 activation quantizers read a BN+ReLU output nothing else reads: their straight-through
-    # backward is folded into that BN's backward (rn_bn_desc.clip); RN_QUANT_BWD_FOLD=0 keeps all 17
-    assert names.count("rn_quant_int8_bwd") == 9 and names.count("rn_stem_quant_clip_grad") == 1
-    assert sum(1 for op in ex.plan.ops if op.kind == "bn" and op.desc.clip) == 8
+    # 16 of the 17 activation quantizers read a BN+ReLU output only quantizers read -- one (8 BNs) or
+    # two (the 4 units' act1: conv1 and the shortcut): their straight-through backwards fold into that
+    # BN's backward (rn_bn_desc.clip, + clip2 / dy2); fc1's stays. RN_QUANT_BWD_FOLD=0 keeps all 17
+    assert names.count("rn_quant_int8_bwd") == 1 and names.count("rn_stem_quant_clip_grad") == 1
+    assert sum(1 for op in ex.plan.ops if op.kind == "bn" and op.desc.clip) == 12
+    assert sum(1 for op in ex.plan.ops if op.kind == "bn" and op.desc.dy2 and op.desc.clip2) == 4
     monkeypatch.setenv("RN_QUANT_BWD_FOLD", "0")
     ex = Executor(Plan(graphs.resnet_int8([1, 1, 1, 1], 4, [64, 256, 512, 1024, 2048], 16),
                        [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")
