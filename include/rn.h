@@ -442,6 +442,25 @@ int rn_quant_int8_fwd_codes_bn2(const rn_bn_desc* d, const void* x, const float*
                                 int32_t nbits, void* out2, void* codes2, float* unit2, float* minmax2,
                                 float ema_decay2, int32_t nbits2, int32_t is_train, int32_t first_batch,
                                 float* ws, rn_stream_t stream);
+/* One weight of rn_weight_quant_pack: the fp32 master (KRSC, c_real channels) of a Quantization_int8
+ * weight (int8_api.py:131-132, per-tensor threshold t = max|w|) and the copies written from it. */
+typedef struct rn_wquant_item {
+  const float* master; /* k * rs * c_real fp32                                         */
+  float* qw;           /* fake-quantized copy round(w/unit)*unit, unit = t/qmax (required) */
+  float* unit;         /* nullable: unit                                                */
+  float* minmax;       /* nullable: the threshold state (:= t)                          */
+  int8_t* w_codes;     /* nullable: int8 codes, KRSC, channel stride c (rn_conv_weight_pack_i8) */
+  void* w_crsk;        /* nullable: data-gradient compute copy of qw, dense CRSK with k_pad
+                        * stride (rn_conv_weight_pack's w_crsk), dtype of the call            */
+  int32_t k, rs, c_real, c, k_pad, nbits;
+} rn_wquant_item;
+/* Every weight quantizer of a network in three launches (max|w| of each tensor, the thresholds, the
+ * copies) instead of rn_quant_int8_fwd_codes + rn_conv_weight_pack + rn_conv_weight_pack_i8 per
+ * weight: bit-identical to those. items: DEVICE array of count entries; ws: >= 2*count floats, the
+ * first count zero on entry (left zero: the quantizers' shared workspace). The padding of w_codes /
+ * w_crsk (channels >= c_real, columns >= k) is not written (zero from their first pack). */
+int rn_weight_quant_pack(const rn_wquant_item* items, int32_t count, int32_t dtype, float* ws,
+                         rn_stream_t stream);
 /* STE backward: dx = dy (weights) or dy * (|x| <= t) (activations). */
 int rn_quant_int8_bwd(int32_t dtype, int64_t n, const void* x, const void* dy, void* dx,
                       const float* minmax, int32_t is_weight, const void* add_src,

@@ -1944,54 +1944,97 @@ __global__ void stem_quant_state_kernel(float* __restrict__ curmax, float* minma
 // rn_stem_shift_grad sums the unmasked gradient; subtract the clipped elements' share:
 // dbeta[c] -= dx[n,c,h,w] at every clipped (n,c,h,w), dx = sum_{k,r,s} w[k,r,s,c] dy[n,p,q,k].
 template <typename T>
-__global__ void stem_clip_grad_kernel(const float* __restrict__ x, const float* __restrict__ scale,
-                                      const float* __restrict__ shift, const float* __restrict__ thr,
-                                      const T* __restrict__ dy, const float* __restrict__ wq,
-                                      float* __restrict__ dbeta, int N, int C, int H, int W, int P, int Q, int K,
-                                      int kpad, int R, int S, int sh, int sw, int ph, int pw) {
-  // A wave tests 64 consecutive input elements, then processes each clipped one (ballot) together:
-  // lanes over the output channels k (coalesced dy rows), taps in a uniform loop, one wave sum and
-  // one atomic per clipped element (no lane runs a long gather while the other 63 wait).
+__global__ __launch_bounds__(256) void stem_clip_grad_kernel(const float* __restrict__ x,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift,
+                                                             const float* __restrict__ thr, const T* __restrict__ dy,
+                                                             const float* __restrict__ wq, float* __restrict__ dbeta,
+                                                             int N, int C, int H, int W, int P, int Q, int K, int kpad,
+                                                             int R, int S, int sh, int sw, int ph, int pw) {
+  // A wave tests 256 consecutive input elements (a 16-byte load per lane), then processes each clipped
+  // one (ballot) together: lanes over the output channels k (coalesced dy rows, the weights from an
+  // LDS copy laid out [c][r][s][k] so lane k reads consecutive words), taps in a uniform loop, one wave
+  // sum per clipped element. Image data saturates (pixel value 255 IS the max), so a few 0.1 % of the
+  // elements clip: the gathers, not the scan, set this kernel's time.
+  extern __shared__ float wl[];
+  __shared__ float wsum[4][8];
+  const int RSK = R * S * K, nwl = C * RSK;
+  for (int i = threadIdx.x; i < nwl; i += blockDim.x) {
+    const int k = i % K, rest = i / K;
+    const int s_ = rest % S, rr = rest / S;
+    const int r = rr % R, c = rr / R;
+    wl[i] = wq[((k * R + r) * S + s_) * C + c];
+  }
+  if (threadIdx.x < 32) wsum[threadIdx.x >> 3][threadIdx.x & 7] = 0.f;
+  __syncthreads();
   const float t = *thr;
   const int HW = H * W, total = N * C * HW;
   const int lane = threadIdx.x & 63;
-  // per-wave channel sums in LDS (the stem has C <= 8 channels: per-element atomics on them would
-  // serialise), one atomic per channel and block at the end
-  __shared__ float wsum[4][8];
-  if (threadIdx.x < 32) wsum[threadIdx.x >> 3][threadIdx.x & 7] = 0.f;
-  __syncthreads();
-  const int nw = gridDim.x * (blockDim.x >> 6);
-  for (int base = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; base < total; base += nw * 64) {
-    const int i = base + lane;
-    bool clipped = false;
-    if (i < total) {
-      const int c = (i / HW) % C;
-      const float v = scale ? fmaf(x[i], scale[c], shift[c]) : x[i];
-      clipped = !(v > -t && v < t);
-    }
-    uint64_t m = __ballot(clipped);
-    while (m) {
-      const int e = base + __ffsll((unsigned long long)m) - 1;
-      m &= m - 1;
-      const int plane = e / HW, hw = e - plane * HW;
-      const int c = plane % C, n = plane / C, h = hw / W, w = hw - (hw / W) * W;
-      float g = 0.f;
-      for (int r = 0; r < R; ++r) {
-        const int hp = h + ph - r;
-        if (hp < 0 || hp % sh) continue;
-        const int pp = hp / sh;
-        if (pp >= P) continue;
-        for (int s_ = 0; s_ < S; ++s_) {
-          const int wp = w + pw - s_;
-          if (wp < 0 || wp % sw) continue;
-          const int qq = wp / sw;
-          if (qq >= Q) continue;
-          const T* dyp = dy + (((int64_t)n * P + pp) * Q + qq) * kpad;
-          for (int k = lane; k < K; k += 64) g += wq[((int64_t)(k * R + r) * S + s_) * C + c] * to_f(dyp[k]);
-        }
+  // taps of an input pixel: r = r0 + a*sh (a < ceil(R/sh) <= 4), s likewise; all 16 dy rows are
+  // loaded before the products (one memory latency per clipped element, not one per tap)
+  // (e is wave-uniform: the index arithmetic -- a few integer divisions -- runs once per element on the
+  // scalar unit; per tap only adds: row p = (h + ph) / sh - a for r = (h + ph) % sh + a * sh)
+  auto gather = [&](int e_) {  // -sum over the clipped element's taps, wave-reduced
+    const int e = __builtin_amdgcn_readfirstlane(e_);
+    const int plane = e / HW, hw = e - plane * HW;
+    const int n = plane / C, c = plane - n * C, h = hw / W, w = hw - h * W;
+    const int hq = (h + ph) / sh, wq_ = (w + pw) / sw;
+    const int r0 = h + ph - hq * sh, s0 = w + pw - wq_ * sw;
+    const T* dyn = dy + (int64_t)n * P * Q * kpad + lane;
+    float dv[4][4];
+    int wo[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const int r = r0 + a * sh, s_ = s0 + b * sw;
+        const int pp = hq - a, qq = wq_ - b;
+        const bool ok = lane < K && r < R && s_ < S && pp >= 0 && qq >= 0 && pp < P && qq < Q;
+        dv[a][b] = ok ? to_f(dyn[(pp * Q + qq) * kpad]) : 0.f;
+        wo[a][b] = ok ? ((c * R + r) * S + s_) * K + lane : 0;
       }
-      g = wave_sum(g);
-      if (lane == 0) wsum[threadIdx.x >> 6][c] -= g;
+    float g = 0.f;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) g = fmaf(wl[wo[a][b]], dv[a][b], g);
+    g = wave_sum(g);
+    if (lane == 0) wsum[threadIdx.x >> 6][c] -= g;
+  };
+  auto clipped_at = [&](float xv, int e) {
+    const int c = (e / HW) % C;
+    const float v = scale ? fmaf(xv, scale[c], shift[c]) : xv;
+    return !(v > -t && v < t);
+  };
+  const int nv = total / 4;  // 16-byte chunks, then the tail
+  const int nwaves = gridDim.x * (blockDim.x >> 6);
+  for (int base = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64; base < nv; base += nwaves * 64) {
+    const int i = base + lane;
+    bool cl[4] = {false, false, false, false};
+    if (i < nv) {
+      const float4 v4 = reinterpret_cast<const float4*>(x)[i];
+      cl[0] = clipped_at(v4.x, 4 * i);
+      cl[1] = clipped_at(v4.y, 4 * i + 1);
+      cl[2] = clipped_at(v4.z, 4 * i + 2);
+      cl[3] = clipped_at(v4.w, 4 * i + 3);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint64_t m = __ballot(cl[j]);
+      while (m) {
+        const int b = __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        gather(4 * (base + b) + j);
+      }
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < 64) {  // the last total % 4 elements: wave 0 of block 0
+    const int e = 4 * nv + lane;
+    uint64_t m = __ballot(e < total && clipped_at(x[e], e));
+    while (m) {
+      const int b = __ffsll((unsigned long long)m) - 1;
+      m &= m - 1;
+      gather(4 * nv + b);
     }
   }
   __syncthreads();
@@ -3032,13 +3075,19 @@ int rn_stem_quant_clip_grad(const rn_conv_desc* d, const float* x, const float* 
   const int64_t total = (int64_t)d->n * d->c_real * d->h * d->w;
   RN_CHECK_ARG(total < (1ll << 31) - 64, "input exceeds 2^31 elements");
   RN_CHECK_ARG(d->c_real <= 8, "the quantized stem has at most 8 input channels");
-  const int planes = grid_for(total);  // (blocks of 4 waves x 64 elements)
+  RN_CHECK_ARG(((uintptr_t)x & 15) == 0, "x must be 16-byte aligned");
+  const size_t lds = (size_t)d->c_real * d->r * d->s * d->k * sizeof(float);  // the weights, [c][r][s][k]
+  RN_CHECK_ARG(lds <= 64 * 1024, "stem weights exceed the LDS copy (c*r*s*k <= 16384)");
+  RN_CHECK_ARG(d->k <= 64 && (d->r + d->stride_h - 1) / d->stride_h <= 4 && (d->s + d->stride_w - 1) / d->stride_w <= 4,
+               "the quantized stem: k <= 64 and at most 4 x 4 taps per input pixel");
+  // blocks of 4 waves x 256 elements; at most ~8 per CU, each stages the weights once
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 1023) / 1024, 2048));
   if (d->dtype == RN_BF16)
-    hipLaunchKernelGGL(stem_clip_grad_kernel<bf16_t>, dim3(planes), dim3(256), 0, st, x, scale, shift,
+    hipLaunchKernelGGL(stem_clip_grad_kernel<bf16_t>, dim3(blocks), dim3(256), lds, st, x, scale, shift,
                        minmax, (const bf16_t*)dy, w_q, dbeta, d->n, d->c_real, d->h, d->w, d->p, d->q, d->k, d->k_pad,
                        d->r, d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w);
   else
-    hipLaunchKernelGGL(stem_clip_grad_kernel<float>, dim3(planes), dim3(256), 0, st, x, scale, shift,
+    hipLaunchKernelGGL(stem_clip_grad_kernel<float>, dim3(blocks), dim3(256), lds, st, x, scale, shift,
                        minmax, (const float*)dy, w_q, dbeta, d->n, d->c_real, d->h, d->w, d->p, d->q, d->k, d->k_pad,
                        d->r, d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w);
   return rn_check_launch("stem_quant_clip_grad");

@@ -619,6 +619,75 @@ __global__ __launch_bounds__(256) void bnq_codes_kernel(const T* __restrict__ x,
     }
   }
 }
+// ---- batched weight quantization (rn_weight_quant_pack): blockIdx.y = weight
+__global__ __launch_bounds__(256) void wq_absmax_kernel(const rn_wquant_item* __restrict__ items,
+                                                        float* __restrict__ curmax) {
+  const rn_wquant_item it = items[blockIdx.y];
+  const int64_t n = (int64_t)it.k * it.rs * it.c_real;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  float m = 0.f;
+  int64_t i0 = 0;
+  if ((reinterpret_cast<uintptr_t>(it.master) & 15) == 0) {  // 16-byte chunks, then the tail
+    const int64_t nc = n / 4;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nc; i += stride) {
+      const float4 v = reinterpret_cast<const float4*>(it.master)[i];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+    i0 = nc * 4;
+  }
+  for (int64_t i = i0 + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride)
+    m = fmaxf(m, fabsf(it.master[i]));
+  m = wave_max(m);
+  __shared__ float wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(reinterpret_cast<unsigned int*>(curmax + blockIdx.y),
+              __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
+}
+__global__ void wq_state_kernel(const rn_wquant_item* __restrict__ items, int count, float* __restrict__ ws) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= count) return;
+  const rn_wquant_item it = items[j];
+  const float t = quant_state_update(ws[j], it.minmax, 1, 1, 0.f, 0);
+  ws[count + j] = t;
+  ws[j] = 0.f;
+  if (it.unit) it.unit[0] = t / (float)((1 << (it.nbits - 1)) - 1);
+}
+template <typename T>
+__global__ __launch_bounds__(256) void wq_pack_kernel(const rn_wquant_item* __restrict__ items, int count,
+                                                      const float* __restrict__ ws) {
+  const rn_wquant_item it = items[blockIdx.y];
+  const float t = ws[count + blockIdx.y];
+  const float qmax = (float)((1 << (it.nbits - 1)) - 1);
+  const float unit = t / qmax;  // (quant_value's and the codes' unit)
+  const int RS = it.rs, cr = it.c_real;
+  const int64_t n = (int64_t)it.k * RS * cr;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  // master order: the fake-quantized copy and the int8 codes (KRSC, channel stride c)
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float q = unit > 0.f ? roundf(it.master[i] / unit) : 0.f;
+    it.qw[i] = q * unit;
+    if (it.w_codes) {
+      const int64_t kt = i / cr;
+      it.w_codes[kt * it.c + (i - kt * cr)] = (int8_t)(int)q;
+    }
+  }
+  // CRSK order (coalesced stores): the data-gradient copy of the fake-quantized values
+  if (it.w_crsk) {
+    T* out = reinterpret_cast<T*>(it.w_crsk);
+    const int64_t m = (int64_t)cr * RS * it.k;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += stride) {
+      const int k = (int)(i % it.k);
+      const int64_t ct = i / it.k;  // c*RS + tap
+      const int tap = (int)(ct % RS), ci = (int)(ct / RS);
+      const float v = it.master[((int64_t)k * RS + tap) * cr + ci];
+      const float q = unit > 0.f ? roundf(v / unit) : 0.f;
+      out[ct * it.k_pad + k] = from_f<T>(q * unit);
+    }
+  }
+}
+
 // the threshold states of NQ quantizers of one tensor from its max (consumed and re-zeroed)
 __global__ void quant_state_multi_kernel(float* __restrict__ curmax, float* minmax0, float* minmax1, int nq,
                                          int is_train, float decay0, float decay1, int first, float* __restrict__ thr) {
@@ -1102,6 +1171,20 @@ int rn_quant_int8_fwd_codes_bn2(const rn_bn_desc* d, const void* x, const float*
   float* mm[2] = {minmax, minmax2};
   const float decay[2] = {ema_decay, ema_decay2};
   return quant_codes_bn<2>(d, x, scale, shift, tg, mm, decay, ws, is_train, first_batch, as_stream(stream));
+}
+
+int rn_weight_quant_pack(const rn_wquant_item* items, int32_t count, int32_t dtype, float* ws,
+                         rn_stream_t stream) {
+  RN_CHECK_ARG(items && ws && count > 0 && count <= 65535, "bad arguments");
+  RN_CHECK_ARG(dtype == RN_BF16 || dtype == RN_F32, "bad dtype");
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(wq_absmax_kernel, dim3(64, count), dim3(256), 0, st, items, ws);
+  hipLaunchKernelGGL(wq_state_kernel, dim3((count + 63) / 64), dim3(64), 0, st, items, count, ws);
+  if (dtype == RN_BF16)
+    hipLaunchKernelGGL(wq_pack_kernel<bf16_t>, dim3(64, count), dim3(256), 0, st, items, count, ws);
+  else
+    hipLaunchKernelGGL(wq_pack_kernel<float>, dim3(64, count), dim3(256), 0, st, items, count, ws);
+  return rn_check_launch("weight_quant_pack");
 }
 
 int rn_quant_int8_bwd(int32_t dtype, int64_t n, const void* x, const void* dy, void* dx, const float* minmax,

@@ -864,6 +864,9 @@ class Executor:
         ws_bytes = 64
         self._descs = []  # keep ctypes structs alive
         self.packs = []   # weight pack calls (bind time / set_params)
+        # every weight quantizer in one rn_weight_quant_pack (RN_WQUANT_BATCH=0: three calls per weight)
+        self._wq_batch = os.environ.get("RN_WQUANT_BATCH", "1") == "1"
+        self._wq_ops = []
         self.fused_packs = {}  # param -> rn_wpack fields: copies rewritten by the SGD kernel itself
         self.unfused_packs = []  # packs that still run after every update (grouped, fake-quantized)
         self.bn_state = {}
@@ -1002,13 +1005,14 @@ class Executor:
                     # forward copy: the int8 codes (KRSC); the data-gradient copy stays the
                     # fake-quantized values in the compute dtype (STE backward)
                     op.wk = None
-                    self._add_pack(op, d, None, op.wc, sp)
                     op.wk8 = self.torch.zeros(int(self.lib.rn_conv_pack_numel(L.C.byref(d), 0)),
                                               dtype=self.torch.int8, device=self.device)
-                    c_ = self._call("rn_conv_weight_pack_i8", L.C.byref(d), self._pp(op.weight), self._p(op.wunit),
-                                    self._p(op.wk8), sp)
-                    self.packs.append(c_)
-                    self.unfused_packs.append(c_)
+                    if not self._wq_batch:  # (batched: written by rn_weight_quant_pack)
+                        self._add_pack(op, d, None, op.wc, sp)
+                        c_ = self._call("rn_conv_weight_pack_i8", L.C.byref(d), self._pp(op.weight),
+                                        self._p(op.wunit), self._p(op.wk8), sp)
+                        self.packs.append(c_)
+                        self.unfused_packs.append(c_)
                 else:
                     op.wk = self._zeros(self.lib.rn_conv_pack_numel(L.C.byref(d), 0), self.tdtype)
                     self._add_pack(op, d, op.wk, op.wc, sp)
@@ -1152,6 +1156,26 @@ class Executor:
             self._fwd_train.extend(F)
             self._fwd_infer.extend(I)
         self.stem_ws = self._zeros(stem_ws, self.torch.float32)
+        if self._wq_ops:
+            items = []
+            for op in self._wq_ops:
+                shape = self.plan.param_shape(op.weight)
+                k, creal = shape[0], shape[1]
+                rs = int(np.prod(shape[2:])) if len(shape) > 2 else 1
+                i8 = getattr(op, "int8", False)
+                d = op.desc if i8 else None
+                assert not i8 or (d.groups <= 1 and d.k == k and d.c_real == creal and d.r * d.s == rs)
+                items.append(L.WQuantItem(
+                    master=self._pp(op.weight).value, qw=op.qw.data_ptr(),
+                    unit=op.wunit.data_ptr() if i8 else None, minmax=self._ap(op.qweight["minmax"]).value,
+                    w_codes=op.wk8.data_ptr() if i8 else None, w_crsk=op.wc.data_ptr() if i8 else None,
+                    k=k, rs=rs, c_real=creal, c=d.c if i8 else creal, k_pad=d.k_pad if i8 else k,
+                    nbits=int(op.qweight["nbits"])))
+            arr = (L.WQuantItem * len(items))(*items)
+            self._wq_items = self.torch.frombuffer(bytearray(arr), dtype=self.torch.uint8).to(self.device)
+            c_ = self._call("rn_weight_quant_pack", self._p(self._wq_items), len(items), self.dtype, qwsp, sp)
+            self.packs.insert(0, c_)
+            self.unfused_packs.insert(0, c_)
 
     def _big_tile(self, op, mode, min_cols=None):
         """Does conv `op` run its forward (mode 0) / data gradient (mode 1) on a 256/224-row LDS-DMA
@@ -1207,6 +1231,12 @@ class Executor:
         op.qw = self._zeros(n, self.torch.float32)
         if getattr(op, "int8", False):  # also keeps the unit for the int8 codes of the forward copy
             op.wunit = self._zeros(1, self.torch.float32)
+        if self._wq_batch:
+            # one batched rn_weight_quant_pack for every weight quantizer (built after the forward):
+            # the fake-quantized copy, and for the int8 convs their codes and data-gradient copy too
+            self._wq_ops.append(op)
+            return self._p(op.qw)
+        if getattr(op, "int8", False):
             c = self._call("rn_quant_int8_fwd_codes", F32, n, self._pp(op.weight), self._p(op.qw), None,
                            self._p(op.wunit), self._ap(q["minmax"]), 1, 1, q["ema"], 0, q["nbits"], qwsp, sp)
         else:

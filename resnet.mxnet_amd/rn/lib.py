@@ -33,6 +33,11 @@ class BNDesc(C.Structure):
                 ("clip2", _P), ("dy2", _P)]
 
 
+class WQuantItem(C.Structure):
+    _fields_ = [("master", _P), ("qw", _P), ("unit", _P), ("minmax", _P), ("w_codes", _P), ("w_crsk", _P),
+                ("k", _i32), ("rs", _i32), ("c_real", _i32), ("c", _i32), ("k_pad", _i32), ("nbits", _i32)]
+
+
 class PoolDesc(C.Structure):
     _fields_ = [(n, _i32) for n in ("dtype", "n", "h", "w", "c", "r", "s", "stride_h", "stride_w", "pad_h", "pad_w",
                                    "type", "global_pool", "p", "q")]
@@ -102,6 +107,7 @@ SIGNATURES = {
     "rn_quant_int8_fwd_codes_bn": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _i32, _f32, _i32, _i32, _P, _P]),
     "rn_quant_int8_fwd_codes_bn2": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _f32, _i32, _P, _P, _P, _P, _f32, _i32,
                                            _i32, _i32, _P, _P]),
+    "rn_weight_quant_pack": (_i32, [_P, _i32, _i32, _P, _P]),
     "rn_quant_int8_bwd": (_i32, [_i32, _i64, _P, _P, _P, _P, _i32, _P, _P]),
     "rn_set_tuning": (_i32, [_i32, _i32]),
     "rn_last_error": (C.c_char_p, []),

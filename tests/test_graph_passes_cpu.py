@@ -176,7 +176,10 @@ def test_int8_forward_plan(dry, monkeypatch):
             assert nbn + nbn2 == sum(op.bn_src is not None for op in qops) > 0
             assert nbn2 == sum(op.bn_peer is not None for op in qops) == npair
             assert all(op.bn_src.apply_in_quant and op.bn_src.y is op.x for op in qops if op.bn_src is not None)
-            assert _call_names(ex.packs).count("rn_conv_weight_pack_i8") == nconv
+            # every weight quantizer (+ the int8 convs' codes and data-gradient copies) in one batched call
+            packs = _call_names(ex.packs)
+            assert packs[0] == "rn_weight_quant_pack" and "rn_conv_weight_pack_i8" not in packs
+            assert len(ex._wq_ops) >= nconv and sum(op.int8 for op in ex._wq_ops if op.kind == "conv") == nconv
     monkeypatch.setenv("RN_INT8_MFMA", "0")
     ex = _bind(graphs.resnet_int8(*R50_SMALL.values()), shape).executor
     assert "rn_conv_fwd_i8" not in _call_names(ex._fwd_train)

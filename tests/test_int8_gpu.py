@@ -288,3 +288,51 @@ def test_bn_backward_quant_pair_fold(gpu, dtype, use_global):
     part = torch.zeros(64, dtype=torch.float32, device=gpu)
     assert lib.rn_bn_bwd_part(C.byref(bdp), p(part), 1, p(xbd), p(dy1), p(dx1), None, p(g_d), p(sm), p(si), p(sc),
                               p(sh), p(dg1), p(db1), p(ws), stream()) != 0
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+def test_weight_quant_pack_batched(gpu, dtype):
+    """rn_weight_quant_pack (every weight quantizer in three launches) == per weight
+    rn_quant_int8_fwd_codes + rn_conv_weight_pack (CRSK) + rn_conv_weight_pack_i8, bit for bit: the
+    fake-quantized copies, units, threshold states, int8 codes and data-gradient copies; an unaligned
+    master (a flat parameter buffer's offset) and items without codes / copies (stem, fc)."""
+    rng = np.random.default_rng(5)
+    # (k, c, r, nbits, int8 conv): 1x1 / 3x3 / ragged channels (c_real < c) / an fc-like item
+    shapes = [(64, 64, 1, 8, True), (48, 40, 3, 8, True), (24, 16, 3, 4, True), (10, 20, 1, 8, False)]
+    total = sum(k * c * r * r for k, c, r, _, _ in shapes) + 1
+    master = torch.tensor(rng.standard_normal(total) * 0.1, dtype=torch.float32, device=gpu)
+    ws = torch.zeros(4096, dtype=torch.float32, device=gpu)
+    items, refs, off = [], [], 1  # (offset 1: a master not 16-byte aligned)
+    for k, c, r, nb, i8 in shapes:
+        n = k * c * r * r
+        wm = master[off:off + n]
+        off += n
+        d = conv_desc(dtype, 2, c, 8, 8, k, r, r, 1, r // 2)
+        bufs = {}
+        for tag in ("a", "b"):
+            bufs[tag] = dict(qw=torch.zeros(n, device=gpu), unit=torch.zeros(1, device=gpu),
+                             mm=torch.zeros(1, device=gpu),
+                             codes=torch.zeros(k * r * r * d.c, dtype=torch.int8, device=gpu) if i8 else None,
+                             wc=torch.zeros(d.c * r * r * d.k_pad, dtype=tdt(dtype), device=gpu) if i8 else None)
+        a = bufs["a"]
+        L.call("rn_quant_int8_fwd_codes", F32, n, p(wm), p(a["qw"]), None, p(a["unit"]), p(a["mm"]), 1, 1, 0.99, 0,
+               nb, p(ws), stream())
+        if i8:
+            L.call("rn_conv_weight_pack", C.byref(d), p(a["qw"]), None, p(a["wc"]), stream())
+            L.call("rn_conv_weight_pack_i8", C.byref(d), p(wm), p(a["unit"]), p(a["codes"]), stream())
+        b = bufs["b"]
+        items.append(L.WQuantItem(master=wm.data_ptr(), qw=b["qw"].data_ptr(), unit=b["unit"].data_ptr(),
+                                  minmax=b["mm"].data_ptr(), w_codes=b["codes"].data_ptr() if i8 else None,
+                                  w_crsk=b["wc"].data_ptr() if i8 else None, k=k, rs=r * r, c_real=c,
+                                  c=d.c, k_pad=d.k_pad, nbits=nb))
+        refs.append(bufs)
+    arr = (L.WQuantItem * len(items))(*items)
+    dev = torch.frombuffer(bytearray(arr), dtype=torch.uint8).to(gpu)
+    L.call("rn_weight_quant_pack", p(dev), len(items), dtype, p(ws), stream())
+    torch.cuda.synchronize()
+    assert not ws[:len(items)].any()
+    for bufs in refs:
+        for key in ("qw", "unit", "mm", "codes", "wc"):
+            if bufs["a"][key] is not None:
+                assert torch.equal(bufs["a"][key], bufs["b"][key]), key
+    assert refs[0]["b"]["unit"].item() > 0

@@ -155,6 +155,12 @@ def test_plan_int8_quantization(monkeypatch):
                        [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")
     assert [c[0] for c in ex._bwd].count("rn_quant_int8_bwd") == 17
     packs = [c[0] for c in ex.packs]
+    # (one batched rn_weight_quant_pack by default; RN_WQUANT_BATCH=0: per weight, counted here)
+    assert packs == ["rn_weight_quant_pack"] + packs[1:] and "rn_quant_int8_fwd" not in packs
+    monkeypatch.setenv("RN_WQUANT_BATCH", "0")
+    ex = Executor(Plan(graphs.resnet_int8([1, 1, 1, 1], 4, [64, 256, 512, 1024, 2048], 16),
+                       [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")
+    packs = [c[0] for c in ex.packs]
     # the 16 non-stem convs' weight quantizers also keep the unit of their int8 codes (int8 forward)
     assert packs.count("rn_quant_int8_fwd") + packs.count("rn_quant_int8_fwd_codes") == 18
     assert packs.count("rn_conv_weight_pack_i8") == 16
