@@ -161,7 +161,12 @@ int64_t rn_conv_pack_numel(const rn_conv_desc* d, int32_t which);
  * Grouped (groups > 1, symbol/resnext.py:23-25 num_group=32): the copies are block-diagonal
  * over RN_GROUP_BLOCK-wide column blocks -- for output column j the reduction runs over the
  * channels of the groups that j's 64-column block touches, zero outside j's own group
- * (w_krsc: [k][r][s][cblk], w_crsk: [c][r][s][kblk]); sizes from rn_conv_pack_numel. */
+ * (w_krsc: [k][r][s][cblk], w_crsk: [c][r][s][kblk]); sizes from rn_conv_pack_numel.
+ * Except where the direct grouped kernel runs (bf16, 3x3 pad 1, c = k, 4 channels per group -- forward
+ * stride 1 / 2, data gradient stride 1 -- or 8 per group, forward stride 2; rn_set_tuning 15): that
+ * mode's copy is compact, [c/8][tap][8][G] with G = c/groups -- w_krsc[k/8][tap][k%8][c'] =
+ * w[k][tap][c'], w_crsk[c/8][tap][c%8][k'] = w[g*G + k'][8 - tap][c - g*G], g = c/G -- and
+ * rn_conv_fwd / rn_conv_bwd_data multiply it with v_dot2_f32_bf16 (no bias, statistics or BN fusions). */
 int rn_conv_weight_pack(const rn_conv_desc* d, const float* w_master, void* w_krsc, void* w_crsk,
                         rn_stream_t stream);
 
@@ -494,7 +499,10 @@ const char* rn_last_error(void);
  * 14 = the same for their bf16 weight gradients (64 x 64 tile: only the two diagonal 32 x 32 blocks,
  *      each wave one of them over half of each M stage; 0 = on, 1 = off, 2 = on, the
  *      diagonal blocks on two of the four waves),
- * 15, 16 = (reserved: round-3 conv-tile experiments, measured and removed -- DESIGN.md §3),
+ * 15 = grouped convolutions with 4 channels per group (ResNeXt 32x4d stage 1; 8 per group at
+ *      stride 2): the direct v_dot2 kernels and their weight copies (0 = on, 1 = the block-diagonal
+ *      64-column tiles; set it before rn_conv_weight_pack: the copies of the two paths differ),
+ * 16 = (reserved: a round-3 conv-tile experiment, measured and removed -- DESIGN.md §3),
  * 17 = deterministic weight gradients (1 = on): every M-split of every weight gradient stores its
  *      partial tile into the workspace slab (rn_conv_bwd_filter_ws / _x; rn_conv_wgrad_ws_bytes is
  *      > 0 for every layer then, fp32 included) and one pass sums the splits in a fixed order, instead

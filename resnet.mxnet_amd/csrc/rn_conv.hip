@@ -1876,6 +1876,123 @@ inline int group_blk(int gcol, int gred) {
   return (gcol >= RN_GROUP_BLOCK ? 1 : RN_GROUP_BLOCK / gcol) * gred;
 }
 
+// ---- direct grouped 3x3 convolution: ResNeXt's 4 channels per group (symbol/resnext.py:23-25,
+// num_group 32 at width 128; and the 8-per-group stride-2 forward). Block-diagonal MFMA tiles spend
+// 15/16 of their products on zeros there; these layers need only 2 x 9 x G multiply-adds per byte, so
+// VALU v_dot2_f32_bf16 (two bf16 products into fp32) on 16-byte channel chunks runs them near memory
+// speed. Lane = (8-channel chunk, pixel lane): one wave instruction reads whole pixel rows
+// (coalesced); a pixel lane computes PL consecutive output pixels of one row from the (PL-1)*ST+3
+// input columns of each tap row (register reuse across the 3 horizontal taps and the PL pixels;
+// interior windows skip the bounds tests); every chunk's weights sit in LDS, [chunk][tap][8 outputs]
+// [G inputs] -- the compact compute copy (rn_conv_weight_pack). The data gradient of a stride-1 layer
+// is the same kernel over dy with the group-transposed, tap-flipped copy (mode 1). (An MFMA variant --
+// one wave per 16-channel chunk, tap pairs as the reduction, operands straight from global memory --
+// measured 2x slower: its 32-byte-per-pixel loads touch 32 cache lines per wave instruction.)
+typedef __bf16 __attribute__((ext_vector_type(2))) gd_bf2;
+__device__ __forceinline__ float gd_dot(uint32_t x, uint32_t w, float acc) {
+  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(gd_bf2, x), __builtin_bit_cast(gd_bf2, w), acc, false);
+}
+struct GdArgs {
+  const bf16_t* x;
+  const bf16_t* w;
+  bf16_t* y;
+  const bf16_t* add;
+  int H, W, C, P, Q, pad, lcpr, qb;  // input H x W, output P x Q, C channels (= 8 << lcpr), qb = ceil(Q / PL)
+  uint32_t items;                    // N * P * qb pixel-lane work items
+  FastDiv fdQB, fdP;
+};
+template <int G, int ST, int PL>
+__global__ __launch_bounds__(256) void grouped_direct_kernel(GdArgs a) {
+  extern __shared__ uint4 gd_w[];
+  const int nw16 = a.C * 9 * G * 2 / 16;
+  for (int i = threadIdx.x; i < nw16; i += blockDim.x) gd_w[i] = reinterpret_cast<const uint4*>(a.w)[i];
+  __syncthreads();
+  constexpr int NC = (PL - 1) * ST + 3;
+  const int lane = threadIdx.x & 63;
+  const int chunk = lane & ((1 << a.lcpr) - 1), pl = lane >> a.lcpr;
+  const int plw = 64 >> a.lcpr;
+  const uint4* wc = gd_w + chunk * 9 * G;
+  const uint32_t step = gridDim.x * (blockDim.x >> 6) * plw;
+  const int64_t cstep = a.C;
+  for (uint32_t it = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * plw + pl; it < a.items; it += step) {
+    const uint32_t t = fdiv(it, a.fdQB);
+    const int q0 = (int)(it - t * a.qb) * PL;
+    const uint32_t n = fdiv(t, a.fdP);
+    const int p = (int)(t - n * a.P);
+    const int w0 = q0 * ST - a.pad;
+    const bool inner_w = w0 >= 0 && w0 + NC <= a.W;
+    float acc[PL][8];
+#pragma unroll
+    for (int j = 0; j < PL; ++j)
+#pragma unroll
+      for (int o = 0; o < 8; ++o) acc[j][o] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const int h = p * ST - a.pad + r;
+      if (h < 0 || h >= a.H) continue;
+      const bf16_t* xrow = a.x + ((int64_t)(n * a.H + h) * a.W + w0) * cstep + chunk * 8;
+      uint4 xc[NC];
+      if (inner_w) {
+#pragma unroll
+        for (int ci = 0; ci < NC; ++ci) xc[ci] = *reinterpret_cast<const uint4*>(xrow + ci * cstep);
+      } else {
+#pragma unroll
+        for (int ci = 0; ci < NC; ++ci) {
+          const int w = w0 + ci;
+          xc[ci] = (w >= 0 && w < a.W) ? *reinterpret_cast<const uint4*>(xrow + ci * cstep) : make_uint4(0, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int s_ = 0; s_ < 3; ++s_) {
+        uint4 wv[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u) wv[u] = wc[(r * 3 + s_) * G + u];
+        const uint32_t* wp = reinterpret_cast<const uint32_t*>(wv);  // pair jj of output o: wp[o * G / 2 + jj]
+#pragma unroll
+        for (int j = 0; j < PL; ++j) {
+          const uint4 xv = xc[j * ST + s_];
+          const uint32_t xp[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+          for (int o = 0; o < 8; ++o) {
+            const int gb = G == 4 ? (o >> 2) * 2 : 0;  // first input pair of output o's group in the chunk
+#pragma unroll
+            for (int jj = 0; jj < G / 2; ++jj) acc[j][o] = gd_dot(xp[gb + jj], wp[o * (G / 2) + jj], acc[j][o]);
+          }
+        }
+      }
+    }
+    const int64_t obase = ((int64_t)(n * a.P + p) * a.Q + q0) * cstep + chunk * 8;
+#pragma unroll
+    for (int j = 0; j < PL; ++j) {
+      if (q0 + j >= a.Q) break;
+      const int64_t off = obase + j * cstep;
+      if (a.add) {
+        float f[8];
+        chunk_to_f(*reinterpret_cast<const uint4*>(a.add + off), f, (const bf16_t*)nullptr);
+#pragma unroll
+        for (int o = 0; o < 8; ++o) acc[j][o] += f[o];
+      }
+      *reinterpret_cast<uint4*>(a.y + off) = f_to_chunk(acc[j], (const bf16_t*)nullptr);
+    }
+  }
+}
+// compact compute copies of a direct grouped convolution (9 taps, G = cpg = kpg channels per group):
+// mode 0: out[k/8][tap][k%8][c'] = w[k][tap][c']; mode 1 (stride-1 data gradient): out[c/8][tap][c%8][k']
+// = w[g*G + k'][8 - tap][c - g*G], g = c / G (the group's outputs for input c, taps flipped)
+__global__ void pack_group_direct_kernel(const float* __restrict__ wm, bf16_t* __restrict__ out, int C, int G,
+                                         int transpose) {
+  const int total = C * 9 * G;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int u = i % G, t = i / G;
+    const int o = t % 8, t2 = t / 8;
+    const int tap = t2 % 9, col = (t2 / 9) * 8 + o;
+    const int g = col / G;
+    const float v = transpose ? wm[((int64_t)(g * G + u) * 9 + (8 - tap)) * G + (col - g * G)]
+                              : wm[((int64_t)col * 9 + tap) * G + u];
+    out[i] = f2bf(v);
+  }
+}
+
 // thread per (row m, 16-byte output chunk): 8 (bf16) / 4 (f32) consecutive im2col columns
 template <typename T>
 __global__ __launch_bounds__(256) void im2col_nchw_kernel(const float* __restrict__ x, const float* __restrict__ scale,
@@ -2491,6 +2608,57 @@ __global__ void pack_krsc_i8_kernel(const float* __restrict__ wm, const float* _
   }
 }
 
+// Does the grouped convolution d run the direct kernel in mode 0 (forward) / 1 (data gradient)?
+// Its compute copy of that mode is then the compact one (pack_group_direct_kernel). rn_set_tuning 15 = 1:
+// the block-diagonal MFMA path (set before packing: the two paths' copies differ).
+// Does the grouped convolution d run the direct kernel in mode 0 (forward) / 1 (data gradient)? Its
+// compute copy of that mode is then the compact one (pack_group_direct_kernel). Where it pays (measured,
+// ResNeXt-50 at batch 256): 4 channels per group -- forward stride 1 / 2, data gradient stride 1 -- and
+// the 8-per-group stride-2 forward; with 8 (stride 1) or 16 per group the v_dot2 work outgrows the
+// memory time and the block-diagonal MFMA tiles win. rn_set_tuning 15 = 1: never (set before packing:
+// the two paths' copies differ).
+bool gd_direct_ok(const rn_conv_desc* d, int mode) {
+  if (!d || d->dtype != RN_BF16 || d->groups <= 1 || g_tune[RN_TUNE_GROUP_DIRECT] == 1) return false;
+  const int cpg = d->c / d->groups;
+  if (d->c != d->c_real || d->k != d->c || d->k_pad != d->k || d->c % d->groups || (cpg != 4 && cpg != 8)) return false;
+  if (d->r != 3 || d->s != 3 || d->pad_h != 1 || d->pad_w != 1 || d->stride_h != d->stride_w) return false;
+  if (d->c % 8 || 64 % (d->c / 8) || (int64_t)d->c * 9 * cpg * 2 > 64 * 1024) return false;
+  if (cpg == 8) return mode == 0 && d->stride_h == 2;
+  if (mode == 0) return d->stride_h == 1 || d->stride_h == 2;
+  return mode == 1 && d->stride_h == 1;
+}
+
+int gd_launch(const rn_conv_desc* d, int mode, const void* x, const void* w, void* y, const void* add,
+              hipStream_t st) {
+  GdArgs a{};
+  a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.y = (bf16_t*)y; a.add = (const bf16_t*)add;
+  a.C = d->c;
+  if (mode == 0) { a.H = d->h; a.W = d->w; a.P = d->p; a.Q = d->q; a.pad = d->pad_h; }
+  else { a.H = d->p; a.W = d->q; a.P = d->h; a.Q = d->w; a.pad = d->r - 1 - d->pad_h; }
+  int lcpr = 0;
+  while ((8 << lcpr) < d->c) ++lcpr;
+  a.lcpr = lcpr;
+  const int cpg = d->c / d->groups;
+  const int stride = mode == 0 ? d->stride_h : 1;
+  const int PL = cpg == 4 && stride == 1 ? 8 : 4;
+  a.qb = (a.Q + PL - 1) / PL;
+  const int64_t items = (int64_t)d->n * a.P * a.qb;
+  RN_CHECK_ARG(items < INT32_MAX && (int64_t)d->n * a.H * a.W * a.C < INT32_MAX, "grouped direct: tensor too large");
+  a.items = (uint32_t)items;
+  a.fdQB = make_fastdiv(a.qb); a.fdP = make_fastdiv(a.P);
+  const int plw = 64 >> lcpr;
+  const int64_t want = (items + 4 * plw - 1) / (4 * plw);
+  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, 1024));
+  const size_t lds = (size_t)d->c * 9 * cpg * 2;
+  if (cpg == 4 && stride == 1)
+    hipLaunchKernelGGL((grouped_direct_kernel<4, 1, 8>), dim3(blocks), dim3(256), lds, st, a);
+  else if (cpg == 4)
+    hipLaunchKernelGGL((grouped_direct_kernel<4, 2, 4>), dim3(blocks), dim3(256), lds, st, a);
+  else
+    hipLaunchKernelGGL((grouped_direct_kernel<8, 2, 4>), dim3(blocks), dim3(256), lds, st, a);
+  return rn_check_launch(mode == 0 ? "grouped_direct_fwd" : "grouped_direct_dgrad");
+}
+
 }  // namespace
 
 extern "C" {
@@ -2532,6 +2700,7 @@ int64_t rn_conv_weight_numel(const rn_conv_desc* d) {
 
 int64_t rn_conv_pack_numel(const rn_conv_desc* d, int32_t which) {
   const int64_t RS = (int64_t)d->r * d->s;
+  if (gd_direct_ok(d, which)) return (int64_t)d->c * 9 * (d->c / d->groups);  // (compact, see rn.h)
   if (d->groups > 1) {
     const int cpg = d->c / d->groups, kpg = d->k / d->groups;
     return which == 0 ? d->k * RS * group_blk(kpg, cpg) : d->c * RS * group_blk(cpg, kpg);
@@ -2545,6 +2714,10 @@ int rn_conv_fwd_x(const rn_conv_desc* d, const void* x, const void* w, void* y, 
   RN_CHECK_ARG(d && x && w && y, "null argument");
   RN_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "in_scale / in_shift must both be set");
   RN_CHECK_ARG(!in_scale || d->groups == 1, "input transform on a grouped conv");
+  if (gd_direct_ok(d, 0)) {
+    RN_CHECK_ARG(!bias && !part && y_dtype == RN_BF16, "grouped direct forward: no bias / statistics, bf16 output");
+    return gd_launch(d, 0, x, w, y, add_src, as_stream(stream));
+  }
   IgemmArgs a = make_igemm_args(d, 0);
   a.x = x; a.w = w; a.y = y; a.add = add_src; a.bias = bias; a.stats = part;
   a.in_sc = in_scale; a.in_sh = in_shift;
@@ -2594,7 +2767,7 @@ int rn_conv_fwd_bnstats(const rn_conv_desc* d, const void* x, const void* w, voi
 
 int32_t rn_conv_tile(const rn_conv_desc* d, int32_t mode) {
   if (d && mode == 2 && d->groups <= 1) return i8_tile_cols(make_igemm_args(d, 0));  // int8 forward
-  if (!d || d->dtype != RN_BF16 || (mode != 0 && mode != 1)) return 0;
+  if (!d || d->dtype != RN_BF16 || (mode != 0 && mode != 1) || gd_direct_ok(d, mode)) return 0;
   const IgemmArgs a = make_igemm_args(d, mode);
   const int64_t xb = (int64_t)a.N * a.H * a.W * a.C * 2, wb = (int64_t)a.K * a.wrow * 2;
   return big_tile_cols(a, xb, wb);
@@ -2632,6 +2805,10 @@ int rn_conv_bwd_data_bnred_clip(const rn_conv_desc* d, const void* dy, const voi
                "the quantizer clip is folded into a bf16 BN+ReLU reduction on an LDS-DMA tile");
   RN_CHECK_ARG(d && dy && w_crsk && (dx || (part && !add_src)), "null argument");
   RN_CHECK_ARG(dx || rn_conv_tile(d, 1) >= 128, "a reduction-only dgrad (dx = NULL) needs the 224/256-row tile");
+  if (gd_direct_ok(d, 1)) {
+    RN_CHECK_ARG(!part && dx, "grouped direct data gradient: no BatchNorm reduction");
+    return gd_launch(d, 1, dy, w_crsk, dx, add_src, as_stream(stream));
+  }
   IgemmArgs a = make_igemm_args(d, 1);
   a.x = dy; a.w = w_crsk; a.y = dx; a.add = add_src; a.bias = nullptr;
   if (part) {
@@ -2981,6 +3158,11 @@ int rn_conv_weight_pack(const rn_conv_desc* d, const float* wm, void* w_krsc, vo
     for (int which = 0; which < 2; ++which) {
       void* out = which == 0 ? w_krsc : w_crsk;
       if (!out) continue;
+      if (gd_direct_ok(d, which)) {
+        hipLaunchKernelGGL(pack_group_direct_kernel, dim3(grid_for((int64_t)d->c * 9 * cpg)), dim3(256), 0, st, wm,
+                           (bf16_t*)out, d->c, cpg, which);
+        continue;
+      }
       const int ncols = which == 0 ? d->k : d->c;
       const int gcol = which == 0 ? kpg : cpg, gred = which == 0 ? cpg : kpg;
       const int cblk = group_blk(gcol, gred);

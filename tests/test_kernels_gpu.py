@@ -428,6 +428,63 @@ def test_grouped_conv(gpu, dtype, case):
     assert rel_err(dw_h, dw_ref) < (TOL[dtype] if dtype == F32 else 5e-3)
 
 
+@pytest.mark.parametrize("case", [
+    (2, 128, 9, 9, 128, 3, 1, 1, 32),     # 4 per group (stage 1), fwd + dgrad direct
+    (3, 128, 15, 13, 128, 3, 1, 1, 32),   # ragged rows (13 = 3 blocks of 4 pixels + 1)
+    (2, 256, 10, 10, 256, 3, 2, 1, 32),   # 8 per group, stride 2: direct forward, block-diagonal dgrad
+    (2, 256, 7, 11, 256, 3, 1, 1, 32),    # 8 per group, stride 1
+    (2, 128, 12, 12, 128, 3, 2, 1, 32),   # 4 per group, stride 2
+    (2, 512, 6, 7, 512, 3, 1, 1, 32),     # 16 per group (stage 3)
+    (2, 512, 9, 9, 512, 3, 2, 1, 32),     # 16 per group, stride 2
+    (1, 64, 5, 5, 64, 3, 1, 1, 8),        # 8 per group, fewer channels than a wave has lanes
+])
+def test_grouped_conv_direct(gpu, case):
+    """The direct grouped kernels (rn_set_tuning 15 = 0: v_dot2_f32_bf16 over 16-byte channel chunks,
+    compact weight copies; 4 per group, and 8 per group at stride 2 forward) vs the oracle and vs the
+    block-diagonal 64-column tiles (15 = 1): forward and data gradient with an add_src (the residual /
+    gradient accumulation operand), both within one bf16 rounding of the fp64 values. (8 per group at
+    stride 1 and 16 per group run the block-diagonal tiles either way.)"""
+    n, c, h, w, k, r, st, pd, g = case
+    rng = np.random.default_rng(13)
+    x = bf16_round(rng.standard_normal((n, c, h, w)))
+    wt = bf16_round(rng.standard_normal((k, c // g, r, r)) / np.sqrt(c // g * r * r))
+    P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+    dy = bf16_round(rng.standard_normal((n, k, P, Q)))
+    ya = bf16_round(rng.standard_normal((n, k, P, Q)))
+    xa = bf16_round(rng.standard_normal((n, c, h, w)))
+    d = L.ConvDesc(dtype=BF16, n=n, h=h, w=w, c=c, c_real=c, k=k, k_pad=k, r=r, s=r, stride_h=st, stride_w=st,
+                   pad_h=pd, pad_w=pd, groups=g)
+    L.call("rn_conv_desc_init", C.byref(d))
+    lib = L.load()
+    master = _master_krsc(wt, gpu)
+    xd, dyd, yad, xad = (to_nhwc(v, BF16, gpu) for v in (x, dy, ya, xa))
+    outs = {}
+    for mode in (0, 1):
+        L.call("rn_set_tuning", 15, mode)
+        try:
+            if mode == 0:
+                if c // g == 4 or (c // g == 8 and st == 2):  # the direct forward: compact [c/8][9][8][G] copy
+                    assert lib.rn_conv_pack_numel(C.byref(d), 0) == c * 9 * (c // g)
+                    assert lib.rn_conv_tile(C.byref(d), 0) == 0
+            wk = torch.zeros(lib.rn_conv_pack_numel(C.byref(d), 0), dtype=torch.bfloat16, device=gpu)
+            wc = torch.zeros(lib.rn_conv_pack_numel(C.byref(d), 1), dtype=torch.bfloat16, device=gpu)
+            L.call("rn_conv_weight_pack", C.byref(d), p(master), p(wk), p(wc), stream())
+            y = torch.zeros((n, P, Q, k), dtype=torch.bfloat16, device=gpu)
+            dx = torch.zeros((n, h, w, c), dtype=torch.bfloat16, device=gpu)
+            L.call("rn_conv_fwd", C.byref(d), p(xd), p(wk), p(y), BF16, p(yad), None, stream())
+            L.call("rn_conv_bwd_data", C.byref(d), p(dyd), p(wc), p(dx), p(xad), stream())
+            torch.cuda.synchronize()
+        finally:
+            L.call("rn_set_tuning", 15, 0)
+        outs[mode] = (from_nhwc(y, k), from_nhwc(dx, c))
+    y_ref = ops.conv2d_fwd(x, wt, (st, st), (pd, pd), g) + ya
+    dx_ref = ops.conv2d_bwd(x, wt, dy, (st, st), (pd, pd), g)[0] + xa
+    for mode in (0, 1):
+        assert np.abs(outs[mode][0] - y_ref).max() <= 2 ** -7 * np.abs(y_ref).max(), mode
+        assert np.abs(outs[mode][1] - dx_ref).max() <= 2 ** -7 * np.abs(dx_ref).max(), mode
+    assert rel_err(outs[0][0], outs[1][0]) < 4e-3 and rel_err(outs[0][1], outs[1][1]) < 4e-3
+
+
 def _im2col_ref(xq, r, st, pd, kc):
     n, c, h, w = xq.shape
     P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
@@ -1167,6 +1224,14 @@ def test_grouped_conv_zero_block_skip(gpu, case):
     are exact zeros, so forward and data gradient equal the unskipped tile's values exactly; the weight
     gradient (fp32 atomics over the M splits: summation order varies) to fp32 rounding."""
     n, c, h, w, k, r, st, pd, g = case
+    L.call("rn_set_tuning", 15, 1)  # (4 / 8 channels per group: the block-diagonal path, not the direct one)
+    try:
+        _zero_block_skip(gpu, n, c, h, w, k, r, st, pd, g)
+    finally:
+        L.call("rn_set_tuning", 15, 0)
+
+
+def _zero_block_skip(gpu, n, c, h, w, k, r, st, pd, g):
     rng = np.random.default_rng(12)
     x = bf16_round(rng.standard_normal((n, c, h, w)))
     wt = bf16_round(rng.standard_normal((k, c // g, r, r)) / np.sqrt(c // g * r * r))
