@@ -502,7 +502,9 @@ const char* rn_last_error(void);
  * 15 = grouped convolutions with 4 channels per group (ResNeXt 32x4d stage 1; 8 per group at
  *      stride 2): the direct v_dot2 kernels and their weight copies (0 = on, 1 = the block-diagonal
  *      64-column tiles; set it before rn_conv_weight_pack: the copies of the two paths differ),
- * 16 = (reserved: a round-3 conv-tile experiment, measured and removed -- DESIGN.md §3),
+ * 16 = 1: block barriers around the LDS staging of the 224/256-row tiles' epilogue (default 0: each
+ *      wave waits only for its own staged rows; the paired-row BatchNorm-statistics epilogue keeps
+ *      its barriers either way),
  * 17 = deterministic weight gradients (1 = on): every M-split of every weight gradient stores its
  *      partial tile into the workspace slab (rn_conv_bwd_filter_ws / _x; rn_conv_wgrad_ws_bytes is
  *      > 0 for every layer then, fp32 included) and one pass sums the splits in a fixed order, instead

@@ -56,6 +56,7 @@ struct IgemmArgs {
   int smallc, lgc, rs; // fwd over C < one stage (the stem's 8 channels): k = tap*C + c flattened
   int diag_l1;         // diagnostic (rn_set_tuning 3): every A row reads the same L1-resident chunk
   int sched;           // igemm_big_kernel schedule experiments (rn_set_tuning 7, bit mask)
+  int epi_sync;        // igemm_big_kernel: block barriers around the epilogue's LDS staging (rn_set_tuning 16)
   int ntiles;          // igemm_big_kernel persistent mode: tiles per class (0: one tile per workgroup)
   int x_bytes, w_bytes;  // LDS-DMA buffer descriptors
   // dgrad only, nullable: the BatchNorm-backward reduction of the gradient this conv completes
@@ -1106,7 +1107,13 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
           if (col0 + 8 <= p.K) xpre[k] = *reinterpret_cast<const uint4*>(bxg + off[k]);
       }
     }
-    if (h > 0) __syncthreads();  // the first half's staged rows have been read
+    // Each wave stages through its own LDS region, so the epilogue needs no block barrier -- a wave's
+    // LDS accesses execute in order, and its reads of a half have returned before the next half's
+    // writes issue -- except where wave row 1 reads wave row 0's pivot row (EPI 1 on paired rows).
+    // rn_set_tuning 16 = 1: block barriers everywhere (the previous form, for A/B).
+    constexpr bool XW = EPI == 1 && PAIR;
+    const bool blk_sync = XW || p.epi_sync;
+    if (h > 0 && blk_sync) __syncthreads();  // the first half's staged rows have been read
     if constexpr (M32) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -1127,7 +1134,8 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
               ep[(i * 16 + (lane >> 4) * 4 + e) * EP_LD + j * 16 + (lane & 15)] =
                   Q8 ? (float)acc[h * 4 + i][j][e] * qscale : (float)acc[h * 4 + i][j][e];
     }
-    __syncthreads();
+    if (blk_sync) __syncthreads();
+    else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's staged rows have landed
     if constexpr (EPI == 1) {
       if (h == 0) {  // pivot: the first (rounded) conv value of each column in the tile's first wave
                      // row (PAIR: both wave rows use it, so their sums add), else in this wave row
@@ -2414,6 +2422,7 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   IgemmArgs b = a;
   b.diag_l1 = g_tune[RN_TUNE_DIAG_IGEMM_L1];
   b.sched = g_tune[RN_TUNE_IGEMM_SCHED];
+  b.epi_sync = g_tune[RN_TUNE_EPI_SYNC];
   const int64_t xb = (int64_t)a.N * a.H * a.W * a.C * (int64_t)sizeof(T);
   const int64_t wb = (int64_t)a.K * a.wrow * (int64_t)sizeof(T);
   b.x_bytes = (int)std::min<int64_t>(xb, INT32_MAX);
@@ -2561,6 +2570,7 @@ int launch_igemm_i8(const IgemmArgs& a, bool f32out, hipStream_t st) {
   if (Mc == 0) return 0;
   IgemmArgs b = a;
   b.sched = g_tune[RN_TUNE_IGEMM_SCHED];
+  b.epi_sync = g_tune[RN_TUNE_EPI_SYNC];
   b.x_bytes = (int)xb;
   b.w_bytes = (int)wb;
   b.ntiles = 0;
@@ -3111,6 +3121,7 @@ int rn_stem_conv_fwd_p4(const rn_conv_desc* d, const void* x4, const void* w4, v
   a.x_bytes = (int)((int64_t)d->n * hp * wp * 4 * 2);
   a.w_bytes = d->k * 256 * 2;
   a.sched = g_tune[RN_TUNE_IGEMM_SCHED];
+  a.epi_sync = g_tune[RN_TUNE_EPI_SYNC];
   a.ntn = 1;
   const int64_t M = (int64_t)d->n * d->p * d->q;
   hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, 2>), dim3((unsigned)ceil_div(M, 256)), dim3(256), 0,
