@@ -84,6 +84,13 @@ int32_t rn_conv_tile(const rn_conv_desc* d, int32_t mode);
 int rn_conv_fwd_i8(const rn_conv_desc* d, const void* x_codes, const void* w_codes, void* y, int32_t y_dtype,
                    const void* add_src, const float* x_unit, const float* w_unit, float* part,
                    rn_stream_t stream);
+/* rn_conv_fwd_i8 that also writes part_mm[block][k_pad]: per channel, the max of the stored output
+ * over the rows of each BatchNorm partial block -- the MIN where mm_sign[channel] < 0 (mm_sign
+ * nullable: the max everywhere; the consuming BatchNorm's gamma, whose sign is its scale's) -- part
+ * required, blocks of rn_conv_bn_part_rows(d, 2) rows: what rn_bn_desc.xmm reads. */
+int rn_conv_fwd_i8_mm(const rn_conv_desc* d, const void* x_codes, const void* w_codes, void* y, int32_t y_dtype,
+                      const void* add_src, const float* x_unit, const float* w_unit, float* part, float* part_mm,
+                      const float* mm_sign, rn_stream_t stream);
 /* w_codes[k][r][s][c] = round(w[k][r][s][c] / unit) (int8, zero for c >= c_real): the int8 compute
  * copy of a per-tensor quantized weight from the fp32 master (unit from rn_quant_int8_fwd_codes). */
 int rn_conv_weight_pack_i8(const rn_conv_desc* d, const float* w_master, const float* unit, void* w_codes,
@@ -222,6 +229,12 @@ typedef struct rn_bn_desc {
    * round = to the storage type, as two rn_quant_int8_bwd calls summing into one buffer store it. */
   const float* clip2;
   const void* dy2;
+  /* nullable (rn_quant_int8_fwd_codes_bn[2] with relu only): per-block per-channel extremes of x,
+   * [xmm_blocks][c], from the producing int8 convolution's epilogue (rn_conv_fwd_i8_mm with mm_sign =
+   * this BN's gamma): the max where scale >= 0, else the min. y = relu(x*scale + shift) is monotone in
+   * x per channel, so the quantizers' max|y| comes from these instead of a pass over x; bit-identical. */
+  const float* xmm;
+  int64_t xmm_blocks;
 } rn_bn_desc;
 
 /* Workspace (bytes) needed by rn_bn_fwd_train / rn_bn_bwd. */

@@ -50,6 +50,8 @@ struct IgemmArgs {
   int gcol, gred;      // grouped: output columns / reduction channels per group (dense: 2^30, 0)
   int cblk;            // reduction channels per column block (dense: C)
   float* stats;        // fwd only, nullable: per-block BatchNorm partials [m tiles][3][ldo]
+  float* stats_mm;     // fwd (EPI 1) only, nullable: per-block extreme of the stored output [m tiles][ldo]:
+  const float* mm_sign;  // the max, or the min where mm_sign[col] < 0 (nullable: the max everywhere)
   const float* in_sc;  // fwd only, nullable: BN+ReLU applied to the gathered input while staging
   const float* in_sh;
   int ntn;             // n tiles (grid = m tiles * ntn)
@@ -730,8 +732,9 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 template <int BN, int NBUF, int EPIX = 0, bool M32 = false, int BM = 256, int SC = 0, int Q8 = 0, int XF = 0, int W4 = 0,
           int GD = 0>
 __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1) void igemm_big_kernel(IgemmArgs p) {
-  constexpr int EPI = EPIX == 4 ? 2 : EPIX;
+  constexpr int EPI = EPIX == 4 ? 2 : EPIX == 5 ? 1 : EPIX;
   constexpr bool CLIP = EPIX == 4;
+  constexpr bool MM = EPIX == 5;  // EPI 1 + the per-block extremes of the stored output (p.stats_mm)
   constexpr int ES = Q8 ? 1 : 2;                 // operand bytes per element
   constexpr int BMA = 256, CE = 16 / ES, BKE = 128 / ES;
   using OutT = typename std::conditional<Q8 == 2, float, bf16_t>::type;
@@ -1057,7 +1060,24 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
   // sum dz * (x - mean)), over its rows; the lanes sharing a column chunk are summed at the end.
   // EPI 3 keeps its coefficients in the same registers: s1 = A, s2 = mean(dz), piv = A2, r_mu = mean.
   constexpr int NS = EPI ? 8 : 1;
-  float s1[NS], s2[NS], piv[NS], r_mu[NS], r_sc[NS], r_sh[NS];
+  constexpr int NM = MM ? 8 : 1;  // (MM: running max of sgn * the stored values)
+  float s1[NS], s2[NS], piv[NS], r_mu[NS], r_sc[NS], r_sh[NS], mxv[NM], sgn[NM];
+  constexpr bool want_mm = MM;
+#pragma unroll
+  for (int e = 0; e < NM; ++e) mxv[e] = -INFINITY;
+  if constexpr (MM) {  // the sign vector's 8 values in two 16-byte loads (host: 16-byte aligned, K % 8 == 0)
+    float4 g0 = make_float4(1.f, 1.f, 1.f, 1.f), g1 = g0;
+    if (p.mm_sign && col0 < p.K) {
+      g0 = reinterpret_cast<const float4*>(p.mm_sign + col0)[0];
+      g1 = reinterpret_cast<const float4*>(p.mm_sign + col0)[1];
+    }
+    const float gv[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+    for (int e = 0; e < NM; ++e) sgn[e] = gv[e] < 0.f ? -1.f : 1.f;
+  } else {
+#pragma unroll
+    for (int e = 0; e < NM; ++e) sgn[e] = 1.f;
+  }
 #pragma unroll
   for (int e = 0; e < NS; ++e) {
     s1[e] = s2[e] = piv[e] = r_mu[e] = r_sc[e] = r_sh[e] = 0.f;
@@ -1192,6 +1212,9 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
               s1[e] += d;
               s2[e] = fmaf(d, d, s2[e]);
             }
+            if (want_mm)
+#pragma unroll
+              for (int e = 0; e < NM; ++e) mxv[e] = fmaxf(mxv[e], sgn[e] * g[e]);
           } else {
             float xv[8];
             chunk_to_f(xpre[XP ? k : 0], xv, (const bf16_t*)nullptr);
@@ -1224,22 +1247,35 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
         s1[e] += __shfl_xor(s1[e], o, 64);
         s2[e] += __shfl_xor(s2[e], o, 64);
       }
-    if constexpr (PAIR) {  // wave row 1 hands its sums to wave row 0 (same columns)
-      float* xch = reinterpret_cast<float*>(smem) + wn * (CPR * 16);
+    if (want_mm)
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1)
+#pragma unroll
+        for (int e = 0; e < NM; ++e) mxv[e] = fmaxf(mxv[e], __shfl_xor(mxv[e], o, 64));
+    if constexpr (PAIR) {  // wave row 1 hands its sums (and max / min) to wave row 0 (same columns)
+      float* xch = reinterpret_cast<float*>(smem) + wn * (CPR * 32);
       __syncthreads();  // every wave is done reading the epilogue staging
-      if (wm == 1 && lane < CPR)
+      if (wm == 1 && lane < CPR) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          xch[lane * 16 + e] = s1[e];
-          xch[lane * 16 + 8 + e] = s2[e];
+          xch[lane * 32 + e] = s1[e];
+          xch[lane * 32 + 8 + e] = s2[e];
         }
+        if (want_mm)
+#pragma unroll
+          for (int e = 0; e < NM; ++e) xch[lane * 32 + 16 + e] = mxv[e];
+      }
       __syncthreads();
-      if (wm == 0 && lane < CPR)
+      if (wm == 0 && lane < CPR) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          s1[e] += xch[lane * 16 + e];
-          s2[e] += xch[lane * 16 + 8 + e];
+          s1[e] += xch[lane * 32 + e];
+          s2[e] += xch[lane * 32 + 8 + e];
         }
+        if (want_mm)
+#pragma unroll
+          for (int e = 0; e < NM; ++e) mxv[e] = fmaxf(mxv[e], xch[lane * 32 + 16 + e]);
+      }
     }
     if (lane < CPR && (!PAIR || wm == 0)) {
       const int c0 = n0 + wn * WN + lane * 8;
@@ -1256,6 +1292,8 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
             dst[0] = okc ? s1[e] : 0.f;
             dst[p.ldo] = okc ? s2[e] : 0.f;
             dst[2 * p.ldo] = piv[e];
+            if (want_mm)
+              p.stats_mm[(int64_t)blk * p.ldo + col] = okc ? sgn[e < NM ? e : 0] * mxv[e < NM ? e : 0] : 0.f;
           }
         } else if (blk < p.mt_max) {  // (a half past the class's rows may lie past its partial slots)
           float* dst = p.bnred + ((int64_t)(blockIdx.z * p.mt_max + blk) * p.ldo + col) * 2;
@@ -2574,7 +2612,7 @@ int launch_igemm_i8(const IgemmArgs& a, bool f32out, hipStream_t st) {
   b.x_bytes = (int)xb;
   b.w_bytes = (int)wb;
   b.ntiles = 0;
-  const int epi = a.stats ? 1 : 0;
+  const int epi = a.stats ? (a.stats_mm ? 5 : 1) : 0;
   const int bn = i8_tile_cols(a);
   const int bm = bn == 64 ? 256 : 224;
   b.ntn = (int)ceil_div(a.K, bn);
@@ -2589,7 +2627,8 @@ int launch_igemm_i8(const IgemmArgs& a, bool f32out, hipStream_t st) {
     if (epi) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 1, false, R, 0, 2>), grid, dim3(T), 0, st, b);        \
     else hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 0, false, R, 0, 2>), grid, dim3(T), 0, st, b);            \
   } else {                                                                                                         \
-    if (epi) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 1, false, R, 0, 1>), grid, dim3(T), 0, st, b);        \
+    if (epi == 5) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 5, false, R, 0, 1>), grid, dim3(T), 0, st, b);   \
+    else if (epi) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 1, false, R, 0, 1>), grid, dim3(T), 0, st, b);   \
     else hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 0, false, R, 0, 1>), grid, dim3(T), 0, st, b);            \
   }
   if (bn == 64) {
@@ -2744,13 +2783,22 @@ int rn_conv_fwd_x(const rn_conv_desc* d, const void* x, const void* w, void* y, 
 int rn_conv_fwd_i8(const rn_conv_desc* d, const void* x_codes, const void* w_codes, void* y, int32_t y_dtype,
                    const void* add_src, const float* x_unit, const float* w_unit, float* part,
                    rn_stream_t stream) {
+  return rn_conv_fwd_i8_mm(d, x_codes, w_codes, y, y_dtype, add_src, x_unit, w_unit, part, nullptr, nullptr, stream);
+}
+
+int rn_conv_fwd_i8_mm(const rn_conv_desc* d, const void* x_codes, const void* w_codes, void* y, int32_t y_dtype,
+                      const void* add_src, const float* x_unit, const float* w_unit, float* part, float* part_mm,
+                      const float* mm_sign, rn_stream_t stream) {
+  RN_CHECK_ARG(!part_mm || (part && y_dtype == RN_BF16), "part_mm comes with the BatchNorm partials (bf16 output)");
+  RN_CHECK_ARG(!mm_sign || (((uintptr_t)mm_sign & 15) == 0 && d->k % 8 == 0), "mm_sign: 16-byte aligned, k % 8 == 0");
   RN_CHECK_ARG(d && x_codes && w_codes && y && x_unit && w_unit, "null argument");
   RN_CHECK_ARG(d->groups <= 1, "int8 convolution is dense");
   RN_CHECK_ARG(y_dtype == RN_BF16 || y_dtype == RN_F32, "bad output dtype");
   RN_CHECK_ARG(!part || d->k % 8 == 0, "BatchNorm statistics need whole 8-channel chunks");
   IgemmArgs a = make_igemm_args(d, 0);
   a.smallc = 0;
-  a.x = x_codes; a.w = w_codes; a.y = y; a.add = add_src; a.bias = nullptr; a.stats = part;
+  a.x = x_codes; a.w = w_codes; a.y = y; a.add = add_src; a.bias = nullptr; a.stats = part; a.stats_mm = part_mm;
+  a.mm_sign = mm_sign;
   a.qunit_x = x_unit; a.qunit_w = w_unit;
   return launch_igemm_i8(a, y_dtype == RN_F32, as_stream(stream));
 }

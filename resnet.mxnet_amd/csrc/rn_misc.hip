@@ -563,6 +563,32 @@ __global__ __launch_bounds__(256) void bnq_absmax_kernel(const T* __restrict__ x
   if (threadIdx.x == 0)
     atomicMax(reinterpret_cast<unsigned int*>(out), __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
 }
+// max y of y = relu(x*scale + shift) (rounded to T) from the per-block per-channel extremes of x
+// (rn_bn_desc.xmm: the max where scale >= 0, else the min): y is monotone in x per channel, so each
+// block's extreme maps to that block's max y -- exactly the max a pass over y finds
+template <typename T, bool RELU>
+__global__ __launch_bounds__(256) void bnq_absmax_mm_kernel(const float* __restrict__ xmm, int64_t nblk, int c,
+                                                            int c_real, const float* __restrict__ scale,
+                                                            const float* __restrict__ shift, float* __restrict__ out) {
+  // thread = one channel over a stride of the blocks (blockIdx.y): scale / shift read once
+  float mx = 0.f;
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch < c_real) {
+    const float sc = scale[ch], sh = shift[ch];
+    for (int64_t b = blockIdx.y; b < nblk; b += gridDim.y) {
+      // (y >= 0: its max sits at the block's extreme on scale's side, which xmm holds)
+      const float v = fmaf(xmm[b * c + ch], sc, sh);
+      mx = fmaxf(mx, to_f(from_f<T>(RELU ? fmaxf(v, 0.f) : v)));
+    }
+  }
+  mx = wave_max(mx);
+  __shared__ float wm[4];
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    atomicMax(reinterpret_cast<unsigned int*>(out), __float_as_uint(fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]))));
+}
+
 // up to two activation quantizers of the same BatchNorm output (symbol/resnet_int8.py: a stage's first
 // unit quantizes act1 once for conv1 and once for the shortcut conv, each with its own threshold state)
 struct BnqTargets {
@@ -1120,7 +1146,12 @@ static void launch_quant_codes_bn(const rn_bn_desc* d, const void* x, const floa
     const int nrb = (int)std::min(want, maxrb);
     return std::make_pair(nrb, (d->m + nrb - 1) / nrb);
   };
-  if (is_train) {  // one max for all the quantizers of the tensor
+  if (is_train && d->xmm && RELU) {  // one max for all the quantizers of the tensor: the producer's block extremes
+    const int gx = (d->c_real + 255) / 256;
+    const int gy = (int)std::max<int64_t>(1, std::min<int64_t>(d->xmm_blocks, std::max(1, 512 / gx)));
+    hipLaunchKernelGGL((bnq_absmax_mm_kernel<T, RELU>), dim3(gx, gy), dim3(256), 0, st, d->xmm, d->xmm_blocks, d->c,
+                       d->c_real, scale, shift, curmax);
+  } else if (is_train) {  // ... or from a pass over x
     const auto g = geo(16);
     hipLaunchKernelGGL((bnq_absmax_kernel<T, RELU>), dim3(gx, g.first), dim3(256), 0, st, (const T*)x, scale, shift,
                        d->m, d->c, ct, g.second, curmax);

@@ -919,6 +919,8 @@ class Executor:
             op.bn_src = None
             op.bn_peer = None  # the second quantizer of the same BN output (written by this op's call)
             op.bn_lead = None  # (the quantizer whose call writes this one)
+            op.want_mm = False
+            op.mm_src = None
             if op.kind == "bn":
                 op.apply_in_quant = False
         for bn, qs in groups.values():
@@ -927,6 +929,14 @@ class Executor:
                 qs[0].bn_src = bn
                 if len(qs) == 2:
                     qs[0].bn_peer, qs[1].bn_lead = qs[1], qs[0]
+                # the quantizers' max from the producing int8 conv's per-block extremes of the BN input
+                # (rn_conv_fwd_i8_mm -> rn_bn_desc.xmm) instead of a pass over it (RN_QUANT_BN_MM=0: the pass)
+                src = bn.part_src
+                if src is not None and getattr(src, "int8", False) and bn.relu and self.dtype == BF16 and \
+                        os.environ.get("RN_QUANT_BN_MM", "1") == "1":
+                    src.want_mm = True
+                    src.mm_gamma = None if bn.fix_gamma else bn.gamma  # (its sign is the BN scale's)
+                    bn.mm_src = src
         for op in plan.ops:
             F, I = [], []  # train-mode, infer-mode call lists
             op.wsrc = self._weight_source(op, qwsp, sp) if getattr(op, "qweight", None) else \
@@ -1028,6 +1038,9 @@ class Executor:
                 gamma = self._pp(op.gamma)
                 # fused into the 1x1 consumers' loads or the quantizer's: coefficients only
                 yptr = None if op.apply_fused or op.apply_in_quant else self._p(self.act(y))
+                if op.mm_src is not None and getattr(op.mm_src, "part_mm", None) is not None:
+                    op.desc.xmm = op.mm_src.part_mm.data_ptr()
+                    op.desc.xmm_blocks = op.mm_src.part_blocks
                 infer = self._call("rn_bn_fwd_infer", L.C.byref(op.desc), self._p(self.act(x)), yptr,
                                    gamma, self._pp(op.beta), self._ap(op.mean), self._ap(op.var), op.sc, op.sh, sp)
                 if op.use_global_stats:
@@ -1206,6 +1219,13 @@ class Executor:
                     op.part_blocks = -(-op.y.rows // op.part_rows)
                     op.part = self._zeros(op.part_blocks * 3 * op.y.cp, self.torch.float32)
                 part = self._p(op.part)
+                if op.want_mm:  # + per-block max / min of y for the quantizers that read bn(y)
+                    if getattr(op, "part_mm", None) is None:
+                        op.part_mm = self._zeros(op.part_blocks * op.y.cp, self.torch.float32)
+                    sign = self._pp(op.mm_gamma) if op.mm_gamma else None
+                    return self._call("rn_conv_fwd_i8_mm", L.C.byref(d), self._p(op.qsrc.codes), self._p(op.wk8),
+                                      y, self.dtype, res, self._p(op.qsrc.unit), self._p(op.wunit), part,
+                                      self._p(op.part_mm), sign, sp)
             return self._call("rn_conv_fwd_i8", L.C.byref(d), self._p(op.qsrc.codes), self._p(op.wk8), y,
                               self.dtype, res, self._p(op.qsrc.unit), self._p(op.wunit), part, sp)
         xf = getattr(op, "xf", None)

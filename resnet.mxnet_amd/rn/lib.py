@@ -30,7 +30,7 @@ class ConvDesc(C.Structure):
 class BNDesc(C.Structure):
     _fields_ = [("dtype", _i32), ("m", _i64), ("c", _i32), ("c_real", _i32), ("eps", _f32), ("momentum", _f32),
                 ("fix_gamma", _i32), ("relu", _i32), ("clip", _P),
-                ("clip2", _P), ("dy2", _P)]
+                ("clip2", _P), ("dy2", _P), ("xmm", _P), ("xmm_blocks", _i64)]
 
 
 class WQuantItem(C.Structure):
@@ -52,6 +52,7 @@ SIGNATURES = {
     "rn_conv_bn_part_rows": (_i32, [_P, _i32]),
     "rn_conv_tile": (_i32, [_P, _i32]),
     "rn_conv_fwd_i8": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P, _P]),
+    "rn_conv_fwd_i8_mm": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P, _P, _P, _P]),
     "rn_conv_weight_pack_i8": (_i32, [_P, _P, _P, _P, _P]),
     "rn_conv_fwd_x": (_i32, [_P, _P, _P, _P, _i32, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_filter_x": (_i32, [_P, _P, _P, _P, _P, _P, _P, _i64, _P]),

@@ -162,10 +162,14 @@ def test_int8_forward_plan(dry, monkeypatch):
             convs = [op for op in ex.plan.ops if op.kind == "conv"]
             assert len(convs) == nconv and all(op.int8 for op in convs)
             names = _call_names(ex._fwd_train)
-            assert names.count("rn_conv_fwd_i8") == nconv
+            # (rn_conv_fwd_i8_mm: + the per-block extremes of y the quantizers of bn(y) take their max from)
+            nmm = names.count("rn_conv_fwd_i8_mm")
+            assert names.count("rn_conv_fwd_i8") + nmm == nconv and (nmm > 0) == (prec == "bfloat16")
+            assert all(op.mm_src is not None for op in ex.plan.ops if op.kind == "bn" and op.apply_in_quant
+                       and op.part_src is not None and prec == "bfloat16")
             # only the stem and fc1 keep a fake-quant / float forward
-            assert sum(1 for nm in names if nm.startswith("rn_conv_fwd") and nm != "rn_conv_fwd_i8") <= 2
-            assert _call_names(ex._fwd_infer).count("rn_conv_fwd_i8") == nconv
+            assert sum(1 for nm in names if nm.startswith("rn_conv_fwd") and not nm.startswith("rn_conv_fwd_i8")) <= 2
+            assert _call_names(ex._fwd_infer).count("rn_conv_fwd_i8") == nconv  # (inference: no statistics)
             qops = [op for op in ex.plan.ops if op.kind == "quant"]
             # every conv's data quantizer emits codes (fc1's, in resnet_int8, does not)
             nbn, nbn2 = names.count("rn_quant_int8_fwd_codes_bn"), names.count("rn_quant_int8_fwd_codes_bn2")

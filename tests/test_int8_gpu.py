@@ -336,3 +336,66 @@ def test_weight_quant_pack_batched(gpu, dtype):
             if bufs["a"][key] is not None:
                 assert torch.equal(bufs["a"][key], bufs["b"][key]), key
     assert refs[0]["b"]["unit"].item() > 0
+
+
+@pytest.mark.parametrize("case", [CASES[1], CASES[2], CASES[0], CASES[3]])
+def test_int8_conv_block_extremes_feed_quantizer_max(gpu, case):
+    """rn_conv_fwd_i8_mm: the same output and BatchNorm partials as rn_conv_fwd_i8, plus per block and
+    channel the max of the stored output (the min where the sign vector -- the consuming BN's gamma --
+    is negative); with them in rn_bn_desc.xmm the BN+ReLU-on-load quantizer (rn_quant_int8_fwd_codes_bn)
+    takes max|y| from the extremes instead of a pass over x -- and writes bit-identical values,
+    codes, unit and EMA state."""
+    n, c, h, w, k, r, st, pd = case
+    rng = np.random.default_rng(sum(case) + 5)
+    lib = L.load()
+    d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd)
+    rows = lib.rn_conv_bn_part_rows(C.byref(d), 2)
+    P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+    m = n * P * Q
+    nblk = -(-m // rows)
+    xd = torch.from_numpy(rng.integers(-127, 128, (n, h, w, d.c)).astype(np.int8)).to(gpu)
+    wd = torch.from_numpy(rng.integers(-127, 128, (k, r, r, d.c)).astype(np.int8)).reshape(-1).to(gpu)
+    ux, uw = (torch.tensor([u], dtype=torch.float32, device=gpu) for u in (0.011, 0.0007))
+    # BN scale with both signs (its gamma's sign), shift
+    sc = torch.tensor(rng.standard_normal(d.k_pad) * 0.02, dtype=torch.float32, device=gpu)
+    sh = torch.tensor(rng.standard_normal(d.k_pad) * 0.5, dtype=torch.float32, device=gpu)
+    sc[k:] = 0
+    sh[k:] = 0
+    sgn = sc.clone()
+    outs = []
+    for mm in (False, True):
+        y = torch.zeros((m, d.k_pad), dtype=torch.bfloat16, device=gpu)
+        part = torch.zeros(nblk * 3 * d.k_pad, dtype=torch.float32, device=gpu)
+        pmm = torch.full((nblk * d.k_pad,), float("nan"), dtype=torch.float32, device=gpu) if mm else None
+        if mm:
+            L.call("rn_conv_fwd_i8_mm", C.byref(d), p(xd), p(wd), p(y), BF16, None, p(ux), p(uw), p(part), p(pmm),
+                   p(sgn), stream())
+        else:
+            L.call("rn_conv_fwd_i8", C.byref(d), p(xd), p(wd), p(y), BF16, None, p(ux), p(uw), p(part), stream())
+        outs.append((y, part, pmm))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    yv = outs[1][0].float().cpu().numpy()
+    pmm = outs[1][2].cpu().numpy().reshape(nblk, d.k_pad)
+    pad = nblk * rows - m
+    yb = np.concatenate([yv, np.full((pad, d.k_pad), np.nan, np.float32)]).reshape(nblk, rows, d.k_pad)
+    neg = sgn.cpu().numpy()[:k] < 0
+    want = np.where(neg[None, :], np.nanmin(yb, axis=1)[:, :k], np.nanmax(yb, axis=1)[:, :k])
+    np.testing.assert_array_equal(pmm[:, :k], want)
+    # the quantizer of relu(bn(y)): max from the extremes == max from a pass over y
+    ws = torch.zeros(4096, dtype=torch.float32, device=gpu)
+    res = []
+    for mm in (False, True):
+        bd = L.BNDesc(dtype=BF16, m=m, c=d.k_pad, c_real=k, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1,
+                      xmm=outs[1][2].data_ptr() if mm else None, xmm_blocks=nblk if mm else 0)
+        out = torch.zeros_like(outs[0][0])
+        codes = torch.zeros(m * d.k_pad, dtype=torch.int8, device=gpu)
+        unit = torch.zeros(1, dtype=torch.float32, device=gpu)
+        mmst = torch.tensor([1.0], dtype=torch.float32, device=gpu)
+        L.call("rn_quant_int8_fwd_codes_bn", C.byref(bd), p(outs[0][0]), p(sc), p(sh), p(out), p(codes), p(unit),
+               p(mmst), 1, 0.99, 1, 8, p(ws), stream())
+        res.append((out, codes, unit, mmst))
+    torch.cuda.synchronize()
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    assert res[1][3].item() > 0  # (first batch: the state is the max itself)
