@@ -67,7 +67,7 @@ def conv_call_bytes(ex, name, args):
 def pmc_traffic(family):
     """HBM bytes per launch of `family` from the committed rocprofv3 PMC summary (tools/pmc_bench.sh +
     tools/pmc_summary.py: FETCH_SIZE doubled per the gfx950 correction, plus WRITE_SIZE)."""
-    path = os.environ.get("RN_PMC_JSON", os.path.join(REPO, "profiles", "r02", "pmc_hbm_bytes_per_launch.json"))
+    path = os.environ.get("RN_PMC_JSON", os.path.join(REPO, "profiles", "r03", "pmc_hbm_bytes_per_launch.json"))
     try:
         with open(path) as f:
             rec = json.load(f).get(family)
