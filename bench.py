@@ -380,8 +380,8 @@ def main():
         main_stream = torch.cuda.Stream(priority=min(lo, hi))
         torch.cuda.synchronize()
 
-    def step(feed=pinned if a.host_input else None):
-        if main_stream is not None:
+    def step(feed=pinned if a.host_input else None, on_current=False):
+        if main_stream is not None and not on_current:
             with torch.cuda.stream(main_stream):
                 mod.forward(feed, is_train=True)
                 mod.backward()
@@ -410,7 +410,7 @@ def main():
         # removes the per-launch gaps between the ~580 kernels of a step; same kernels, same work
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
-            step()
+            step(on_current=True)  # (on the capture stream itself; the side stream joins it by events)
         torch.cuda.synchronize()
         graph.replay()  # one untimed replay
         torch.cuda.synchronize()
