@@ -409,12 +409,22 @@ def main():
         # the whole training step (forward, backward, SGD, weight repack) as ONE HIP graph:
         # removes the per-launch gaps between the ~580 kernels of a step; same kernels, same work
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            step(on_current=True)  # (on the capture stream itself; the side stream joins it by events)
+        # (on the capture stream itself -- the high-priority one when there is one; the side stream
+        # joins the capture by the fork events)
+        with torch.cuda.graph(graph, stream=main_stream):
+            step(on_current=True)
         torch.cuda.synchronize()
-        graph.replay()  # one untimed replay
+
+        def replay():
+            if main_stream is not None:
+                with torch.cuda.stream(main_stream):
+                    graph.replay()
+                torch.cuda.current_stream().wait_stream(main_stream)
+            else:
+                graph.replay()
+        replay()  # one untimed replay
         torch.cuda.synchronize()
-        run = graph.replay
+        run = replay
     else:
         timer.wrap()  # HIP events around every launch of the dominant family, inside the timed region
         run = step
