@@ -169,8 +169,8 @@ int64_t rn_conv_pack_numel(const rn_conv_desc* d, int32_t which);
  * over RN_GROUP_BLOCK-wide column blocks -- for output column j the reduction runs over the
  * channels of the groups that j's 64-column block touches, zero outside j's own group
  * (w_krsc: [k][r][s][cblk], w_crsk: [c][r][s][kblk]); sizes from rn_conv_pack_numel.
- * Except where the direct grouped kernel runs (bf16, 3x3 pad 1, c = k, 4 channels per group -- forward
- * stride 1 / 2, data gradient stride 1 -- or 8 per group, forward stride 2; rn_set_tuning 15): that
+ * Except where the direct grouped kernel runs (bf16, 3x3 pad 1, c = k, 4 channels per group at
+ * stride 1 or 2, or 8 per group at stride 2 -- forward and data gradient; rn_set_tuning 15): that
  * mode's copy is compact, [c/8][tap][8][G] with G = c/groups -- w_krsc[k/8][tap][k%8][c'] =
  * w[k][tap][c'], w_crsk[c/8][tap][c%8][k'] = w[g*G + k'][8 - tap][c - g*G], g = c/G -- and
  * rn_conv_fwd / rn_conv_bwd_data multiply it with v_dot2_f32_bf16 (no bias, statistics or BN fusions). */
@@ -513,7 +513,7 @@ const char* rn_last_error(void);
  *      each wave one of them over half of each M stage; 0 = on, 1 = off, 2 = on, the
  *      diagonal blocks on two of the four waves),
  * 15 = grouped convolutions with 4 channels per group (ResNeXt 32x4d stage 1; 8 per group at
- *      stride 2): the direct v_dot2 kernels and their weight copies (0 = on, 1 = the block-diagonal
+ *      stride 2, stage 2 unit 1): the direct v_dot2 kernels and their weight copies (0 = on, 1 = the block-diagonal
  *      64-column tiles; set it before rn_conv_weight_pack: the copies of the two paths differ),
  * 16 = 1: block barriers around the LDS staging of the 224/256-row tiles' epilogue (default 0: each
  *      wave waits only for its own staged rows; the paired-row BatchNorm-statistics epilogue keeps

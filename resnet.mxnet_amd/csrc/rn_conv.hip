@@ -2022,6 +2022,86 @@ __global__ __launch_bounds__(256) void grouped_direct_kernel(GdArgs a) {
     }
   }
 }
+// The data gradient of a STRIDE-2 direct grouped layer (3x3, pad 1): dx[h][w] = sum over the taps
+// with (h + 1 - r) and (w + 1 - s) even of dy[(h + 1 - r) / 2][(w + 1 - s) / 2] * w[tap] -- an even
+// output row takes tap row 1, an odd one rows 0 and 2; likewise columns, so a pixel lane's PL output
+// pixels (from an even w0) read the PL/2 + 1 dy columns w0/2 .. w0/2 + PL/2 of each tap row. Same
+// compact copy as the stride-1 data gradient (mode 1: tap 8 - t holds tap t), same lane layout.
+template <int G, int PL>
+__global__ __launch_bounds__(256) void grouped_dgrad_s2_kernel(GdArgs a) {
+  extern __shared__ uint4 gd_w[];
+  const int nw16 = a.C * 9 * G * 2 / 16;
+  for (int i = threadIdx.x; i < nw16; i += blockDim.x) gd_w[i] = reinterpret_cast<const uint4*>(a.w)[i];
+  __syncthreads();
+  constexpr int ND = PL / 2 + 1;  // dy columns per tap row
+  const int lane = threadIdx.x & 63;
+  const int chunk = lane & ((1 << a.lcpr) - 1), pl = lane >> a.lcpr;
+  const int plw = 64 >> a.lcpr;
+  const uint4* wc = gd_w + chunk * 9 * G;
+  const uint32_t step = gridDim.x * (blockDim.x >> 6) * plw;
+  const int64_t cstep = a.C;
+  for (uint32_t it = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * plw + pl; it < a.items; it += step) {
+    const uint32_t t = fdiv(it, a.fdQB);
+    const int w0 = (int)(it - t * a.qb) * PL;  // (even)
+    const uint32_t n = fdiv(t, a.fdP);
+    const int h = (int)(t - n * a.P);
+    float acc[PL][8];
+#pragma unroll
+    for (int j = 0; j < PL; ++j)
+#pragma unroll
+      for (int o = 0; o < 8; ++o) acc[j][o] = 0.f;
+#pragma unroll
+    for (int rr = 0; rr < 2; ++rr) {
+      // even h: tap row 1 (dy row h / 2); odd h: rows 0 and 2 (dy rows (h + 1) / 2, (h - 1) / 2)
+      const bool odd = h & 1;
+      if (!odd && rr == 1) continue;
+      const int r = odd ? 2 * rr : 1;
+      const int pr = (h + 1 - r) >> 1;
+      if (pr < 0 || pr >= a.H) continue;
+      const bf16_t* dyrow = a.x + ((int64_t)(n * a.H + pr) * a.W + (w0 >> 1)) * cstep + chunk * 8;
+      uint4 dc[ND];
+#pragma unroll
+      for (int ci = 0; ci < ND; ++ci)
+        dc[ci] = ((w0 >> 1) + ci < a.W) ? *reinterpret_cast<const uint4*>(dyrow + ci * cstep) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int s_ = 0; s_ < 3; ++s_) {
+        uint4 wv[G];
+#pragma unroll
+        for (int u = 0; u < G; ++u) wv[u] = wc[(8 - (r * 3 + s_)) * G + u];
+        const uint32_t* wp = reinterpret_cast<const uint32_t*>(wv);
+#pragma unroll
+        for (int j = 0; j < PL; ++j) {
+          // even j (even w): tap column 1, dy column j / 2; odd j: columns 0 and 2, dy (j + 1) / 2, (j - 1) / 2
+          if ((j & 1) == 0 && s_ != 1) continue;
+          if ((j & 1) == 1 && s_ == 1) continue;
+          const int ci = (j & 1) == 0 ? j / 2 : (s_ == 0 ? (j + 1) / 2 : (j - 1) / 2);
+          const uint4 xv = dc[ci];
+          const uint32_t xp[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+          for (int o = 0; o < 8; ++o) {
+            const int gb = G == 4 ? (o >> 2) * 2 : 0;
+#pragma unroll
+            for (int jj = 0; jj < G / 2; ++jj) acc[j][o] = gd_dot(xp[gb + jj], wp[o * (G / 2) + jj], acc[j][o]);
+          }
+        }
+      }
+    }
+    const int64_t obase = ((int64_t)(n * a.P + h) * a.Q + w0) * cstep + chunk * 8;
+#pragma unroll
+    for (int j = 0; j < PL; ++j) {
+      if (w0 + j >= a.Q) break;
+      const int64_t off = obase + j * cstep;
+      if (a.add) {
+        float f[8];
+        chunk_to_f(*reinterpret_cast<const uint4*>(a.add + off), f, (const bf16_t*)nullptr);
+#pragma unroll
+        for (int o = 0; o < 8; ++o) acc[j][o] += f[o];
+      }
+      *reinterpret_cast<uint4*>(a.y + off) = f_to_chunk(acc[j], (const bf16_t*)nullptr);
+    }
+  }
+}
+
 // compact compute copies of a direct grouped convolution (9 taps, G = cpg = kpg channels per group):
 // mode 0: out[k/8][tap][k%8][c'] = w[k][tap][c']; mode 1 (stride-1 data gradient): out[c/8][tap][c%8][k']
 // = w[g*G + k'][8 - tap][c - g*G], g = c / G (the group's outputs for input c, taps flipped)
@@ -2666,9 +2746,9 @@ __global__ void pack_krsc_i8_kernel(const float* __restrict__ wm, const float* _
 // the block-diagonal MFMA path (set before packing: the two paths' copies differ).
 // Does the grouped convolution d run the direct kernel in mode 0 (forward) / 1 (data gradient)? Its
 // compute copy of that mode is then the compact one (pack_group_direct_kernel). Where it pays (measured,
-// ResNeXt-50 at batch 256): 4 channels per group -- forward stride 1 / 2, data gradient stride 1 -- and
-// the 8-per-group stride-2 forward; with 8 (stride 1) or 16 per group the v_dot2 work outgrows the
-// memory time and the block-diagonal MFMA tiles win. rn_set_tuning 15 = 1: never (set before packing:
+// ResNeXt-50 at batch 256): 4 channels per group -- forward and data gradient, stride 1 / 2 -- and the
+// 8-per-group stride-2 layers; with 8 (stride 1) or 16 per group the v_dot2 work outgrows the memory
+// time and the block-diagonal MFMA tiles win. rn_set_tuning 15 = 1: never (set before packing:
 // the two paths' copies differ).
 bool gd_direct_ok(const rn_conv_desc* d, int mode) {
   if (!d || d->dtype != RN_BF16 || d->groups <= 1 || g_tune[RN_TUNE_GROUP_DIRECT] == 1) return false;
@@ -2676,9 +2756,8 @@ bool gd_direct_ok(const rn_conv_desc* d, int mode) {
   if (d->c != d->c_real || d->k != d->c || d->k_pad != d->k || d->c % d->groups || (cpg != 4 && cpg != 8)) return false;
   if (d->r != 3 || d->s != 3 || d->pad_h != 1 || d->pad_w != 1 || d->stride_h != d->stride_w) return false;
   if (d->c % 8 || 64 % (d->c / 8) || (int64_t)d->c * 9 * cpg * 2 > 64 * 1024) return false;
-  if (cpg == 8) return mode == 0 && d->stride_h == 2;
-  if (mode == 0) return d->stride_h == 1 || d->stride_h == 2;
-  return mode == 1 && d->stride_h == 1;
+  if (cpg == 8) return (mode == 0 || mode == 1) && d->stride_h == 2;  // (stride 1: the MFMA tile wins)
+  return (mode == 0 || mode == 1) && (d->stride_h == 1 || d->stride_h == 2);
 }
 
 int gd_launch(const rn_conv_desc* d, int mode, const void* x, const void* w, void* y, const void* add,
@@ -2693,7 +2772,8 @@ int gd_launch(const rn_conv_desc* d, int mode, const void* x, const void* w, voi
   a.lcpr = lcpr;
   const int cpg = d->c / d->groups;
   const int stride = mode == 0 ? d->stride_h : 1;
-  const int PL = cpg == 4 && stride == 1 ? 8 : 4;
+  const bool s2t = mode == 1 && d->stride_h == 2;  // the transposed stride-2 data gradient
+  const int PL = s2t ? 8 : cpg == 4 && stride == 1 ? 8 : 4;
   a.qb = (a.Q + PL - 1) / PL;
   const int64_t items = (int64_t)d->n * a.P * a.qb;
   RN_CHECK_ARG(items < INT32_MAX && (int64_t)d->n * a.H * a.W * a.C < INT32_MAX, "grouped direct: tensor too large");
@@ -2703,7 +2783,10 @@ int gd_launch(const rn_conv_desc* d, int mode, const void* x, const void* w, voi
   const int64_t want = (items + 4 * plw - 1) / (4 * plw);
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, 1024));
   const size_t lds = (size_t)d->c * 9 * cpg * 2;
-  if (cpg == 4 && stride == 1)
+  if (s2t) {
+    if (cpg == 4) hipLaunchKernelGGL((grouped_dgrad_s2_kernel<4, 8>), dim3(blocks), dim3(256), lds, st, a);
+    else hipLaunchKernelGGL((grouped_dgrad_s2_kernel<8, 8>), dim3(blocks), dim3(256), lds, st, a);
+  } else if (cpg == 4 && stride == 1)
     hipLaunchKernelGGL((grouped_direct_kernel<4, 1, 8>), dim3(blocks), dim3(256), lds, st, a);
   else if (cpg == 4)
     hipLaunchKernelGGL((grouped_direct_kernel<4, 2, 4>), dim3(blocks), dim3(256), lds, st, a);

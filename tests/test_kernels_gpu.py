@@ -433,7 +433,8 @@ def test_grouped_conv(gpu, dtype, case):
     (3, 128, 15, 13, 128, 3, 1, 1, 32),   # ragged rows (13 = 3 blocks of 4 pixels + 1)
     (2, 256, 10, 10, 256, 3, 2, 1, 32),   # 8 per group, stride 2: direct forward, block-diagonal dgrad
     (2, 256, 7, 11, 256, 3, 1, 1, 32),    # 8 per group, stride 1
-    (2, 128, 12, 12, 128, 3, 2, 1, 32),   # 4 per group, stride 2
+    (2, 128, 12, 12, 128, 3, 2, 1, 32),   # 4 per group, stride 2 (the transposed stride-2 data gradient too)
+    (2, 128, 11, 13, 128, 3, 2, 1, 32),   # stride 2, odd input sizes
     (2, 512, 6, 7, 512, 3, 1, 1, 32),     # 16 per group (stage 3)
     (2, 512, 9, 9, 512, 3, 2, 1, 32),     # 16 per group, stride 2
     (1, 64, 5, 5, 64, 3, 1, 1, 8),        # 8 per group, fewer channels than a wave has lanes
