@@ -176,6 +176,13 @@ int64_t rn_conv_pack_numel(const rn_conv_desc* d, int32_t which);
  * rn_conv_fwd / rn_conv_bwd_data multiply it with v_dot2_f32_bf16 (no bias, statistics or BN fusions). */
 int rn_conv_weight_pack(const rn_conv_desc* d, const float* w_master, void* w_krsc, void* w_crsk,
                         rn_stream_t stream);
+/* rn_conv_weight_pack for count layers (host arrays: descs[i], w_masters[i], w_krsc[i], w_crsk[i],
+ * the last two nullable): the grouped layers' copies in one launch per 32 copies (the grouped
+ * weights are repacked after every update -- a ResNeXt-50 step's 33 separate launches were ~6 us
+ * each on its critical path), dense layers through rn_conv_weight_pack. Same bytes as per layer;
+ * the grouped layers of one call share a dtype. */
+int rn_conv_weight_pack_multi(const rn_conv_desc* descs, const float* const* w_masters, void* const* w_krsc,
+                              void* const* w_crsk, int32_t count, rn_stream_t stream);
 
 /* Stem: explicit im2col of an NCHW fp32 image (the `data` input, train.py:70-73) with an
  * optional per-channel affine (bn_data, symbol/resnet.py:90) into cols[m][kc] (dtype),

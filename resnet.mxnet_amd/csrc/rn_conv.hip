@@ -2119,6 +2119,51 @@ __global__ void pack_group_direct_kernel(const float* __restrict__ wm, bf16_t* _
   }
 }
 
+// Many grouped compute copies in one launch (rn_conv_weight_pack_multi): blockIdx.y = copy, the
+// items travel by value in the kernel argument. Element maps as pack_group_direct_kernel (direct)
+// and pack_group_kernel (block-diagonal).
+struct GpackItem {
+  const float* wm;
+  void* out;
+  int64_t total;
+  int direct, transpose, ncols, rs, cblk, gcol, gred, cpg;
+};
+constexpr int kGpackMax = 32;
+struct GpackBatch {
+  GpackItem it[kGpackMax];
+};
+template <typename T>
+__global__ __launch_bounds__(256) void pack_group_multi_kernel(const GpackBatch b) {
+  const GpackItem& p = b.it[blockIdx.y];
+  T* __restrict__ out = reinterpret_cast<T*>(p.out);
+  const float* __restrict__ wm = p.wm;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < p.total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    if (p.direct) {  // [C/8][9][8][G]
+      const int G = p.cpg;
+      const int u = (int)(i % G), t = (int)(i / G);
+      const int o = t % 8, t2 = t / 8;
+      const int tap = t2 % 9, col = (t2 / 9) * 8 + o;
+      const int g = col / G;
+      v = p.transpose ? wm[((int64_t)(g * G + u) * 9 + (8 - tap)) * G + (col - g * G)]
+                      : wm[((int64_t)col * 9 + tap) * G + u];
+    } else {  // [ncols][rs][cblk], block-diagonal
+      const int j = (int)(i % p.cblk);
+      const int64_t t = i / p.cblk;
+      const int tap = (int)(t % p.rs);
+      const int col = (int)(t / p.rs);
+      const int n0 = col / RN_GROUP_BLOCK * RN_GROUP_BLOCK;
+      const int red = (n0 / p.gcol) * p.gred + j;
+      const int g = col / p.gcol;
+      if (red / p.gred == g)
+        v = p.transpose ? wm[((int64_t)red * p.rs + tap) * p.cpg + (col - g * p.gcol)]
+                        : wm[((int64_t)col * p.rs + tap) * p.cpg + (red - g * p.gred)];
+    }
+    out[i] = from_f<T>(v);
+  }
+}
+
 // thread per (row m, 16-byte output chunk): 8 (bf16) / 4 (f32) consecutive im2col columns
 template <typename T>
 __global__ __launch_bounds__(256) void im2col_nchw_kernel(const float* __restrict__ x, const float* __restrict__ scale,
@@ -3341,6 +3386,69 @@ int rn_conv_weight_pack(const rn_conv_desc* d, const float* wm, void* w_krsc, vo
                          (float*)w_crsk, d->k, d->k_pad, RS, d->c_real, d->c);
   }
   return rn_check_launch("weight_pack");
+}
+
+int rn_conv_weight_pack_multi(const rn_conv_desc* descs, const float* const* w_masters, void* const* w_krsc,
+                              void* const* w_crsk, int32_t count, rn_stream_t stream) {
+  RN_CHECK_ARG(count >= 0 && (count == 0 || (descs && w_masters && w_krsc && w_crsk)), "null argument");
+  hipStream_t st = as_stream(stream);
+  int32_t dtype = -1;
+  for (int32_t i = 0; i < count; ++i) {
+    const rn_conv_desc* d = descs + i;
+    RN_CHECK_ARG(w_masters[i], "null master weight");
+    if (d->groups <= 1) continue;
+    RN_CHECK_ARG(d->c % d->groups == 0 && d->k % d->groups == 0, "channels not divisible by groups");
+    RN_CHECK_ARG(dtype < 0 || dtype == d->dtype, "grouped copies of one call must share a dtype");
+    dtype = d->dtype;
+  }
+  GpackBatch b;
+  int nb = 0;
+  int64_t most = 0;
+  auto flush = [&]() {
+    if (!nb) return;
+    const dim3 grid((unsigned)std::min(grid_for(most), 1024), (unsigned)nb);
+    if (dtype == RN_BF16)
+      hipLaunchKernelGGL(pack_group_multi_kernel<bf16_t>, grid, dim3(256), 0, st, b);
+    else
+      hipLaunchKernelGGL(pack_group_multi_kernel<float>, grid, dim3(256), 0, st, b);
+    nb = 0;
+    most = 0;
+  };
+  for (int32_t i = 0; i < count; ++i) {
+    const rn_conv_desc* d = descs + i;
+    if (d->groups <= 1) {  // dense: the per-layer pack
+      const int r = rn_conv_weight_pack(d, w_masters[i], w_krsc[i], w_crsk[i], stream);
+      if (r) return r;
+      continue;
+    }
+    const int cpg = d->c / d->groups, kpg = d->k / d->groups;
+    for (int which = 0; which < 2; ++which) {
+      void* out = which == 0 ? w_krsc[i] : w_crsk[i];
+      if (!out) continue;
+      GpackItem& p = b.it[nb];
+      p.wm = w_masters[i];
+      p.out = out;
+      p.transpose = which;
+      p.cpg = cpg;
+      p.rs = d->r * d->s;
+      p.direct = gd_direct_ok(d, which) ? 1 : 0;
+      if (p.direct) {
+        p.ncols = d->c;
+        p.total = (int64_t)d->c * 9 * cpg;
+        p.cblk = p.gcol = p.gred = 0;
+      } else {
+        p.ncols = which == 0 ? d->k : d->c;
+        p.gcol = which == 0 ? kpg : cpg;
+        p.gred = which == 0 ? cpg : kpg;
+        p.cblk = group_blk(p.gcol, p.gred);
+        p.total = (int64_t)p.ncols * p.rs * p.cblk;
+      }
+      most = std::max(most, p.total);
+      if (++nb == kGpackMax) flush();
+    }
+  }
+  flush();
+  return rn_check_launch("weight_pack_multi");
 }
 
 }  // extern "C"

@@ -869,6 +869,9 @@ class Executor:
         self._wq_ops = []
         self.fused_packs = {}  # param -> rn_wpack fields: copies rewritten by the SGD kernel itself
         self.unfused_packs = []  # packs that still run after every update (grouped, fake-quantized)
+        # the grouped layers' repacks in one rn_conv_weight_pack_multi (RN_GPACK_BATCH=0: one call each)
+        self._gpack_batch = os.environ.get("RN_GPACK_BATCH", "1") == "1"
+        self._gpacks = []
         self.bn_state = {}
         stem_ws = 64
         # BatchNorm statistics straight from the producing conv's epilogue (no separate stats pass)
@@ -1189,6 +1192,16 @@ class Executor:
             c_ = self._call("rn_weight_quant_pack", self._p(self._wq_items), len(items), self.dtype, qwsp, sp)
             self.packs.insert(0, c_)
             self.unfused_packs.insert(0, c_)
+        if self._gpacks:
+            n = len(self._gpacks)
+            vp = lambda v: v.value if isinstance(v, L.C.c_void_p) else v  # noqa: E731
+            self._gp_arrays = ((type(self._gpacks[0][0]) * n)(*[g[0] for g in self._gpacks]),
+                               (L.C.c_void_p * n)(*[vp(g[1]) for g in self._gpacks]),
+                               (L.C.c_void_p * n)(*[g[2].data_ptr() if g[2] is not None else None
+                                                    for g in self._gpacks]),
+                               (L.C.c_void_p * n)(*[g[3].data_ptr() if g[3] is not None else None
+                                                    for g in self._gpacks]))
+            self.unfused_packs.append(self._call("rn_conv_weight_pack_multi", *self._gp_arrays, n, sp))
 
     def _big_tile(self, op, mode, min_cols=None):
         """Does conv `op` run its forward (mode 0) / data gradient (mode 1) on a 256/224-row LDS-DMA
@@ -1276,6 +1289,8 @@ class Executor:
             self.fused_packs[op.weight] = (wk.data_ptr() if wk is not None else 0,
                                            wc.data_ptr() if wc is not None else 0,
                                            d.k, d.r * d.s, d.c_real, d.c, d.k_pad)
+        elif d.groups > 1 and self._gpack_batch:
+            self._gpacks.append((d, op.wsrc, wk, wc))  # -> one rn_conv_weight_pack_multi
         else:
             self.unfused_packs.append(c)
 

@@ -72,6 +72,7 @@ SIGNATURES = {
     "rn_conv_weight_numel": (_i64, [_P]),
     "rn_conv_pack_numel": (_i64, [_P, _i32]),
     "rn_conv_weight_pack": (_i32, [_P, _P, _P, _P, _P]),
+    "rn_conv_weight_pack_multi": (_i32, [_P, _P, _P, _P, _i32, _P]),
     "rn_stem_prepare": (_i32, [_P, _P, _i32, _i32, _i32, _i32, _P, _i32, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rn_stem_prepare_p4": (_i32, [_P, _P, _i32, _i32, _i32, _i32, _P, _i32, _i32, _i32, _i32, _i32, _P, _P, _P, _P,
                                   _P, _P, _P, _P, _P, _P]),

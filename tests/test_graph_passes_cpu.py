@@ -237,3 +237,18 @@ def test_oracle_fix_bn_keeps_moving_stats():
     onet.forward(g, args, aux, data, label, True)
     for k in aux:
         np.testing.assert_array_equal(aux[k], before[k])
+
+
+def test_grouped_repacks_batched(dry, monkeypatch):
+    """ResNeXt's grouped weights are repacked after every update (the SGD kernel writes only dense
+    copies): one rn_conv_weight_pack_multi for all 16 grouped layers; RN_GPACK_BATCH=0 = one
+    rn_conv_weight_pack each."""
+    sym = graphs.resnext([3, 4, 6, 3], 4, [64, 256, 512, 1024, 2048], 16, "float32", 32)
+    ex = _bind(sym, precision="bfloat16").executor
+    names = _call_names(ex.unfused_packs)  # + the stem's 4-channel copy (rn_stem_weight_pack_p4)
+    assert names == ["rn_stem_weight_pack_p4", "rn_conv_weight_pack_multi"]
+    descs = ex.unfused_packs[1][2][0]
+    assert len(descs) == 16 and all(d.groups == 32 for d in descs)
+    monkeypatch.setenv("RN_GPACK_BATCH", "0")
+    ex0 = _bind(sym, precision="bfloat16").executor
+    assert _call_names(ex0.unfused_packs) == ["rn_stem_weight_pack_p4"] + ["rn_conv_weight_pack"] * 16

@@ -486,6 +486,47 @@ def test_grouped_conv_direct(gpu, case):
     assert rel_err(outs[0][0], outs[1][0]) < 4e-3 and rel_err(outs[0][1], outs[1][1]) < 4e-3
 
 
+@pytest.mark.parametrize("dtype", [F32, BF16])
+def test_weight_pack_multi(gpu, dtype):
+    """rn_conv_weight_pack_multi writes exactly the bytes of one rn_conv_weight_pack per layer: the
+    direct (compact) and block-diagonal grouped copies batched 32 to a launch, dense layers and a NULL
+    copy passed through. 40 grouped layers -> two launches."""
+    geoms = [(128, 3, 1, 32), (256, 3, 2, 32), (256, 3, 1, 32), (512, 3, 1, 32), (1024, 3, 2, 32),
+             (128, 1, 1, 2), (64, 3, 1, 8)] * 6
+    geoms += [(64, 1, 1, 1), (96, 3, 1, 1)]  # dense
+    lib = L.load()
+    rng = np.random.default_rng(17)
+    ds, ms, refs, outs = [], [], [], []
+    for i, (c, r, st, g) in enumerate(geoms):
+        d = L.ConvDesc(dtype=dtype, n=2, h=8, w=8, c=c, c_real=c, k=c, k_pad=c, r=r, s=r, stride_h=st,
+                       stride_w=st, pad_h=r // 2, pad_w=r // 2, groups=g)
+        L.call("rn_conv_desc_init", C.byref(d))
+        wt = rng.standard_normal((c, c // g, r, r)).astype(np.float32)
+        ms.append(_master_krsc(wt, gpu))
+        ds.append(d)
+        pair = []
+        for which in (0, 1):
+            nel = lib.rn_conv_pack_numel(C.byref(d), which)
+            pair.append([torch.full((nel,), 7.0, dtype=tdt(dtype), device=gpu) for _ in range(2)])
+        if i == 3:  # a layer without its data-gradient copy
+            pair[1] = [None, None]
+        L.call("rn_conv_weight_pack", C.byref(d), p(ms[-1]), p(pair[0][0]), p(pair[1][0]), stream())
+        refs.append((pair[0][0], pair[1][0]))
+        outs.append((pair[0][1], pair[1][1]))
+    n = len(ds)
+    vp = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    L.call("rn_conv_weight_pack_multi", (L.ConvDesc * n)(*ds), (C.c_void_p * n)(*[m.data_ptr() for m in ms]),
+           (C.c_void_p * n)(*[vp(o[0]) for o in outs]), (C.c_void_p * n)(*[vp(o[1]) for o in outs]), n, stream())
+    torch.cuda.synchronize()
+    for i in range(n):
+        for a, b in zip(refs[i], outs[i]):
+            if a is None:
+                assert b is None
+                continue
+            assert torch.equal(a.view(torch.int16) if dtype == BF16 else a.view(torch.int32),
+                               b.view(torch.int16) if dtype == BF16 else b.view(torch.int32)), (i, geoms[i])
+
+
 def _im2col_ref(xq, r, st, pd, kc):
     n, c, h, w = xq.shape
     P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
