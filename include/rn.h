@@ -333,6 +333,13 @@ int rn_bn_bwd(const rn_bn_desc* d, const void* x, const void* dy, void* dx, cons
               const float* gamma, const float* save_mean, const float* save_invstd,
               const float* scale, const float* shift, float* dgamma, float* dbeta, void* ws,
               rn_stream_t stream);
+/* dx rows [row0, row0 + rows) of rn_bn_bwd, from the coefficients an rn_bn_bwd call with dx = NULL
+ * (reductions and dgamma/dbeta only) left in ws -- same d, x, dy, ws. Lets a consumer of dx start on
+ * the first rows while later ones are applied (the stem: its weight gradient per image chunk on the
+ * side stream). Bit-identical to rn_bn_bwd's dx. row0 * c a multiple of 16 bytes; no dy2. */
+int rn_bn_bwd_apply_rows(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const void* add_src,
+                         const float* scale, const float* shift, const void* ws, int64_t row0, int64_t rows,
+                         rn_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------
  * Pooling -- mx.sym.Pooling (symbol/resnet.py:97 max 3x3/s2/p1; :113 global avg).

@@ -1020,6 +1020,35 @@ int rn_bn_bwd(const rn_bn_desc* d, const void* x, const void* dy, void* dx, cons
                          st);
 }
 
+int rn_bn_bwd_apply_rows(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const void* add_src,
+                         const float* scale, const float* shift, const void* ws, int64_t row0, int64_t rows,
+                         rn_stream_t stream) {
+  if (check_bn(d)) return -1;
+  RN_CHECK_ARG(x && dy && dx && scale && shift && ws, "null argument");
+  RN_CHECK_ARG(!d->dy2, "dy2: rn_bn_bwd only");
+  RN_CHECK_ARG(row0 >= 0 && rows > 0 && row0 + rows <= d->m, "row range outside the tensor");
+  const int64_t es = d->dtype == RN_BF16 ? 2 : 4;
+  RN_CHECK_ARG(row0 * d->c * es % 16 == 0, "row0 * c must be a whole number of 16-byte chunks");
+  // the coefficients rn_bn_bwd (dx = NULL) left in ws, located by the whole tensor's geometry
+  Geo g = d->dtype == RN_BF16 ? make_geo<bf16_t>(d->m, d->c) : make_geo<float>(d->m, d->c);
+  const float* coef = reinterpret_cast<const float*>(ws) + (int64_t)g.nrb * d->c * 2;
+  coef = reinterpret_cast<const float*>((reinterpret_cast<uintptr_t>(coef) + 15) & ~uintptr_t(15));
+  rn_bn_desc dd = *d;
+  dd.m = rows;
+  const int64_t off = row0 * d->c * es;
+  auto at = [&](const void* p) { return p ? (const void*)((const char*)p + off) : nullptr; };
+  hipStream_t st = as_stream(stream);
+  void* dxo = (char*)dx + off;
+  if (d->dtype == RN_BF16) {
+    if (d->relu) launch_bwd_apply<bf16_t, true>(&dd, at(x), at(dy), dxo, at(add_src), coef, scale, shift, st);
+    else launch_bwd_apply<bf16_t, false>(&dd, at(x), at(dy), dxo, at(add_src), coef, scale, shift, st);
+  } else {
+    if (d->relu) launch_bwd_apply<float, true>(&dd, at(x), at(dy), dxo, at(add_src), coef, scale, shift, st);
+    else launch_bwd_apply<float, false>(&dd, at(x), at(dy), dxo, at(add_src), coef, scale, shift, st);
+  }
+  return rn_check_launch("bn_bwd_apply_rows");
+}
+
 int rn_bn_bwd_global(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const void* add_src,
                      const float* gamma, const float* moving_mean, const float* moving_var, const float* scale,
                      const float* shift, float* dgamma, float* dbeta, void* ws, rn_stream_t stream) {

@@ -1255,6 +1255,23 @@ class Executor:
         return self._call("rn_conv_fwd_x", L.C.byref(d), xptr, self._p(op.wk), y, self.dtype, res, None, sc, sh,
                           part, sp)
 
+    def _stem_chunks(self, op, dy):
+        """Image chunks of the stem's BN-backward apply + weight gradient (RN_STEM_CHUNKS, default 4;
+        1 = one rn_bn_bwd and one wgrad): the NHWC4 stem with a side stream, whose output gradient is
+        the dx of the rn_bn_bwd call just emitted (no add operand, no paired gradient)."""
+        nch = int(os.environ.get("RN_STEM_CHUNKS", "4"))
+        side = self._side_stream is not None or (self.dry_run and os.environ.get("RN_WGRAD_STREAM", "1") == "1")
+        if nch <= 1 or not op.p4 or not side or dy is None or op.dfull.n % nch or not self._bwd:
+            return 1
+        name, _, args = self._bwd[-1]
+        if name != "rn_bn_bwd" or args[3] is None or args[4] is not None:
+            return 1
+        bn = args[0]._obj
+        if bn.dy2 or bn.c != op.dfull.k_pad or bn.m != op.dfull.n * op.dfull.p * op.dfull.q or \
+                args[3].value != self._p(dy).value:
+            return 1
+        return nch
+
     def _weight_source(self, op, qwsp, sp):
         """Quantization_int8 on a weight (int8_api.py:131-132): the compute copies are packed from a
         fake-quantized fp32 copy of the master, refreshed with every repack; the STE passes the
@@ -1439,7 +1456,28 @@ class Executor:
                 if op.res is not None and op.res.needs_grad:
                     gs.alias(op.res, dy)
             elif op.kind == "stem":
-                if op.p4:
+                nch = self._stem_chunks(op, dy)
+                if nch > 1:
+                    # the stem BN's dx (= dy here) per image chunk, each chunk's weight gradient (side
+                    # stream) starting as soon as its rows are applied: only the last chunk's wgrad
+                    # stays on the step's critical path (rn_bn_bwd then reduces + finalizes only)
+                    bname, bfn, bargs = self._bwd[-1]
+                    self._bwd[-1] = (bname, bfn, bargs[:3] + (None,) + bargs[4:])
+                    d, hp, wp = op.dfull, op.p4[0], op.p4[1]
+                    nc = d.n // nch
+                    rows = nc * d.p * d.q
+                    for i in range(nch):
+                        dc = self._conv_desc(nc, d.h, d.w, d.c, d.c_real, d.k, (d.r, d.s), (d.stride_h, d.stride_w),
+                                             (d.pad_h, d.pad_w))
+                        self._descs.append(dc)
+                        self._bwd.append(self._call("rn_bn_bwd_apply_rows", bargs[0], bargs[1], bargs[2], bargs[3],
+                                                    None, bargs[8], bargs[9], bargs[12], i * rows, rows, sp))
+                        self._bwd.append(self._call(
+                            "rn_stem_conv_wgrad_p4", L.C.byref(dc),
+                            L.C.c_void_p(op.x8.data_ptr() + i * nc * hp * wp * 4 * 2),
+                            L.C.c_void_p(self._p(dy).value + i * rows * d.k_pad * 2), self._gp(op.weight), hp, wp,
+                            sp))
+                elif op.p4:
                     self._bwd.append(self._call("rn_stem_conv_wgrad_p4", L.C.byref(op.dfull), self._p(op.x8),
                                                 self._p(dy), self._gp(op.weight), op.p4[0], op.p4[1], sp))
                 else:

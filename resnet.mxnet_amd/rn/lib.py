@@ -90,6 +90,7 @@ SIGNATURES = {
     "rn_bn_fwd_infer": (_i32, [_P] * 10),
     "rn_bn_apply": (_i32, [_P] * 6),
     "rn_bn_bwd": (_i32, [_P] * 14),
+    "rn_bn_bwd_apply_rows": (_i32, [_P] * 8 + [_i64, _i64, _P]),
     "rn_bn_bwd_global": (_i32, [_P] * 14),
     "rn_pool_desc_init": (_i32, [_P]),
     "rn_pool_fwd": (_i32, [_P, _P, _P, _P, _P]),

@@ -17,7 +17,10 @@ reductions they emit), weight gradients (split-M slabs, BN+ReLU on load), BatchN
 dgamma, dbeta), gradient fan-in adds, pooling backward (through the device's own arg-max taps), the FC
 bias gradient. References follow the ops' MXNet semantics (oracle/ops.py restated in torch).
 """
+import types
+
 import numpy as np
+
 import torch
 import torch.nn.functional as F
 
@@ -386,7 +389,37 @@ class Checker:
         return self._wgrad(args, state, xf=True)
 
     def _h_rn_stem_conv_wgrad_p4(self, args, state):
-        return self._wgrad(args, state, p4=True)
+        d = args[0]._obj
+        op = [o for o in self.ex.plan.ops if o.kind == "stem"][0]
+        if d.n == op.dfull.n:
+            return self._wgrad(args, state, p4=True)
+        # an image chunk (executor._stem_chunks): dW is complete after the last one -> check it there
+        # against the whole batch
+        hp, wp = op.p4
+        i = (args[1].value - op.x8.data_ptr()) // (d.n * hp * wp * 4 * 2)
+        if (i + 1) * d.n < op.dfull.n:
+            return None, (lambda: None)
+        dy0 = args[2].value - i * d.n * d.p * d.q * d.k_pad * 2
+        full = (types.SimpleNamespace(_obj=op.dfull), types.SimpleNamespace(value=op.x8.data_ptr()),
+                types.SimpleNamespace(value=dy0), args[3])
+        return self._wgrad(full, state, p4=True)
+
+    def _h_rn_bn_bwd_apply_rows(self, args, state):
+        """dx rows of a BN backward whose reductions rn_bn_bwd did (dx = NULL): the whole dx checked
+        after the last row chunk."""
+        d = args[0]._obj
+        if args[8] + args[9] < d.m:
+            return None, (lambda: None)
+        if not hasattr(self, "bn_by_sm_x"):
+            self.bn_by_sm_x = {self.ex.act(op.x).data_ptr(): op for op in self.ex.plan.ops if op.kind == "bn"}
+        op = self.bn_by_sm_x[args[1].value]
+        xp, dyp, dxp = args[1], args[2], args[3]
+        assert args[4] is None
+
+        def post():
+            t = op.x
+            self._bn_bwd_check(op, self.nchw(self.t(dyp), t.n, t.h, t.w, t.cp, t.c).double(), None, dxp)
+        return None, post
 
     def _bn_bwd(self, args, state, part):
         if part:

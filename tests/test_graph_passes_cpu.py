@@ -252,3 +252,22 @@ def test_grouped_repacks_batched(dry, monkeypatch):
     monkeypatch.setenv("RN_GPACK_BATCH", "0")
     ex0 = _bind(sym, precision="bfloat16").executor
     assert _call_names(ex0.unfused_packs) == ["rn_stem_weight_pack_p4"] + ["rn_conv_weight_pack"] * 16
+
+
+def test_stem_backward_chunked(dry, monkeypatch):
+    """The NHWC4 stem's BN backward: rn_bn_bwd reduces + finalizes only, then per image chunk the
+    rows of dx (rn_bn_bwd_apply_rows) and that chunk's weight gradient (side stream), the chunks
+    tiling the batch; RN_STEM_CHUNKS=1 = the single apply + wgrad."""
+    sym = graphs.resnet(**R50_SMALL)
+    ex = _bind(sym, shape=(8, 3, 64, 64), precision="bfloat16").executor
+    names = _call_names(ex._bwd)
+    i = names.index("rn_bn_bwd_apply_rows")
+    assert names[i - 1] == "rn_bn_bwd" and ex._bwd[i - 1][2][3] is None
+    assert names[i:i + 8] == ["rn_bn_bwd_apply_rows", "rn_stem_conv_wgrad_p4"] * 4
+    rows = [ex._bwd[i + 2 * j][2][8:10] for j in range(4)]
+    m = ex._bwd[i - 1][2][0]._obj.m
+    assert [r[0] for r in rows] == [j * m // 4 for j in range(4)] and all(r[1] == m // 4 for r in rows)
+    assert sum(ex._bwd[i + 2 * j + 1][2][0]._obj.n for j in range(4)) == 8
+    monkeypatch.setenv("RN_STEM_CHUNKS", "1")
+    names1 = _call_names(_bind(sym, shape=(8, 3, 64, 64), precision="bfloat16").executor._bwd)
+    assert "rn_bn_bwd_apply_rows" not in names1 and names1.count("rn_stem_conv_wgrad_p4") == 1

@@ -177,7 +177,17 @@ def test_bn_relu(gpu, dtype, case):
     dg, db = torch.zeros(cp, dtype=torch.float32, device=gpu), torch.zeros(cp, dtype=torch.float32, device=gpu)
     L.call("rn_bn_bwd", C.byref(d), p(xd), p(dyd), p(dxd), p(addd), p(g_d), p(sm), p(si), p(sc), p(sh), p(dg), p(db),
            p(ws), stream())
+    # rn_bn_bwd with dx = NULL (reductions, dgamma / dbeta) + dx in row chunks: the same bits
+    dx2 = torch.zeros_like(xd)
+    dg2, db2 = torch.zeros_like(dg), torch.zeros_like(db)
+    L.call("rn_bn_bwd", C.byref(d), p(xd), p(dyd), None, None, p(g_d), p(sm), p(si), p(sc), p(sh), p(dg2), p(db2),
+           p(ws), stream())
+    m, step = n * h * w, max(1, (n * h * w) // 3)  # (cp = 8k channels: every row starts on 16 bytes)
+    for r0 in range(0, m, step):
+        L.call("rn_bn_bwd_apply_rows", C.byref(d), p(xd), p(dyd), p(dx2), p(addd), p(sc), p(sh), p(ws), r0,
+               min(step, m - r0), stream())
     torch.cuda.synchronize()
+    assert torch.equal(dx2, dxd) and torch.equal(dg2, dg) and torch.equal(db2, db)
     tol = TOL[dtype]
     assert rel_err(from_nhwc(yd, c), y_ref) < tol
     assert rel_err(mm.cpu().numpy()[:c], mm_ref) < 1e-4
