@@ -2231,21 +2231,42 @@ __global__ void stem_quant_state_kernel(float* __restrict__ curmax, float* minma
 // The activation STE zeroes the gradient where |v| >= t (clip_grad_quantization_int8.py:56-67).
 // rn_stem_shift_grad sums the unmasked gradient; subtract the clipped elements' share:
 // dbeta[c] -= dx[n,c,h,w] at every clipped (n,c,h,w), dx = sum_{k,r,s} w[k,r,s,c] dy[n,p,q,k].
+__device__ __forceinline__ void load4f(const bf16_t* p, float* o) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  o[0] = bf2f((bf16_t)(u.x & 0xffffu));
+  o[1] = bf2f((bf16_t)(u.x >> 16));
+  o[2] = bf2f((bf16_t)(u.y & 0xffffu));
+  o[3] = bf2f((bf16_t)(u.y >> 16));
+}
+__device__ __forceinline__ void load4f(const float* p, float* o) {
+  const float4 v = *reinterpret_cast<const float4*>(p);
+  o[0] = v.x;
+  o[1] = v.y;
+  o[2] = v.z;
+  o[3] = v.w;
+}
+struct ClipGeo {
+  int N, C, H, W, P, Q, K, kpad, R, S, sh, sw, ph, pw;
+  FastDiv fdHW, fdC, fdW, fdSH, fdSW;
+};
 template <typename T>
 __global__ __launch_bounds__(256) void stem_clip_grad_kernel(const float* __restrict__ x,
                                                              const float* __restrict__ scale,
                                                              const float* __restrict__ shift,
                                                              const float* __restrict__ thr, const T* __restrict__ dy,
                                                              const float* __restrict__ wq, float* __restrict__ dbeta,
-                                                             int N, int C, int H, int W, int P, int Q, int K, int kpad,
-                                                             int R, int S, int sh, int sw, int ph, int pw) {
-  // A wave tests 256 consecutive input elements (a 16-byte load per lane), then processes each clipped
-  // one (ballot) together: lanes over the output channels k (coalesced dy rows, the weights from an
-  // LDS copy laid out [c][r][s][k] so lane k reads consecutive words), taps in a uniform loop, one wave
-  // sum per clipped element. Image data saturates (pixel value 255 IS the max), so a few 0.1 % of the
-  // elements clip: the gathers, not the scan, set this kernel's time.
-  extern __shared__ float wl[];
+                                                             const ClipGeo gm) {
+  // A wave tests 256 consecutive input elements (a 16-byte load per lane), then takes the clipped ones
+  // (ballot) four at a time: a 16-lane group per element, each lane 4 consecutive output channels k
+  // (one 8-byte dy load per tap, the group reading the tap's whole 128-byte row; the weights from an
+  // LDS copy laid out [c][r][s][k], one 16-byte read per tap), the index math per lane on the vector
+  // unit. (The first form -- one element per wave, lanes over k, its index math and tap tests on the
+  // scalar unit -- was bound by that unit, which a CU's four SIMDs share: ~700 scalar instructions per
+  // clipped element, 0.96 ms at the bench's ~1.2 % clipped elements.) Image data saturates (pixel
+  // value 255 IS the max), so a few 0.1 % of the elements clip.
+  extern __shared__ __attribute__((aligned(16))) float wl[];
   __shared__ float wsum[4][8];
+  const int C = gm.C, H = gm.H, W = gm.W, P = gm.P, Q = gm.Q, K = gm.K, R = gm.R, S = gm.S;
   const int RSK = R * S * K, nwl = C * RSK;
   for (int i = threadIdx.x; i < nwl; i += blockDim.x) {
     const int k = i % K, rest = i / K;
@@ -2256,47 +2277,68 @@ __global__ __launch_bounds__(256) void stem_clip_grad_kernel(const float* __rest
   if (threadIdx.x < 32) wsum[threadIdx.x >> 3][threadIdx.x & 7] = 0.f;
   __syncthreads();
   const float t = *thr;
-  const int HW = H * W, total = N * C * HW;
-  const int lane = threadIdx.x & 63;
-  // taps of an input pixel: r = r0 + a*sh (a < ceil(R/sh) <= 4), s likewise; all 16 dy rows are
-  // loaded before the products (one memory latency per clipped element, not one per tap)
-  // (e is wave-uniform: the index arithmetic -- a few integer divisions -- runs once per element on the
-  // scalar unit; per tap only adds: row p = (h + ph) / sh - a for r = (h + ph) % sh + a * sh)
-  auto gather = [&](int e_) {  // -sum over the clipped element's taps, wave-reduced
-    const int e = __builtin_amdgcn_readfirstlane(e_);
-    const int plane = e / HW, hw = e - plane * HW;
-    const int n = plane / C, c = plane - n * C, h = hw / W, w = hw - h * W;
-    const int hq = (h + ph) / sh, wq_ = (w + pw) / sw;
-    const int r0 = h + ph - hq * sh, s0 = w + pw - wq_ * sw;
-    const T* dyn = dy + (int64_t)n * P * Q * kpad + min(lane, K - 1);  // (lanes >= K: an in-range address, unused)
-    float dv[4][4];
-    int wo[4][4];
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const int r = r0 + a * sh, s_ = s0 + b * sw;
-        const int pp = hq - a, qq = wq_ - b;
-        const bool ok = lane < K && r < R && s_ < S && pp >= 0 && qq >= 0 && pp < P && qq < Q;
-        // unconditional load from a clamped (in-range) address, the value selected after it: the 16
-        // loads issue back to back instead of as 16 branches with a wait each
-        const int ppc = min(max(pp, 0), P - 1), qqc = min(max(qq, 0), Q - 1);
-        const float v = to_f(dyn[(ppc * Q + qqc) * kpad]);
-        dv[a][b] = ok ? v : 0.f;
-        wo[a][b] = ok ? ((c * R + r) * S + s_) * K + lane : 0;
-      }
+  const int HW = H * W, total = gm.N * C * HW;
+  const int lane = threadIdx.x & 63, grp = lane >> 4, l4 = (lane & 15) * 4;
+  const bool kok = l4 < K;
+  auto gather4 = [&](int e) {  // e < 0: no element for this lane group
     float g = 0.f;
+    int c = 0;
+    if (e >= 0) {
+      const int plane = (int)fdiv((uint32_t)e, gm.fdHW), hw = e - plane * HW;
+      const int n = (int)fdiv((uint32_t)plane, gm.fdC);
+      c = plane - n * C;
+      const int h = (int)fdiv((uint32_t)hw, gm.fdW), w = hw - h * W;
+      const int hq = (int)fdiv((uint32_t)(h + gm.ph), gm.fdSH), wq_ = (int)fdiv((uint32_t)(w + gm.pw), gm.fdSW);
+      const int r0 = h + gm.ph - hq * gm.sh, s0 = w + gm.pw - wq_ * gm.sw;
+      const T* dyn = dy + (int64_t)n * P * Q * gm.kpad + (kok ? l4 : 0);
+      float dv[4][4][4];
+      int wo[4][4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int b = 0; b < 4; ++b) g = fmaf(wl[wo[a][b]], dv[a][b], g);
-    g = wave_sum(g);
-    if (lane == 0) wsum[threadIdx.x >> 6][c] -= g;
+        for (int b = 0; b < 4; ++b) {
+          const int r = r0 + a * gm.sh, s_ = s0 + b * gm.sw;
+          const int pp = hq - a, qq = wq_ - b;
+          const bool ok = kok && r < R && s_ < S && pp >= 0 && qq >= 0 && pp < P && qq < Q;
+          // unconditional load from a clamped (in-range) address, the value selected after it
+          const int ppc = min(max(pp, 0), P - 1), qqc = min(max(qq, 0), Q - 1);
+          load4f(dyn + (int64_t)(ppc * Q + qqc) * gm.kpad, dv[a][b]);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) dv[a][b][u] = ok ? dv[a][b][u] : 0.f;
+          wo[a][b] = ok ? ((c * R + r) * S + s_) * K + l4 : 0;
+        }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const float4 wv = *reinterpret_cast<const float4*>(wl + wo[a][b]);
+          g = fmaf(wv.x, dv[a][b][0], g);
+          g = fmaf(wv.y, dv[a][b][1], g);
+          g = fmaf(wv.z, dv[a][b][2], g);
+          g = fmaf(wv.w, dv[a][b][3], g);
+        }
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) g += __shfl_xor(g, off, 64);  // the group's 16 lanes
+    if ((lane & 15) == 0 && e >= 0) atomicAdd(&wsum[threadIdx.x >> 6][c], -g);
   };
   auto clipped_at = [&](float xv, int e) {
     const int c = (e / HW) % C;
     const float v = scale ? fmaf(xv, scale[c], shift[c]) : xv;
     return !(v > -t && v < t);
+  };
+  // up to four set bits of the (wave-uniform) mask m, lowest first, to the four lane groups
+  auto take4 = [&](uint64_t& m, int e0) {
+    int eg = -1;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (m) {
+        const int b = __ffsll((unsigned long long)m) - 1;
+        m &= m - 1;
+        if (grp == q) eg = e0 + b;
+      }
+    }
+    return eg;
   };
   const int nv = total / 4;  // 16-byte chunks, then the tail
   const int nwaves = gridDim.x * (blockDim.x >> 6);
@@ -2313,21 +2355,16 @@ __global__ __launch_bounds__(256) void stem_clip_grad_kernel(const float* __rest
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       uint64_t m = __ballot(cl[j]);
-      while (m) {
-        const int b = __ffsll((unsigned long long)m) - 1;
-        m &= m - 1;
-        gather(4 * (base + b) + j);
+      while (m) {  // element of bit b: 4 * (base + b) + j
+        const int b4 = take4(m, 0);
+        gather4(b4 >= 0 ? 4 * (base + b4) + j : -1);
       }
     }
   }
   if (blockIdx.x == 0 && threadIdx.x < 64) {  // the last total % 4 elements: wave 0 of block 0
     const int e = 4 * nv + lane;
     uint64_t m = __ballot(e < total && clipped_at(x[e], e));
-    while (m) {
-      const int b = __ffsll((unsigned long long)m) - 1;
-      m &= m - 1;
-      gather(4 * nv + b);
-    }
+    while (m) gather4(take4(m, 4 * nv));
   }
   __syncthreads();
   if (threadIdx.x < C) {
@@ -3516,16 +3553,19 @@ int rn_stem_quant_clip_grad(const rn_conv_desc* d, const float* x, const float* 
   RN_CHECK_ARG(lds <= 64 * 1024, "stem weights exceed the LDS copy (c*r*s*k <= 16384)");
   RN_CHECK_ARG(d->k <= 64 && (d->r + d->stride_h - 1) / d->stride_h <= 4 && (d->s + d->stride_w - 1) / d->stride_w <= 4,
                "the quantized stem: k <= 64 and at most 4 x 4 taps per input pixel");
+  RN_CHECK_ARG(d->k % 4 == 0 && d->k_pad % 4 == 0, "the quantized stem: k a multiple of 4");
+  RN_CHECK_ARG(((uintptr_t)dy & 15) == 0, "dy must be 16-byte aligned");
+  const ClipGeo gm{d->n, d->c_real, d->h, d->w, d->p, d->q, d->k, d->k_pad, d->r, d->s, d->stride_h, d->stride_w,
+                   d->pad_h, d->pad_w, make_fastdiv(d->h * d->w), make_fastdiv(d->c_real), make_fastdiv(d->w),
+                   make_fastdiv(d->stride_h), make_fastdiv(d->stride_w)};
   // blocks of 4 waves x 256 elements; at most ~8 per CU, each stages the weights once
   const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>((total + 1023) / 1024, 2048));
   if (d->dtype == RN_BF16)
     hipLaunchKernelGGL(stem_clip_grad_kernel<bf16_t>, dim3(blocks), dim3(256), lds, st, x, scale, shift,
-                       minmax, (const bf16_t*)dy, w_q, dbeta, d->n, d->c_real, d->h, d->w, d->p, d->q, d->k, d->k_pad,
-                       d->r, d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w);
+                       minmax, (const bf16_t*)dy, w_q, dbeta, gm);
   else
     hipLaunchKernelGGL(stem_clip_grad_kernel<float>, dim3(blocks), dim3(256), lds, st, x, scale, shift,
-                       minmax, (const float*)dy, w_q, dbeta, d->n, d->c_real, d->h, d->w, d->p, d->q, d->k, d->k_pad,
-                       d->r, d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w);
+                       minmax, (const float*)dy, w_q, dbeta, gm);
   return rn_check_launch("stem_quant_clip_grad");
 }
 

@@ -680,37 +680,46 @@ __global__ void wq_state_kernel(const rn_wquant_item* __restrict__ items, int co
   ws[j] = 0.f;
   if (it.unit) it.unit[0] = t / (float)((1 << (it.nbits - 1)) - 1);
 }
+// One read of the master per weight: 64(k) x 64(c) tiles of one tap (as sgd_mom_pack_kernel), each
+// element's q = round(w / unit) computed once; the fake-quantized copy and the int8 codes stored in
+// master (KRSC) order, the data-gradient copy (CRSK) transposed through LDS so its rows are coalesced
+// too. (The first form walked the CRSK copy in its own order, reading the master with a stride of
+// RS*c_real floats per lane: 280 us per ResNet-50 step.) blockIdx.y = weight; blocks stride its tiles.
 template <typename T>
 __global__ __launch_bounds__(256) void wq_pack_kernel(const rn_wquant_item* __restrict__ items, int count,
                                                       const float* __restrict__ ws) {
+  __shared__ float tile[64][65];
   const rn_wquant_item it = items[blockIdx.y];
   const float t = ws[count + blockIdx.y];
   const float qmax = (float)((1 << (it.nbits - 1)) - 1);
   const float unit = t / qmax;  // (quant_value's and the codes' unit)
-  const int RS = it.rs, cr = it.c_real;
-  const int64_t n = (int64_t)it.k * RS * cr;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  // master order: the fake-quantized copy and the int8 codes (KRSC, channel stride c)
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += stride) {
-    const float q = unit > 0.f ? roundf(it.master[i] / unit) : 0.f;
-    it.qw[i] = q * unit;
-    if (it.w_codes) {
-      const int64_t kt = i / cr;
-      it.w_codes[kt * it.c + (i - kt * cr)] = (int8_t)(int)q;
+  const int RS = it.rs, cr = it.c_real, K = it.k;
+  const int kt = (K + 63) / 64, ct = (cr + 63) / 64;
+  const int ntiles = kt * RS * ct;
+  T* __restrict__ out = reinterpret_cast<T*>(it.w_crsk);
+  const int cl = threadIdx.x & 63, r0 = threadIdx.x >> 6;
+  for (int tl = blockIdx.x; tl < ntiles; tl += gridDim.x) {
+    const int c0 = (tl % ct) * 64, rest = tl / ct;
+    const int tap = rest % RS, k0 = (rest / RS) * 64;
+#pragma unroll 4
+    for (int j = 0; j < 16; ++j) {  // rows k0 + r, columns c0 + cl: coalesced over c
+      const int r = r0 + 4 * j, k = k0 + r, ci = c0 + cl;
+      if (k < K && ci < cr) {
+        const int64_t kt_ = (int64_t)k * RS + tap;
+        const float q = unit > 0.f ? roundf(it.master[kt_ * cr + ci] / unit) : 0.f;
+        it.qw[kt_ * cr + ci] = q * unit;
+        if (it.w_codes) it.w_codes[kt_ * it.c + ci] = (int8_t)(int)q;
+        tile[r][cl] = q * unit;
+      }
     }
-  }
-  // CRSK order (coalesced stores): the data-gradient copy of the fake-quantized values
-  if (it.w_crsk) {
-    T* out = reinterpret_cast<T*>(it.w_crsk);
-    const int64_t m = (int64_t)cr * RS * it.k;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < m; i += stride) {
-      const int k = (int)(i % it.k);
-      const int64_t ct = i / it.k;  // c*RS + tap
-      const int tap = (int)(ct % RS), ci = (int)(ct / RS);
-      const float v = it.master[((int64_t)k * RS + tap) * cr + ci];
-      const float q = unit > 0.f ? roundf(v / unit) : 0.f;
-      out[ct * it.k_pad + k] = from_f<T>(q * unit);
+    if (!out) continue;  // (uniform over the block)
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < 16; ++j) {  // rows c, columns k: coalesced over k
+      const int r = r0 + 4 * j, ci = c0 + r, k = k0 + cl;
+      if (k < K && ci < cr) out[((int64_t)ci * RS + tap) * it.k_pad + k] = from_f<T>(tile[cl][r]);
     }
+    __syncthreads();
   }
 }
 
@@ -1212,9 +1221,9 @@ int rn_weight_quant_pack(const rn_wquant_item* items, int32_t count, int32_t dty
   hipLaunchKernelGGL(wq_absmax_kernel, dim3(64, count), dim3(256), 0, st, items, ws);
   hipLaunchKernelGGL(wq_state_kernel, dim3((count + 63) / 64), dim3(64), 0, st, items, count, ws);
   if (dtype == RN_BF16)
-    hipLaunchKernelGGL(wq_pack_kernel<bf16_t>, dim3(64, count), dim3(256), 0, st, items, count, ws);
+    hipLaunchKernelGGL(wq_pack_kernel<bf16_t>, dim3(256, count), dim3(256), 0, st, items, count, ws);
   else
-    hipLaunchKernelGGL(wq_pack_kernel<float>, dim3(64, count), dim3(256), 0, st, items, count, ws);
+    hipLaunchKernelGGL(wq_pack_kernel<float>, dim3(256, count), dim3(256), 0, st, items, count, ws);
   return rn_check_launch("weight_quant_pack");
 }
 
