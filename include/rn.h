@@ -200,7 +200,8 @@ int rn_im2col_nchw_quant(const rn_conv_desc* d, const float* x_nchw, const float
                          rn_stream_t stream);
 /* The activation STE zeroes the gradient of clipped inputs (|affine(x)| >= minmax):
  * dbeta[c] -= sum over clipped (n,c,h,w) of (conv0 data-gradient), with w_q the fp32 KRSC
- * quantized weight conv0 ran with. Run after rn_stem_shift_grad. */
+ * quantized weight conv0 ran with. Run after rn_stem_shift_grad. Limits: c_real <= 8, k <= 64 and
+ * a multiple of 4, at most 4 x 4 taps per input pixel, x and dy 16-byte aligned. */
 int rn_stem_quant_clip_grad(const rn_conv_desc* d, const float* x_nchw, const float* scale,
                             const float* shift, const float* minmax, const void* dy, const float* w_q,
                             float* dbeta, rn_stream_t stream);
