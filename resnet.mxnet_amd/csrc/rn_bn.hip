@@ -181,13 +181,26 @@ __global__ __launch_bounds__(256) void bn_part_merge_kernel(const float* __restr
   double s1 = 0.0, s2 = 0.0, n = 0.0, q = 0.0;
   if (ch < c) {
     q = part[(int64_t)b0 * 3 * ld + 2 * ld + ch];
-    for (int b = b0 + sub; b < b1; b += 4) {
-      const float* pb = part + (int64_t)b * 3 * ld + ch;
+    // every load of the group issued before the (same-order) fp64 sums: one memory latency, not 16
+    constexpr int kPer = kPartGroup / 4;
+    float va[kPer], vs[kPer], vp[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int b = b0 + sub + 4 * u;
+      const float* pb = part + (int64_t)min(b, b1 - 1) * 3 * ld + ch;
+      va[u] = pb[0];
+      vs[u] = pb[ld];
+      vp[u] = pb[2 * ld];
+    }
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int b = b0 + sub + 4 * u;
+      if (b >= b1) break;
       const double nb = (double)min<int64_t>(rows_blk, m - (int64_t)b * rows_blk);
-      const double d = (double)pb[2 * ld] - q;
-      const double a = pb[0];
+      const double d = (double)vp[u] - q;
+      const double a = va[u];
       s1 += a + nb * d;
-      s2 += (double)pb[ld] + 2.0 * d * a + nb * d * d;
+      s2 += (double)vs[u] + 2.0 * d * a + nb * d * d;
       n += nb;
     }
   }
@@ -224,11 +237,23 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_part_kernel(const double*
   double s1 = 0.0, s2 = 0.0, q = 0.0;
   if (ch < c) {
     q = part2[3 * c + ch];  // group 0's pivot
-    for (int gi = sub; gi < ngrp; gi += 4) {
-      const double* pg = part2 + (int64_t)gi * 4 * c + ch;
-      const double d = pg[3 * c] - q, a = pg[0], nb = pg[2 * c];
-      s1 += a + nb * d;
-      s2 += pg[c] + 2.0 * d * a + nb * d * d;
+    for (int g0 = sub; g0 < ngrp; g0 += 16) {  // 4 groups' loads in flight, summed in group order
+      double va[4], vs[4], vn[4], vp[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double* pg = part2 + (int64_t)min(g0 + 4 * u, ngrp - 1) * 4 * c + ch;
+        va[u] = pg[0];
+        vs[u] = pg[c];
+        vn[u] = pg[2 * c];
+        vp[u] = pg[3 * c];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (g0 + 4 * u >= ngrp) break;
+        const double d = vp[u] - q, a = va[u], nb = vn[u];
+        s1 += a + nb * d;
+        s2 += vs[u] + 2.0 * d * a + nb * d * d;
+      }
     }
   }
   red[0][sub][threadIdx.x & 63] = s1;
@@ -563,10 +588,17 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
                                                               float global_eps = 0.f) {
   const int ch = blockIdx.x;
   double s = 0.0, q = 0.0;
-  for (int b = threadIdx.x; b < nrb; b += blockDim.x) {
-    const float2 v = reinterpret_cast<const float2*>(part)[(int64_t)b * c + ch];
-    s += v.x;
-    q += v.y;
+  for (int b0 = threadIdx.x; b0 < nrb; b0 += 8 * blockDim.x) {  // 8 loads in flight, summed in order
+    float2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      v[u] = reinterpret_cast<const float2*>(part)[(int64_t)min(b0 + u * (int)blockDim.x, nrb - 1) * c + ch];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (b0 + u * (int)blockDim.x >= nrb) break;
+      s += v[u].x;
+      q += v[u].y;
+    }
   }
   block_sum2(s, q);
   if (threadIdx.x != 0) return;
