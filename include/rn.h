@@ -537,7 +537,12 @@ const char* rn_last_error(void);
  *      partial tile into the workspace slab (rn_conv_bwd_filter_ws / _x; rn_conv_wgrad_ws_bytes is
  *      > 0 for every layer then, fp32 included) and one pass sums the splits in a fixed order, instead
  *      of fp32 atomic adds; the FullyConnected forward's split-K atomics are off. Bitwise
- *      run-to-run reproducible steps (the parity tests' mode). */
+ *      run-to-run reproducible steps (the parity tests' mode),
+ * 18 = cache hints of the BatchNorm apply passes (rn_bn_fwd_train / _part / rn_bn_apply outputs,
+ *      rn_bn_bwd / _part data gradients), bit mask: 1 = nontemporal 16-byte stores, 2 = nontemporal
+ *      loads, 4 (with 2) = nontemporal loads in the reduction / residual-tail passes too
+ *      (rn_bn_bwd's reduction, rn_relu_bwd_bnred, rn_bn_apply_add); default 3. The same bits either
+ *      way: only the cache policy changes. */
 int rn_set_tuning(int32_t key, int32_t value);
 int32_t rn_version(void);
 /* Number of compute units of the current device (for split heuristics / reporting). */

@@ -13,6 +13,33 @@
 
 #include "rn_common.h"
 
+// 16-byte chunk loads / stores of the streaming BatchNorm passes, NT = rn_set_tuning 18 bit mask:
+// 1 = nontemporal stores, 2 = nontemporal loads (the streaming hint: lines are evicted first, so
+// fewer dirty lines are left for the kernel-boundary L2 write-back and the other stream's tiles keep
+// their L2 share).
+typedef unsigned int rn_u32x4 __attribute__((ext_vector_type(4)));
+template <int NT>
+__device__ __forceinline__ uint4 ld16(const void* p) {
+  if constexpr ((NT & 2) != 0) {
+    const rn_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const rn_u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  } else {
+    return *reinterpret_cast<const uint4*>(p);
+  }
+}
+template <int NT>
+__device__ __forceinline__ void st16(void* p, uint4 v) {
+  if constexpr ((NT & 1) != 0) {
+    const rn_u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<rn_u32x4*>(p));
+  } else {
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+}
+// bit 4: the reduction / residual-tail read passes (bn_bwd_reduce, relu_bwd_bnred, bn_add) load
+// with the same hint
+inline bool nt_reads() { return (g_tune[RN_TUNE_BN_NT] & 6) == 6; }
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -385,7 +412,7 @@ __global__ void bn_infer_coef_kernel(int c, int c_real, float eps, int fix_gamma
 
 // 2D elementwise layout: thread (tc, tr) owns channel chunk blockIdx.x*ct+tc for rows
 // blockIdx.y*rows_per_block + tr (step rl) -> per-channel coefficients live in registers.
-template <typename T, bool RELU>
+template <typename T, bool RELU, int NT = 0>
 __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x, T* __restrict__ y,
                                                        const float* __restrict__ scale,
                                                        const float* __restrict__ shift, int64_t m, int c, int ct,
@@ -403,13 +430,13 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x, 
   }
   for (int64_t r = r0 + tr; r < r1; r += rl) {
     float f[CE];
-    chunk_to_f(*reinterpret_cast<const uint4*>(x + r * c + cbase), f, (const T*)nullptr);
+    chunk_to_f(ld16<NT>(x + r * c + cbase), f, (const T*)nullptr);
 #pragma unroll
     for (int e = 0; e < CE; ++e) {
       const float v = fmaf(f[e], sc[e], sh[e]);
       f[e] = RELU ? fmaxf(v, 0.f) : v;
     }
-    *reinterpret_cast<uint4*>(y + r * c + cbase) = f_to_chunk(f, (const T*)nullptr);
+    st16<NT>(y + r * c + cbase, f_to_chunk(f, (const T*)nullptr));
   }
 }
 
@@ -417,7 +444,7 @@ __global__ __launch_bounds__(256) void bn_apply_kernel(const T* __restrict__ x, 
 // b) with b = bn_b(xb) (the shortcut's BatchNorm) or xb itself. Each BatchNorm output is rounded to
 // the storage type before the add, exactly as the unfused bn_apply + eltwise_add pair stores and
 // re-reads it, so the result is bit-identical and the BatchNorm outputs are never written.
-template <typename T, bool RELU, bool BNB>
+template <typename T, bool RELU, bool BNB, int NT = 0>
 __global__ __launch_bounds__(256) void bn_add_kernel(const T* __restrict__ xa, const float* __restrict__ sca,
                                                      const float* __restrict__ sha, const T* __restrict__ xb,
                                                      const float* __restrict__ scb, const float* __restrict__ shb,
@@ -440,8 +467,8 @@ __global__ __launch_bounds__(256) void bn_add_kernel(const T* __restrict__ xa, c
   }
   for (int64_t r = r0 + tr; r < r1; r += rl) {
     float fa[CE], fb[CE];
-    chunk_to_f(*reinterpret_cast<const uint4*>(xa + r * c + cbase), fa, (const T*)nullptr);
-    chunk_to_f(*reinterpret_cast<const uint4*>(xb + r * c + cbase), fb, (const T*)nullptr);
+    chunk_to_f(ld16<NT>(xa + r * c + cbase), fa, (const T*)nullptr);
+    chunk_to_f(ld16<NT>(xb + r * c + cbase), fb, (const T*)nullptr);
 #pragma unroll
     for (int e = 0; e < CE; ++e) {
       const float va = to_f(from_f<T>(fmaf(fa[e], a_sc[e], a_sh[e])));
@@ -454,7 +481,7 @@ __global__ __launch_bounds__(256) void bn_add_kernel(const T* __restrict__ xa, c
 }
 
 // ---- backward reduce: sum dz, sum dz*(x - mean)
-template <typename T, bool RELU, bool PAIR = false>
+template <typename T, bool RELU, bool PAIR = false, int NT = 0>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                                             int64_t m, int c, int ct, int64_t rows_per_block,
                                                             const float* __restrict__ mean,
@@ -481,12 +508,12 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
     s[e] = q[e] = 0.f;
   }
   for (int64_t r = r0 + tr; r < r1; r += rl) {
-    uint4 ux = *reinterpret_cast<const uint4*>(x + r * c + cbase);
-    uint4 ud = *reinterpret_cast<const uint4*>(dy + r * c + cbase);
+    uint4 ux = ld16<NT>(x + r * c + cbase);
+    uint4 ud = ld16<NT>(dy + r * c + cbase);
     float fx[CE], fd[CE], f2[CE];
     chunk_to_f(ux, fx, (const T*)nullptr);
     chunk_to_f(ud, fd, (const T*)nullptr);
-    if constexpr (PAIR) chunk_to_f(*reinterpret_cast<const uint4*>(dy2 + r * c + cbase), f2, (const T*)nullptr);
+    if constexpr (PAIR) chunk_to_f(ld16<NT>(dy2 + r * c + cbase), f2, (const T*)nullptr);
 #pragma unroll
     for (int e = 0; e < CE; ++e) {
       const float dz = PAIR ? relu_clip2_dz<T>(fx[e], sc[e], sh[e], fd[e], t, f2[e], t2)
@@ -516,7 +543,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(const T* __restrict_
 // residual add) written once, and in the same pass the backward reductions of the BatchNorm(s) that
 // feed the add (sum g, sum g*(x - mean); rn_bn_bwd_part finalizes and applies them): the gradient
 // and the BN inputs are not read a second time by separate reduction passes.
-template <typename T, bool BNB>
+template <typename T, bool BNB, int NT = 0>
 __global__ __launch_bounds__(256) void relu_bwd_bnred_kernel(const T* __restrict__ y, const T* __restrict__ dy,
                                                              T* __restrict__ g, const T* __restrict__ xa,
                                                              const float* __restrict__ mean_a, float* __restrict__ part_a,
@@ -540,10 +567,10 @@ __global__ __launch_bounds__(256) void relu_bwd_bnred_kernel(const T* __restrict
   for (int64_t r = r0 + tr; r < r1; r += rl) {
     const int64_t off = r * c + cbase;
     float fy[CE], fd[CE], fx[NB][CE];
-    chunk_to_f(*reinterpret_cast<const uint4*>(y + off), fy, (const T*)nullptr);
-    chunk_to_f(*reinterpret_cast<const uint4*>(dy + off), fd, (const T*)nullptr);
-    chunk_to_f(*reinterpret_cast<const uint4*>(xa + off), fx[0], (const T*)nullptr);
-    if constexpr (BNB) chunk_to_f(*reinterpret_cast<const uint4*>(xb + off), fx[NB - 1], (const T*)nullptr);
+    chunk_to_f(ld16<NT>(y + off), fy, (const T*)nullptr);
+    chunk_to_f(ld16<NT>(dy + off), fd, (const T*)nullptr);
+    chunk_to_f(ld16<NT>(xa + off), fx[0], (const T*)nullptr);
+    if constexpr (BNB) chunk_to_f(ld16<NT>(xb + off), fx[NB - 1], (const T*)nullptr);
 #pragma unroll
     for (int e = 0; e < CE; ++e) {
       fd[e] = fy[e] > 0.f ? fd[e] : 0.f;  // (exact in the storage type: dy or 0)
@@ -624,7 +651,7 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize_kernel(const float* __res
   coef[ch * 4 + 3] = save_mean[ch];
 }
 
-template <typename T, bool RELU, bool PAIR = false>
+template <typename T, bool RELU, bool PAIR = false, int NT = 0>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__ x, const T* __restrict__ dy,
                                                            T* __restrict__ dx, const T* __restrict__ add,
                                                            const float* __restrict__ coef,
@@ -656,10 +683,10 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
   for (int64_t r = r0 + tr; r < r1; r += rl) {
     const int64_t off = r * c + cbase;
     float fx[CE], fd[CE], fa[CE], f2[CE];
-    chunk_to_f(*reinterpret_cast<const uint4*>(x + off), fx, (const T*)nullptr);
-    chunk_to_f(*reinterpret_cast<const uint4*>(dy + off), fd, (const T*)nullptr);
-    if constexpr (PAIR) chunk_to_f(*reinterpret_cast<const uint4*>(dy2 + off), f2, (const T*)nullptr);
-    if (add) chunk_to_f(*reinterpret_cast<const uint4*>(add + off), fa, (const T*)nullptr);
+    chunk_to_f(ld16<NT>(x + off), fx, (const T*)nullptr);
+    chunk_to_f(ld16<NT>(dy + off), fd, (const T*)nullptr);
+    if constexpr (PAIR) chunk_to_f(ld16<NT>(dy2 + off), f2, (const T*)nullptr);
+    if (add) chunk_to_f(ld16<NT>(add + off), fa, (const T*)nullptr);
 #pragma unroll
     for (int e = 0; e < CE; ++e) {
       const float dz = PAIR ? relu_clip2_dz<T>(fx[e], sc[e], sh[e], fd[e], t, f2[e], t2)
@@ -668,7 +695,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(const T* __restrict__
       if (add) v += fa[e];
       fd[e] = v;
     }
-    *reinterpret_cast<uint4*>(dx + off) = f_to_chunk(fd, (const T*)nullptr);
+    st16<NT>(dx + off, f_to_chunk(fd, (const T*)nullptr));
   }
 }
 
@@ -688,22 +715,37 @@ template <typename T, bool RELU>
 void launch_apply(const rn_bn_desc* d, const void* x, void* y, const float* scale, const float* shift,
                   hipStream_t st) {
   Geo a = make_apply_geo<T>(d->m, d->c);
-  hipLaunchKernelGGL((bn_apply_kernel<T, RELU>), dim3(a.gx, a.nrb), dim3(kThreads), 0, st, (const T*)x, (T*)y,
-                     scale, shift, d->m, d->c, a.ct, a.rows_per_block);
+  const int nt = g_tune[RN_TUNE_BN_NT] & 3;
+#define RN_APPLY(NT)                                                                                       \
+  hipLaunchKernelGGL((bn_apply_kernel<T, RELU, NT>), dim3(a.gx, a.nrb), dim3(kThreads), 0, st, (const T*)x, \
+                     (T*)y, scale, shift, d->m, d->c, a.ct, a.rows_per_block)
+  if (nt == 1) RN_APPLY(1);
+  else if (nt == 2) RN_APPLY(2);
+  else if (nt == 3) RN_APPLY(3);
+  else RN_APPLY(0);
+#undef RN_APPLY
 }
 
 template <typename T, bool RELU>
 void launch_bwd_apply(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const void* add,
                       const float* coef, const float* scale, const float* shift, hipStream_t st) {
   Geo a = make_apply_geo<T>(d->m, d->c);
+  const int nt = g_tune[RN_TUNE_BN_NT] & 3;
   if (RELU && d->dy2)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true>), dim3(a.gx, a.nrb), dim3(kThreads), 0, st, (const T*)x,
                        (const T*)dy, (T*)dx, (const T*)add, coef, scale, shift, d->m, d->c, a.ct, a.rows_per_block,
                        d->clip, (const T*)d->dy2, d->clip2);
-  else
-    hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RELU>), dim3(a.gx, a.nrb), dim3(kThreads), 0, st, (const T*)x,
-                       (const T*)dy, (T*)dx, (const T*)add, coef, scale, shift, d->m, d->c, a.ct, a.rows_per_block,
-                       d->clip);
+  else {
+#define RN_BWD_APPLY(NT)                                                                                       \
+  hipLaunchKernelGGL((bn_bwd_apply_kernel<T, RELU, false, NT>), dim3(a.gx, a.nrb), dim3(kThreads), 0, st,      \
+                     (const T*)x, (const T*)dy, (T*)dx, (const T*)add, coef, scale, shift, d->m, d->c, a.ct,   \
+                     a.rows_per_block, d->clip)
+    if (nt == 1) RN_BWD_APPLY(1);
+    else if (nt == 2) RN_BWD_APPLY(2);
+    else if (nt == 3) RN_BWD_APPLY(3);
+    else RN_BWD_APPLY(0);
+#undef RN_BWD_APPLY
+  }
 }
 
 template <typename T>
@@ -744,6 +786,10 @@ int bn_bwd_t(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true, true>), dim3(g.gx, g.nrb), dim3(kThreads), 0, st, (const T*)x,
                        (const T*)dy, d->m, d->c, g.ct, g.rows_per_block, smean, scale, shift, part, d->clip,
                        (const T*)d->dy2, d->clip2);
+  else if (d->relu && nt_reads())
+    hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true, false, 2>), dim3(g.gx, g.nrb), dim3(kThreads), 0, st,
+                       (const T*)x, (const T*)dy, d->m, d->c, g.ct, g.rows_per_block, smean, scale, shift, part,
+                       d->clip);
   else if (d->relu)
     hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(g.gx, g.nrb), dim3(kThreads), 0, st, (const T*)x,
                        (const T*)dy, d->m, d->c, g.ct, g.rows_per_block, smean, scale, shift, part, d->clip);
@@ -978,24 +1024,25 @@ int rn_bn_apply_add(const rn_bn_desc* d, const void* xa, const float* scale_a, c
   RN_CHECK_ARG((scale_b == nullptr) == (shift_b == nullptr), "scale_b / shift_b must both be set or both null");
   hipStream_t st = as_stream(stream);
   const bool bnb = scale_b != nullptr;
-#define RN_BN_ADD(T)                                                                                           \
+#define RN_BN_ADD(T, NT)                                                                                         \
   {                                                                                                            \
     Geo g = make_apply_geo<T>(d->m, d->c);                                                                     \
     dim3 gr(g.gx, g.nrb), bl(kThreads);                                                                        \
-    if (relu && bnb) hipLaunchKernelGGL((bn_add_kernel<T, true, true>), gr, bl, 0, st, (const T*)xa, scale_a,  \
+    if (relu && bnb) hipLaunchKernelGGL((bn_add_kernel<T, true, true, NT>), gr, bl, 0, st, (const T*)xa, scale_a,  \
                                         shift_a, (const T*)xb, scale_b, shift_b, (T*)y, d->m, d->c, g.ct,      \
                                         g.rows_per_block);                                                     \
-    else if (relu) hipLaunchKernelGGL((bn_add_kernel<T, true, false>), gr, bl, 0, st, (const T*)xa, scale_a,   \
+    else if (relu) hipLaunchKernelGGL((bn_add_kernel<T, true, false, NT>), gr, bl, 0, st, (const T*)xa, scale_a,   \
                                       shift_a, (const T*)xb, scale_b, shift_b, (T*)y, d->m, d->c, g.ct,        \
                                       g.rows_per_block);                                                       \
-    else if (bnb) hipLaunchKernelGGL((bn_add_kernel<T, false, true>), gr, bl, 0, st, (const T*)xa, scale_a,    \
+    else if (bnb) hipLaunchKernelGGL((bn_add_kernel<T, false, true, NT>), gr, bl, 0, st, (const T*)xa, scale_a,    \
                                      shift_a, (const T*)xb, scale_b, shift_b, (T*)y, d->m, d->c, g.ct,         \
                                      g.rows_per_block);                                                        \
-    else hipLaunchKernelGGL((bn_add_kernel<T, false, false>), gr, bl, 0, st, (const T*)xa, scale_a, shift_a,   \
+    else hipLaunchKernelGGL((bn_add_kernel<T, false, false, NT>), gr, bl, 0, st, (const T*)xa, scale_a, shift_a,   \
                             (const T*)xb, scale_b, shift_b, (T*)y, d->m, d->c, g.ct, g.rows_per_block);        \
   }
-  if (d->dtype == RN_BF16) RN_BN_ADD(bf16_t)
-  else RN_BN_ADD(float)
+  if (d->dtype == RN_BF16 && nt_reads()) RN_BN_ADD(bf16_t, 2)
+  else if (d->dtype == RN_BF16) RN_BN_ADD(bf16_t, 0)
+  else RN_BN_ADD(float, 0)
 #undef RN_BN_ADD
   return rn_check_launch("bn_apply_add");
 }
@@ -1013,18 +1060,19 @@ int rn_relu_bwd_bnred(const rn_bn_desc* d, const void* y, const void* dy, void* 
   RN_CHECK_ARG((xb == nullptr) == (mean_b == nullptr) && (xb == nullptr) == (part_b == nullptr),
                "xb / mean_b / part_b must all be set or all null");
   hipStream_t st = as_stream(stream);
-#define RN_RBR(T)                                                                                              \
+#define RN_RBR(T, NT)                                                                                           \
   {                                                                                                            \
     Geo gm = make_geo<T>(d->m, d->c);                                                                          \
-    if (xb) hipLaunchKernelGGL((relu_bwd_bnred_kernel<T, true>), dim3(gm.gx, gm.nrb), dim3(kThreads), 0, st,   \
+    if (xb) hipLaunchKernelGGL((relu_bwd_bnred_kernel<T, true, NT>), dim3(gm.gx, gm.nrb), dim3(kThreads), 0, st,   \
                                (const T*)y, (const T*)dy, (T*)g, (const T*)xa, mean_a, part_a, (const T*)xb,   \
                                mean_b, part_b, d->m, d->c, gm.ct, gm.rows_per_block);                          \
-    else hipLaunchKernelGGL((relu_bwd_bnred_kernel<T, false>), dim3(gm.gx, gm.nrb), dim3(kThreads), 0, st,     \
+    else hipLaunchKernelGGL((relu_bwd_bnred_kernel<T, false, NT>), dim3(gm.gx, gm.nrb), dim3(kThreads), 0, st,     \
                             (const T*)y, (const T*)dy, (T*)g, (const T*)xa, mean_a, part_a, (const T*)nullptr, \
                             (const float*)nullptr, (float*)nullptr, d->m, d->c, gm.ct, gm.rows_per_block);      \
   }
-  if (d->dtype == RN_BF16) RN_RBR(bf16_t)
-  else RN_RBR(float)
+  if (d->dtype == RN_BF16 && nt_reads()) RN_RBR(bf16_t, 2)
+  else if (d->dtype == RN_BF16) RN_RBR(bf16_t, 0)
+  else RN_RBR(float, 0)
 #undef RN_RBR
   return rn_check_launch("relu_bwd_bnred");
 }

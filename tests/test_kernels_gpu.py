@@ -141,6 +141,44 @@ BN_CASES = [(4, 64, 9, 9, False, True), (2, 24, 5, 7, True, False), (8, 256, 4, 
 
 
 @pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("relu", [False, True])
+def test_bn_streaming_hint_variants(gpu, dtype, relu):
+    """rn_set_tuning 18 (nontemporal stores / loads in the BatchNorm passes) changes only the cache
+    policy: rn_bn_fwd_train's y and rn_bn_bwd's reduction and dx (with the residual add) are
+    bit-identical for every mask value."""
+    n, c, h, w = 4, 200, 9, 13
+    rng = np.random.default_rng(61)
+    x = rng.standard_normal((n, c, h, w)) * 2 + 0.5
+    dy = rng.standard_normal((n, c, h, w))
+    add = rng.standard_normal((n, c, h, w))
+    gamma, beta = rng.uniform(0.5, 1.5, c), rng.standard_normal(c) * 0.1
+    d = L.BNDesc(dtype=dtype, m=n * h * w, c=c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=int(relu))
+    f = lambda a: torch.tensor(a, dtype=torch.float32, device=gpu)
+    xd, dyd, addd = to_nhwc(x, dtype, gpu), to_nhwc(dy, dtype, gpu), to_nhwc(add, dtype, gpu)
+    ws = torch.zeros(L.load().rn_bn_workspace_bytes(C.byref(d)) // 4 + 16, dtype=torch.float32, device=gpu)
+    outs = []
+    try:
+        for mode in (0, 1, 2, 3, 6, 7):
+            L.call("rn_set_tuning", 18, mode)
+            g_d, b_d, mm, mv = f(gamma), f(beta), f(np.zeros(c)), f(np.ones(c))
+            sm, si, sc, sh = [torch.zeros(c, dtype=torch.float32, device=gpu) for _ in range(4)]
+            yd, dxd = torch.zeros_like(xd), torch.zeros_like(xd)
+            dg, db = torch.zeros(c, dtype=torch.float32, device=gpu), torch.zeros(c, dtype=torch.float32, device=gpu)
+            L.call("rn_bn_fwd_train", C.byref(d), p(xd), p(yd), p(g_d), p(b_d), p(mm), p(mv), p(sm), p(si), p(sc),
+                   p(sh), p(ws), stream())
+            L.call("rn_bn_bwd", C.byref(d), p(xd), p(dyd), p(dxd), p(addd), p(g_d), p(sm), p(si), p(sc), p(sh),
+                   p(dg), p(db), p(ws), stream())
+            torch.cuda.synchronize()
+            outs.append((yd.cpu(), dxd.cpu(), dg.cpu(), db.cpu()))
+    finally:
+        L.call("rn_set_tuning", 18, 3)  # the default
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
+    assert outs[0][0].abs().sum() > 0 and outs[0][1].abs().sum() > 0
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
 @pytest.mark.parametrize("case", BN_CASES)
 def test_bn_relu(gpu, dtype, case):
     n, c, h, w, fix_gamma, relu = case
