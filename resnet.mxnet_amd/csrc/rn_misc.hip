@@ -522,11 +522,21 @@ __global__ void quant_bwd_kernel(int64_t n, const T* __restrict__ x, const T* __
 // r0 + tr, r0 + tr + rl, ...; y = [relu](fmaf(x, scale, shift)) rounded to T exactly as bn_apply_kernel
 // stores it, so max|y|, the codes and the fake-quantized values equal rn_bn_apply followed by
 // rn_quant_int8_fwd_codes bit for bit, without the BatchNorm output's write and two re-reads.
-template <typename T, bool RELU>
+typedef unsigned int bnq_u32x4 __attribute__((ext_vector_type(4)));
+template <typename T, bool RELU, bool NT = false>
 __device__ __forceinline__ void bnq_load(const T* __restrict__ x, const float* sc, const float* sh, float* f) {
   constexpr int CE = 16 / sizeof(T);
 #pragma unroll
-  for (int h = 0; h < 16 / CE; ++h) chunk_to_f(reinterpret_cast<const uint4*>(x)[h], f + h * CE, (const T*)nullptr);
+  for (int h = 0; h < 16 / CE; ++h) {
+    uint4 u;
+    if constexpr (NT) {  // rn_set_tuning 18 bit 8: the streaming hint (as rn_bn.hip's BatchNorm passes)
+      const bnq_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const bnq_u32x4*>(x) + h);
+      u = make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+      u = reinterpret_cast<const uint4*>(x)[h];
+    }
+    chunk_to_f(u, f + h * CE, (const T*)nullptr);
+  }
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const float v = fmaf(f[e], sc[e], sh[e]);
@@ -597,7 +607,7 @@ struct BnqTargets {
   float* unit[2];
   float qmax[2];
 };
-template <typename T, bool RELU, int NQ>
+template <typename T, bool RELU, int NQ, bool NT = false>
 __global__ __launch_bounds__(256) void bnq_codes_kernel(const T* __restrict__ x, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, int64_t m, int c, int ct,
                                                         int64_t rows_per_block, BnqTargets tg,
@@ -623,7 +633,7 @@ __global__ __launch_bounds__(256) void bnq_codes_kernel(const T* __restrict__ x,
   }
   for (int64_t r = r0 + tr; r < r1; r += rl) {
     float f[16];
-    bnq_load<T, RELU>(x + r * c + cb, sc, sh, f);
+    bnq_load<T, RELU, NT>(x + r * c + cb, sc, sh, f);
     const int64_t off = r * c + cb;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
@@ -639,8 +649,15 @@ __global__ __launch_bounds__(256) void bnq_codes_kernel(const T* __restrict__ x,
         else cw[e >> 2] |= b << (8 * (e & 3));
       }
 #pragma unroll
-      for (int h = 0; h < 16 / CE; ++h)
-        reinterpret_cast<uint4*>(reinterpret_cast<T*>(tg.out[k]) + off)[h] = f_to_chunk(g + h * CE, (const T*)nullptr);
+      for (int h = 0; h < 16 / CE; ++h) {
+        const uint4 o = f_to_chunk(g + h * CE, (const T*)nullptr);
+        if constexpr (NT) {  // the fake-quantized copy is read only by the weight gradients, later
+          const bnq_u32x4 w = {o.x, o.y, o.z, o.w};
+          __builtin_nontemporal_store(w, reinterpret_cast<bnq_u32x4*>(reinterpret_cast<T*>(tg.out[k]) + off) + h);
+        } else {
+          reinterpret_cast<uint4*>(reinterpret_cast<T*>(tg.out[k]) + off)[h] = o;
+        }
+      }
       reinterpret_cast<uint4*>(tg.codes[k] + off)[0] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
     }
   }
@@ -733,7 +750,7 @@ __global__ void quant_state_multi_kernel(float* __restrict__ curmax, float* minm
 
 }  // namespace
 
-int g_tune[RN_TUNE_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512, 0, 0, 0, 0, 0, 0, 0, 3};
+int g_tune[RN_TUNE_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512, 0, 0, 0, 0, 0, 0, 0, 7};
 
 extern "C" {
 
@@ -1168,8 +1185,12 @@ static void launch_quant_codes_bn(const rn_bn_desc* d, const void* x, const floa
   hipLaunchKernelGGL(quant_state_multi_kernel, dim3(1), dim3(1), 0, st, curmax, minmax[0], minmax[NQ - 1], NQ,
                      is_train, decay[0], decay[NQ - 1], first_batch, thr);
   const auto g = geo(8);
-  hipLaunchKernelGGL((bnq_codes_kernel<T, RELU, NQ>), dim3(gx, g.first), dim3(256), 0, st, (const T*)x, scale, shift,
-                     d->m, d->c, ct, g.second, tg, thr);
+  if (g_tune[RN_TUNE_BN_NT] & 8)
+    hipLaunchKernelGGL((bnq_codes_kernel<T, RELU, NQ, true>), dim3(gx, g.first), dim3(256), 0, st, (const T*)x, scale,
+                       shift, d->m, d->c, ct, g.second, tg, thr);
+  else
+    hipLaunchKernelGGL((bnq_codes_kernel<T, RELU, NQ>), dim3(gx, g.first), dim3(256), 0, st, (const T*)x, scale,
+                       shift, d->m, d->c, ct, g.second, tg, thr);
 }
 template <int NQ>
 static int quant_codes_bn(const rn_bn_desc* d, const void* x, const float* scale, const float* shift,
