@@ -543,8 +543,9 @@ const char* rn_last_error(void);
  *      loads, 4 (with 2) = nontemporal loads in the reduction / residual-tail passes too
  *      (rn_bn_bwd's reduction, rn_relu_bwd_bnred, rn_bn_apply_add), 8 = the BatchNorm-folded int8
  *      quantizer pass (rn_quant_int8_fwd_codes_bn / _bn2: x loads, the fake-quantized copy's stores;
- *      measured slower: C5 24.1 -> 25.1 ms per step). Default 7. The same bits either way: only the
- *      cache policy changes. */
+ *      measured slower: C5 24.1 -> 25.1 ms per step), 16 = the 224/256-row conv tiles' output stores
+ *      (rn_conv_fwd* / rn_conv_bwd_data*). Default 23. The same bits either way: only the cache
+ *      policy changes. */
 int rn_set_tuning(int32_t key, int32_t value);
 int32_t rn_version(void);
 /* Number of compute units of the current device (for split heuristics / reporting). */

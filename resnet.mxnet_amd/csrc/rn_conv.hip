@@ -59,6 +59,7 @@ struct IgemmArgs {
   int diag_l1;         // diagnostic (rn_set_tuning 3): every A row reads the same L1-resident chunk
   int sched;           // igemm_big_kernel schedule experiments (rn_set_tuning 7, bit mask)
   int epi_sync;        // igemm_big_kernel: block barriers around the epilogue's LDS staging (rn_set_tuning 16)
+  int nt_store;        // igemm_big_kernel: output stores with the nontemporal hint (rn_set_tuning 18 bit 16)
   int ntiles;          // igemm_big_kernel persistent mode: tiles per class (0: one tile per workgroup)
   int x_bytes, w_bytes;  // LDS-DMA buffer descriptors
   // dgrad only, nullable: the BatchNorm-backward reduction of the gradient this conv completes
@@ -1199,8 +1200,19 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
         for (int u = 0; u < AW; ++u) out[u] = f_to_chunk(v + u * (8 / AW), (const OutT*)nullptr);
         if (yg && (!(kRnDiag && (p.sched & 32)) || (out[0].x & 0xFFFF) == 0x7FC1))  // (EPI 2 may only reduce;
                                                                                   // diagnostic bit 32: no stores)
+        {
+          if (p.nt_store) {  // streaming hint: fewer dirty lines left for the end-of-kernel L2 write-back
+            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-          for (int u = 0; u < AW; ++u) reinterpret_cast<uint4*>(yg + off[k])[u] = out[u];
+            for (int u = 0; u < AW; ++u) {
+              const u32x4 w = {out[u].x, out[u].y, out[u].z, out[u].w};
+              __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(yg + off[k]) + u);
+            }
+          } else {
+#pragma unroll
+            for (int u = 0; u < AW; ++u) reinterpret_cast<uint4*>(yg + off[k])[u] = out[u];
+          }
+        }
         if constexpr (EPI == 1 || EPI == 2) {  // on the stored (rounded) values, as a separate pass would read them
           float g[8];
 #pragma unroll
@@ -2627,6 +2639,7 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   b.diag_l1 = g_tune[RN_TUNE_DIAG_IGEMM_L1];
   b.sched = g_tune[RN_TUNE_IGEMM_SCHED];
   b.epi_sync = g_tune[RN_TUNE_EPI_SYNC];
+  b.nt_store = (g_tune[RN_TUNE_BN_NT] & 16) != 0;
   const int64_t xb = (int64_t)a.N * a.H * a.W * a.C * (int64_t)sizeof(T);
   const int64_t wb = (int64_t)a.K * a.wrow * (int64_t)sizeof(T);
   b.x_bytes = (int)std::min<int64_t>(xb, INT32_MAX);
@@ -2775,6 +2788,7 @@ int launch_igemm_i8(const IgemmArgs& a, bool f32out, hipStream_t st) {
   IgemmArgs b = a;
   b.sched = g_tune[RN_TUNE_IGEMM_SCHED];
   b.epi_sync = g_tune[RN_TUNE_EPI_SYNC];
+  b.nt_store = (g_tune[RN_TUNE_BN_NT] & 16) != 0;
   b.x_bytes = (int)xb;
   b.w_bytes = (int)wb;
   b.ntiles = 0;
@@ -3339,6 +3353,7 @@ int rn_stem_conv_fwd_p4(const rn_conv_desc* d, const void* x4, const void* w4, v
   a.w_bytes = d->k * 256 * 2;
   a.sched = g_tune[RN_TUNE_IGEMM_SCHED];
   a.epi_sync = g_tune[RN_TUNE_EPI_SYNC];
+  a.nt_store = (g_tune[RN_TUNE_BN_NT] & 16) != 0;
   a.ntn = 1;
   const int64_t M = (int64_t)d->n * d->p * d->q;
   hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, 2>), dim3((unsigned)ceil_div(M, 256)), dim3(256), 0,

@@ -171,7 +171,7 @@ def test_bn_streaming_hint_variants(gpu, dtype, relu):
             torch.cuda.synchronize()
             outs.append((yd.cpu(), dxd.cpu(), dg.cpu(), db.cpu()))
     finally:
-        L.call("rn_set_tuning", 18, 7)  # the default
+        L.call("rn_set_tuning", 18, 23)  # the default
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert torch.equal(a, b)
