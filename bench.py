@@ -64,16 +64,36 @@ def conv_call_bytes(ex, name, args):
     return x + y + 2 * d.k * d.r * d.s * d.c_real * 4  # wgrad: fp32 dW read-modify-write (slabs not counted)
 
 
-def pmc_traffic(family):
+PMC_ROUNDS = ("r04", "r03")  # newest first: the committed PMC summary of the latest round that has one
+
+
+def pmc_json_path():
+    env = os.environ.get("RN_PMC_JSON")
+    if env:
+        return env
+    for r in PMC_ROUNDS:
+        p = os.path.join(REPO, "profiles", r, "pmc_hbm_bytes_per_launch.json")
+        if os.path.exists(p):
+            return p
+    return None
+
+
+def pmc_traffic(family, path=None):
     """HBM bytes per launch of `family` from the committed rocprofv3 PMC summary (tools/pmc_bench.sh +
-    tools/pmc_summary.py: FETCH_SIZE doubled per the gfx950 correction, plus WRITE_SIZE)."""
-    path = os.environ.get("RN_PMC_JSON", os.path.join(REPO, "profiles", "r03", "pmc_hbm_bytes_per_launch.json"))
+    tools/pmc_summary.py: FETCH_SIZE doubled per the gfx950 correction, plus WRITE_SIZE). The summary
+    nests the families under "hbm" (with "sq" and "last_step_hbm_bytes" beside it); a flat
+    {family: record} file (round 2) is read too."""
+    path = path or pmc_json_path()
+    if not path:
+        return None, None
     try:
         with open(path) as f:
-            rec = json.load(f).get(family)
+            doc = json.load(f)
     except OSError:
         return None, None
-    if not rec:
+    fams = doc.get("hbm") if isinstance(doc.get("hbm"), dict) else doc
+    rec = fams.get(family)
+    if not rec or "hbm_bytes" not in rec:
         return None, None
     return rec["hbm_bytes"], os.path.relpath(path, REPO)
 
@@ -247,13 +267,19 @@ def _free_port():
     return port
 
 
-def launch_ranks(n, argv):
+class _Interrupted(Exception):
+    pass
+
+
+def launch_ranks(n, argv, cmd=None):
     """`python bench.py --gpus N` without a torch.distributed launcher (how the driver runs it):
     start N fresh rank processes of this script -- one per GPU, RANK / LOCAL_RANK / WORLD_SIZE /
     MASTER_* set as torch.distributed.run would -- before this process touches the GPU, wait for
     them and return the exit status. The reference drives its GPUs from one `python train.py`
     (train.py:34-35, core/solver.py:58-61,121); here each GPU gets its own process and RCCL sums the
-    gradients. A rank that fails takes the others down (they would block in a collective)."""
+    gradients. A rank that fails takes the others down (they would block in a collective); so does
+    a SIGTERM / SIGINT to this launcher (each rank runs in its own session, so a signal to the
+    launcher alone would otherwise leave them holding their GPUs). `cmd`: the rank command (tests)."""
     import signal
     import subprocess
     import torch
@@ -264,29 +290,51 @@ def launch_ranks(n, argv):
               "fewer GPUs)" % (n, ngpu), file=sys.stderr)
         return 2
     port = os.environ.get("MASTER_PORT") or str(_free_port())
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)] + argv
     procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port, RN_BENCH_LAUNCHED="1")
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
-                                      start_new_session=True))
+
+    def stop_live():
+        for pr in procs:
+            if pr.poll() is None:
+                try:
+                    os.killpg(pr.pid, signal.SIGKILL)
+                except OSError:
+                    pass
+        for pr in procs:
+            try:
+                pr.wait(timeout=30)
+            except Exception:
+                pass
+
+    def on_signal(signum, frame):
+        raise _Interrupted(signum)
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
     rc = 0
-    live = list(range(n))
-    while live:
-        time.sleep(0.2)
-        for r in list(live):
-            c = procs[r].poll()
-            if c is None:
-                continue
-            live.remove(r)
-            if c != 0 and rc == 0:
-                rc = c if c > 0 else 128 - c
-                print("bench.py: rank %d exited with %d; stopping the other ranks" % (r, c), file=sys.stderr)
-                for q in live:
-                    try:
-                        os.killpg(procs[q].pid, signal.SIGKILL)
-                    except OSError:
-                        pass
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port, RN_BENCH_LAUNCHED="1")
+            procs.append(subprocess.Popen(cmd, env=env, start_new_session=True))
+        live = list(range(n))
+        while live:
+            time.sleep(0.2)
+            for r in list(live):
+                c = procs[r].poll()
+                if c is None:
+                    continue
+                live.remove(r)
+                if c != 0 and rc == 0:
+                    rc = c if c > 0 else 128 - c
+                    print("bench.py: rank %d exited with %d; stopping the other ranks" % (r, c), file=sys.stderr)
+                    stop_live()
+    except _Interrupted as e:
+        print("bench.py: launcher got signal %d; stopping every rank" % e.args[0], file=sys.stderr)
+        rc = 128 + e.args[0]
+    finally:
+        stop_live()
+        for s, h in old.items():
+            signal.signal(s, h)
     return rc
 
 
@@ -429,6 +477,10 @@ def main():
         timer.wrap()  # HIP events around every launch of the dominant family, inside the timed region
         run = step
 
+    reducer = mod._reducer
+    if reducer is not None and not use_graph:
+        reducer.timing = True  # overlap evidence: HIP events at the backward's ends and each bucket
+        reducer.records = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -439,6 +491,15 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    overlap = None
+    if reducer is not None and reducer.timing:
+        reducer.timing = False
+        overlap = reducer.timing_summary(world)
+        if overlap is not None and world > 1:
+            t = torch.tensor([overlap["exposed_ms"], overlap["exposed_ms_max"]], device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            overlap["exposed_ms_max_over_ranks"] = round(float(t[1].item()), 3)
+            overlap["exposed_ms_mean_max_over_ranks"] = round(float(t[0].item()), 3)
     if use_graph:
         # graph nodes cannot carry timing events: time the family's launches in one eager step
         # run directly after the timed region (same kernels and shapes as the replayed graph)
@@ -540,6 +601,9 @@ def main():
                                 "launch": "one process per GPU (%s)" % (
                                     "bench.py --gpus" if os.environ.get("RN_BENCH_LAUNCHED") else "torch.distributed.run"),
                                 "overlap": "buckets launched from the backward plan on the weight-gradient stream"}
+            if overlap is not None:
+                # exposed_ms: end of the backward -> last bucket summed (what the backward did not hide)
+                out["allreduce"].update(overlap)
             if force_ar:
                 out["allreduce"]["note"] = "RCCL bucket all-reduce hooks on at N=1 (RN_BENCH_ALLREDUCE=1)"
         if world == 1 and not a.no_cpu_baseline and a.model == "resnet50":

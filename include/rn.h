@@ -49,6 +49,9 @@ typedef struct rn_conv_desc {
   int32_t pad_h, pad_w;
   int32_t groups;                 /* num_group (ResNeXt grouped conv)                         */
   int32_t p, q;                   /* output spatial size, filled by rn_conv_desc_init         */
+  int32_t grouped_direct;         /* filled by rn_conv_desc_init: 1 = this grouped 3x3 runs the
+                                     direct v_dot2 kernels with compact weight copies (see
+                                     rn_conv_pack_numel); fixed for the descriptor's lifetime    */
 } rn_conv_desc;
 
 /* Validate and fill p, q (MXNet 'valid' convention: p = (h + 2*pad - r)/stride + 1). */
@@ -170,7 +173,8 @@ int64_t rn_conv_pack_numel(const rn_conv_desc* d, int32_t which);
  * channels of the groups that j's 64-column block touches, zero outside j's own group
  * (w_krsc: [k][r][s][cblk], w_crsk: [c][r][s][kblk]); sizes from rn_conv_pack_numel.
  * Except where the direct grouped kernel runs (bf16, 3x3 pad 1, c = k, 4 channels per group at
- * stride 1 or 2, or 8 per group at stride 2 -- forward and data gradient; rn_set_tuning 15): that
+ * stride 1 or 2, or 8 per group at stride 2 -- forward and data gradient; d->grouped_direct, which
+ * rn_conv_desc_init sets from rn_set_tuning 15 at that time): that
  * mode's copy is compact, [c/8][tap][8][G] with G = c/groups -- w_krsc[k/8][tap][k%8][c'] =
  * w[k][tap][c'], w_crsk[c/8][tap][c%8][k'] = w[g*G + k'][8 - tap][c - g*G], g = c/G -- and
  * rn_conv_fwd / rn_conv_bwd_data multiply it with v_dot2_f32_bf16 (no bias, statistics or BN fusions). */
@@ -489,8 +493,9 @@ typedef struct rn_wquant_item {
 } rn_wquant_item;
 /* Every weight quantizer of a network in three launches (max|w| of each tensor, the thresholds, the
  * copies) instead of rn_quant_int8_fwd_codes + rn_conv_weight_pack + rn_conv_weight_pack_i8 per
- * weight: bit-identical to those. items: DEVICE array of count entries; ws: >= 2*count floats, the
- * first count zero on entry (left zero: the quantizers' shared workspace). The padding of w_codes /
+ * weight: bit-identical to those. items: DEVICE array of count entries; ws: >= 2*count floats (the
+ * quantizers' shared workspace: the first count are cleared on entry and left zero, whatever the
+ * activation quantizers left in them). The padding of w_codes /
  * w_crsk (channels >= c_real, columns >= k) is not written (zero from their first pack). */
 int rn_weight_quant_pack(const rn_wquant_item* items, int32_t count, int32_t dtype, float* ws,
                          rn_stream_t stream);

@@ -21,6 +21,16 @@
 
 namespace {
 
+// CUs of the device (cached once per process; 256 -- gfx950 MI355X -- on a host without a GPU, where
+// only plan-time sizing runs): the split-M weight gradients size their grids to one round of it
+int chip_cus() {
+  static const int cus = [] {
+    const int n = rn_device_cu_count();
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
+
 // ------------------------------------------------------------------------------ igemm
 struct IgemmCls {
   int a, b;          // output parity class (dgrad) -- (0,0) for fwd
@@ -2837,23 +2847,25 @@ __global__ void pack_krsc_i8_kernel(const float* __restrict__ wm, const float* _
   }
 }
 
-// Does the grouped convolution d run the direct kernel in mode 0 (forward) / 1 (data gradient)?
-// Its compute copy of that mode is then the compact one (pack_group_direct_kernel). rn_set_tuning 15 = 1:
-// the block-diagonal MFMA path (set before packing: the two paths' copies differ).
 // Does the grouped convolution d run the direct kernel in mode 0 (forward) / 1 (data gradient)? Its
 // compute copy of that mode is then the compact one (pack_group_direct_kernel). Where it pays (measured,
 // ResNeXt-50 at batch 256): 4 channels per group -- forward and data gradient, stride 1 / 2 -- and the
 // 8-per-group stride-2 layers; with 8 (stride 1) or 16 per group the v_dot2 work outgrows the memory
-// time and the block-diagonal MFMA tiles win. rn_set_tuning 15 = 1: never (set before packing:
-// the two paths' copies differ).
-bool gd_direct_ok(const rn_conv_desc* d, int mode) {
-  if (!d || d->dtype != RN_BF16 || d->groups <= 1 || g_tune[RN_TUNE_GROUP_DIRECT] == 1) return false;
+// time and the block-diagonal MFMA tiles win.
+bool gd_direct_shape(const rn_conv_desc* d, int mode) {
+  if (!d || d->dtype != RN_BF16 || d->groups <= 1) return false;
   const int cpg = d->c / d->groups;
   if (d->c != d->c_real || d->k != d->c || d->k_pad != d->k || d->c % d->groups || (cpg != 4 && cpg != 8)) return false;
   if (d->r != 3 || d->s != 3 || d->pad_h != 1 || d->pad_w != 1 || d->stride_h != d->stride_w) return false;
   if (d->c % 8 || 64 % (d->c / 8) || (int64_t)d->c * 9 * cpg * 2 > 64 * 1024) return false;
   if (cpg == 8) return (mode == 0 || mode == 1) && d->stride_h == 2;  // (stride 1: the MFMA tile wins)
   return (mode == 0 || mode == 1) && (d->stride_h == 1 || d->stride_h == 2);
+}
+// The choice is recorded in the descriptor by rn_conv_desc_init (rn_set_tuning 15 = 1 at that time:
+// the block-diagonal path), so the packs and the launches of one descriptor always agree on the
+// layout of its copies, whatever the tuning key says later.
+bool gd_direct_ok(const rn_conv_desc* d, int mode) {
+  return d && d->grouped_direct == 1 && gd_direct_shape(d, mode);
 }
 
 int gd_launch(const rn_conv_desc* d, int mode, const void* x, const void* w, void* y, const void* add,
@@ -2921,6 +2933,7 @@ int rn_conv_desc_init(rn_conv_desc* d) {
   d->p = (d->h + 2 * d->pad_h - d->r) / d->stride_h + 1;
   d->q = (d->w + 2 * d->pad_w - d->s) / d->stride_w + 1;
   RN_CHECK_ARG(d->p > 0 && d->q > 0, "empty output");
+  d->grouped_direct = (g_tune[RN_TUNE_GROUP_DIRECT] != 1 && gd_direct_shape(d, 0)) ? 1 : 0;
   RN_CHECK_ARG((int64_t)d->n * d->h * d->w < (1ll << 31) && (int64_t)d->n * d->p * d->q < (1ll << 31),
                "too many pixels");
   return 0;
@@ -2972,9 +2985,9 @@ int rn_conv_fwd_i8(const rn_conv_desc* d, const void* x_codes, const void* w_cod
 int rn_conv_fwd_i8_mm(const rn_conv_desc* d, const void* x_codes, const void* w_codes, void* y, int32_t y_dtype,
                       const void* add_src, const float* x_unit, const float* w_unit, float* part, float* part_mm,
                       const float* mm_sign, rn_stream_t stream) {
+  RN_CHECK_ARG(d && x_codes && w_codes && y && x_unit && w_unit, "null argument");
   RN_CHECK_ARG(!part_mm || (part && y_dtype == RN_BF16), "part_mm comes with the BatchNorm partials (bf16 output)");
   RN_CHECK_ARG(!mm_sign || (((uintptr_t)mm_sign & 15) == 0 && d->k % 8 == 0), "mm_sign: 16-byte aligned, k % 8 == 0");
-  RN_CHECK_ARG(d && x_codes && w_codes && y && x_unit && w_unit, "null argument");
   RN_CHECK_ARG(d->groups <= 1, "int8 convolution is dense");
   RN_CHECK_ARG(y_dtype == RN_BF16 || y_dtype == RN_F32, "bad output dtype");
   RN_CHECK_ARG(!part || d->k % 8 == 0, "BatchNorm statistics need whole 8-channel chunks");
@@ -3193,7 +3206,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     a.nkt = (int)ceil_div(a.K, 128);
     const int64_t tiles = (int64_t)a.nct * a.nkt;
     const int64_t mtiles = ceil_div(a.M, 64);
-    const int64_t target = 256 * (g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU] > 0 ? g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU] : 2);
+    const int64_t target = chip_cus() * (g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU] > 0 ? g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU] : 2);
     int64_t split = std::min<int64_t>(std::max<int64_t>(1, target / tiles), std::max<int64_t>(1, mtiles / 8));
     a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
     split = ceil_div(a.M, a.m_per_split);
@@ -3234,10 +3247,10 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
   // of each tile variant (VGPR / LDS bound): 128x128 -> 2, 64x128 / 128x64 -> 3, 64x64 -> 5.
   // (the bf16 grouped block-diagonal-skip kernel (gdiag): 8, measured on the ResNeXt-50 3x3 layers --
   // 2.08 vs 2.39 ms per step at 5, 2.23 at 3, 2.20 at 12; tools/runs/gsplit.sh. Other grouped
-  // variants keep the 64x64 tile's 5.) The chip size is the gfx950 constant kSplitCus, not a device
-  // query: rn_conv_wgrad_ws_bytes sizes the slab workspace from this same split at plan time, possibly
-  // on a host without a GPU, and the launch must agree with it.
-  constexpr int kSplitCus = 256;
+  // variants keep the 64x64 tile's 5.) The chip size is chip_cus(): the device's CU count, cached
+  // once per process (rn_conv_wgrad_ws_bytes sizes the slab workspace from this same split at plan
+  // time, and the launch agrees with it), 256 on a host without a GPU (plan-only dry runs).
+  const int kSplitCus = chip_cus();
   int per_cu = (grouped && a.gdiag) ? 8 : (bmk == 128 && bnc == 128) ? 2 : (bmk == 64 && bnc == 64) ? (in_scale ? 4 : 5) : 3;
   if (g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU] > 0) per_cu = g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU];
   int64_t want = std::max<int64_t>(1, (int64_t)per_cu * kSplitCus / tiles);

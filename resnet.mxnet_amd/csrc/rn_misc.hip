@@ -1239,6 +1239,9 @@ int rn_weight_quant_pack(const rn_wquant_item* items, int32_t count, int32_t dty
   RN_CHECK_ARG(items && ws && count > 0 && count <= 65535, "bad arguments");
   RN_CHECK_ARG(dtype == RN_BF16 || dtype == RN_F32, "bad dtype");
   hipStream_t st = as_stream(stream);
+  // ws is the quantizers' shared workspace: the activation quantizers leave their thresholds in
+  // ws[1..2], so the per-weight max accumulators are cleared here, not assumed zero
+  if (hipMemsetAsync(ws, 0, sizeof(float) * (size_t)count, st) != hipSuccess) return rn_check_launch("weight_quant_pack");
   hipLaunchKernelGGL(wq_absmax_kernel, dim3(64, count), dim3(256), 0, st, items, ws);
   hipLaunchKernelGGL(wq_state_kernel, dim3((count + 63) / 64), dim3(64), 0, st, items, count, ws);
   if (dtype == RN_BF16)

@@ -340,6 +340,8 @@ class Module:
         if out_grads is not None:
             raise MXNetError("head gradients are not supported (SoftmaxOutput is a loss head)")
         ex = self._exec
+        if self._reducer is not None:
+            self._reducer.begin_step()
         ex.backward(hooks=self._reducer.hooks() if self._reducer else None)
         if self._reducer is not None:
             self._reducer.launched_step = True  # every bucket was launched by its backward hook

@@ -36,6 +36,24 @@ class BucketAllReducer:
         self.group = group
         self.works = []
         self.launched_step = False  # set by Module.backward once the hooks launched every bucket
+        # overlap evidence (bench.py, N > 1): HIP events per step at the backward's start, at each
+        # bucket's launch, at the end of the backward (the stream that waits for the buckets) and after
+        # each bucket's wait; off by default
+        self.timing = False
+        self.records = []
+        self._cur = None
+
+    def begin_step(self):
+        """Module.backward calls this before the backward's first kernel is enqueued."""
+        if self.timing:
+            self._cur = {"start": self._event(), "launch": {}, "done": []}
+
+    @staticmethod
+    def _event():
+        import torch
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
 
     def hooks(self):
         h = {}
@@ -50,6 +68,8 @@ class BucketAllReducer:
     def launch(self, i):
         import torch.distributed as dist
         s, e, _ = self.buckets[i]
+        if self._cur is not None:
+            self._cur["launch"][i] = self._event()
         self.works.append(dist.all_reduce(self.flat[s:e], op=dist.ReduceOp.SUM, group=self.group, async_op=True))
 
     def launch_all(self):
@@ -57,6 +77,44 @@ class BucketAllReducer:
             self.launch(i)
 
     def wait(self):
+        cur = self._cur if self.works else None
+        if cur is not None:
+            cur["bwd_end"] = self._event()  # every backward kernel is enqueued before this point
         for w in self.works:
             w.wait()
+            if cur is not None:
+                cur["done"].append(self._event())  # = max(end of the backward, this bucket's completion)
         self.works = []
+        if cur is not None:
+            self.records.append(cur)
+            self._cur = None
+
+    def timing_summary(self, world):
+        """Overlap of the bucket all-reduces with the backward over the recorded steps (call after a
+        device synchronize): exposed_ms = end of the backward -> last bucket done (the communication
+        the backward did not hide), per-bucket launch offsets from the backward's start, and the
+        algorithmic bus bandwidth 2(n-1)/n x bytes over the window first launch -> last done (a
+        lower bound: the window includes waiting for gradients)."""
+        if not self.records:
+            return None
+        nbytes = sum((e - s) * self.flat.element_size() for s, e, _ in self.buckets)
+        exp, win, bwd, offs = [], [], [], []
+        for r in self.records:
+            if not r["done"] or not r["launch"]:
+                continue
+            st = r["start"]
+            bwd_ms = st.elapsed_time(r["bwd_end"])
+            last = st.elapsed_time(r["done"][-1])
+            first = min(st.elapsed_time(ev) for ev in r["launch"].values())
+            exp.append(max(0.0, last - bwd_ms))
+            win.append(max(1e-6, last - first))
+            bwd.append(bwd_ms)
+            offs.append([round(st.elapsed_time(r["launch"][i]), 3) for i in sorted(r["launch"])])
+        if not exp:
+            return None
+        mean = lambda v: sum(v) / len(v)  # noqa: E731
+        return {"steps_timed": len(exp), "exposed_ms": round(mean(exp), 3), "exposed_ms_max": round(max(exp), 3),
+                "backward_ms": round(mean(bwd), 3), "comm_window_ms": round(mean(win), 3),
+                "bucket_launch_offsets_ms": offs[-1],
+                "bus_gbs": round(2.0 * (world - 1) / world * nbytes / (mean(win) * 1e-3) / 1e9, 2),
+                "bytes_per_step": int(nbytes)}

@@ -24,7 +24,8 @@ _f32 = C.c_float
 
 class ConvDesc(C.Structure):
     _fields_ = [(n, _i32) for n in ("dtype", "n", "h", "w", "c", "c_real", "k", "k_pad", "r", "s", "stride_h",
-                                   "stride_w", "pad_h", "pad_w", "groups", "p", "q")]
+                                   "stride_w", "pad_h", "pad_w", "groups", "p", "q",
+                                   "grouped_direct")]
 
 
 class BNDesc(C.Structure):

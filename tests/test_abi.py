@@ -80,3 +80,29 @@ def test_diagnostic_modes_are_not_in_the_product_library():
         assert b"diagnostic" in lib.rn_last_error()
         assert lib.rn_set_tuning(key, 0) == 0
     assert lib.rn_set_tuning(12, 0) == 0  # ordinary variant keys stay available
+
+
+def test_grouped_layout_is_fixed_at_descriptor_init():
+    """the grouped direct / block-diagonal choice (rn_set_tuning 15) is recorded in the
+    descriptor by rn_conv_desc_init, so a later change of the key cannot make a launch read a copy
+    packed in the other layout: the pack size of an initialised descriptor never changes."""
+    lib = L.load()
+
+    def desc():
+        d = L.ConvDesc(dtype=L.RN_BF16, n=2, h=14, w=14, c=128, c_real=128, k=128, k_pad=128, r=3, s=3,
+                       stride_h=1, stride_w=1, pad_h=1, pad_w=1, groups=32)
+        assert lib.rn_conv_desc_init(C.byref(d)) == 0
+        return d
+    d = desc()
+    assert d.grouped_direct == 1
+    compact = lib.rn_conv_pack_numel(C.byref(d), 0)
+    assert compact == 128 * 9 * 4
+    try:
+        assert lib.rn_set_tuning(15, 1) == 0
+        assert lib.rn_conv_pack_numel(C.byref(d), 0) == compact  # the same descriptor keeps its layout
+        d2 = desc()
+        assert d2.grouped_direct == 0 and lib.rn_conv_pack_numel(C.byref(d2), 0) > compact
+    finally:
+        lib.rn_set_tuning(15, 0)
+    d.groups = 1  # a dense conv is never direct
+    assert lib.rn_conv_desc_init(C.byref(d)) == 0 and d.grouped_direct == 0

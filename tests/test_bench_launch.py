@@ -69,7 +69,73 @@ def test_bench_gpus2_runs_two_ranks(gpu):
     assert out["config"]["global_batch"] == 512
     assert out["allreduce"]["backend"] == "gloo" and out["allreduce"]["world"] == 2
     assert out["allreduce"]["buckets"] >= 4  # 102 MB of gradients in 25 MB buckets
+    # overlap evidence: per-bucket launch offsets inside the backward, the exposed
+    # communication after it, bus bandwidth
+    ar = out["allreduce"]
+    for key in ("exposed_ms", "exposed_ms_max_over_ranks", "backward_ms", "comm_window_ms",
+                "bucket_launch_offsets_ms", "bus_gbs", "bytes_per_step", "steps_timed"):
+        assert key in ar, key
+    assert ar["steps_timed"] == 3 and len(ar["bucket_launch_offsets_ms"]) == ar["buckets"]
+    offs = ar["bucket_launch_offsets_ms"]
+    assert offs == sorted(offs) and offs[0] < ar["backward_ms"]  # the first bucket leaves during the backward
+    assert ar["exposed_ms"] >= 0 and ar["bus_gbs"] > 0
     assert out["allreduce"]["launch"].startswith("one process per GPU (bench.py --gpus")
     assert abs(out["config"]["per_gpu_images_per_sec"] * 2 - out["value"]) < 0.05 * out["value"]
     assert out["outputs_finite"]
     assert "cpu_baseline" not in out
+
+
+@pytest.mark.parametrize("sig", ["SIGTERM", "SIGINT"])
+def test_launcher_signal_stops_every_rank(tmp_path, sig):
+    """the ranks run in their own sessions, so a SIGTERM / SIGINT to the launcher (a
+    driver timeout, Ctrl-C) must take them down explicitly instead of orphaning them on their GPUs.
+    Two stand-in ranks (sleepers that record their pids) under bench.launch_ranks; the launcher
+    is signalled and must exit non-zero with both ranks gone."""
+    import signal
+    import time
+    pidfile = tmp_path / "pids"
+    rank_cmd = [sys.executable, "-c",
+                "import os, time; open(%r, 'a').write('%%d\\n' %% os.getpid()); time.sleep(300)" % str(pidfile)]
+    code = ("import sys; sys.path.insert(0, %r); import bench; sys.exit(bench.launch_ranks(2, [], cmd=%r))"
+            % (REPO, rank_cmd))
+    parent = subprocess.Popen([sys.executable, "-c", code], env=_env(RN_DIST_BACKEND="gloo"),
+                              stderr=subprocess.PIPE, text=True)
+    deadline = time.time() + 120
+    while time.time() < deadline:
+        if pidfile.exists() and len(pidfile.read_text().split()) == 2:
+            break
+        time.sleep(0.2)
+    pids = [int(x) for x in pidfile.read_text().split()]
+    assert len(pids) == 2
+    parent.send_signal(getattr(signal, sig))
+    _, err = parent.communicate(timeout=60)
+    assert parent.returncode == 128 + getattr(signal, sig), err
+    assert "stopping every rank" in err
+    for pid in pids:
+        gone = False
+        for _ in range(50):
+            try:
+                os.kill(pid, 0)
+            except ProcessLookupError:
+                gone = True
+                break
+            time.sleep(0.1)
+        assert gone, pid
+
+
+def test_pmc_traffic_reads_the_committed_summary(tmp_path):
+    """roofline.traffic went null when the PMC summary started nesting families
+    under "hbm". The committed summary must resolve the dominant family; the flat round-2 form and a
+    missing family are handled."""
+    sys.path.insert(0, REPO)
+    import bench
+    b, src = bench.pmc_traffic("igemm_big_kernel<224x256>")
+    assert src is not None and src.startswith("profiles/")
+    assert 2.0e8 < b < 4.0e8, b  # ~275 MB per launch (r03)
+    flat = tmp_path / "flat.json"
+    flat.write_text(json.dumps({"fam": {"launches": 3, "hbm_bytes": 123.0}}))
+    assert bench.pmc_traffic("fam", str(flat))[0] == 123.0
+    assert bench.pmc_traffic("other", str(flat)) == (None, None)
+    nested = tmp_path / "nested.json"
+    nested.write_text(json.dumps({"hbm": {"fam": {"hbm_bytes": 7.0}}, "sq": {}, "last_step_hbm_bytes": 1.0}))
+    assert bench.pmc_traffic("fam", str(nested))[0] == 7.0

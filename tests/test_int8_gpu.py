@@ -328,6 +328,9 @@ def test_weight_quant_pack_batched(gpu, dtype):
         refs.append(bufs)
     arr = (L.WQuantItem * len(items))(*items)
     dev = torch.frombuffer(bytearray(arr), dtype=torch.uint8).to(gpu)
+    # the shared workspace as the executor hands it over after a forward: the activation quantizers
+    # leave their thresholds in ws[1..2] (they were taken as weight maxima)
+    ws[1:3] = 1e3
     L.call("rn_weight_quant_pack", p(dev), len(items), dtype, p(ws), stream())
     torch.cuda.synchronize()
     assert not ws[:len(items)].any()
@@ -399,3 +402,58 @@ def test_int8_conv_block_extremes_feed_quantizer_max(gpu, case):
     for a, b in zip(*res):
         assert torch.equal(a, b)
     assert res[1][3].item() > 0  # (first batch: the state is the max itself)
+
+
+def test_weight_quant_pack_batched_multistep(gpu, monkeypatch):
+    """The int8 graph (symbol/resnet_int8.py, one unit per stage) for three bf16 QAT steps with the
+    batched weight quantizer (RN_WQUANT_BATCH=1, the default) and with one call per weight (=0):
+    after steps 2 and 3 -- repacks that follow a forward whose activation quantizers left their
+    thresholds in the shared workspace -- every fake-quantized weight, weight unit, int8 weight code,
+    data-gradient copy and minmax state is bit-identical, and so are the outputs (the
+    batched form took the stale thresholds as weight maxima from step 2 on)."""
+    import mxnet as mx
+    from oracle import net as onet
+    from rn import graphs
+    from step_util import oracle_state
+    cfg = ([1, 1, 1, 1], 4, [64, 256, 512, 1024, 2048], 16)
+    g = onet.resnet_int8(*cfg)
+    args, aux = oracle_state(g)
+    data, label = onet.synthetic_batch(4, (3, 64, 64), 16)
+    runs = []
+    for batched in ("1", "0"):
+        monkeypatch.setenv("RN_WQUANT_BATCH", batched)
+        mod = mx.mod.Module(graphs.resnet_int8(*cfg), context=[mx.gpu(0)], precision="bfloat16")
+        mod.bind(data_shapes=[("data", data.shape)], label_shapes=[("softmax_label", label.shape)])
+        mod.init_params(arg_params={k: v.astype(np.float32) for k, v in args.items()},
+                        aux_params={k: v.astype(np.float32) for k, v in aux.items()}, allow_missing=True)
+        mod.init_optimizer(kvstore="device", optimizer="sgd",
+                           optimizer_params={"learning_rate": 0.05, "wd": 1e-4, "momentum": 0.9})
+        batch = mx.io.DataBatch(data=[mx.nd.array(data)], label=[mx.nd.array(label)])
+        probs = []
+        for _ in range(3):
+            mod.forward(batch, is_train=True)
+            probs.append(mod.get_outputs()[0].asnumpy().copy())
+            mod.backward()
+            mod.update()
+        ex = mod.executor
+        assert ex._wq_batch == (batched == "1")
+        state = {}
+        for op in ex.plan.ops:
+            if getattr(op, "qweight", None) is None:
+                continue
+            for attr in ("qw", "wunit", "wk8", "wc"):
+                t = getattr(op, attr, None)
+                if t is not None:
+                    state[(op.weight, attr)] = t.detach().cpu().clone()
+        torch.cuda.synchronize()
+        st = {k: v.asnumpy() for k, v in mod.get_params()[1].items() if k.endswith("_minmax")}
+        runs.append((probs, state, st))
+    (p1, s1, m1), (p0, s0, m0) = runs
+    assert len(s1) >= 4 * 5 and set(s1) == set(s0)
+    for k in s1:
+        assert torch.equal(s1[k], s0[k]), k
+    assert set(m1) == set(m0) and any(k.endswith("_weight_minmax") for k in m1)
+    for k in m1:
+        np.testing.assert_array_equal(m1[k], m0[k], err_msg=k)
+    for a, b in zip(p1, p0):
+        np.testing.assert_array_equal(a, b)

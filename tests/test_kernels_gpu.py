@@ -511,6 +511,8 @@ def test_grouped_conv_direct(gpu, case):
     for mode in (0, 1):
         L.call("rn_set_tuning", 15, mode)
         try:
+            L.call("rn_conv_desc_init", C.byref(d))  # (the layout is recorded in the descriptor at init)
+            assert d.grouped_direct == (1 if mode == 0 and (c // g == 4 or (c // g == 8 and st == 2)) else 0)
             if mode == 0:
                 if c // g == 4 or (c // g == 8 and st == 2):  # the direct forward: compact [c/8][9][8][G] copy
                     assert lib.rn_conv_pack_numel(C.byref(d), 0) == c * 9 * (c // g)
