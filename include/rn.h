@@ -550,7 +550,12 @@ const char* rn_last_error(void);
  *      quantizer pass (rn_quant_int8_fwd_codes_bn / _bn2: x loads, the fake-quantized copy's stores;
  *      measured slower: C5 24.1 -> 25.1 ms per step), 16 = the 224/256-row conv tiles' output stores
  *      (rn_conv_fwd* / rn_conv_bwd_data*). Default 23. The same bits either way: only the cache
- *      policy changes. */
+ *      policy changes,
+ * 19 = the whole-dW weight gradients of ResNet-50 stage 1 (rn_conv_bwd_filter_ws / _x; one
+ *      workgroup holds the whole dW, dy and x read once, needs the slab workspace): the image-band
+ *      kernel of the 3x3 stride-1 64 -> 64-channel convolutions and the streaming kernel of the 1x1
+ *      stride-1 ones with K x C = 256 x 64, 64 x 256 or 64 x 64: 0 = on (default), 1 = the tiled
+ *      kernels. */
 int rn_set_tuning(int32_t key, int32_t value);
 int32_t rn_version(void);
 /* Number of compute units of the current device (for split heuristics / reporting). */

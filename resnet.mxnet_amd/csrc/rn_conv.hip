@@ -1846,6 +1846,277 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
     }
 }
 
+// ------------------------------------------------------------------------------ wgrad, image bands
+// The weight gradient of a 3x3 / stride-1 / pad-1 convolution with 64 input and 64 output channels
+// (ResNet-50 stage 1 conv2, symbol/resnet.py:19-21, 56x56): dW[k][tap][c] = sum_m dy[m][k] *
+// x[m + tap shift][c]. The whole dW (64 x 576 fp32) stays in the accumulators of ONE workgroup, which
+// walks its images in bands of two output rows: per band, the two dy rows and the four x rows they
+// read are staged once (LDS-DMA) and every tap multiplies the same LDS image at a shifted row. dy and
+// x are read from HBM exactly once (the tiled kernels re-read dy per column tile and gather x per tap:
+// 340 us per launch, 6x this shape's memory time). Both images use a row stride of 64 pixels with
+// the x pixel (ih, iw) at column iw + 1: columns 0 and W + 1.. of x and W.. of dy are zero, so the
+// tap shift r * 64 + s of a dy pixel never needs an in-image test (dy is zero where a shifted read
+// wraps). 8 waves: wave (kp, cb) owns output channels 32 kp..+32 and input channels 16 cb..+16 over all
+// 9 taps (18 16x16 accumulators). Each workgroup stores its partial dW into the slab; the split
+// reduction pass sums them (deterministic order).
+struct Wg3Args {
+  const bf16_t* x;   // [N][H][W][64]
+  const bf16_t* dy;  // [N][H][W][64]
+  float* slab;       // [G][64][576]
+  int N, H, W, ipw;  // images per workgroup
+};
+constexpr int kWg3XPix = 4 * 64 + 8;              // x image: 4 rows of 64 pixels + a zero slack
+constexpr int kWg3Buf = (kWg3XPix + 2 * 64) * 8;  // 16-byte chunks per band buffer (x, then dy)
+template <int NBUF>
+__global__ __launch_bounds__(512, 1) void wgrad_band3_kernel(Wg3Args p) {
+  __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * kWg3Buf];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int n_first = blockIdx.x * p.ipw;
+  const int n_end = min(p.N, n_first + p.ipw);
+  const int bpi = (p.H + 1) / 2;               // bands per image
+  const int nb = (n_end - n_first) * bpi;
+  // the x images' slack pixels (read only against zero dy) are zeroed once; DMAs never write them
+  for (int i = tid; i < NBUF * 64; i += 512) smem[(i >> 6) * kWg3Buf + 4 * 64 * 8 + (i & 63)] = make_uint4(0, 0, 0, 0);
+  // per-lane DMA geometry: wave w issues x pieces 4w..4w+3 (pixels 32w..32w+31 of the 4 x rows) and dy
+  // pieces 2w, 2w+1; lane = (pixel lane / 8 of the piece, LDS chunk slot lane % 8), the source chunk is
+  // the slot XOR the image's read swizzle
+  int x_rr[4], x_iw[4], x_ch[4], d_rr[2], d_q[2], d_ch[2];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int px = (4 * wid + j) * 8 + (lane >> 3);
+    x_rr[j] = px >> 6;
+    x_iw[j] = (px & 63) - 1;
+    x_ch[j] = 8 * ((lane & 7) ^ (swz_tr(px) & 7));
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int px = (2 * wid + j) * 8 + (lane >> 3);
+    d_rr[j] = px >> 6;
+    d_q[j] = px & 63;
+    d_ch[j] = 8 * ((lane & 7) ^ (swz_tr(px) & 7));
+  }
+  const char* zb = reinterpret_cast<const char*>(&g_zero_chunk);
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  auto issue = [&](int t, int buf) __attribute__((always_inline)) {
+    const int n = n_first + t / bpi, p0 = 2 * (t % bpi);
+    const uint32_t base = lds0 + buf * (kWg3Buf * 16);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ih = p0 - 1 + x_rr[j];
+      const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)x_iw[j] < (unsigned)p.W;
+      const bf16_t* src = p.x + ((int64_t)(n * p.H + ih) * p.W + x_iw[j]) * 64 + x_ch[j];
+      dma16_global(ok ? (const void*)src : (const void*)zb, base + (4 * wid + j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int oh = p0 + d_rr[j];
+      const bool ok = oh < p.H && d_q[j] < p.W;
+      const bf16_t* src = p.dy + ((int64_t)(n * p.H + oh) * p.W + d_q[j]) * 64 + d_ch[j];
+      dma16_global(ok ? (const void*)src : (const void*)zb, base + kWg3XPix * 128 + (2 * wid + j) * 1024);
+    }
+  };
+
+  const int kp = wid >> 2, cb = wid & 3;
+  v4f acc[2][9];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[i][t] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  // transposed 8-byte read of the 4 x 4 block at (pixel row, element column col) of a 128-byte-row image
+  auto rd = [&](const char* img, int row, int col) __attribute__((always_inline)) {
+    const int byte = row * 128 + ((((col * 2) >> 4) ^ (swz_tr(row) & 7)) << 4) + ((col * 2) & 15);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(img + byte));
+  };
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const char* Xb = reinterpret_cast<const char*>(smem + buf * kWg3Buf);
+    const char* Db = Xb + kWg3XPix * 128;
+#pragma unroll
+    for (int ms = 0; ms < 4; ++ms) {  // 32 dy pixels per step
+      v8s af[2], bfv[9];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = ms * 32 + 8 * g + 4 * h + q;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const v4s v = rd(Db, row, kp * 32 + i * 16 + 4 * pp);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) af[i][4 * h + e] = v[e];
+        }
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const v4s v = rd(Xb, row + (t / 3) * 64 + (t % 3), cb * 16 + 4 * pp);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bfv[t][4 * h + e] = v[e];
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[t], acc[i][t], 0, 0, 0);
+    }
+  };
+  __syncthreads();  // (the slack zeros)
+#pragma unroll
+  for (int s = 0; s < NBUF - 1; ++s)
+    if (s < nb) issue(s, s);
+  for (int t = 0; t < nb; ++t) {
+    // band t has landed once at most the DMAs of the bands issued after it are outstanding
+    if (NBUF == 3 && t + 1 < nb) wait_vmcnt<6>();
+    else wait_vmcnt<0>();
+    __syncthreads();  // ... for every wave; and every wave is done with the buffer refilled next
+    if (t + NBUF - 1 < nb) issue(t + NBUF - 1, (t + NBUF - 1) % NBUF);
+    compute(t % NBUF);
+  }
+  // the workgroup's partial dW: slab[block][k][tap * 64 + c]
+  float* dst = p.slab + (int64_t)blockIdx.x * 64 * 576;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = kp * 32 + i * 16 + (lane >> 4) * 4 + e;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) dst[(int64_t)k * 576 + t * 64 + cb * 16 + (lane & 15)] = acc[i][t][e];
+    }
+}
+
+// The weight gradient of a 1x1 / stride-1 convolution whose whole dW fits one workgroup's accumulators
+// (K x C <= 256 x 64 or 64 x 256: ResNet-50 stage 1's conv1 / conv3 / shortcut, symbol/resnet.py:17-31):
+// dW = dy^T x over M = N*P*Q. Each workgroup streams ONE contiguous M range through NBUF LDS-DMA
+// buffers of 64 rows (dy row: K channels, x row: C channels), so both operands are read from HBM once
+// (the tiled kernels re-read one operand per output tile and ran at 3 TB/s, 2-3x this shape's memory
+// time); the split partials go to the slab (wgrad_slab_reduce_kernel). XF: the producing
+// BatchNorm+ReLU applied to the x fragments after their transposed read, as wgrad_big_kernel XF.
+// 8 waves, wave (wk, wc) owns MI x NI 16x16 blocks of dW.
+template <int K, int C, int XF, int NBUF>
+__global__ __launch_bounds__(512, 1) void wgrad_stream_kernel(WgradArgs p) {
+  constexpr int BKM = 64;
+  constexpr int A_CPR = K / 8, B_CPR = C / 8;              // 16-byte chunks per LDS row
+  constexpr int A_RPI = 64 / A_CPR, B_RPI = 64 / B_CPR;    // rows per 1 KiB DMA instruction
+  constexpr int A_INS = BKM / A_RPI, B_INS = BKM / B_RPI;  // instructions per M-tile
+  static_assert((A_INS + B_INS) % 8 == 0, "DMA pieces per wave");
+  constexpr int LPT = (A_INS + B_INS) / 8;
+  constexpr int KB = K / 16, CB = C / 16;
+  constexpr int WK = KB >= 8 ? 8 : (CB >= 8 ? 1 : 4), WC = 8 / WK;
+  constexpr int MI = KB / WK, NI = CB / WC;
+  static_assert(MI * WK == KB && NI * WC == CB && MI * NI <= 16, "wave tile");
+  constexpr int A_SZ = BKM * A_CPR, B_SZ = BKM * B_CPR, kStage = A_SZ + B_SZ;
+  __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * kStage];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wk = wid / WC, wc = wid % WC;
+  const int zs = blockIdx.x;
+  const int mbeg = zs * p.m_per_split;
+  const int mend = min(p.M, mbeg + p.m_per_split);
+  if (mbeg >= mend) return;
+  // this wave's DMA pieces: piece j of the M-tile (A pieces first, then B)
+  int d_row[LPT], d_col[LPT];
+  bool d_isa[LPT];
+#pragma unroll
+  for (int j = 0; j < LPT; ++j) {
+    const int piece = wid * LPT + j;
+    d_isa[j] = piece < A_INS;
+    const int cpr = d_isa[j] ? A_CPR : B_CPR;
+    const int row = d_isa[j] ? piece * A_RPI + lane / A_CPR : (piece - A_INS) * B_RPI + lane / B_CPR;
+    d_row[j] = row;
+    d_col[j] = 8 * ((lane % cpr) ^ (swz_tr(row) & (cpr - 1)));
+  }
+  const char* __restrict__ dyb = reinterpret_cast<const char*>(p.dy);
+  const char* __restrict__ xb = reinterpret_cast<const char*>(p.x);
+  const char* zb = reinterpret_cast<const char*>(&g_zero_chunk);
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  auto issue = [&](int mb, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < LPT; ++j) {
+      const int piece = wid * LPT + j;
+      const int m = mb + d_row[j];
+      const bool ok = m < mend;
+      const uint32_t off = d_isa[j] ? (uint32_t)(m * p.ldy + d_col[j]) * 2u : (uint32_t)(m * p.C + d_col[j]) * 2u;
+      const char* src = d_isa[j] ? dyb + off : xb + off;
+      const uint32_t la = lds0 + buf * (kStage * 16) +
+                          (d_isa[j] ? piece * 1024 : A_SZ * 16 + (piece - A_INS) * 1024);
+      dma16_global(ok ? (const void*)src : (const void*)zb, la);
+    }
+  };
+
+  v4f acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+  float xsc[XF ? NI : 1], xsh[XF ? NI : 1];
+  if constexpr (XF) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int col = (wc * NI + j) * 16 + (lane & 15);
+      xsc[j] = p.in_sc[col];
+      xsh[j] = p.in_sh[col];
+    }
+  }
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const char* Ab = reinterpret_cast<const char*>(smem + buf * kStage);
+    const char* Bb = Ab + A_SZ * 16;
+#pragma unroll
+    for (int slab = 0; slab < 2; ++slab) {
+      v8s af[MI], bfv[NI];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = slab * 32 + 8 * g + 4 * h + q;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int col = (wk * MI + i) * 16 + 4 * pp;
+          const int byte = row * (A_CPR * 16) + ((((col * 2) >> 4) ^ (swz_tr(row) & (A_CPR - 1))) << 4) + ((col * 2) & 15);
+          const v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(Ab + byte));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) af[i][4 * h + e] = v[e];
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int col = (wc * NI + j) * 16 + 4 * pp;
+          const int byte = row * (B_CPR * 16) + ((((col * 2) >> 4) ^ (swz_tr(row) & (B_CPR - 1))) << 4) + ((col * 2) & 15);
+          const v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(Bb + byte));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bfv[j][4 * h + e] = v[e];
+        }
+      }
+      if constexpr (XF) {  // (rows past the M range: their dy rows are zero)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            bfv[j][e] = (short)f2bf(fmaxf(fmaf(bf2f((bf16_t)bfv[j][e]), xsc[j], xsh[j]), 0.f));
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j], acc[i][j], 0, 0, 0);
+    }
+  };
+  const int nstage = (mend - mbeg + BKM - 1) / BKM;
+#pragma unroll
+  for (int s = 0; s < NBUF - 1; ++s) issue(mbeg + s * BKM, s);
+  for (int t = 0; t < nstage; ++t) {
+    if (NBUF == 3) wait_vmcnt<LPT>();  // the later M-tile's DMAs (real or past the range) may stay in flight
+    else wait_vmcnt<0>();
+    __syncthreads();
+    issue(mbeg + (t + NBUF - 1) * BKM, (t + NBUF - 1) % NBUF);
+    compute(t % NBUF);
+  }
+  wait_vmcnt<0>();
+  float* dst = p.slab + (int64_t)zs * K * C;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = (wk * MI + i) * 16 + (lane >> 4) * 4 + e;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) dst[(int64_t)k * C + (wc * NI + j) * 16 + (lane & 15)] = acc[i][j][e];
+    }
+}
+
 // dw[i] += sum_z slab[z][i] (the split-M partial tiles of wgrad_big_kernel), float4 per thread
 __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __restrict__ slab, int nsplit,
                                                                 int64_t n, float* __restrict__ dw) {
@@ -3163,6 +3434,51 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     }
     return true;
   };
+  // 3x3 / stride 1 / pad 1, 64 -> 64 channels (stage-1 conv2): image bands, the whole dW per workgroup
+  // (wgrad_band3_kernel; rn_set_tuning 19 = 1: the tiled kernels below). Needs the slab workspace.
+  if (d->dtype == RN_BF16 && !grouped && !in_scale && d->r == 3 && d->s == 3 && d->stride_h == 1 &&
+      d->stride_w == 1 && d->pad_h == 1 && d->pad_w == 1 && d->c == 64 && d->c_real == 64 && d->k == 64 &&
+      d->k_pad == 64 && d->w <= 62 && g_tune[RN_TUNE_WGRAD_BAND] != 1 &&
+      (int64_t)d->n * d->h * d->w * 64 < INT32_MAX) {
+    Wg3Args g{};
+    g.x = (const bf16_t*)x; g.dy = (const bf16_t*)dy; g.N = d->n; g.H = d->h; g.W = d->w;
+    g.ipw = (int)std::max<int64_t>(1, ceil_div(d->n, chip_cus()));
+    const int64_t split = ceil_div(d->n, g.ipw);
+    if (!launch) return finish(split, "wgrad_band3");
+    if (ws && ws_bytes >= split * a.K * (int64_t)a.ldw * 4) {
+      if (!use_slab(split)) return -1;
+      g.slab = a.slab;
+      hipLaunchKernelGGL(wgrad_band3_kernel<3>, dim3((unsigned)split), dim3(512), 0, st, g);
+      return finish(split, "wgrad_band3");
+    }
+  }
+  // 1x1 / stride 1 with the whole dW in one workgroup (K x C = 256 x 64, 64 x 256 or 64 x 64: stage 1):
+  // one streaming pass over M per workgroup (wgrad_stream_kernel; rn_set_tuning 19 = 1: off)
+  const bool one = d->r == 1 && d->s == 1 && d->stride_h == 1 && d->stride_w == 1 && d->pad_h == 0 && d->pad_w == 0;
+  const int kc = (d->k == 256 && d->c == 64) ? 1 : (d->k == 64 && d->c == 256) ? 2 : (d->k == 64 && d->c == 64) ? 3 : 0;
+  if (d->dtype == RN_BF16 && !grouped && one && kc && d->c_real == d->c && d->k_pad == d->k &&
+      g_tune[RN_TUNE_WGRAD_BAND] != 1 && (int64_t)a.M * (d->k + d->c) * 2 < INT32_MAX) {
+    const int64_t mtiles = ceil_div(a.M, 64);
+    const int64_t split = std::min<int64_t>(chip_cus(), std::max<int64_t>(1, mtiles / 4));
+    a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
+    const int64_t nsplit = ceil_div(a.M, a.m_per_split);
+    if (!launch) return finish(nsplit, "wgrad_stream");
+    if (ws && ws_bytes >= nsplit * a.K * (int64_t)a.ldw * 4) {
+      if (!use_slab(nsplit)) return -1;
+      const dim3 grid((unsigned)nsplit);
+      if (kc == 1) {
+        if (in_scale) hipLaunchKernelGGL((wgrad_stream_kernel<256, 64, 1, 3>), grid, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((wgrad_stream_kernel<256, 64, 0, 3>), grid, dim3(512), 0, st, a);
+      } else if (kc == 2) {
+        if (in_scale) hipLaunchKernelGGL((wgrad_stream_kernel<64, 256, 1, 3>), grid, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((wgrad_stream_kernel<64, 256, 0, 3>), grid, dim3(512), 0, st, a);
+      } else {
+        if (in_scale) hipLaunchKernelGGL((wgrad_stream_kernel<64, 64, 1, 3>), grid, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((wgrad_stream_kernel<64, 64, 0, 3>), grid, dim3(512), 0, st, a);
+      }
+      return finish(nsplit, "wgrad_stream");
+    }
+  }
   // 256-column, 8-wave LDS-DMA tiles (rn_set_tuning 5: 1 = on, default off) for dense bf16 layers
   // with >= 128 output channels and >= 256 columns; the M range is split so that the grid is one
   // round of one workgroup per CU, with >= 4 M-tiles per workgroup. Measured slower than the

@@ -16,6 +16,15 @@ SoftmaxOutput. Backward: every call of the backward plan, checked in a hook righ
 reductions they emit), weight gradients (split-M slabs, BN+ReLU on load), BatchNorm backward (dx,
 dgamma, dbeta), gradient fan-in adds, pooling backward (through the device's own arg-max taps), the FC
 bias gradient. References follow the ops' MXNet semantics (oracle/ops.py restated in torch).
+
+ResNeXt (C4): grouped convolutions (direct v_dot2 and block-diagonal MFMA kernels) against the bf16
+rounding of the fp32 master weights, per group; the post-activation unit tail (rn_bn_apply_add) and
+its backward (rn_relu_bwd_bnred). Int8 QAT (C5): every quantizer bit for bit -- the activation codes,
+fake-quantized values, units and EMA threshold states (symbol/quant_ops.py:17-31,
+clip_grad_quantization_int8.py:37-54), every weight quantizer's threshold, unit, codes and copies
+(rn_weight_quant_pack) -- the int8 convolutions as exact fp64 sums of the device's own codes times
+the two units, and the straight-through clips folded into the BatchNorm backwards, the stem's and
+the FullyConnected input's.
 """
 import types
 
@@ -59,58 +68,110 @@ def _chunks(n, per_image_bytes, budget=1 << 30):
     return range(0, n, step), step
 
 
-def ref_fwd(x, w, stride, pad):
-    """fp32 conv forward: x (n,c,h,w), w (k,c,r,s)."""
+def ref_fwd(x, w, stride, pad, groups=1):
+    """conv forward in x's dtype (fp32, or fp64 for the exact integer sums of int8 codes): x (n,c,h,w),
+    w (k,c/groups,r,s); a grouped conv multiplies each group's unfolded channels with its own filters."""
     n, c, h, wd = x.shape
-    k, _, r, s = w.shape
+    k, cg, r, s = w.shape
     p = (h + 2 * pad[0] - r) // stride[0] + 1
     q = (wd + 2 * pad[1] - s) // stride[1] + 1
-    out = torch.empty(n, k, p, q, device=x.device, dtype=torch.float32)
-    wm = w.reshape(k, -1)
-    rng, step = _chunks(n, c * r * s * p * q * 4)
+    out = torch.empty(n, k, p, q, device=x.device, dtype=x.dtype)
+    wm = w.to(x.dtype).reshape(groups, k // groups, cg * r * s)
+    rng, step = _chunks(n, c * r * s * p * q * x.element_size())
     for i in rng:
-        cols = F.unfold(x[i:i + step], (r, s), padding=pad, stride=stride)
-        out[i:i + step] = torch.matmul(wm, cols).view(-1, k, p, q)
+        cols = F.unfold(x[i:i + step], (r, s), padding=pad, stride=stride)  # (ch, c*r*s, pq), channel-major
+        cols = cols.view(cols.shape[0], groups, cg * r * s, p * q)
+        out[i:i + step] = torch.einsum("gkj,ngjl->ngkl", wm, cols).reshape(-1, k, p, q)
     return out
 
 
-def ref_dgrad(dy, w, hw, stride, pad):
-    """fp32 data gradient: dy (n,k,p,q), w (k,c,r,s) -> (n,c,h,w)."""
+def ref_dgrad(dy, w, hw, stride, pad, groups=1):
+    """fp32 data gradient: dy (n,k,p,q), w (k,c/groups,r,s) -> (n,c,h,w)."""
     n, k, p, q = dy.shape
-    _, c, r, s = w.shape
+    _, cg, r, s = w.shape
+    c = cg * groups
     out = torch.empty(n, c, hw[0], hw[1], device=dy.device, dtype=torch.float32)
-    wt = w.reshape(k, -1).t()
+    wt = w.reshape(groups, k // groups, cg * r * s).transpose(1, 2)  # (g, cg*r*s, k/g)
     rng, step = _chunks(n, c * r * s * p * q * 4)
     for i in rng:
-        cols = torch.matmul(wt, dy[i:i + step].reshape(-1, k, p * q))
+        d = dy[i:i + step].reshape(-1, groups, k // groups, p * q)
+        cols = torch.einsum("gjk,ngkl->ngjl", wt, d).reshape(d.shape[0], c * r * s, p * q)
         out[i:i + step] = F.fold(cols, hw, (r, s), padding=pad, stride=stride)
     return out
 
 
-def ref_wgrad(x, dy, rs, stride, pad, with_abs=False):
-    """Weight gradient (k,c,r,s) in fp64 (a sum over N*P*Q terms that cancels heavily: the BatchNorm
-    backward makes dy zero-mean per channel). with_abs: also sum |dy| |x| (fp32), the scale that
-    bounds any fp32 summation's error."""
+def ref_wgrad(x, dy, rs, stride, pad, with_abs=False, groups=1):
+    """Weight gradient (k,c/groups,r,s) in fp64 (a sum over N*P*Q terms that cancels heavily: the
+    BatchNorm backward makes dy zero-mean per channel). with_abs: also sum |dy| |x| (fp32), the scale
+    that bounds any fp32 summation's error."""
     n, c = x.shape[:2]
     k, p, q = dy.shape[1:]
-    acc = torch.zeros(k, c * rs[0] * rs[1], device=x.device, dtype=torch.float64)
-    accb = torch.zeros(k, c * rs[0] * rs[1], device=x.device, dtype=torch.float32) if with_abs else None
+    cg, kg, crs = c // groups, k // groups, c // groups * rs[0] * rs[1]
+    acc = torch.zeros(groups, kg, crs, device=x.device, dtype=torch.float64)
+    accb = torch.zeros(groups, kg, crs, device=x.device, dtype=torch.float32) if with_abs else None
     rng, step = _chunks(n, 4 * c * rs[0] * rs[1] * p * q * 4)
     for i in rng:
-        cols = F.unfold(x[i:i + step], rs, padding=pad, stride=stride)  # (ch, crs, pq)
+        cols = F.unfold(x[i:i + step], rs, padding=pad, stride=stride)  # (ch, c*r*s, pq)
         ch = cols.shape[0]
-        a = dy[i:i + step].reshape(ch, k, p * q).permute(1, 0, 2).reshape(k, ch * p * q)
-        b = cols.permute(1, 0, 2).reshape(-1, ch * p * q)
-        acc += torch.matmul(a.double(), b.double().t())
+        b = cols.view(ch, groups, crs, p * q).permute(1, 2, 0, 3).reshape(groups, crs, ch * p * q)
+        a = dy[i:i + step].reshape(ch, groups, kg, p * q).permute(1, 2, 0, 3).reshape(groups, kg, ch * p * q)
+        acc += torch.matmul(a.double(), b.double().transpose(1, 2))
         if with_abs:
-            accb += torch.matmul(a.abs(), b.abs().t())
-    out = acc.view(k, c, rs[0], rs[1])
-    return (out, accb.view(k, c, rs[0], rs[1])) if with_abs else out
+            accb += torch.matmul(a.abs(), b.abs().transpose(1, 2))
+    out = acc.view(k, cg, rs[0], rs[1])
+    return (out, accb.view(k, cg, rs[0], rs[1])) if with_abs else out
+
+
+def _round_away(v):
+    """mx.nd.round / roundf: half away from zero (torch.round is half to even)."""
+    return torch.sign(v) * torch.floor(v.abs() + 0.5)
+
+
+def f32(v):
+    """Round an fp64 result to fp32 once: for one +, -, * or / of fp32 operands this IS the correctly
+    rounded fp32 operation (53 >= 2 * 24 + 2 bits: no double-rounding error)."""
+    return v.float()
+
+
+def quant_ref(y, t, qmax=127.0, clip=True):
+    """Quantization_int8 of the fp32 tensor y with threshold t as the device computes it
+    (symbol/quant_ops.py:17-31 with mx.round half away from zero): unit = t / qmax,
+    code = roundf(clip(y, -t, t) / unit), value = code * unit, each an fp32 operation.
+    Returns (codes fp64, values fp32, unit fp32 scalar tensor)."""
+    tt = torch.tensor(float(t), dtype=torch.float32)
+    unit = f32(tt.double() / qmax)
+    v = torch.clamp(y.float(), -float(t), float(t)) if clip else y.float()
+    if float(unit) <= 0.0:
+        z = torch.zeros_like(v, dtype=torch.float64)
+        return z, z.float(), unit
+    u = unit.to(v.device)
+    qf = f32(v.double() / u.double())
+    code = _round_away(qf.double())
+    return code, f32(code * u.double()), unit
+
+
+def ema_refs(prev, cur, decay):
+    """The quantizer's EMA state update (quant_state_update: minmax * decay + curmax * (1 - decay)) in
+    fp32, both as two rounded products and a rounded sum and as the contracted fma the compiler may
+    form: the device's value must be one of them."""
+    d = torch.tensor(decay, dtype=torch.float32).double()
+    p, c = torch.tensor(prev, dtype=torch.float32).double(), torch.tensor(cur, dtype=torch.float32).double()
+    om = f32(1.0 - d).double()
+    b = f32(c * om).double()
+    return {float(f32(f32(p * d).double() + b)), float(f32(p * d + b)), float(f32(c * om + f32(p * d).double())),
+            float(f32(c * om + p * d))}
+
+
+EXACT = {"mismatch": 0.0}  # bit-identical: the fraction of differing elements
 
 
 class Checker:
-    def __init__(self, ex):
+    def __init__(self, ex, prev_aux=None, first_batch=True):
+        """prev_aux: {aux name: fp32 tensor} snapshot taken before the checked forward (the quantizers'
+        EMA states); first_batch: whether that forward was the executor's first training forward."""
         self.ex = ex
+        self.prev_aux = prev_aux or {}
+        self.first_batch = first_batch
         self.rec = []  # (kind, layer, metrics dict, bar dict)
         self.byptr = {}
         for b in list(ex._acts.values()) + list(ex._grads.values()):
@@ -118,6 +179,7 @@ class Checker:
         for op in ex.plan.ops:
             if op.kind == "stem":
                 self.byptr[op.x8.data_ptr()] = op.x8
+        self.aux_by_ptr = {ex._ap(nm).value: nm for nm in ex.aux_off}
         self.wc_op = {}
         self.wk_op = {}
         for op in ex.plan.ops:
@@ -169,6 +231,24 @@ class Checker:
         b = op.buf
         return b[0:cp], b[cp:2 * cp], b[2 * cp:3 * cp], b[3 * cp:4 * cp]
 
+    def aux_val(self, ptr):
+        """The fp32 value an aux pointer (a quantizer's threshold state) holds."""
+        v = ptr.value if hasattr(ptr, "value") else ptr
+        return float(self.ex.aview(self.aux_by_ptr[v])[0])
+
+    def master_oihw(self, name, groups=1):
+        """An fp32 master weight (KRSC in the flat buffer) as OIHW (k, c/groups, r, s)."""
+        shp = self.ex.param_shape[name]
+        m = self.param(name)
+        if len(shp) == 2:
+            return m.view(shp[0], shp[1], 1, 1)
+        k, cg, r, s_ = shp
+        return m.view(k, r, s_, cg).permute(0, 3, 1, 2)
+
+    def mismatch(self, dev, ref):
+        dev, ref = dev.double(), ref.double()
+        return {"mismatch": float((dev != ref).double().mean()) if dev.numel() else 0.0}
+
     def conv_input(self, op):
         """What the conv's kernel multiplies: its stored input, or relu(bn(x)) rounded to bf16 as the
         BN+ReLU-on-load transform produces it."""
@@ -188,15 +268,45 @@ class Checker:
         ex = self.ex
         bar = BF16_BAR if ex.dtype == 0 else F32_BAR
         for op in ex.plan.ops:
+            if getattr(op, "qweight", None) is not None:
+                self.check_weight_quant(op)
             if op.kind == "conv":
-                if op.groups != 1 or getattr(op, "int8", False):
-                    continue
                 d = op.desc
-                w = self.w_from_krsc(op.wk, d)
-                y = ref_fwd(self.conv_input(op), w, op.stride, op.pad)
+                if getattr(op, "int8", False):
+                    # exact fp64 sums of the device's own int8 codes, times the two units
+                    qs, x = op.qsrc, op.x
+                    xc = self.nchw(qs.codes, x.n, x.h, x.w, x.cp, x.c).double()
+                    wc = self.w_from_krsc(op.wk8, d).double()
+                    y = ref_fwd(xc, wc, op.stride, op.pad) * (float(qs.unit[0]) * float(op.wunit[0]))
+                    kind = "conv_fwd_i8"
+                elif op.groups != 1:
+                    # grouped: against the bf16 rounding of the fp32 master, group by group (the compact /
+                    # block-diagonal compute copies themselves are the kernel's business)
+                    w = _bf16(self.master_oihw(op.weight, op.groups))
+                    y = ref_fwd(self.conv_input(op), w, op.stride, op.pad, op.groups)
+                    kind = "conv_fwd_grouped"
+                else:
+                    w = self.w_from_krsc(op.wk, d)
+                    if not getattr(op, "qweight", None):  # the compute copies ARE the master rounded once
+                        wm = self.master_oihw(op.weight)
+                        ref = _bf16(wm) if ex.dtype == 0 else wm
+                        self.add_metric("weight_copy", op.name + ":krsc", self.mismatch(w, ref), EXACT)
+                        self.add_metric("weight_copy", op.name + ":crsk", self.mismatch(self.w_from_crsk(op.wc, d), ref),
+                                        EXACT)
+                    y = ref_fwd(self.conv_input(op), w, op.stride, op.pad)
+                    kind = "conv_fwd"
                 if op.res is not None:
-                    y = y + self.act_nchw(op.res)
-                self.add("conv_fwd", op.name, self.act_nchw(op.y), y, bar)
+                    y = y + self.act_nchw(op.res).to(y.dtype)
+                self.add(kind, op.name, self.act_nchw(op.y), y, bar)
+            elif op.kind == "quant":
+                self.check_quant(op)
+            elif op.kind == "add":
+                self.check_add(op, bar)
+            elif op.kind == "relu":
+                self.add_metric("relu_fwd", op.name, self.mismatch(self.act_nchw(op.y), torch.relu(self.act_nchw(op.x))),
+                                EXACT)
+            elif op.kind == "stem" and op.bn is not None and op.quant is not None:
+                self.check_stem_quant(op, bar)
             elif op.kind == "stem" and op.bn is not None and op.quant is None:
                 x = op.x
                 b = op.bnbuf
@@ -271,6 +381,124 @@ class Checker:
                 dl = ex.grad_buf(x).view(x.n, x.cp)[:, :x.c]
                 self.add("softmax_grad", op.name, dl.float(), g * op.grad_scale, bar)
 
+    def check_add(self, op, bar):
+        """Residual add (+ ReLU); with BatchNorms applied inside it (rn_bn_apply_add, the post-activation
+        unit tail): each BN output rounded to the storage type as rn_bn_apply stores it, then the add."""
+        ex = self.ex
+
+        def side(key):
+            bn = None
+            if getattr(op, "bn_a", None) is not None:
+                if op.bn_a_key == key:
+                    bn = op.bn_a
+                elif op.bn_b is not None:
+                    bn = op.bn_b
+            if bn is None:
+                return self.act_nchw(getattr(op, key))
+            _, _, sc, sh = self.bn_coefs(bn)
+            c = bn.x.c
+            v = _fma(self.act_nchw(bn.x), sc[:c].view(1, c, 1, 1), sh[:c].view(1, c, 1, 1))
+            return _bf16(v) if ex.dtype == 0 else v
+        y = side("a") + side("b")
+        if op.relu:
+            y = torch.relu(y)
+        self.add("bn_apply_add" if getattr(op, "bn_a", None) is not None else "add_fwd", op.name,
+                 self.act_nchw(op.y), _bf16(y) if ex.dtype == 0 else y, bar)
+
+    def _quant_state(self, q, cur, is_weight=False):
+        """|device state - the state the update must produce| / state: 0 when it is one of the fp32
+        evaluations (first batch / weights: the max itself; else the EMA, ema_refs)."""
+        dev = float(self.ex.aview(q["minmax"])[0])
+        if is_weight or self.first_batch:
+            want = {float(torch.tensor(cur, dtype=torch.float32))}
+        else:
+            want = ema_refs(float(self.prev_aux[q["minmax"]][0]), cur, q["ema"])
+        if dev in want:
+            return 0.0, dev
+        return min(abs(dev - w) for w in want) / max(abs(dev), 1e-30), dev
+
+    def check_quant(self, op):
+        """An activation Quantization_int8, bit for bit from the device's own input: max|y| -> threshold
+        state (EMA), unit, int8 codes, fake-quantized values. y = the stored input, or the BatchNorm(+ReLU)
+        output the quantizer applies on load (rn_quant_int8_fwd_codes_bn[2]), rounded as rn_bn_apply
+        stores it."""
+        x = op.x
+        if op.bn_src is not None:
+            bn = op.bn_src
+            _, _, sc, sh = self.bn_coefs(bn)
+            c = bn.x.c
+            v = _fma(self.act_nchw(bn.x), sc[:c].view(1, c, 1, 1), sh[:c].view(1, c, 1, 1))
+            if bn.relu:
+                v = torch.relu(v)
+            y = _bf16(v) if self.ex.dtype == 0 else v
+        else:
+            y = self.act_nchw(x)
+        cur = float(y.abs().max()) if y.numel() else 0.0
+        st, t = self._quant_state(op.q, cur)
+        code, val, unit = quant_ref(y, t, float((1 << (int(op.q["nbits"]) - 1)) - 1))
+        val = _bf16(val) if self.ex.dtype == 0 else val
+        m = {"state": st, "values": self.mismatch(self.act_nchw(op.y), val)["mismatch"]}
+        if getattr(op, "codes", None) is not None:
+            m["codes"] = self.mismatch(self.nchw(op.codes, x.n, x.h, x.w, x.cp, x.c), code)["mismatch"]
+            m["unit"] = 0.0 if float(op.unit[0]) == float(unit) else 1.0
+        self.add_metric("quant", op.q["name"], m, {k: 0.0 for k in m})
+
+    def check_weight_quant(self, op):
+        """A weight Quantization_int8 (rn_weight_quant_pack / the per-weight calls): threshold = max|w| of
+        the fp32 master, the fake-quantized fp32 copy, and for int8 convolutions the unit, the int8 KRSC
+        codes and the bf16 CRSK data-gradient copy; else the compute copy = the fake-quantized values
+        rounded once."""
+        ex = self.ex
+        q = op.qweight
+        wm = self.master_oihw(op.weight)
+        cur = float(wm.abs().max())
+        st, t = self._quant_state(q, cur, is_weight=True)
+        code, val, unit = quant_ref(wm, t, float((1 << (int(q["nbits"]) - 1)) - 1), clip=False)
+        shp = ex.param_shape[op.weight]
+        k, cr = shp[0], shp[1]
+        r_, s_ = (shp[2], shp[3]) if len(shp) == 4 else (1, 1)
+        qw = op.qw.view(k, r_, s_, cr).permute(0, 3, 1, 2)
+        m = {"state": st, "values": self.mismatch(qw, val)["mismatch"]}
+        low = _bf16(val) if ex.dtype == 0 else val
+        d = op.dfull if op.kind == "stem" else op.desc
+        if getattr(op, "int8", False):
+            m["unit"] = 0.0 if float(op.wunit[0]) == float(unit) else 1.0
+            m["codes"] = self.mismatch(self.w_from_krsc(op.wk8, d), code)["mismatch"]
+            m["crsk"] = self.mismatch(self.w_from_crsk(op.wc, d), low)["mismatch"]
+        elif op.kind == "fc":
+            m["krsc"] = self.mismatch(op.wk.view(d.k, d.c)[:, :d.c_real].float(), low.view(k, cr))["mismatch"]
+        elif op.kind == "stem" and op.p4 is None:
+            m["krsc"] = self.mismatch(self.w_from_krsc(op.wk, d), low)["mismatch"]
+        self.add_metric("weight_quant", q["name"], m, {kk: 0.0 for kk in m})
+
+    def check_stem_quant(self, op, bar):
+        """The quantized stem (symbol/resnet_int8.py:96-98): bn_data's statistics, the NHWC-8 copy
+        quantized in place (the stored bf16 affine input through Quantization_int8, bit for bit) and conv0
+        over it."""
+        ex = self.ex
+        x = op.x
+        b = op.bnbuf
+        sc, sh = b[16:16 + x.c], b[24:24 + x.c]
+        data = ex._in_bufs[ex._in_idx].view(x.n, x.c, x.h, x.w).float()
+        mean = data.double().mean(dim=(0, 2, 3))
+        var = data.double().var(dim=(0, 2, 3), unbiased=False)
+        inv = 1.0 / torch.sqrt(var + op.bn["eps"])
+        self.add_metric("bn_fwd", "bn_data", {"mean": float(((b[0:x.c].double() - mean).abs() /
+                                                               torch.sqrt(var)).max()),
+                                              "invstd": _maxr(b[8:8 + x.c], inv)},
+                        {"mean": 1e-5, "invstd": 1e-5})
+        aff = _fma(data, sc.view(1, -1, 1, 1), sh.view(1, -1, 1, 1))
+        y = _bf16(aff) if ex.dtype == 0 else aff
+        cur = float(y.abs().max())
+        st, t = self._quant_state(op.quant, cur)
+        _, val, _ = quant_ref(y, t, float((1 << (int(op.quant["nbits"]) - 1)) - 1))
+        val = _bf16(val) if ex.dtype == 0 else val
+        x8 = self.nchw(op.x8, x.n, x.h, x.w, 8, x.c)
+        self.add_metric("quant", op.quant["name"], {"state": st, "values": self.mismatch(x8, val)["mismatch"]},
+                        {"state": 0.0, "values": 0.0})
+        y0 = ref_fwd(x8, self.w_from_krsc(op.wk, op.dfull), op.stride, op.pad)
+        self.add("conv_fwd", op.name, self.act_nchw(op.y), y0, bar)
+
     # ------------------------------------------------------------------ backward (hooks)
     def backward_hooks(self):
         ex = self.ex
@@ -310,12 +538,15 @@ class Checker:
         def post():
             n, p, q = d.n, d.p, d.q
             dy = self.nchw(self.t(dyp), n, p, q, d.k_pad, d.k)
-            w = self.w_from_crsk(op.wc, d)
-            ref = ref_dgrad(dy, w, (d.h, d.w), (d.stride_h, d.stride_w), (d.pad_h, d.pad_w))
+            if d.groups > 1:  # the bf16 rounding of the master, per group (as the forward)
+                w = _bf16(self.master_oihw(op.weight, d.groups))
+            else:
+                w = self.w_from_crsk(op.wc, d)
+            ref = ref_dgrad(dy, w, (d.h, d.w), (d.stride_h, d.stride_w), (d.pad_h, d.pad_w), d.groups)
             if state.get("add") is not None:
                 ref = ref + self.nchw(state["add"], n, d.h, d.w, d.c, d.c_real)
             dev = self.nchw(self.t(outp), n, d.h, d.w, d.c, d.c_real)
-            self.add("dgrad_bnred" if bnred else "dgrad", op.name, dev,
+            self.add(("dgrad_bnred" if bnred else "dgrad") + ("_grouped" if d.groups > 1 else ""), op.name, dev,
                      ref, BF16_BAR if self.ex.dtype == 0 else F32_BAR)
         return (self._snap(addp, state, "add") if addp is not None else None), post
 
@@ -325,6 +556,10 @@ class Checker:
     def _h_rn_conv_bwd_data_bnred(self, args, state):
         if args[3] is None:  # reduction only (the first pass of the recompute): nothing stored; its partials
             return None, (lambda: None)  # are checked through dgamma / dbeta / dx of the apply below
+        return self._dgrad(args, state, bnred=True)
+
+    def _h_rn_conv_bwd_data_bnred_clip(self, args, state):
+        # (its reduction carries the folded quantizer clip: checked through the BN backward it feeds)
         return self._dgrad(args, state, bnred=True)
 
     def _h_rn_bn_bwd_finalize(self, args, state):
@@ -366,15 +601,16 @@ class Checker:
                     x = self.bn_relu_input(self.bn_by_sm_x[xp.value])
                 else:
                     x = self.nchw(self.t(xp), n, d.h, d.w, d.c, d.c_real)
-                ref, rab = ref_wgrad(x, dy, (d.r, d.s), (d.stride_h, d.stride_w), (d.pad_h, d.pad_w), with_abs=True)
-            dev = self.ex.gview(name).view(d.k, d.r, d.s, d.c_real).permute(0, 3, 1, 2)
+                ref, rab = ref_wgrad(x, dy, (d.r, d.s), (d.stride_h, d.stride_w), (d.pad_h, d.pad_w), with_abs=True,
+                                     groups=d.groups)
+            dev = self.ex.gview(name).view(d.k, d.r, d.s, d.c_real // d.groups).permute(0, 3, 1, 2)
             if self.ex.param_layout[name] != "krsc":  # FC: (k, c)
                 dev = self.ex.gview(name).view(d.k, d.c_real, 1, 1)
             # cond: |dev - ref| per element over sum |dy| |x| of its terms (an fp32 summation of n terms
             # errs by at most ~n * 2^-24 of that; blocked / split sums far less)
             m = {"fro": _fro(dev, ref), "max": _maxr(dev, ref),
                  "cond": float(((dev.double() - ref).abs() / (rab.double() + 1e-30)).max())}
-            self.add_metric("wgrad", name, m, WGRAD_BAR)
+            self.add_metric("wgrad_grouped" if d.groups > 1 else "wgrad", name, m, WGRAD_BAR)
         return None, post
 
     def _h_rn_conv_bwd_filter(self, args, state):
@@ -444,7 +680,19 @@ class Checker:
         x = self.act_nchw(t).double()
         mu, inv = sm[:c].double().view(1, c, 1, 1), si[:c].double().view(1, c, 1, 1)
         dz = dy
-        if op.relu:
+        desc = op.desc
+        if op.relu and desc.clip:
+            # the folded straight-through clips of the quantizer(s) that read this BN's output
+            # (rn_bn_desc.clip / clip2 / dy2): dz = [y > 0] * [y < t] * dy (two: rounded sum), y as stored
+            yv = torch.relu(_fma(x.float(), sc[:c].view(1, c, 1, 1), sh[:c].view(1, c, 1, 1)))
+            yv = _bf16(yv) if self.ex.dtype == 0 else yv
+            g = dy * (yv < self.aux_val(desc.clip))
+            if desc.dy2:
+                dy2 = self.nchw(self.byptr[desc.dy2], t.n, t.h, t.w, t.cp, c).double()
+                g = g + dy2 * (yv < self.aux_val(desc.clip2))
+                g = (_bf16(g.float()) if self.ex.dtype == 0 else g.float()).double()
+            dz = g * (yv > 0)
+        elif op.relu:
             dz = dy * ((x * sc[:c].double().view(1, c, 1, 1) + sh[:c].double().view(1, c, 1, 1)) > 0)
         xc = x - mu
         m = t.n * t.h * t.w
@@ -475,6 +723,54 @@ class Checker:
 
     def _h_rn_bn_bwd(self, args, state):
         return self._bn_bwd(args, state, False)
+
+    def _h_rn_relu_bwd_bnred(self, args, state):
+        """The post-activation unit tail's backward: g = dy * [y > 0] (exact); its BatchNorm reductions are
+        checked through the rn_bn_bwd_part calls that finish those BNs (dgamma, dbeta, dx)."""
+        d, yp, dyp, gp = args[0]._obj, args[1], args[2], args[3]
+        snap = self._snap(dyp, state, "dy")
+
+        def post():
+            m, cp = d.m, d.c
+            y = self.t(yp)[:m * cp].float()
+            ref = state["dy"][:m * cp].float() * (y > 0)
+            self.add_metric("relu_bwd_bnred", "add", self.mismatch(self.t(gp)[:m * cp].float(), ref), EXACT)
+        return snap, post
+
+    def _h_rn_relu_bwd(self, args, state):
+        n, yp, dyp, dxp, addp = args[0], args[2], args[3], args[4], args[5]
+        sd, sa = self._snap(dyp, state, "dy"), self._snap(addp, state, "add")
+
+        def pre():
+            sd()
+            sa()
+
+        def post():
+            ref = state["dy"][:n].float() * (self.t(yp)[:n].float() > 0)
+            if state["add"] is not None:
+                ref = ref + state["add"][:n].float()
+            self.add("relu_bwd", "relu", self.t(dxp)[:n].float(), ref, BF16_BAR if self.ex.dtype == 0 else F32_BAR)
+        return pre, post
+
+    def _h_rn_quant_int8_bwd(self, args, state):
+        """A Quantization_int8's straight-through backward that is not folded into a BatchNorm (the
+        FullyConnected input's): dx = dy * [-t < x < t] (+ add) (clip_grad_quantization_int8.py:55-67)."""
+        n, xp, dyp, dxp, mmp, is_w, addp = args[1], args[2], args[3], args[4], args[5], args[6], args[7]
+        sd, sa = self._snap(dyp, state, "dy"), self._snap(addp, state, "add")
+
+        def pre():
+            sd()
+            sa()
+
+        def post():
+            x = self.t(xp)[:n].float()
+            t = float("inf") if (is_w or mmp is None) else self.aux_val(mmp)
+            ref = state["dy"][:n].float() * ((x > -t) & (x < t))
+            if state["add"] is not None:
+                ref = ref + state["add"][:n].float()
+            ref = _bf16(ref) if self.ex.dtype == 0 else ref
+            self.add_metric("quant_bwd", "ste", self.mismatch(self.t(dxp)[:n].float(), ref), EXACT)
+        return pre, post
 
     def _h_rn_eltwise_add(self, args, state):
         n, _, ap, bp, dp = args[0], args[1], args[2], args[3], args[4]
@@ -526,22 +822,52 @@ class Checker:
             self.add("fc_bias_grad", "fc1_bias", dev, x.sum(0), F32_BAR)
         return None, post
 
+    def _stem_weight(self, wmp, d):
+        """conv0's fp32 KRSC weight behind a pointer: the master, or (int8 graph) its fake-quantized copy."""
+        n = d.k * d.r * d.s * d.c_real
+        for buf in [self.ex.master] + [op.qw for op in self.ex.plan.ops if getattr(op, "qw", None) is not None]:
+            off = (wmp.value - buf.data_ptr()) // 4
+            if 0 <= off and off + n <= buf.numel():
+                return buf[off:off + n].view(d.k, d.r, d.s, d.c_real).permute(0, 3, 1, 2).float()
+        raise KeyError(wmp.value)
+
+    def _stem_dbeta(self, d, dyp, wmp, dbp, clip=None):
+        name = self.grad_name(dbp)
+        dy = self.nchw(self.t(dyp), d.n, d.p, d.q, d.k_pad, d.k)
+        w = self._stem_weight(wmp, d)
+        args_ = ((d.h, d.w), (d.stride_h, d.stride_w), (d.pad_h, d.pad_w))
+        g = ref_dgrad(dy, w, *args_).double()
+        ga = ref_dgrad(dy.abs(), w.abs(), *args_).double()
+        if clip is not None:  # the input quantizer's straight-through clip: no gradient where it clipped
+            g, ga = g * clip, ga * clip
+        ref, rab = g.sum(dim=(0, 2, 3)), ga.sum(dim=(0, 2, 3))
+        dev = self.ex.gview(name)[:d.c_real].double()
+        self.add_metric("stem_dbeta", name, {"cond": float(((dev - ref).abs() / rab).max()),
+                                             "fro": _fro(dev, ref)}, {"cond": 2e-6, "fro": 1e-3})
+
     def _h_rn_stem_shift_grad(self, args, state):
         """bn_data's beta gradient without the stem's data gradient: dbeta[c] = sum over the image of
-        conv0's data gradient (fix_gamma BatchNorm), from the fp32 master weights."""
+        conv0's data gradient (fix_gamma BatchNorm), from the weights conv0 ran with. With an input
+        quantizer the clip gradient that follows completes it (checked there)."""
         d, dyp, wmp, dbp = args[0]._obj, args[1], args[2], args[3]
-        name = self.grad_name(dbp)
+        if any(nm == "rn_stem_quant_clip_grad" for nm, _, _ in self.ex._bwd):
+            return None, (lambda: None)
+        return None, (lambda: self._stem_dbeta(d, dyp, wmp, dbp))
+
+    def _h_rn_stem_quant_clip_grad(self, args, state):
+        """rn_stem_shift_grad + this: dbeta[c] = sum of conv0's data gradient over the unclipped inputs,
+        clipped = !(-t < fmaf(x, scale, shift) < t) on the fp32 input (the STE of
+        clip_grad_quantization_int8.py on bn_data's fp32 output)."""
+        d, xp, scp, shp, mmp, dyp, wmp, dbp = args[0]._obj, args[1], args[2], args[3], args[4], args[5], args[6], args[7]
+        op = [o for o in self.ex.plan.ops if o.kind == "stem"][0]
 
         def post():
-            dy = self.nchw(self.t(dyp), d.n, d.p, d.q, d.k_pad, d.k)
-            off = (wmp.value - self.ex.master.data_ptr()) // 4
-            w = self.ex.master[off:off + d.k * d.r * d.s * d.c_real].view(d.k, d.r, d.s, d.c_real).permute(0, 3, 1, 2)
-            args_ = ((d.h, d.w), (d.stride_h, d.stride_w), (d.pad_h, d.pad_w))
-            ref = ref_dgrad(dy, w.float(), *args_).double().sum(dim=(0, 2, 3))
-            rab = ref_dgrad(dy.abs(), w.float().abs(), *args_).double().sum(dim=(0, 2, 3))
-            dev = self.ex.gview(name)[:d.c_real].double()
-            self.add_metric("stem_dbeta", name, {"cond": float(((dev - ref).abs() / rab).max()),
-                                                 "fro": _fro(dev, ref)}, {"cond": 2e-6, "fro": 1e-3})
+            x = op.x
+            data = self.ex._in_bufs[self.ex._in_idx].view(x.n, x.c, x.h, x.w).float()
+            sc, sh = op.bnbuf[16:16 + x.c], op.bnbuf[24:24 + x.c]
+            v = _fma(data, sc.view(1, -1, 1, 1), sh.view(1, -1, 1, 1))
+            t = self.aux_val(mmp)
+            self._stem_dbeta(d, dyp, wmp, dbp, clip=((v > -t) & (v < t)).double())
         return None, post
 
     # ------------------------------------------------------------------ results

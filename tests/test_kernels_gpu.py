@@ -1357,3 +1357,92 @@ def _zero_block_skip(gpu, n, c, h, w, k, r, st, pd, g):
     assert rel_err(outs[0][2], outs[1][2]) < 1e-5 and rel_err(outs[2][2], outs[1][2]) < 1e-5
     _, dw_ref = ops.conv2d_bwd(x, wt, dy, (st, st), (pd, pd), g)
     assert rel_err(outs[0][2].reshape(k, r, r, c // g).transpose(0, 3, 1, 2), dw_ref) < 5e-3
+
+
+@pytest.mark.parametrize("case", [
+    (3, 64, 56, 56, 64, 3, 1, 1),   # the stage-1 conv2 shape (one image per workgroup)
+    (5, 64, 9, 13, 64, 3, 1, 1),    # odd rows: the last band has one output row
+    (2, 64, 7, 62, 64, 3, 1, 1),    # the widest row the 64-pixel band image holds
+])
+def test_wgrad_image_bands(gpu, case):
+    """wgrad_band3_kernel (the 3x3 stride-1 64 -> 64 weight gradient, rn_set_tuning 19 = 0): the whole
+    dW per workgroup over bands of two output rows, every tap a shifted read of one staged x image.
+    Against the fp64 oracle (the sums of products of bf16 values, fp32 accumulation: 2e-6 of the sum of
+    the terms' magnitudes per element), bit-identical run to run (one writer per slab element, the
+    reduction in split order), and equal to the tiled kernels (rn_set_tuning 19 = 1) within fp32
+    summation-order rounding."""
+    n, c, h, w, k, r, st, pd = case
+    x, _ = _conv_data(case, 9)
+    x = bf16_round(x)
+    rng = np.random.default_rng(10)
+    dy = bf16_round(rng.standard_normal((n, k, h, w)))
+    _, dw_ref = ops.conv2d_bwd(x, np.zeros((k, c, r, r)), dy, (st, st), (pd, pd))
+    dw_abs = ops.conv2d_bwd(np.abs(x), np.zeros((k, c, r, r)), np.abs(dy), (st, st), (pd, pd))[1]
+    d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd)
+    lib = L.load()
+    need = lib.rn_conv_wgrad_ws_bytes(C.byref(d))
+    assert need >= 64 * 576 * 4
+    ws = torch.full((need // 4 + 4,), float("nan"), dtype=torch.float32, device=gpu)
+    xd, dyd = to_nhwc(x, BF16, gpu), to_nhwc(dy, BF16, gpu)
+    outs = []
+    for band in (0, 0, 1):
+        L.call("rn_set_tuning", 19, band)
+        try:
+            dw = torch.zeros(k * r * r * c, dtype=torch.float32, device=gpu)
+            L.call("rn_conv_bwd_filter_ws", C.byref(d), p(xd), p(dyd), p(dw), p(ws), need, stream())
+            torch.cuda.synchronize()
+        finally:
+            L.call("rn_set_tuning", 19, 0)
+        outs.append(dw.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2).astype(np.float64))
+    assert np.array_equal(outs[0], outs[1])
+    cond = np.abs(outs[0] - dw_ref) / (dw_abs + 1e-30)
+    assert cond.max() < 2e-6, cond.max()
+    assert np.abs(outs[0] - outs[2]).max() <= 1e-5 * np.abs(dw_abs).max()
+
+
+@pytest.mark.parametrize("kc", [(256, 64), (64, 256), (64, 64)])
+@pytest.mark.parametrize("xf", [False, True], ids=["plain", "bnrelu_on_load"])
+def test_wgrad_stream_1x1(gpu, kc, xf):
+    """wgrad_stream_kernel (1x1 stride-1 weight gradients whose whole dW fits one workgroup: stage 1's
+    conv1 / conv3 / shortcut; rn_set_tuning 19 = 0): one streaming pass per workgroup over its M range,
+    the split partials through the slab. Plain and with the producing BatchNorm+ReLU applied to x on load
+    (rn_conv_bwd_filter_x): against the fp64 oracle of the same (rounded) operands, bit-identical run to
+    run, and equal to the tiled kernels (19 = 1) within fp32 summation-order rounding; a ragged M (the
+    last rows of the last split past the range)."""
+    k, c = kc
+    n, h, w = 3, 13, 11
+    rng = np.random.default_rng(11)
+    x = bf16_round(rng.standard_normal((n, c, h, w)))
+    dy = bf16_round(rng.standard_normal((n, k, h, w)))
+    d = conv_desc(BF16, n, c, h, w, k, 1, 1, 1, 0)
+    sc = torch.tensor(rng.standard_normal(c) * 0.5, dtype=torch.float32, device=gpu)
+    sh = torch.tensor(rng.standard_normal(c) * 0.3, dtype=torch.float32, device=gpu)
+    xin = x
+    if xf:  # the kernel multiplies bf16(max(fmaf(x, sc, sh), 0)), as the BN apply pass stores it
+        xt = torch.from_numpy(x).to(gpu).float()
+        v = torch.relu((xt.double() * sc.double().view(1, c, 1, 1) + sh.double().view(1, c, 1, 1)).float())
+        xin = v.to(torch.bfloat16).float().cpu().numpy().astype(np.float64)
+    _, dw_ref = ops.conv2d_bwd(xin, np.zeros((k, c, 1, 1)), dy, (1, 1), (0, 0))
+    dw_abs = ops.conv2d_bwd(np.abs(xin), np.zeros((k, c, 1, 1)), np.abs(dy), (1, 1), (0, 0))[1]
+    lib = L.load()
+    need = lib.rn_conv_wgrad_ws_bytes(C.byref(d))
+    assert need >= k * c * 4
+    ws = torch.full((need // 4 + 4,), float("nan"), dtype=torch.float32, device=gpu)
+    xd, dyd = to_nhwc(x, BF16, gpu), to_nhwc(dy, BF16, gpu)
+    outs = []
+    for band in (0, 0, 1):
+        L.call("rn_set_tuning", 19, band)
+        try:
+            dw = torch.zeros(k * c, dtype=torch.float32, device=gpu)
+            if xf:
+                L.call("rn_conv_bwd_filter_x", C.byref(d), p(xd), p(dyd), p(dw), p(sc), p(sh), p(ws), need, stream())
+            else:
+                L.call("rn_conv_bwd_filter_ws", C.byref(d), p(xd), p(dyd), p(dw), p(ws), need, stream())
+            torch.cuda.synchronize()
+        finally:
+            L.call("rn_set_tuning", 19, 0)
+        outs.append(dw.cpu().numpy().reshape(k, c, 1, 1).astype(np.float64))
+    assert np.array_equal(outs[0], outs[1])
+    cond = np.abs(outs[0] - dw_ref) / (dw_abs + 1e-30)
+    assert cond.max() < 2e-6, cond.max()
+    assert np.abs(outs[0] - outs[2]).max() <= 1e-5 * np.abs(dw_abs).max()

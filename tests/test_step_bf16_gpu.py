@@ -129,9 +129,12 @@ def test_resnet50_bf16_full_size_gradients(gpu):
     assert abs(ce_loss(res["prob"][0], label) - ce_loss(prob, label)) < 0.01 * ce_loss(prob, label)
 
 
-def _layerwise(sym, n, image, precision, tune=None):
+def _layerwise(sym, n, image, precision, tune=None, warm=0):
     """One training step (forward + backward, serialised on one stream) with every kernel checked
-    against its fp32 torch restatement from the device's own inputs (tests/layerwise.py)."""
+    against its fp32 torch restatement from the device's own inputs (tests/layerwise.py). warm: full
+    steps (forward, backward, SGD update + the weight repacks after it) run before the checked one, so
+    the checked forward reads weights the post-update packs wrote and quantizer states that follow
+    the EMA."""
     import json
     import os
     import mxnet as mx
@@ -153,9 +156,16 @@ def _layerwise(sym, n, image, precision, tune=None):
         ex = mod.executor
         ex.side_enabled = False  # the checks read buffers between calls: one stream, in plan order
         batch = mx.io.DataBatch(data=[mx.nd.array(data)], label=[mx.nd.array(label)])
+        for _ in range(warm):
+            mod.forward(batch, is_train=True)
+            mod.backward()
+            mod.update()
+        torch.cuda.synchronize()
+        prev_aux = {nm: ex.aview(nm).clone() for nm in ex.aux_off if nm.endswith("minmax")}
+        first = bool(ex._qfirst.value)
         mod.forward(batch, is_train=True)
         torch.cuda.synchronize()
-        ck = Checker(ex)
+        ck = Checker(ex, prev_aux=prev_aux, first_batch=first)
         with torch.no_grad():
             ck.check_forward()
             ex.backward(hooks=ck.backward_hooks())
@@ -195,6 +205,71 @@ def test_resnet50_bf16_full_size_layerwise(gpu):
     assert sum(1 for r in ck.rec if r[0] == "conv_fwd") == 53
     bad = ck.failures()
     assert not bad, bad[:10]
+
+
+def test_resnext50_bf16_full_size_layerwise(gpu):
+    """BASELINE C4 at its bench configuration (ResNeXt-50 32x4d, 256 x 224 x 224, bf16, default knobs),
+    with the same absolute per-kernel bars as C2, after one full step (so the grouped weights' compute
+    copies are the ones rn_conv_weight_pack_multi rewrites after an update): every grouped 3x3
+    convolution (the direct v_dot2 kernels at 4 channels per group and at 8 per group with stride 2,
+    the block-diagonal MFMA tiles elsewhere) forward / data gradient / weight gradient against the
+    bf16-rounded master per group, the post-activation unit tail (rn_bn_apply_add) and its backward
+    (rn_relu_bwd_bnred, then rn_bn_bwd_part), every dense layer and BatchNorm as in C2
+    (symbol/resnext.py:17-47)."""
+    _c4_layerwise(256, 224)
+
+
+def _c4_layerwise(n, image):
+    from rn import graphs
+    ck = _layerwise(graphs.resnext50_32x4d(), n, image, "bfloat16", warm=1)
+    assert not ck.skipped, ck.skipped
+    kinds = {r[0] for r in ck.rec}
+    assert {"conv_fwd", "conv_fwd_grouped", "dgrad_grouped", "wgrad_grouped", "wgrad", "bn_apply_add",
+            "relu_bwd_bnred", "bn_fwd", "bn_bwd_dx", "bn_bwd_params", "weight_copy", "stem_dbeta"} <= kinds, kinds
+    assert sum(1 for r in ck.rec if r[0] == "conv_fwd_grouped") == 16
+    assert sum(1 for r in ck.rec if r[0] in ("wgrad", "wgrad_grouped")) == 54  # 53 convs + fc1
+    assert sum(1 for r in ck.rec if r[0] == "bn_apply_add") == 16
+    bad = ck.failures()
+    assert not bad, bad[:10]
+
+
+def test_resnet50_int8_full_size_layerwise(gpu):
+    """BASELINE C5 at its bench configuration (symbol/resnet_int8.py, 256 x 224 x 224, int8 forward /
+    bf16 backward, default knobs), after one full step (the batched weight quantizer's repack after an
+    update, quantizer EMA states): every activation quantizer -- BatchNorm+ReLU applied on load, the
+    pairs, the block-extreme max from rn_conv_fwd_i8_mm -- bit for bit (state, unit, int8 codes,
+    fake-quantized values); every weight quantizer bit for bit (threshold, unit, codes, fake-quantized
+    fp32 and bf16 CRSK copies); every int8 convolution against the exact fp64 sum of the device's codes
+    times its units (BF16 bar); the folded straight-through clips in the BatchNorm backwards
+    (rn_conv_bwd_data_bnred_clip, rn_bn_desc.clip / clip2 / dy2), the FullyConnected input's STE and
+    the stem's clip gradient (symbol/int8_api.py:120-171, clip_grad_quantization_int8.py:37-67)."""
+    _c5_layerwise(256, 224)
+
+
+def _c5_layerwise(n, image):
+    from rn import graphs
+    ck = _layerwise(graphs.resnet50_int8(), n, image, "bfloat16", warm=1)
+    assert not ck.skipped, ck.skipped
+    kinds = {r[0] for r in ck.rec}
+    assert {"conv_fwd_i8", "quant", "weight_quant", "dgrad_bnred", "bn_bwd_dx", "bn_bwd_params", "wgrad",
+            "quant_bwd", "stem_dbeta", "fc_fwd"} <= kinds, kinds
+    n_i8 = sum(1 for r in ck.rec if r[0] == "conv_fwd_i8")
+    assert n_i8 == 52, n_i8
+    assert sum(1 for r in ck.rec if r[0] == "weight_quant") == 54  # 53 convs + fc1
+    assert sum(1 for r in ck.rec if r[0] == "quant") == 54  # 52 int8 inputs + conv0's + fc1's
+    assert sum(1 for r in ck.rec if r[0] == "wgrad") == 54
+    bad = ck.failures()
+    assert not bad, bad[:10]
+
+
+def test_resnext50_bf16_layerwise_small(gpu):
+    """The C4 per-kernel checks at 8 images of 64x64 (a fast first gate before the full size)."""
+    _c4_layerwise(8, 64)
+
+
+def test_resnet50_int8_layerwise_small(gpu):
+    """The C5 per-kernel checks at 8 images of 64x64 (a fast first gate before the full size)."""
+    _c5_layerwise(8, 64)
 
 
 def test_resnet50_fp32_layerwise(gpu):
