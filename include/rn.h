@@ -551,11 +551,12 @@ const char* rn_last_error(void);
  *      measured slower: C5 24.1 -> 25.1 ms per step), 16 = the 224/256-row conv tiles' output stores
  *      (rn_conv_fwd* / rn_conv_bwd_data*). Default 23. The same bits either way: only the cache
  *      policy changes,
- * 19 = the whole-dW weight gradients of ResNet-50 stage 1 (rn_conv_bwd_filter_ws / _x; one
- *      workgroup holds the whole dW, dy and x read once, needs the slab workspace): the image-band
- *      kernel of the 3x3 stride-1 64 -> 64-channel convolutions and the streaming kernel of the 1x1
- *      stride-1 ones with K x C = 256 x 64, 64 x 256 or 64 x 64: 0 = on (default), 1 = the tiled
- *      kernels. */
+ * 19 = the slice-resident weight gradients (rn_conv_bwd_filter[_ws / _x]; a workgroup keeps its dW
+ *      slice for all of its images in registers, so dy and x are read once per slice; they need the
+ *      slab workspace, rn_conv_wgrad_ws_bytes): the image-band kernels of the 3x3 stride-1 pad-1
+ *      convolutions -- dense with C = K in {64, 128, 256, 512}, and grouped (32 groups) with 4 / 8 / 16
+ *      channels per group -- and the streaming kernel of the 1x1 stride-1 ones with K x C = 256 x 64,
+ *      64 x 256 or 64 x 64: 0 = on (default), 1 = the tiled kernels. */
 int rn_set_tuning(int32_t key, int32_t value);
 int32_t rn_version(void);
 /* Number of compute units of the current device (for split heuristics / reporting). */

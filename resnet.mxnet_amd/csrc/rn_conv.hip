@@ -1847,114 +1847,138 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
 }
 
 // ------------------------------------------------------------------------------ wgrad, image bands
-// The weight gradient of a 3x3 / stride-1 / pad-1 convolution with 64 input and 64 output channels
-// (ResNet-50 stage 1 conv2, symbol/resnet.py:19-21, 56x56): dW[k][tap][c] = sum_m dy[m][k] *
-// x[m + tap shift][c]. The whole dW (64 x 576 fp32) stays in the accumulators of ONE workgroup, which
-// walks its images in bands of two output rows: per band, the two dy rows and the four x rows they
-// read are staged once (LDS-DMA) and every tap multiplies the same LDS image at a shifted row. dy and
-// x are read from HBM exactly once (the tiled kernels re-read dy per column tile and gather x per tap:
-// 340 us per launch, 6x this shape's memory time). Both images use a row stride of 64 pixels with
-// the x pixel (ih, iw) at column iw + 1: columns 0 and W + 1.. of x and W.. of dy are zero, so the
-// tap shift r * 64 + s of a dy pixel never needs an in-image test (dy is zero where a shifted read
-// wraps). 8 waves: wave (kp, cb) owns output channels 32 kp..+32 and input channels 16 cb..+16 over all
-// 9 taps (18 16x16 accumulators). Each workgroup stores its partial dW into the slab; the split
-// reduction pass sums them (deterministic order).
-struct Wg3Args {
-  const bf16_t* x;   // [N][H][W][64]
-  const bf16_t* dy;  // [N][H][W][64]
-  float* slab;       // [G][64][576]
-  int N, H, W, ipw;  // images per workgroup
+// The weight gradient of a dense 3x3 / stride-1 / pad-1 convolution (the conv2 of every ResNet-50
+// bottleneck unit but a stage's first, symbol/resnet.py:19-21): dW[k][tap][c] = sum_m dy[m][k] *
+// x[m + tap shift][c]. A workgroup keeps a KS x 9 x CS slice of dW (channel slices: blockIdx.y over the
+// input channels, blockIdx.z over the output channels) in its accumulators for all of its images,
+// which it walks in bands of R output rows: per band the R dy rows and the R + 2 x rows they read are
+// staged once (LDS-DMA) and every tap multiplies the same LDS image at a shifted row. Both images use
+// a row stride of WP pixels with the x pixel (ih, iw) at column iw + 1: columns 0 and W + 1.. of x
+// and W.. of dy are zero, so the shift r * WP + s of a dy pixel never needs an in-image test (dy is
+// zero where a shifted read wraps). Each operand is read from HBM once per slice of the other (stage 1:
+// the whole 64 x 576 dW in one workgroup, once); the tiled kernels gathered x per tap and column tile
+// and ran at 6x these layers' memory time. 8 waves, wave (wk, wc) owns KB_W x CB_W 16-channel block
+// pairs over all 9 taps (18 accumulators). Each workgroup stores its partial dW slice into the slab
+// [split][K][9][C]; the split reduction pass sums them (deterministic order).
+struct DbArgs {
+  const bf16_t* x;   // [N][H][W][C]
+  const bf16_t* dy;  // [N][H][W][K]
+  float* slab;       // [split][K][9 * C]
+  int N, H, W, C, K, ipw;
 };
-constexpr int kWg3XPix = 4 * 64 + 8;              // x image: 4 rows of 64 pixels + a zero slack
-constexpr int kWg3Buf = (kWg3XPix + 2 * 64) * 8;  // 16-byte chunks per band buffer (x, then dy)
-template <int NBUF>
-__global__ __launch_bounds__(512, 1) void wgrad_band3_kernel(Wg3Args p) {
-  __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * kWg3Buf];
+template <int CS, int KS, int WP, int R>
+struct DbShape {
+  static constexpr int XCPR = CS / 8, DCPR = KS / 8;   // 16-byte chunks per pixel (x, dy slices)
+  static constexpr int XPPI = 64 / XCPR, DPPI = 64 / DCPR;  // pixels per 1 KiB DMA instruction
+  static constexpr int XPIX = (R + 2) * WP + 8;        // x rows oh0-1..oh0+R + a zero slack
+  static constexpr int XINS = (R + 2) * WP / XPPI, DINS = R * WP / DPPI;
+  static constexpr int INS = XINS + DINS, LPTM = (INS + 7) / 8;  // DMA instructions per band; per wave (max)
+  static constexpr int XBYTES = XPIX * XCPR * 16;
+  static constexpr int BUF = XPIX * XCPR + R * WP * DCPR;  // 16-byte chunks per band buffer
+  static constexpr int CB = CS / 16, KB = KS / 16;
+  static constexpr int WC = CB >= 8 ? 8 : CB, WK = 8 / WC;
+  static constexpr int CB_W = CB / WC, KB_W = KB / WK;
+  static_assert(CB_W * WC == CB && KB_W * WK == KB && CB_W * KB_W <= 2 && (R * WP) % 32 == 0 &&
+                XPPI >= 1 && DPPI >= 1 && (R * WP) % DPPI == 0, "dense band shape");
+};
+template <int CS, int KS, int WP, int R, int NBUF>
+__global__ __launch_bounds__(512, 1) void wgrad_dband_kernel(DbArgs p) {
+  using S = DbShape<CS, KS, WP, R>;
+  constexpr int XCPR = S::XCPR, DCPR = S::DCPR, KB_W = S::KB_W, CB_W = S::CB_W;
+  __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * S::BUF];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int n_first = blockIdx.x * p.ipw;
   const int n_end = min(p.N, n_first + p.ipw);
-  const int bpi = (p.H + 1) / 2;               // bands per image
+  const int bpi = (p.H + R - 1) / R;
   const int nb = (n_end - n_first) * bpi;
-  // the x images' slack pixels (read only against zero dy) are zeroed once; DMAs never write them
-  for (int i = tid; i < NBUF * 64; i += 512) smem[(i >> 6) * kWg3Buf + 4 * 64 * 8 + (i & 63)] = make_uint4(0, 0, 0, 0);
-  // per-lane DMA geometry: wave w issues x pieces 4w..4w+3 (pixels 32w..32w+31 of the 4 x rows) and dy
-  // pieces 2w, 2w+1; lane = (pixel lane / 8 of the piece, LDS chunk slot lane % 8), the source chunk is
-  // the slot XOR the image's read swizzle
-  int x_rr[4], x_iw[4], x_ch[4], d_rr[2], d_q[2], d_ch[2];
+  const int c0 = blockIdx.y * CS, k0 = blockIdx.z * KS;  // the channel slices
+  for (int i = tid; i < NBUF * 8 * XCPR; i += 512)
+    smem[(i / (8 * XCPR)) * S::BUF + (R + 2) * WP * XCPR + i % (8 * XCPR)] = make_uint4(0, 0, 0, 0);
+  // this wave's DMA pieces: w, w + 8, ... (x pieces first, then dy); lane = (pixel, LDS chunk slot), the
+  // source chunk is the slot XOR the image's read swizzle
+  const int cnt = (S::INS - wid + 7) / 8;
+  int dr[S::LPTM], dc[S::LPTM], dch[S::LPTM];
+  uint32_t dla[S::LPTM];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int px = (4 * wid + j) * 8 + (lane >> 3);
-    x_rr[j] = px >> 6;
-    x_iw[j] = (px & 63) - 1;
-    x_ch[j] = 8 * ((lane & 7) ^ (swz_tr(px) & 7));
-  }
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int px = (2 * wid + j) * 8 + (lane >> 3);
-    d_rr[j] = px >> 6;
-    d_q[j] = px & 63;
-    d_ch[j] = 8 * ((lane & 7) ^ (swz_tr(px) & 7));
+  for (int j = 0; j < S::LPTM; ++j) {
+    const int piece = wid + 8 * j;
+    const bool isx = piece < S::XINS;
+    const int cpr = isx ? XCPR : DCPR;
+    const int px = isx ? piece * S::XPPI + lane / XCPR : (piece - S::XINS) * S::DPPI + lane / DCPR;
+    dr[j] = isx ? px / WP : -1 - px / WP;  // (dy pieces: -1 - row)
+    dc[j] = px % WP;
+    dch[j] = (isx ? c0 : k0) + 8 * ((lane % cpr) ^ (swz_tr(px) & (cpr - 1)));
+    dla[j] = isx ? piece * 1024 : S::XBYTES + (piece - S::XINS) * 1024;
   }
   const char* zb = reinterpret_cast<const char*>(&g_zero_chunk);
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
   auto issue = [&](int t, int buf) __attribute__((always_inline)) {
-    const int n = n_first + t / bpi, p0 = 2 * (t % bpi);
-    const uint32_t base = lds0 + buf * (kWg3Buf * 16);
+    const int n = n_first + t / bpi, oh0 = R * (t % bpi);
+    const uint32_t base = lds0 + buf * (S::BUF * 16);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int ih = p0 - 1 + x_rr[j];
-      const bool ok = (unsigned)ih < (unsigned)p.H && (unsigned)x_iw[j] < (unsigned)p.W;
-      const bf16_t* src = p.x + ((int64_t)(n * p.H + ih) * p.W + x_iw[j]) * 64 + x_ch[j];
-      dma16_global(ok ? (const void*)src : (const void*)zb, base + (4 * wid + j) * 1024);
-    }
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int oh = p0 + d_rr[j];
-      const bool ok = oh < p.H && d_q[j] < p.W;
-      const bf16_t* src = p.dy + ((int64_t)(n * p.H + oh) * p.W + d_q[j]) * 64 + d_ch[j];
-      dma16_global(ok ? (const void*)src : (const void*)zb, base + kWg3XPix * 128 + (2 * wid + j) * 1024);
+    for (int j = 0; j < S::LPTM; ++j) {
+      if (j >= cnt) break;  // (wave-uniform)
+      const bf16_t* src;
+      bool ok;
+      if (dr[j] >= 0) {
+        const int ih = oh0 - 1 + dr[j], iw = dc[j] - 1;
+        ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        src = p.x + ((int64_t)(n * p.H + ih) * p.W + iw) * p.C + dch[j];
+      } else {
+        const int oh = oh0 - 1 - dr[j];
+        ok = oh < p.H && dc[j] < p.W;
+        src = p.dy + ((int64_t)(n * p.H + oh) * p.W + dc[j]) * p.K + dch[j];
+      }
+      dma16_global(ok ? (const void*)src : (const void*)zb, base + dla[j]);
     }
   };
 
-  const int kp = wid >> 2, cb = wid & 3;
-  v4f acc[2][9];
+  const int wk = wid / S::WC, wc = wid % S::WC;
+  v4f acc[KB_W][CB_W][9];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < KB_W; ++i)
 #pragma unroll
-    for (int t = 0; t < 9; ++t) acc[i][t] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < CB_W; ++j)
+#pragma unroll
+      for (int t = 0; t < 9; ++t) acc[i][j][t] = v4f{0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
-  // transposed 8-byte read of the 4 x 4 block at (pixel row, element column col) of a 128-byte-row image
-  auto rd = [&](const char* img, int row, int col) __attribute__((always_inline)) {
-    const int byte = row * 128 + ((((col * 2) >> 4) ^ (swz_tr(row) & 7)) << 4) + ((col * 2) & 15);
+  // transposed 8-byte read of the 4 x 4 block at (pixel row, element column col) of an image with cpr
+  // 16-byte chunks per pixel
+  auto rd = [&](const char* img, int cpr, int row, int col) __attribute__((always_inline)) {
+    const int byte = row * (cpr * 16) + ((((col * 2) >> 4) ^ (swz_tr(row) & (cpr - 1))) << 4) + ((col * 2) & 15);
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(img + byte));
   };
   auto compute = [&](int buf) __attribute__((always_inline)) {
-    const char* Xb = reinterpret_cast<const char*>(smem + buf * kWg3Buf);
-    const char* Db = Xb + kWg3XPix * 128;
+    const char* Xb = reinterpret_cast<const char*>(smem + buf * S::BUF);
+    const char* Db = Xb + S::XBYTES;
 #pragma unroll
-    for (int ms = 0; ms < 4; ++ms) {  // 32 dy pixels per step
-      v8s af[2], bfv[9];
+    for (int ms = 0; ms < R * WP / 32; ++ms) {  // 32 dy pixels per step
+      v8s af[KB_W], bfv[CB_W][9];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int row = ms * 32 + 8 * g + 4 * h + q;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const v4s v = rd(Db, row, kp * 32 + i * 16 + 4 * pp);
+        for (int i = 0; i < KB_W; ++i) {
+          const v4s v = rd(Db, DCPR, row, (wk * KB_W + i) * 16 + 4 * pp);
 #pragma unroll
           for (int e = 0; e < 4; ++e) af[i][4 * h + e] = v[e];
         }
 #pragma unroll
-        for (int t = 0; t < 9; ++t) {
-          const v4s v = rd(Xb, row + (t / 3) * 64 + (t % 3), cb * 16 + 4 * pp);
+        for (int j = 0; j < CB_W; ++j)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) bfv[t][4 * h + e] = v[e];
-        }
+          for (int t = 0; t < 9; ++t) {
+            const v4s v = rd(Xb, XCPR, row + (t / 3) * WP + (t % 3), (wc * CB_W + j) * 16 + 4 * pp);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bfv[j][t][4 * h + e] = v[e];
+          }
       }
 #pragma unroll
       for (int t = 0; t < 9; ++t)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
-          acc[i][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[t], acc[i][t], 0, 0, 0);
+        for (int j = 0; j < CB_W; ++j)
+#pragma unroll
+          for (int i = 0; i < KB_W; ++i)
+            acc[i][j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j][t], acc[i][j][t], 0, 0, 0);
     }
   };
   __syncthreads();  // (the slack zeros)
@@ -1962,33 +1986,189 @@ __global__ __launch_bounds__(512, 1) void wgrad_band3_kernel(Wg3Args p) {
   for (int s = 0; s < NBUF - 1; ++s)
     if (s < nb) issue(s, s);
   for (int t = 0; t < nb; ++t) {
-    // band t has landed once at most the DMAs of the bands issued after it are outstanding
-    if (NBUF == 3 && t + 1 < nb) wait_vmcnt<6>();
-    else wait_vmcnt<0>();
+    // band t has landed once at most the DMAs of the band issued after it are outstanding
+    if (NBUF == 3 && t + 1 < nb) {
+      if (cnt == S::LPTM) wait_vmcnt<S::LPTM>();
+      else wait_vmcnt<S::LPTM - 1>();
+    } else {
+      wait_vmcnt<0>();
+    }
     __syncthreads();  // ... for every wave; and every wave is done with the buffer refilled next
     if (t + NBUF - 1 < nb) issue(t + NBUF - 1, (t + NBUF - 1) % NBUF);
     compute(t % NBUF);
   }
-  // the workgroup's partial dW: slab[block][k][tap * 64 + c]
-  float* dst = p.slab + (int64_t)blockIdx.x * 64 * 576;
+  // the workgroup's partial dW slice: slab[block][k][tap * C + c]
+  float* dst = p.slab + (int64_t)blockIdx.x * p.K * 9 * p.C;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < KB_W; ++i)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const int k = kp * 32 + i * 16 + (lane >> 4) * 4 + e;
+      const int k = k0 + (wk * KB_W + i) * 16 + (lane >> 4) * 4 + e;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) dst[(int64_t)k * 576 + t * 64 + cb * 16 + (lane & 15)] = acc[i][t][e];
+      for (int j = 0; j < CB_W; ++j)
+#pragma unroll
+        for (int t = 0; t < 9; ++t)
+          dst[(int64_t)k * 9 * p.C + t * p.C + c0 + (wc * CB_W + j) * 16 + (lane & 15)] = acc[i][j][t][e];
+    }
+}
+
+// The grouped form (ResNeXt's 3x3 / stride-1 convolutions, symbol/resnext.py:23-25, num_group = 32:
+// 4 channels per group at C = 128 (stage 1, 56x56), 8 at C = 256 (stage 2, 28x28), 16 at C = 512
+// (stage 3, 14x14)): the whole block-diagonal dW of a workgroup's images and channel slice in its
+// accumulators. 16-channel block b of dy pairs with block b of x only (dW is zero across blocks), so
+// wave w owns blocks w * BPW.. of the slice and every tap of them (9 * BPW accumulators); the MFMAs
+// multiply whole 16 x 16 blocks and the epilogue keeps their group-diagonal G x G parts (with G < 16
+// the MFMA work over the zero parts is the price of reading dy and x once: these layers are
+// HBM-bound). Image rows of WP pixels (the x pixel (ih, iw) at column iw + 1), bands of R output
+// rows; channel slices of CS channels (blockIdx.y; groups never straddle one) keep the band buffers
+// double-buffered at C = 512. dW stored [K][3][3][G] into the slab. (The tiled grouped kernel re-read
+// x per 64-column block and tap.)
+struct GbArgs {
+  const bf16_t* x;   // [N][H][W][C]
+  const bf16_t* dy;  // [N][H][W][C]
+  float* slab;       // [split][C][9 * G]
+  int N, H, W, C, ipw;
+};
+template <int CS, int G, int WP, int R>
+struct GbShape {
+  static constexpr int CPR = CS / 8;                   // 16-byte chunks per pixel of the slice
+  static constexpr int PPI = 64 / CPR;                 // pixels per 1 KiB DMA instruction
+  static constexpr int XPIX = (R + 2) * WP + 8;        // x rows oh0-1..oh0+R + a zero slack
+  static constexpr int XINS = (R + 2) * WP / PPI, DINS = R * WP / PPI;
+  static constexpr int LPT = (XINS + DINS) / 8;        // DMA instructions per wave per band
+  static constexpr int BUF = (XPIX + R * WP) * CPR;    // 16-byte chunks per band buffer
+  static constexpr int BPW = CS / 16 / 8;              // 16-channel blocks per wave
+  static_assert((XINS + DINS) % 8 == 0 && BPW >= 1 && (R * WP) % 32 == 0 && G <= 16, "grouped band shape");
+};
+template <int CS, int G, int WP, int R, int NBUF>
+__global__ __launch_bounds__(512, 1) void wgrad_gband_kernel(GbArgs p) {
+  using S = GbShape<CS, G, WP, R>;
+  constexpr int CPR = S::CPR, PPI = S::PPI, BPW = S::BPW;
+  __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * S::BUF];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int n_first = blockIdx.x * p.ipw;
+  const int n_end = min(p.N, n_first + p.ipw);
+  const int bpi = (p.H + R - 1) / R;
+  const int nb = (n_end - n_first) * bpi;
+  const int c0 = blockIdx.y * CS;  // the channel slice
+  for (int i = tid; i < NBUF * 8 * CPR; i += 512)
+    smem[(i / (8 * CPR)) * S::BUF + (R + 2) * WP * CPR + i % (8 * CPR)] = make_uint4(0, 0, 0, 0);
+  int dr[S::LPT], dc[S::LPT], dch[S::LPT];
+  bool dx_[S::LPT];
+#pragma unroll
+  for (int j = 0; j < S::LPT; ++j) {
+    const int piece = wid * S::LPT + j;
+    dx_[j] = piece < S::XINS;
+    const int px = (dx_[j] ? piece : piece - S::XINS) * PPI + lane / CPR;
+    dr[j] = px / WP;
+    dc[j] = px % WP;
+    dch[j] = c0 + 8 * ((lane % CPR) ^ (swz_tr(px) & (CPR - 1)));
+  }
+  const char* zb = reinterpret_cast<const char*>(&g_zero_chunk);
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  auto issue = [&](int t, int buf) __attribute__((always_inline)) {
+    const int n = n_first + t / bpi, oh0 = R * (t % bpi);
+    const uint32_t base = lds0 + buf * (S::BUF * 16);
+#pragma unroll
+    for (int j = 0; j < S::LPT; ++j) {
+      const int piece = wid * S::LPT + j;
+      const bf16_t* src;
+      bool ok;
+      uint32_t la;
+      if (dx_[j]) {
+        const int ih = oh0 - 1 + dr[j], iw = dc[j] - 1;
+        ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        src = p.x + ((int64_t)(n * p.H + ih) * p.W + iw) * p.C + dch[j];
+        la = base + piece * 1024;
+      } else {
+        const int oh = oh0 + dr[j];
+        ok = oh < p.H && dc[j] < p.W;
+        src = p.dy + ((int64_t)(n * p.H + oh) * p.W + dc[j]) * p.C + dch[j];
+        la = base + S::XPIX * CPR * 16 + (piece - S::XINS) * 1024;
+      }
+      dma16_global(ok ? (const void*)src : (const void*)zb, la);
+    }
+  };
+  v4f acc[BPW][9];
+#pragma unroll
+  for (int b = 0; b < BPW; ++b)
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[b][t] = v4f{0.f, 0.f, 0.f, 0.f};
+  const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+  auto rd = [&](const char* img, int row, int col) __attribute__((always_inline)) {
+    const int byte = row * (CPR * 16) + ((((col * 2) >> 4) ^ (swz_tr(row) & (CPR - 1))) << 4) + ((col * 2) & 15);
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(img + byte));
+  };
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const char* Xb = reinterpret_cast<const char*>(smem + buf * S::BUF);
+    const char* Db = Xb + S::XPIX * CPR * 16;
+#pragma unroll
+    for (int ms = 0; ms < R * WP / 32; ++ms) {
+#pragma unroll
+      for (int b = 0; b < BPW; ++b) {
+        const int col = (wid * BPW + b) * 16 + 4 * pp;
+        v8s af, bfv[9];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int row = ms * 32 + 8 * g + 4 * h + q;
+          const v4s v = rd(Db, row, col);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) af[4 * h + e] = v[e];
+#pragma unroll
+          for (int t = 0; t < 9; ++t) {
+            const v4s u = rd(Xb, row + (t / 3) * WP + (t % 3), col);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) bfv[t][4 * h + e] = u[e];
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[b][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfv[t], acc[b][t], 0, 0, 0);
+      }
+    }
+  };
+  __syncthreads();  // (the slack zeros)
+#pragma unroll
+  for (int s = 0; s < NBUF - 1; ++s)
+    if (s < nb) issue(s, s);
+  for (int t = 0; t < nb; ++t) {
+    if (NBUF == 3 && t + 1 < nb) wait_vmcnt<S::LPT>();
+    else wait_vmcnt<0>();
+    __syncthreads();
+    if (t + NBUF - 1 < nb) issue(t + NBUF - 1, (t + NBUF - 1) % NBUF);
+    compute(t % NBUF);
+  }
+  // the group-diagonal G x G parts: slab[block][k][tap * G + c - group base]
+  float* dst = p.slab + (int64_t)blockIdx.x * p.C * 9 * G;
+#pragma unroll
+  for (int b = 0; b < BPW; ++b)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = c0 + (wid * BPW + b) * 16 + (lane >> 4) * 4 + e;
+      const int c = c0 + (wid * BPW + b) * 16 + (lane & 15);
+      if (k / G != c / G) continue;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) dst[(int64_t)k * 9 * G + t * G + c % G] = acc[b][t][e];
     }
 }
 
 // The weight gradient of a 1x1 / stride-1 convolution whose whole dW fits one workgroup's accumulators
-// (K x C <= 256 x 64 or 64 x 256: ResNet-50 stage 1's conv1 / conv3 / shortcut, symbol/resnet.py:17-31):
+// (K, C in {64, 128, 256}, K x C <= 32768: ResNet-50 / ResNeXt-50 stage 1's conv1 / conv3 / shortcut and
+// stage 2's first conv1, symbol/resnet.py:17-31):
 // dW = dy^T x over M = N*P*Q. Each workgroup streams ONE contiguous M range through NBUF LDS-DMA
 // buffers of 64 rows (dy row: K channels, x row: C channels), so both operands are read from HBM once
 // (the tiled kernels re-read one operand per output tile and ran at 3 TB/s, 2-3x this shape's memory
 // time); the split partials go to the slab (wgrad_slab_reduce_kernel). XF: the producing
 // BatchNorm+ReLU applied to the x fragments after their transposed read, as wgrad_big_kernel XF.
 // 8 waves, wave (wk, wc) owns MI x NI 16x16 blocks of dW.
+constexpr int stream_wk(int kb, int cb) {  // waves along K (of 8) minimizing the wave's A + B fragments
+  int best = 0, cost = 1 << 30;
+  for (int wk = 1; wk <= 8; wk *= 2) {
+    const int wc = 8 / wk;
+    if (kb % wk || cb % wc || (kb / wk) * (cb / wc) > 16) continue;
+    if (kb / wk + cb / wc < cost) cost = kb / wk + cb / wc, best = wk;
+  }
+  return best;
+}
 template <int K, int C, int XF, int NBUF>
 __global__ __launch_bounds__(512, 1) void wgrad_stream_kernel(WgradArgs p) {
   constexpr int BKM = 64;
@@ -1998,9 +2178,9 @@ __global__ __launch_bounds__(512, 1) void wgrad_stream_kernel(WgradArgs p) {
   static_assert((A_INS + B_INS) % 8 == 0, "DMA pieces per wave");
   constexpr int LPT = (A_INS + B_INS) / 8;
   constexpr int KB = K / 16, CB = C / 16;
-  constexpr int WK = KB >= 8 ? 8 : (CB >= 8 ? 1 : 4), WC = 8 / WK;
+  constexpr int WK = stream_wk(KB, CB), WC = 8 / WK;  // (the split with the fewest fragment reads)
   constexpr int MI = KB / WK, NI = CB / WC;
-  static_assert(MI * WK == KB && NI * WC == CB && MI * NI <= 16, "wave tile");
+  static_assert(WK > 0 && MI * WK == KB && NI * WC == CB && MI * NI <= 16, "wave tile");
   constexpr int A_SZ = BKM * A_CPR, B_SZ = BKM * B_CPR, kStage = A_SZ + B_SZ;
   __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * kStage];
 
@@ -2117,10 +2297,14 @@ __global__ __launch_bounds__(512, 1) void wgrad_stream_kernel(WgradArgs p) {
     }
 }
 
-// dw[i] += sum_z slab[z][i] (the split-M partial tiles of wgrad_big_kernel), float4 per thread
+// dw[i] += sum_z slab[z][i] (the split-M partial tiles of the weight-gradient kernels). A block takes 16
+// float4 columns x 16 split groups: thread (g, c) sums splits g, g + 16, ... of column c in order, then
+// the 16 group sums are added in group order (deterministic). (The first form gave each thread a whole
+// column's splits, one block per 1,024 columns: ~36 blocks and a 256-long dependent chain per thread on
+// a 64 x 576 dW -- ~2 TB/s.)
 __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __restrict__ slab, int nsplit,
                                                                 int64_t n, float* __restrict__ dw) {
-  if (n & 3) {  // (a split's slab not a whole number of 16-byte chunks: scalar, same summation order)
+  if (n & 3) {  // (a split's slab not a whole number of 16-byte chunks: scalar, split order)
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
       float a = dw[i];
       for (int z = 0; z < nsplit; ++z) a += slab[(int64_t)z * n + i];
@@ -2129,29 +2313,37 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __r
     return;
   }
   const int64_t n4 = n / 4;
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
-    float4 a = reinterpret_cast<const float4*>(dw)[i];
-    int z = 0;
-    for (; z + 4 <= nsplit; z += 4) {
+  const int cl = threadIdx.x & 15, sg = threadIdx.x >> 4;
+  const int64_t col = blockIdx.x * 16 + cl;
+  const float4* __restrict__ s4 = reinterpret_cast<const float4*>(slab);
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (col < n4) {
+    int z = sg;
+    for (; z + 48 < nsplit; z += 64) {  // four loads in flight
       float4 v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = reinterpret_cast<const float4*>(slab + (int64_t)(z + u) * n)[i];
+      for (int u = 0; u < 4; ++u) v[u] = s4[(int64_t)(z + 16 * u) * n4 + col];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w;
       }
     }
-    for (; z < nsplit; ++z) {
-      const float4 v = reinterpret_cast<const float4*>(slab + (int64_t)z * n)[i];
+    for (; z < nsplit; z += 16) {
+      const float4 v = s4[(int64_t)z * n4 + col];
       a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
     }
-    reinterpret_cast<float4*>(dw)[i] = a;
   }
-  if (blockIdx.x == 0 && threadIdx.x < n - n4 * 4) {  // tail
-    const int64_t i = n4 * 4 + threadIdx.x;
-    float a = dw[i];
-    for (int z = 0; z < nsplit; ++z) a += slab[(int64_t)z * n + i];
-    dw[i] = a;
+  __shared__ float4 red[16][16];
+  red[sg][cl] = a;
+  __syncthreads();
+  if (sg == 0 && col < n4) {
+    float4 t = reinterpret_cast<const float4*>(dw)[col];
+#pragma unroll
+    for (int gi = 0; gi < 16; ++gi) {
+      const float4 v = red[gi][cl];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    reinterpret_cast<float4*>(dw)[col] = t;
   }
 }
 
@@ -2776,6 +2968,11 @@ int grid_for(int64_t total, int block = 256) {
   if (g > 8192) g = 8192;
   if (g < 1) g = 1;
   return (int)g;
+}
+// wgrad_slab_reduce_kernel's grid: 16 float4 columns per block (the scalar path: a grid-stride loop)
+int slab_reduce_blocks(int64_t n) {
+  if (n & 3) return grid_for(n);
+  return (int)std::max<int64_t>(1, (n / 4 + 15) / 16);
 }
 
 // Build igemm args for fwd (mode 0) or dgrad (mode 1).
@@ -3420,7 +3617,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     if (rn_check_launch(what)) return -1;
     if (a.slab) {
       const int64_t n = (int64_t)a.K * a.ldw;
-      hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, st, a.slab, (int)split, n, dw);
+      hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3(slab_reduce_blocks(n)), dim3(256), 0, st, a.slab, (int)split, n, dw);
       return rn_check_launch("wgrad_slab_reduce");
     }
     return 0;
@@ -3434,30 +3631,67 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     }
     return true;
   };
-  // 3x3 / stride 1 / pad 1, 64 -> 64 channels (stage-1 conv2): image bands, the whole dW per workgroup
-  // (wgrad_band3_kernel; rn_set_tuning 19 = 1: the tiled kernels below). Needs the slab workspace.
-  if (d->dtype == RN_BF16 && !grouped && !in_scale && d->r == 3 && d->s == 3 && d->stride_h == 1 &&
-      d->stride_w == 1 && d->pad_h == 1 && d->pad_w == 1 && d->c == 64 && d->c_real == 64 && d->k == 64 &&
-      d->k_pad == 64 && d->w <= 62 && g_tune[RN_TUNE_WGRAD_BAND] != 1 &&
-      (int64_t)d->n * d->h * d->w * 64 < INT32_MAX) {
-    Wg3Args g{};
-    g.x = (const bf16_t*)x; g.dy = (const bf16_t*)dy; g.N = d->n; g.H = d->h; g.W = d->w;
-    g.ipw = (int)std::max<int64_t>(1, ceil_div(d->n, chip_cus()));
+  // dense 3x3 / stride 1 / pad 1 with C = K in {64, 128, 256, 512} (every bottleneck conv2 but a stage's
+  // first): image bands, dW slices per workgroup (wgrad_dband_kernel; rn_set_tuning 19 = 1: the tiled
+  // kernels below). Needs the slab workspace.
+  const int db = (d->c == 64 && d->w <= 62) ? 1 : (d->c == 128 && d->w <= 30) ? 2 :
+                 ((d->c == 256 || d->c == 512) && d->w <= 14) ? 3 : 0;
+  if (d->dtype == RN_BF16 && !grouped && !in_scale && db && d->r == 3 && d->s == 3 && d->stride_h == 1 &&
+      d->stride_w == 1 && d->pad_h == 1 && d->pad_w == 1 && d->c_real == d->c && d->k == d->c &&
+      d->k_pad == d->k && g_tune[RN_TUNE_WGRAD_BAND] != 1 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX) {
+    DbArgs g{};
+    g.x = (const bf16_t*)x; g.dy = (const bf16_t*)dy; g.N = d->n; g.H = d->h; g.W = d->w; g.C = d->c; g.K = d->k;
+    const int cs = db == 1 ? 64 : 128, ks = db == 1 ? 64 : 32;
+    const int slices = (d->c / cs) * (d->k / ks);
+    const int64_t want = std::max<int64_t>(1, chip_cus() / slices);  // (the slab stays ~ CUs x slice)
+    g.ipw = (int)ceil_div(d->n, std::min<int64_t>(d->n, want));
     const int64_t split = ceil_div(d->n, g.ipw);
-    if (!launch) return finish(split, "wgrad_band3");
+    if (!launch) return finish(split, "wgrad_dband");
     if (ws && ws_bytes >= split * a.K * (int64_t)a.ldw * 4) {
       if (!use_slab(split)) return -1;
       g.slab = a.slab;
-      hipLaunchKernelGGL(wgrad_band3_kernel<3>, dim3((unsigned)split), dim3(512), 0, st, g);
-      return finish(split, "wgrad_band3");
+      const dim3 grid((unsigned)split, d->c / cs, d->k / ks);
+      if (db == 1) hipLaunchKernelGGL((wgrad_dband_kernel<64, 64, 64, 2, 3>), grid, dim3(512), 0, st, g);
+      else if (db == 2) hipLaunchKernelGGL((wgrad_dband_kernel<128, 32, 32, 1, 3>), grid, dim3(512), 0, st, g);
+      else hipLaunchKernelGGL((wgrad_dband_kernel<128, 32, 16, 2, 3>), grid, dim3(512), 0, st, g);
+      return finish(split, "wgrad_dband");
     }
   }
-  // 1x1 / stride 1 with the whole dW in one workgroup (K x C = 256 x 64, 64 x 256 or 64 x 64: stage 1):
-  // one streaming pass over M per workgroup (wgrad_stream_kernel; rn_set_tuning 19 = 1: off)
+  // grouped 3x3 / stride 1 / pad 1 with 4 / 8 / 16 channels per group (ResNeXt stages 1-3, C = 128 /
+  // 256 / 512): the whole block-diagonal dW per workgroup and channel slice (wgrad_gband_kernel;
+  // rn_set_tuning 19 = 1: off)
+  const int gb = (d->c == 128 && d->w <= 62) ? 1 : (d->c == 256 && d->w <= 30) ? 2 : (d->c == 512 && d->w <= 14) ? 3 : 0;
+  if (d->dtype == RN_BF16 && grouped && gb && d->groups == 32 && d->r == 3 && d->s == 3 && d->stride_h == 1 &&
+      d->stride_w == 1 && d->pad_h == 1 && d->pad_w == 1 && d->c == d->k && d->c == d->c_real &&
+      g_tune[RN_TUNE_WGRAD_BAND] != 1 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX) {
+    GbArgs g{};
+    g.x = (const bf16_t*)x; g.dy = (const bf16_t*)dy; g.N = d->n; g.H = d->h; g.W = d->w; g.C = d->c;
+    const int slices = gb == 3 ? 2 : 1;
+    g.ipw = (int)std::max<int64_t>(1, ceil_div((int64_t)d->n * slices, chip_cus()));
+    const int64_t split = ceil_div(d->n, g.ipw);
+    const int64_t need = split * a.K * (int64_t)a.ldw * 4;  // (a.ldw = 9 * channels per group)
+    if (ws_need) *ws_need = need;
+    if (!launch) return 0;
+    if (ws && ws_bytes >= need) {
+      g.slab = a.slab = ws;
+      const dim3 grid((unsigned)split, slices);
+      if (gb == 1) hipLaunchKernelGGL((wgrad_gband_kernel<128, 4, 64, 1, 2>), grid, dim3(512), 0, st, g);
+      else if (gb == 2) hipLaunchKernelGGL((wgrad_gband_kernel<256, 8, 32, 1, 2>), grid, dim3(512), 0, st, g);
+      else hipLaunchKernelGGL((wgrad_gband_kernel<256, 16, 16, 2, 2>), grid, dim3(512), 0, st, g);
+      if (rn_check_launch("wgrad_gband")) return -1;
+      const int64_t n = (int64_t)a.K * a.ldw;
+      hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3(slab_reduce_blocks(n)), dim3(256), 0, st, a.slab, (int)split, n, dw);
+      return rn_check_launch("wgrad_slab_reduce");
+    }
+    if (ws_need) *ws_need = 0;
+  }
+  // 1x1 / stride 1 with the whole dW in one workgroup (K, C in {64, 128, 256}, K x C <= 32768): one
+  // streaming pass over M per workgroup (wgrad_stream_kernel; rn_set_tuning 19 = 1: off)
   const bool one = d->r == 1 && d->s == 1 && d->stride_h == 1 && d->stride_w == 1 && d->pad_h == 0 && d->pad_w == 0;
-  const int kc = (d->k == 256 && d->c == 64) ? 1 : (d->k == 64 && d->c == 256) ? 2 : (d->k == 64 && d->c == 64) ? 3 : 0;
-  if (d->dtype == RN_BF16 && !grouped && one && kc && d->c_real == d->c && d->k_pad == d->k &&
-      g_tune[RN_TUNE_WGRAD_BAND] != 1 && (int64_t)a.M * (d->k + d->c) * 2 < INT32_MAX) {
+  auto pw2 = [](int v) { return v == 64 || v == 128 || v == 256; };
+  if (d->dtype == RN_BF16 && !grouped && one && pw2(d->k) && pw2(d->c) && d->k * d->c <= 32768 &&
+      d->c_real == d->c && d->k_pad == d->k && g_tune[RN_TUNE_WGRAD_BAND] != 1 &&
+      (int64_t)a.M * (d->k + d->c) * 2 < INT32_MAX) {
     const int64_t mtiles = ceil_div(a.M, 64);
     const int64_t split = std::min<int64_t>(chip_cus(), std::max<int64_t>(1, mtiles / 4));
     a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
@@ -3466,16 +3700,15 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     if (ws && ws_bytes >= nsplit * a.K * (int64_t)a.ldw * 4) {
       if (!use_slab(nsplit)) return -1;
       const dim3 grid((unsigned)nsplit);
-      if (kc == 1) {
-        if (in_scale) hipLaunchKernelGGL((wgrad_stream_kernel<256, 64, 1, 3>), grid, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((wgrad_stream_kernel<256, 64, 0, 3>), grid, dim3(512), 0, st, a);
-      } else if (kc == 2) {
-        if (in_scale) hipLaunchKernelGGL((wgrad_stream_kernel<64, 256, 1, 3>), grid, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((wgrad_stream_kernel<64, 256, 0, 3>), grid, dim3(512), 0, st, a);
-      } else {
-        if (in_scale) hipLaunchKernelGGL((wgrad_stream_kernel<64, 64, 1, 3>), grid, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((wgrad_stream_kernel<64, 64, 0, 3>), grid, dim3(512), 0, st, a);
-      }
+      const bool t = in_scale != nullptr;
+#define RN_STREAM(KK, CC)                                                                         \
+  if (d->k == KK && d->c == CC) {                                                                 \
+    if (t) hipLaunchKernelGGL((wgrad_stream_kernel<KK, CC, 1, 3>), grid, dim3(512), 0, st, a);    \
+    else hipLaunchKernelGGL((wgrad_stream_kernel<KK, CC, 0, 3>), grid, dim3(512), 0, st, a);      \
+  }
+      RN_STREAM(64, 64) RN_STREAM(64, 128) RN_STREAM(64, 256) RN_STREAM(128, 64) RN_STREAM(128, 128)
+      RN_STREAM(128, 256) RN_STREAM(256, 64) RN_STREAM(256, 128)
+#undef RN_STREAM
       return finish(nsplit, "wgrad_stream");
     }
   }

@@ -423,8 +423,9 @@ class Checker:
         output the quantizer applies on load (rn_quant_int8_fwd_codes_bn[2]), rounded as rn_bn_apply
         stores it."""
         x = op.x
-        if op.bn_src is not None:
-            bn = op.bn_src
+        # (the second quantizer of a pair is written by its lead's call, rn_quant_int8_fwd_codes_bn2)
+        bn = op.bn_src if op.bn_src is not None else (op.bn_lead.bn_src if op.bn_lead is not None else None)
+        if bn is not None:
             _, _, sc, sh = self.bn_coefs(bn)
             c = bn.x.c
             v = _fma(self.act_nchw(bn.x), sc[:c].view(1, c, 1, 1), sh[:c].view(1, c, 1, 1))

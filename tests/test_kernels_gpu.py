@@ -1360,13 +1360,17 @@ def _zero_block_skip(gpu, n, c, h, w, k, r, st, pd, g):
 
 
 @pytest.mark.parametrize("case", [
-    (3, 64, 56, 56, 64, 3, 1, 1),   # the stage-1 conv2 shape (one image per workgroup)
-    (5, 64, 9, 13, 64, 3, 1, 1),    # odd rows: the last band has one output row
-    (2, 64, 7, 62, 64, 3, 1, 1),    # the widest row the 64-pixel band image holds
+    (3, 64, 56, 56, 64, 3, 1, 1),    # the stage-1 conv2 shape (one image per workgroup)
+    (5, 64, 9, 13, 64, 3, 1, 1),     # odd rows: the last band has one output row
+    (2, 64, 7, 62, 64, 3, 1, 1),     # the widest row the 64-pixel band image holds
+    (6, 128, 28, 28, 128, 3, 1, 1),  # stage 2: 4 output-channel slices, 32-pixel rows, one-row bands
+    (3, 128, 5, 30, 128, 3, 1, 1),   # the widest 32-pixel row
+    (9, 256, 14, 14, 256, 3, 1, 1),  # stage 3: 2 x 8 slices, 16-pixel rows, two-row bands
+    (5, 512, 7, 7, 512, 3, 1, 1),    # stage 4: 4 x 16 slices, odd rows
 ])
 def test_wgrad_image_bands(gpu, case):
-    """wgrad_band3_kernel (the 3x3 stride-1 64 -> 64 weight gradient, rn_set_tuning 19 = 0): the whole
-    dW per workgroup over bands of two output rows, every tap a shifted read of one staged x image.
+    """wgrad_dband_kernel (dense 3x3 stride-1 weight gradients with C = K, rn_set_tuning 19 = 0): dW
+    slices per workgroup over bands of output rows, every tap a shifted read of one staged x image.
     Against the fp64 oracle (the sums of products of bf16 values, fp32 accumulation: 2e-6 of the sum of
     the terms' magnitudes per element), bit-identical run to run (one writer per slab element, the
     reduction in split order), and equal to the tiled kernels (rn_set_tuning 19 = 1) within fp32
@@ -1381,7 +1385,7 @@ def test_wgrad_image_bands(gpu, case):
     d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd)
     lib = L.load()
     need = lib.rn_conv_wgrad_ws_bytes(C.byref(d))
-    assert need >= 64 * 576 * 4
+    assert need >= k * 9 * c * 4
     ws = torch.full((need // 4 + 4,), float("nan"), dtype=torch.float32, device=gpu)
     xd, dyd = to_nhwc(x, BF16, gpu), to_nhwc(dy, BF16, gpu)
     outs = []
@@ -1400,11 +1404,12 @@ def test_wgrad_image_bands(gpu, case):
     assert np.abs(outs[0] - outs[2]).max() <= 1e-5 * np.abs(dw_abs).max()
 
 
-@pytest.mark.parametrize("kc", [(256, 64), (64, 256), (64, 64)])
+@pytest.mark.parametrize("kc", [(256, 64), (64, 256), (64, 64), (128, 64), (64, 128), (128, 128), (128, 256),
+                                (256, 128)])
 @pytest.mark.parametrize("xf", [False, True], ids=["plain", "bnrelu_on_load"])
 def test_wgrad_stream_1x1(gpu, kc, xf):
-    """wgrad_stream_kernel (1x1 stride-1 weight gradients whose whole dW fits one workgroup: stage 1's
-    conv1 / conv3 / shortcut; rn_set_tuning 19 = 0): one streaming pass per workgroup over its M range,
+    """wgrad_stream_kernel (1x1 stride-1 weight gradients whose whole dW fits one workgroup, K x C <= 32768:
+    stage 1's conv1 / conv3 / shortcut; rn_set_tuning 19 = 0): one streaming pass per workgroup over its M range,
     the split partials through the slab. Plain and with the producing BatchNorm+ReLU applied to x on load
     (rn_conv_bwd_filter_x): against the fp64 oracle of the same (rounded) operands, bit-identical run to
     run, and equal to the tiled kernels (19 = 1) within fp32 summation-order rounding; a ragged M (the
@@ -1442,6 +1447,52 @@ def test_wgrad_stream_1x1(gpu, kc, xf):
         finally:
             L.call("rn_set_tuning", 19, 0)
         outs.append(dw.cpu().numpy().reshape(k, c, 1, 1).astype(np.float64))
+    assert np.array_equal(outs[0], outs[1])
+    cond = np.abs(outs[0] - dw_ref) / (dw_abs + 1e-30)
+    assert cond.max() < 2e-6, cond.max()
+    assert np.abs(outs[0] - outs[2]).max() <= 1e-5 * np.abs(dw_abs).max()
+
+
+@pytest.mark.parametrize("case", [
+    (3, 128, 9, 56, 128, 3, 1, 1, 32),   # ResNeXt stage 1: 4 channels per group, 56-wide rows
+    (2, 256, 7, 28, 256, 3, 1, 1, 32),   # stage 2: 8 per group, 28-wide rows (32-pixel image rows)
+    (4, 128, 5, 7, 128, 3, 1, 1, 32),    # short rows, several images
+    (3, 512, 7, 14, 512, 3, 1, 1, 32),   # stage 3: 16 per group, two channel slices, bands of two rows
+])
+def test_wgrad_grouped_image_bands(gpu, case):
+    """wgrad_gband_kernel (ResNeXt's grouped 3x3 stride-1 weight gradients, 4 / 8 / 16 channels per group;
+    rn_set_tuning 19 = 0): the whole block-diagonal dW per workgroup, one output row per band, the
+    group-diagonal parts of each 16 x 16 MFMA block kept. Against the fp64 oracle (2e-6 of the sum of
+    the terms' magnitudes per element), bit-identical run to run, and equal to the tiled grouped kernel
+    (19 = 1) within fp32 summation-order rounding."""
+    n, c, h, w, k, r, st, pd, g = case
+    rng = np.random.default_rng(12)
+    x = bf16_round(rng.standard_normal((n, c, h, w)))
+    dy = bf16_round(rng.standard_normal((n, k, h, w)))
+    w0 = np.zeros((k, c // g, r, r))
+    _, dw_ref = ops.conv2d_bwd(x, w0, dy, (st, st), (pd, pd), g)
+    dw_abs = ops.conv2d_bwd(np.abs(x), w0, np.abs(dy), (st, st), (pd, pd), g)[1]
+    d = L.ConvDesc(dtype=BF16, n=n, h=h, w=w, c=c, c_real=c, k=k, k_pad=k, r=r, s=r, stride_h=st, stride_w=st,
+                   pad_h=pd, pad_w=pd, groups=g)
+    L.call("rn_conv_desc_init", C.byref(d))
+    lib = L.load()
+    need = lib.rn_conv_wgrad_ws_bytes(C.byref(d))
+    assert need >= k * 9 * (c // g) * 4
+    ws = torch.full((need // 4 + 4,), float("nan"), dtype=torch.float32, device=gpu)
+    xd, dyd = to_nhwc(x, BF16, gpu), to_nhwc(dy, BF16, gpu)
+    outs = []
+    for band in (0, 0, 1):
+        L.call("rn_set_tuning", 19, band)
+        try:
+            dw = torch.zeros(k * r * r * (c // g), dtype=torch.float32, device=gpu)
+            if band == 0:
+                L.call("rn_conv_bwd_filter_ws", C.byref(d), p(xd), p(dyd), p(dw), p(ws), need, stream())
+            else:
+                L.call("rn_conv_bwd_filter", C.byref(d), p(xd), p(dyd), p(dw), stream())
+            torch.cuda.synchronize()
+        finally:
+            L.call("rn_set_tuning", 19, 0)
+        outs.append(dw.cpu().numpy().reshape(k, r, r, c // g).transpose(0, 3, 1, 2).astype(np.float64))
     assert np.array_equal(outs[0], outs[1])
     cond = np.abs(outs[0] - dw_ref) / (dw_abs + 1e-30)
     assert cond.max() < 2e-6, cond.max()

@@ -225,7 +225,7 @@ def _c4_layerwise(n, image):
     assert not ck.skipped, ck.skipped
     kinds = {r[0] for r in ck.rec}
     assert {"conv_fwd", "conv_fwd_grouped", "dgrad_grouped", "wgrad_grouped", "wgrad", "bn_apply_add",
-            "relu_bwd_bnred", "bn_fwd", "bn_bwd_dx", "bn_bwd_params", "weight_copy", "stem_dbeta"} <= kinds, kinds
+            "relu_bwd_bnred", "bn_fwd", "bn_bwd_dx", "bn_bwd_params", "weight_copy"} <= kinds, kinds
     assert sum(1 for r in ck.rec if r[0] == "conv_fwd_grouped") == 16
     assert sum(1 for r in ck.rec if r[0] in ("wgrad", "wgrad_grouped")) == 54  # 53 convs + fc1
     assert sum(1 for r in ck.rec if r[0] == "bn_apply_add") == 16
