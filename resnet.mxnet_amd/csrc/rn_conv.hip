@@ -70,6 +70,7 @@ struct IgemmArgs {
   int sched;           // igemm_big_kernel schedule experiments (rn_set_tuning 7, bit mask)
   int epi_sync;        // igemm_big_kernel: block barriers around the epilogue's LDS staging (rn_set_tuning 16)
   int nt_store;        // igemm_big_kernel: output stores with the nontemporal hint (rn_set_tuning 18 bit 16)
+  int prio;            // igemm_big_kernel 8-wave tiles: waves 4-7 at s_setprio 1 for the whole kernel (rn_set_tuning 20)
   int ntiles;          // igemm_big_kernel persistent mode: tiles per class (0: one tile per workgroup)
   int x_bytes, w_bytes;  // LDS-DMA buffer descriptors
   // dgrad only, nullable: the BatchNorm-backward reduction of the gradient this conv completes
@@ -773,17 +774,20 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
   constexpr int EP_WAVE = 64 * EP_LD;            // floats per wave per epilogue half
   constexpr int kEpChunks = NW * EP_WAVE / 4;
   static_assert(BN != 64 || !SC || EPI == 0, "the stem modes have no BatchNorm epilogue");
-  static_assert(!XF || (!SC && !Q8 && EPI != 2 && BN >= 128), "input transform: bf16 forward, 128/256 columns");
+  static_assert(!XF || (!SC && !Q8 && EPI != 2 && (BN >= 128 || XF == 2)), "input transform: bf16 forward");
   constexpr int kMain = NBUF * kStage > kEpChunks ? NBUF * kStage : kEpChunks;
-  constexpr int kXfChunks = XF ? 2 * XFC / 4 : 0;  // fp32 scale[XFC], shift[XFC]
+  constexpr int kXfChunks = XF == 1 ? 2 * XFC / 4 : 0;  // fp32 scale[XFC], shift[XFC] (XF 2: registers)
   __shared__ __attribute__((aligned(16))) uint4 smem[kMain + kXfChunks];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WAVES_N, wn = wid % WAVES_N;
   const IgemmCls& cl = p.cls[blockIdx.z];
+  // static priority for the second-dispatched half of an 8-wave workgroup (MI355X_MICROARCH.md, two
+  // waves per SIMD, item 4: the younger half loses every arbitration at equal priority)
+  if (NW == 8 && (p.prio & 1) && wid >= 4) __builtin_amdgcn_s_setprio(1);
   const int Mc = p.N * cl.Pc * cl.Qc;
   float* const xs = reinterpret_cast<float*>(smem + kMain);  // (XF) scale, then shift
-  if constexpr (XF) {
+  if constexpr (XF == 1) {
     for (int i = tid; i < p.C; i += NW * 64) {
       xs[i] = p.in_sc[i];
       xs[XFC + i] = p.in_sh[i];
@@ -905,7 +909,13 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
     d_toffb = ((cl.r0 + p.rstep * tr) * p.S + cl.s0 + p.sstep * ts) * p.cblk + cb * BKE;
     d_la = lds0 + buf * (kStage * 16);
   };
+  // the A rows past a 224-row tile's last (the 256-row A region's last 32 rows) are never read: a wave
+  // whose 8 rows of a DMA round lie there skips that piece (8-wave tiles: 4 of the K-tile's 64 pieces;
+  // at most one per wave and K-tile)
+  static_assert(BMA - BM <= RPR, "at most one skipped A piece per wave");
+  const bool skip_last = 8 * wid + RPR * (AR - 1) >= BM && !(p.prio & 2);  // (rn_set_tuning 20 bit 2: no skip)
   auto piece = [&](int k) __attribute__((always_inline)) {
+    if (k == AR - 1 && skip_last) return;
     if (k < AR) {
       const bool ok = W4 ? d_cok && a_h[k] >= 0
                          : d_cok && (unsigned)(a_h[k] + d_dh) < (unsigned)p.H && (unsigned)(a_w[k] + d_dw) < (unsigned)p.W;
@@ -993,14 +1003,32 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
     }
   };
 
+  // (XF 2: C = 64, one channel block: this thread's chunk is always channels lch * 8.., its scale / shift
+  // two registers each, no LDS table -- the 64-column tile keeps two workgroups per CU)
+  float xa[XF == 2 ? 8 : 1], xb[XF == 2 ? 8 : 1];
+  if constexpr (XF == 2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      xa[e] = p.in_sc[lch * CE + e];
+      xb[e] = p.in_sh[lch * CE + e];
+    }
+  }
   // (XF) this thread's landed A chunks of the K-tile in buffer buf, channel block cb, rewritten in place
   auto xform = [&](int buf, int cb) __attribute__((always_inline)) {
-    const int c0 = min(cb * BKE + lch * CE, p.C - CE);  // (clamped: a chunk past C was zero-filled)
     float a[8], b[8];
-    *reinterpret_cast<float4*>(a) = *reinterpret_cast<const float4*>(xs + c0);
-    *reinterpret_cast<float4*>(a + 4) = *reinterpret_cast<const float4*>(xs + c0 + 4);
-    *reinterpret_cast<float4*>(b) = *reinterpret_cast<const float4*>(xs + XFC + c0);
-    *reinterpret_cast<float4*>(b + 4) = *reinterpret_cast<const float4*>(xs + XFC + c0 + 4);
+    if constexpr (XF == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        a[e] = xa[e];
+        b[e] = xb[e];
+      }
+    } else {
+      const int c0 = min(cb * BKE + lch * CE, p.C - CE);  // (clamped: a chunk past C was zero-filled)
+      *reinterpret_cast<float4*>(a) = *reinterpret_cast<const float4*>(xs + c0);
+      *reinterpret_cast<float4*>(a + 4) = *reinterpret_cast<const float4*>(xs + c0 + 4);
+      *reinterpret_cast<float4*>(b) = *reinterpret_cast<const float4*>(xs + XFC + c0);
+      *reinterpret_cast<float4*>(b + 4) = *reinterpret_cast<const float4*>(xs + XFC + c0 + 4);
+    }
 #pragma unroll
     for (int k = 0; k < AR; ++k) {
       uint4* cp = smem + buf * kStage + k * (RPR * 8) + tid;
@@ -1031,8 +1059,12 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
     }
     // K-tile t has landed for this thread once at most the later K-tiles' DMAs are outstanding
     if (!(kRnDiag && (p.sched & 4))) {  // (diagnostic bit 4: no wait, no barrier -- wrong results)
-      if (NBUF == 3) wait_vmcnt<LPT>();
-      else wait_vmcnt<0>();
+      if (NBUF == 3) {
+        if (skip_last) wait_vmcnt<(LPT > 0 ? LPT - 1 : 0)>();  // (one piece fewer per K-tile)
+        else wait_vmcnt<LPT>();
+      } else {
+        wait_vmcnt<0>();
+      }
       if constexpr (XF) {
         xform(t % NBUF, xf_cb);
         if (++xf_cb == ncb) xf_cb = 0;
@@ -1864,6 +1896,8 @@ struct DbArgs {
   const bf16_t* x;   // [N][H][W][C]
   const bf16_t* dy;  // [N][H][W][K]
   float* slab;       // [split][K][9 * C]
+  const float* in_sc;  // (XF) the producing BatchNorm's scale / shift: x := relu(x * sc + sh) on load
+  const float* in_sh;
   int N, H, W, C, K, ipw;
 };
 template <int CS, int KS, int WP, int R>
@@ -1881,11 +1915,17 @@ struct DbShape {
   static_assert(CB_W * WC == CB && KB_W * WK == KB && CB_W * KB_W <= 2 && (R * WP) % 32 == 0 &&
                 XPPI >= 1 && DPPI >= 1 && (R * WP) % DPPI == 0, "dense band shape");
 };
-template <int CS, int KS, int WP, int R, int NBUF>
+// XF: the producing BatchNorm+ReLU (act2 = relu(bn2(conv1 out)), symbol/resnet.py:19-21) applied to
+// the staged x image in place -- each thread rewrites the chunks its own DMAs landed, between its
+// vmcnt wait and the band's barrier, max(x * sc + sh, 0) rounded to bf16 as bn_apply_kernel stores
+// it; the chunks the DMA zero-filled (padding columns, rows outside the image) stay zero, as the conv
+// pads the BN+ReLU output -- so act2 is never written (the forward applies it on load too).
+template <int CS, int KS, int WP, int R, int NBUF, int XF = 0>
 __global__ __launch_bounds__(512, 1) void wgrad_dband_kernel(DbArgs p) {
   using S = DbShape<CS, KS, WP, R>;
   constexpr int XCPR = S::XCPR, DCPR = S::DCPR, KB_W = S::KB_W, CB_W = S::CB_W;
   __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * S::BUF];
+  __shared__ __attribute__((aligned(16))) float xtab[XF ? 2 * CS : 1];  // (XF) scale, shift of the slice
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int n_first = blockIdx.x * p.ipw;
   const int n_end = min(p.N, n_first + p.ipw);
@@ -1894,6 +1934,13 @@ __global__ __launch_bounds__(512, 1) void wgrad_dband_kernel(DbArgs p) {
   const int c0 = blockIdx.y * CS, k0 = blockIdx.z * KS;  // the channel slices
   for (int i = tid; i < NBUF * 8 * XCPR; i += 512)
     smem[(i / (8 * XCPR)) * S::BUF + (R + 2) * WP * XCPR + i % (8 * XCPR)] = make_uint4(0, 0, 0, 0);
+  if constexpr (XF) {
+    for (int i = tid; i < CS; i += 512) {
+      xtab[i] = p.in_sc[c0 + i];
+      xtab[CS + i] = p.in_sh[c0 + i];
+    }
+  }
+  uint32_t okb = 0;  // (XF) bit buf * LPTM + j: x piece j of the band in buffer buf holds image data
   // this wave's DMA pieces: w, w + 8, ... (x pieces first, then dy); lane = (pixel, LDS chunk slot), the
   // source chunk is the slot XOR the image's read swizzle
   const int cnt = (S::INS - wid + 7) / 8;
@@ -1912,9 +1959,13 @@ __global__ __launch_bounds__(512, 1) void wgrad_dband_kernel(DbArgs p) {
   }
   const char* zb = reinterpret_cast<const char*>(&g_zero_chunk);
   const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  // band t's DMAs into buffer buf; past the last band (t >= nb) every lane reads the zero chunk, so each
+  // wave issues the same count per band and the counted waits below hold to the end
   auto issue = [&](int t, int buf) __attribute__((always_inline)) {
+    const bool live = t < nb;
     const int n = n_first + t / bpi, oh0 = R * (t % bpi);
     const uint32_t base = lds0 + buf * (S::BUF * 16);
+    if constexpr (XF) okb &= ~(((1u << S::LPTM) - 1u) << (buf * S::LPTM));
 #pragma unroll
     for (int j = 0; j < S::LPTM; ++j) {
       if (j >= cnt) break;  // (wave-uniform)
@@ -1922,11 +1973,12 @@ __global__ __launch_bounds__(512, 1) void wgrad_dband_kernel(DbArgs p) {
       bool ok;
       if (dr[j] >= 0) {
         const int ih = oh0 - 1 + dr[j], iw = dc[j] - 1;
-        ok = (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
+        ok = live && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W;
         src = p.x + ((int64_t)(n * p.H + ih) * p.W + iw) * p.C + dch[j];
+        if constexpr (XF) okb |= (uint32_t)ok << (buf * S::LPTM + j);
       } else {
         const int oh = oh0 - 1 - dr[j];
-        ok = oh < p.H && dc[j] < p.W;
+        ok = live && oh < p.H && dc[j] < p.W;
         src = p.dy + ((int64_t)(n * p.H + oh) * p.W + dc[j]) * p.K + dch[j];
       }
       dma16_global(ok ? (const void*)src : (const void*)zb, base + dla[j]);
@@ -1981,22 +2033,36 @@ __global__ __launch_bounds__(512, 1) void wgrad_dband_kernel(DbArgs p) {
             acc[i][j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfv[j][t], acc[i][j][t], 0, 0, 0);
     }
   };
-  __syncthreads();  // (the slack zeros)
+  __syncthreads();  // (the slack zeros, the XF table)
 #pragma unroll
-  for (int s = 0; s < NBUF - 1; ++s)
-    if (s < nb) issue(s, s);
+  for (int s = 0; s < NBUF - 1; ++s) issue(s, s);
   for (int t = 0; t < nb; ++t) {
-    // band t has landed once at most the DMAs of the band issued after it are outstanding
-    if (NBUF == 3 && t + 1 < nb) {
-      if (cnt == S::LPTM) wait_vmcnt<S::LPTM>();
-      else wait_vmcnt<S::LPTM - 1>();
-    } else {
-      wait_vmcnt<0>();
+    // band t has landed once at most the DMAs of the NBUF - 2 bands issued after it are outstanding
+    if (cnt == S::LPTM) wait_vmcnt<(NBUF - 2) * S::LPTM>();
+    else wait_vmcnt<(NBUF - 2) * (S::LPTM - 1)>();
+    if constexpr (XF) {  // this thread's landed x chunks of band t, transformed in place
+      const int buf = t % NBUF;
+#pragma unroll
+      for (int j = 0; j < S::LPTM; ++j) {
+        if (j >= cnt || dr[j] < 0) continue;  // (wave-uniform: the x pieces of this wave)
+        uint4* cp = smem + buf * S::BUF + (dla[j] >> 4) + lane;
+        const int cc = dch[j] - c0;
+        float f[8], a[8], b[8];
+        *reinterpret_cast<float4*>(a) = *reinterpret_cast<const float4*>(xtab + cc);
+        *reinterpret_cast<float4*>(a + 4) = *reinterpret_cast<const float4*>(xtab + cc + 4);
+        *reinterpret_cast<float4*>(b) = *reinterpret_cast<const float4*>(xtab + CS + cc);
+        *reinterpret_cast<float4*>(b + 4) = *reinterpret_cast<const float4*>(xtab + CS + cc + 4);
+        chunk_to_f(*cp, f, (const bf16_t*)nullptr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], a[e], b[e]), 0.f);
+        *cp = ((okb >> (buf * S::LPTM + j)) & 1u) ? f_to_chunk(f, (const bf16_t*)nullptr) : make_uint4(0, 0, 0, 0);
+      }
     }
     __syncthreads();  // ... for every wave; and every wave is done with the buffer refilled next
-    if (t + NBUF - 1 < nb) issue(t + NBUF - 1, (t + NBUF - 1) % NBUF);
+    issue(t + NBUF - 1, (t + NBUF - 1) % NBUF);
     compute(t % NBUF);
   }
+  wait_vmcnt<0>();  // (the zero-chunk DMAs past the last band land before the workgroup's LDS is released)
   // the workgroup's partial dW slice: slab[block][k][tap * C + c]
   float* dst = p.slab + (int64_t)blockIdx.x * p.K * 9 * p.C;
 #pragma unroll
@@ -3076,8 +3142,9 @@ int big_tile_cols(const IgemmArgs& a, int64_t xb, int64_t wb) {
   if (a.smallc)  // the stem (C = 8): the 256x64 tile in its small-C mode (rn_set_tuning 4 = 1 or 5: never)
     return (big != 1 && big != 5 && a.C == 8 && a.K <= 64 && !a.in_sc && !a.bias && !g_tune[RN_TUNE_DIAG_IGEMM_L1] &&
             xb < INT32_MAX && wb < INT32_MAX) ? 64 : 0;
-  // the BN+ReLU input transform (in_sc) runs on the 224-row 128/256-column tiles only
-  const bool xf_ok = !a.in_sc || (a.C <= kXfMaxC && a.K > 64 && g_tune[RN_TUNE_IGEMM_ROWS] != 1);
+  // the BN+ReLU input transform (in_sc) runs on the 224-row 128/256-column tiles, and on the 64-column
+  // tile when C = 64 (its scale / shift in registers)
+  const bool xf_ok = !a.in_sc || (a.K > 64 ? a.C <= kXfMaxC && g_tune[RN_TUNE_IGEMM_ROWS] != 1 : a.C == 64 && a.cblk == 64);
   const bool eligible = big != 1 && xf_ok && a.gred == 0 && !g_tune[RN_TUNE_DIAG_IGEMM_L1] &&
                         !a.bias && xb < INT32_MAX && wb < INT32_MAX && max_taps <= 32;
   if (!eligible) return 0;
@@ -3118,6 +3185,7 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   b.sched = g_tune[RN_TUNE_IGEMM_SCHED];
   b.epi_sync = g_tune[RN_TUNE_EPI_SYNC];
   b.nt_store = (g_tune[RN_TUNE_BN_NT] & 16) != 0;
+  b.prio = g_tune[RN_TUNE_IGEMM_PRIO];
   const int64_t xb = (int64_t)a.N * a.H * a.W * a.C * (int64_t)sizeof(T);
   const int64_t wb = (int64_t)a.K * a.wrow * (int64_t)sizeof(T);
   b.x_bytes = (int)std::min<int64_t>(xb, INT32_MAX);
@@ -3148,6 +3216,10 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
       dim3 grid((unsigned)(ceil_div(maxMc, 256) * b.ntn), 1, a.ncls);
       persist(grid);
       if (a.smallc) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, 1>), grid, dim3(256), 0, st, b);
+      else if (epi == 1 && a.in_sc)  // (big_tile_cols: C = 64)
+        hipLaunchKernelGGL((igemm_big_kernel<64, 2, 1, true, 256, 0, 0, 2>), grid, dim3(256), 0, st, b);
+      else if (epi == 0 && a.in_sc)
+        hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, 0, 0, 2>), grid, dim3(256), 0, st, b);
       else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 1, true>), grid, dim3(256), 0, st, b);
       else if (epi == 2) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 2, true>), grid, dim3(256), 0, st, b);
       else if (epi == 4) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 4, true>), grid, dim3(256), 0, st, b);
@@ -3608,7 +3680,10 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
   const bool xf_big = !in_scale || (d->r == 1 && d->s == 1 && d->pad_h == 0 && d->pad_w == 0);
   // deterministic mode (rn_set_tuning 17): slabs for every kernel and dtype, never atomics
   const bool det = g_tune[RN_TUNE_DETERMINISTIC] == 1;
-  const bool slab_ok = det || (d->dtype == RN_BF16 && !grouped && xf_big && d->c_real == d->c);
+  // (the band kernels apply a 3x3 input transform too, with their slab)
+  const bool band_xf = in_scale && d->r == 3 && d->s == 3 && d->pad_h == 1 && d->pad_w == 1 && d->stride_h == 1 &&
+                       d->stride_w == 1;
+  const bool slab_ok = det || (d->dtype == RN_BF16 && !grouped && (xf_big || band_xf) && d->c_real == d->c);
   if (det) a.gspread = 0;  // (grouped: each diagonal block on one wave, so one writer per element)
   auto finish = [&](int64_t split, const char* what) -> int {
     const int64_t need = slab_ok ? split * a.K * (int64_t)a.ldw * 4 : 0;
@@ -3636,11 +3711,12 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
   // kernels below). Needs the slab workspace.
   const int db = (d->c == 64 && d->w <= 62) ? 1 : (d->c == 128 && d->w <= 30) ? 2 :
                  ((d->c == 256 || d->c == 512) && d->w <= 14) ? 3 : 0;
-  if (d->dtype == RN_BF16 && !grouped && !in_scale && db && d->r == 3 && d->s == 3 && d->stride_h == 1 &&
+  if (d->dtype == RN_BF16 && !grouped && db && d->r == 3 && d->s == 3 && d->stride_h == 1 &&
       d->stride_w == 1 && d->pad_h == 1 && d->pad_w == 1 && d->c_real == d->c && d->k == d->c &&
       d->k_pad == d->k && g_tune[RN_TUNE_WGRAD_BAND] != 1 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX) {
     DbArgs g{};
     g.x = (const bf16_t*)x; g.dy = (const bf16_t*)dy; g.N = d->n; g.H = d->h; g.W = d->w; g.C = d->c; g.K = d->k;
+    g.in_sc = in_scale; g.in_sh = in_shift;
     const int cs = db == 1 ? 64 : 128, ks = db == 1 ? 64 : 32;
     const int slices = (d->c / cs) * (d->k / ks);
     const int64_t want = std::max<int64_t>(1, chip_cus() / slices);  // (the slab stays ~ CUs x slice)
@@ -3651,9 +3727,16 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
       if (!use_slab(split)) return -1;
       g.slab = a.slab;
       const dim3 grid((unsigned)split, d->c / cs, d->k / ks);
-      if (db == 1) hipLaunchKernelGGL((wgrad_dband_kernel<64, 64, 64, 2, 3>), grid, dim3(512), 0, st, g);
-      else if (db == 2) hipLaunchKernelGGL((wgrad_dband_kernel<128, 32, 32, 1, 3>), grid, dim3(512), 0, st, g);
-      else hipLaunchKernelGGL((wgrad_dband_kernel<128, 32, 16, 2, 3>), grid, dim3(512), 0, st, g);
+#define RN_DBAND(XFV)                                                                                            \
+  if (db == 1) hipLaunchKernelGGL((wgrad_dband_kernel<64, 64, 64, 2, 3, XFV>), grid, dim3(512), 0, st, g);     \
+  else if (db == 2) hipLaunchKernelGGL((wgrad_dband_kernel<128, 32, 32, 1, 5, XFV>), grid, dim3(512), 0, st, g); \
+  else hipLaunchKernelGGL((wgrad_dband_kernel<128, 32, 16, 2, 6, XFV>), grid, dim3(512), 0, st, g);
+      if (in_scale) {
+        RN_DBAND(1)
+      } else {
+        RN_DBAND(0)
+      }
+#undef RN_DBAND
       return finish(split, "wgrad_dband");
     }
   }

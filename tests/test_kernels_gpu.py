@@ -805,7 +805,11 @@ def test_conv_bnrelu_on_load(gpu, dtype, case):
 
 @pytest.mark.parametrize("case", [(4, 256, 28, 28, 512, 1, 1, 0), (4, 256, 28, 28, 128, 1, 2, 0),
                                   (2, 1024, 14, 14, 256, 1, 1, 0), (2, 2048, 7, 7, 512, 1, 1, 0),
-                                  (3, 64, 20, 20, 256, 3, 1, 1), (2, 200, 9, 11, 136, 1, 1, 0)])
+                                  (3, 64, 20, 20, 256, 3, 1, 1), (2, 200, 9, 11, 136, 1, 1, 0),
+                                  # act2 -> conv2 (3x3 stride 1, C = K): the 64-column tile's register table,
+                                  # the 224-row tiles, the image-band weight gradients' in-place transform
+                                  (3, 64, 20, 20, 64, 3, 1, 1), (4, 128, 14, 14, 128, 3, 1, 1),
+                                  (3, 256, 9, 9, 256, 3, 1, 1), (2, 512, 7, 7, 512, 3, 1, 1)])
 @pytest.mark.parametrize("ws", [False, True], ids=["atomic", "slab"])
 def test_conv_bnrelu_on_load_tiles(gpu, case, ws, big_tiles, tile_variant):
     """BN+ReLU applied on load by the LDS-DMA tiles (igemm_big_kernel XF: the landed A chunks rewritten
@@ -845,7 +849,8 @@ def test_conv_bnrelu_on_load_tiles(gpu, case, ws, big_tiles, tile_variant):
     torch.cuda.synchronize()
     if tile_variant[0] == 0 and not (big_tiles == "w4" and c > 512):  # the same tile both ways (else the transform
         assert torch.equal(y.view(torch.int16), y0.view(torch.int16))  # falls back to another tile)
-    if r == 1 and wsb > 0:  # the slab path is deterministic; atomics / the 3x3 fallback kernel are not
+    band = r == 3 and st == 1 and c == k  # (the image-band weight gradient, slab and in-place transform)
+    if (r == 1 or band) and wsb > 0:  # the slab path is deterministic; atomics / the 3x3 fallback kernel are not
         assert torch.equal(dw, dw0)
     else:
         assert rel_err(dw.cpu().numpy(), dw0.cpu().numpy()) < 1e-5
