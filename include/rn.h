@@ -556,7 +556,8 @@ const char* rn_last_error(void);
  *      slab workspace, rn_conv_wgrad_ws_bytes): the image-band kernels of the 3x3 stride-1 pad-1
  *      convolutions -- dense with C = K in {64, 128, 256, 512}, and grouped (32 groups) with 4 / 8 / 16
  *      channels per group -- and the streaming kernel of the 1x1 stride-1 ones with K, C in
- *      {64, 128, 256} and K x C <= 32768: 0 = on (default), 1 = the tiled kernels,
+ *      {64, 128, 256} and K x C <= 32768: 0 = on (default; the dense band kernel for C = 64 only),
+ *      1 = the tiled kernels, 2 = on, the dense band kernel for C = 128..512 too (measured slower),
  * 20 = conv tile schedule A/B bits: 1 = static priority of the 8-wave tiles' second half (waves 4-7 at
  *      s_setprio 1 for the whole kernel; default off), 2 = the 224-row tiles issue the DMAs of the A
  *      rows past the tile too (default: skipped, those rows are never read). */

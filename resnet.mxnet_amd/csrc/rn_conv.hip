@@ -3709,8 +3709,11 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
   // dense 3x3 / stride 1 / pad 1 with C = K in {64, 128, 256, 512} (every bottleneck conv2 but a stage's
   // first): image bands, dW slices per workgroup (wgrad_dband_kernel; rn_set_tuning 19 = 1: the tiled
   // kernels below). Needs the slab workspace.
-  const int db = (d->c == 64 && d->w <= 62) ? 1 : (d->c == 128 && d->w <= 30) ? 2 :
-                 ((d->c == 256 || d->c == 512) && d->w <= 14) ? 3 : 0;
+  // (measured in isolation, tools/conv_bench.py: stage 1 89 vs 156 us on the tiled kernel; the 128 / 256 /
+  // 512-channel forms lost to the 256-column tiled kernels -- 123 vs 106, 109 vs 76, 230 vs 80 us -- so
+  // rn_set_tuning 19 = 2 is needed to run them)
+  const int db = (d->c == 64 && d->w <= 62) ? 1 : g_tune[RN_TUNE_WGRAD_BAND] != 2 ? 0 :
+                 (d->c == 128 && d->w <= 30) ? 2 : ((d->c == 256 || d->c == 512) && d->w <= 14) ? 3 : 0;
   if (d->dtype == RN_BF16 && !grouped && db && d->r == 3 && d->s == 3 && d->stride_h == 1 &&
       d->stride_w == 1 && d->pad_h == 1 && d->pad_w == 1 && d->c_real == d->c && d->k == d->c &&
       d->k_pad == d->k && g_tune[RN_TUNE_WGRAD_BAND] != 1 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX) {

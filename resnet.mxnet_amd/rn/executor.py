@@ -352,10 +352,11 @@ class Plan:
         # 22.17 ms per step on one box; RN_BN_APPLY_FUSION=0 writes act1 / act3
         if os.environ.get("RN_BN_APPLY_FUSION", "1") != "1":
             return
-        # the 3x3 stride-1 consumers too (act2 -> conv2 of units >= 2, symbol/resnet.py:19-21): their
-        # forward tiles apply it on load (the 224-row tiles, or the 64-column tile at C = 64) and their
-        # weight gradient is the image-band kernel, which transforms its staged x images in place (bf16;
-        # C = K in 64..512 at the widths the band images hold). RN_BN_APPLY_FUSION_3X3=0: act2 written.
+        # the 3x3 stride-1 consumers too (act2 -> conv2, symbol/resnet.py:19-21) where the weight gradient
+        # is the image-band kernel (stage 1: C = K = 64), which transforms its staged x images in place;
+        # the forward's 64-column tile applies it on load from a register table (bf16).
+        # RN_BN_APPLY_FUSION_3X3=0: act2 written. (Stages 2-4, on the 224-row tiles' per-K-tile transform
+        # and the band weight gradients, measured 4 % slower per step.)
         band3 = self.dtype == BF16 and os.environ.get("RN_BN_APPLY_FUSION_3X3", "1") == "1"
 
         def xf_ok(u):
@@ -365,8 +366,7 @@ class Plan:
                 return True
             c, k, w = u.x.c, u.y.c, u.x.w
             return (band3 and tuple(u.kernel) == (3, 3) and tuple(u.stride) == (1, 1) and tuple(u.pad) == (1, 1)
-                    and c == k and u.x.cp == c and u.y.cp == k and
-                    ((c == 64 and w <= 62) or (c == 128 and w <= 30) or (c in (256, 512) and w <= 14)))
+                    and c == k and u.x.cp == c and u.y.cp == k and c == 64 and w <= 62)
         for bn in self.ops:
             if bn.kind != "bn" or not bn.relu or id(bn.y) in out_ids:
                 continue

@@ -1374,7 +1374,8 @@ def _zero_block_skip(gpu, n, c, h, w, k, r, st, pd, g):
     (5, 512, 7, 7, 512, 3, 1, 1),    # stage 4: 4 x 16 slices, odd rows
 ])
 def test_wgrad_image_bands(gpu, case):
-    """wgrad_dband_kernel (dense 3x3 stride-1 weight gradients with C = K, rn_set_tuning 19 = 0): dW
+    """wgrad_dband_kernel (dense 3x3 stride-1 weight gradients with C = K; rn_set_tuning 19 = 2 runs it at
+    every C, the default at C = 64 only): dW
     slices per workgroup over bands of output rows, every tap a shifted read of one staged x image.
     Against the fp64 oracle (the sums of products of bf16 values, fp32 accumulation: 2e-6 of the sum of
     the terms' magnitudes per element), bit-identical run to run (one writer per slab element, the
@@ -1389,16 +1390,19 @@ def test_wgrad_image_bands(gpu, case):
     dw_abs = ops.conv2d_bwd(np.abs(x), np.zeros((k, c, r, r)), np.abs(dy), (st, st), (pd, pd))[1]
     d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd)
     lib = L.load()
+    L.call("rn_set_tuning", 19, 2)
     need = lib.rn_conv_wgrad_ws_bytes(C.byref(d))
-    assert need >= k * 9 * c * 4
+    L.call("rn_set_tuning", 19, 0)
     ws = torch.full((need // 4 + 4,), float("nan"), dtype=torch.float32, device=gpu)
     xd, dyd = to_nhwc(x, BF16, gpu), to_nhwc(dy, BF16, gpu)
     outs = []
-    for band in (0, 0, 1):
+    assert need >= k * 9 * c * 4
+    for band in (2, 2, 1):  # (2: the band kernel at every C, 1: the tiled kernels)
         L.call("rn_set_tuning", 19, band)
         try:
             dw = torch.zeros(k * r * r * c, dtype=torch.float32, device=gpu)
-            L.call("rn_conv_bwd_filter_ws", C.byref(d), p(xd), p(dyd), p(dw), p(ws), need, stream())
+            # (the buffer's own size: the tiled kernels fall back to atomics when their slab needs more)
+            L.call("rn_conv_bwd_filter_ws", C.byref(d), p(xd), p(dyd), p(dw), p(ws), ws.numel() * 4, stream())
             torch.cuda.synchronize()
         finally:
             L.call("rn_set_tuning", 19, 0)
