@@ -355,9 +355,10 @@ class Plan:
         # the 3x3 stride-1 consumers too (act2 -> conv2, symbol/resnet.py:19-21) where the weight gradient
         # is the image-band kernel (stage 1: C = K = 64), which transforms its staged x images in place;
         # the forward's 64-column tile applies it on load from a register table (bf16).
-        # RN_BN_APPLY_FUSION_3X3=0: act2 written. (Stages 2-4, on the 224-row tiles' per-K-tile transform
-        # and the band weight gradients, measured 4 % slower per step.)
-        band3 = self.dtype == BF16 and os.environ.get("RN_BN_APPLY_FUSION_3X3", "1") == "1"
+        # Opt-in (RN_BN_APPLY_FUSION_3X3=1): measured 0.6 % slower per step (two alternating pairs, r04d:
+        # the per-K-tile transform of the 3x3 forward costs more than the act2 pass it saves); stages 2-4
+        # too, on the 224-row tiles and the band weight gradients, 4 % slower (r04c).
+        band3 = self.dtype == BF16 and os.environ.get("RN_BN_APPLY_FUSION_3X3", "0") == "1"
 
         def xf_ok(u):
             if u.groups != 1 or getattr(u, "qweight", None):

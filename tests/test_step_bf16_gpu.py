@@ -262,6 +262,21 @@ def _c5_layerwise(n, image):
     assert not bad, bad[:10]
 
 
+def test_resnet50_bf16_layerwise_act2_on_load(gpu, monkeypatch):
+    """The opt-in act2 fusion (RN_BN_APPLY_FUSION_3X3=1: stage 1's bn2+ReLU applied on load by conv2's
+    64-column forward tile and its image-band weight gradient, act2 never written), per kernel at 8 images
+    of 112x112 with the C2 bars."""
+    from rn import graphs
+    monkeypatch.setenv("RN_BN_APPLY_FUSION_3X3", "1")
+    ck = _layerwise(graphs.resnet50(), 8, 112, "bfloat16")
+    assert not ck.skipped, ck.skipped
+    fused = [op for op in ck.ex.plan.ops if op.kind == "bn" and op.name.startswith("stage1") and op.name.endswith("bn2")]
+    assert fused and all(op.apply_fused for op in fused)
+    assert ck.covered.get("rn_conv_bwd_filter_x", 0) >= 3 + 36  # the three fused conv2 weight gradients too
+    bad = ck.failures()
+    assert not bad, bad[:10]
+
+
 def test_resnext50_bf16_layerwise_small(gpu):
     """The C4 per-kernel checks at 8 images of 64x64 (a fast first gate before the full size)."""
     _c4_layerwise(8, 64)
