@@ -467,7 +467,8 @@ int rn_quant_int8_fwd_codes(int32_t dtype, int64_t n, const void* x, void* out, 
  * y = [relu](x*scale + shift) (d->relu) rounded to d->dtype as rn_bn_apply stores it, then
  * rn_quant_int8_fwd_codes(y) with is_weight = 0 -- bit-identical to that pair, but y is never
  * written nor re-read. scale / shift from rn_bn_fwd_train[_part] / rn_bn_fwd_infer with y = NULL;
- * d->c a multiple of 16; out and codes required. */
+ * d->c a multiple of 16; codes required, out nullable (codes only: the values are expanded where
+ * they are read, by rn_quant_int8_expand -- the int8 graph's weight gradients). */
 int rn_quant_int8_fwd_codes_bn(const rn_bn_desc* d, const void* x, const float* scale, const float* shift,
                                void* out, void* codes, float* unit, float* minmax, int32_t is_train,
                                float ema_decay, int32_t first_batch, int32_t nbits, float* ws,
@@ -479,6 +480,13 @@ int rn_quant_int8_fwd_codes_bn2(const rn_bn_desc* d, const void* x, const float*
                                 int32_t nbits, void* out2, void* codes2, float* unit2, float* minmax2,
                                 float ema_decay2, int32_t nbits2, int32_t is_train, int32_t first_batch,
                                 float* ws, rn_stream_t stream);
+/* out[i] = codes[i] * unit[0] rounded to dtype: the fake-quantized values of an activation quantizer
+ * from its int8 codes and unit (rn_quant_int8_fwd_codes*), bit-identical to the out those calls write.
+ * The int8 graph defers them to the weight-gradient stream, just before the weight gradient that
+ * reads them (the forward writes 1 byte per element instead of 3). n a multiple of 16; codes / out
+ * 16-byte aligned. */
+int rn_quant_int8_expand(int32_t dtype, int64_t n, const void* codes, const float* unit, void* out,
+                         rn_stream_t stream);
 /* One weight of rn_weight_quant_pack: the fp32 master (KRSC, c_real channels) of a Quantization_int8
  * weight (int8_api.py:131-132, per-tensor threshold t = max|w|) and the copies written from it. */
 typedef struct rn_wquant_item {

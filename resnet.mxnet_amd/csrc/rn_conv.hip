@@ -2497,18 +2497,95 @@ struct GdArgs {
   int H, W, C, P, Q, pad, lcpr, qb;  // input H x W, output P x Q, C channels (= 8 << lcpr), qb = ceil(Q / PL)
   uint32_t items;                    // N * P * qb pixel-lane work items
   FastDiv fdQB, fdP;
+  // data gradient (RED), nullable: the BatchNorm-backward reduction of the gradient this layer completes,
+  // as igemm_big_kernel's EPI 2 computes it (sum dz, sum dz*(x - mean), dz = dx * relu'(x sc + sh) on the
+  // stored dx) -> bnred[block][C][2], one partial per workgroup
+  float* bnred;
+  const bf16_t* bn_x;
+  const float *bn_mean, *bn_sc, *bn_sh;
+  int bn_relu;
 };
-template <int G, int ST, int PL>
+constexpr int kGdRedMaxC = 512;  // (gd_direct_shape: C / 8 divides 64)
+
+// RED: one lane's stored output chunk into its BatchNorm-backward sums (channels chunk*8 .. +7). The
+// per-channel mean / scale / shift sit in an LDS table (tab[3][C], loaded before the kernel's first
+// barrier), not in registers: the direct kernels are latency bound and the 24 registers cost a wave
+// per SIMD
+struct GdRed {
+  float s1[8], s2[8];
+  __device__ __forceinline__ static void load_tab(const GdArgs& a, float* tab) {
+    for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+      tab[c] = a.bn_mean[c];
+      tab[kGdRedMaxC + c] = a.bn_sc[c];
+      tab[2 * kGdRedMaxC + c] = a.bn_sh[c];
+    }
+  }
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+  }
+  __device__ __forceinline__ void add(const GdArgs& a, const float* tab, int chunk, const uint4& out, int64_t off) {
+    float g[8], xv[8], mu[8], sc[8], sh[8];
+    chunk_to_f(out, g, (const bf16_t*)nullptr);
+    chunk_to_f(*reinterpret_cast<const uint4*>(a.bn_x + off), xv, (const bf16_t*)nullptr);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      *reinterpret_cast<float4*>(mu + 4 * h) = reinterpret_cast<const float4*>(tab + chunk * 8)[h];
+      *reinterpret_cast<float4*>(sc + 4 * h) = reinterpret_cast<const float4*>(tab + kGdRedMaxC + chunk * 8)[h];
+      *reinterpret_cast<float4*>(sh + 4 * h) = reinterpret_cast<const float4*>(tab + 2 * kGdRedMaxC + chunk * 8)[h];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float dz = (!a.bn_relu || fmaf(xv[e], sc[e], sh[e]) > 0.f) ? g[e] : 0.f;
+      s1[e] += dz;
+      s2[e] = fmaf(dz, xv[e] - mu[e], s2[e]);
+    }
+  }
+  // lanes of one chunk (lane & (cpr - 1)) across the wave, then the block's waves through LDS, in a
+  // fixed order: bnred[blockIdx.x][c][2]
+  __device__ __forceinline__ void finish(const GdArgs& a, int chunk) {
+    __shared__ float red[4][2][kGdRedMaxC];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int o = 1 << a.lcpr; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += __shfl_xor(s1[e], o, 64);
+        s2[e] += __shfl_xor(s2[e], o, 64);
+      }
+    if (lane < (1 << a.lcpr))
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[wid][0][chunk * 8 + e] = s1[e];
+        red[wid][1][chunk * 8 + e] = s2[e];
+      }
+    __syncthreads();
+    for (int c = threadIdx.x; c < a.C; c += blockDim.x) {
+      float t1 = 0.f, t2 = 0.f;
+      for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        t1 += red[w][0][c];
+        t2 += red[w][1][c];
+      }
+      float* dst = a.bnred + ((int64_t)blockIdx.x * a.C + c) * 2;
+      dst[0] = t1;
+      dst[1] = t2;
+    }
+  }
+};
+template <int G, int ST, int PL, bool RED = false>
 __global__ __launch_bounds__(256) void grouped_direct_kernel(GdArgs a) {
   extern __shared__ uint4 gd_w[];
+  __shared__ __attribute__((aligned(16))) float gd_tab[RED ? 3 * kGdRedMaxC : 4];
   const int nw16 = a.C * 9 * G * 2 / 16;
   for (int i = threadIdx.x; i < nw16; i += blockDim.x) gd_w[i] = reinterpret_cast<const uint4*>(a.w)[i];
+  if constexpr (RED) GdRed::load_tab(a, gd_tab);
   __syncthreads();
   constexpr int NC = (PL - 1) * ST + 3;
   const int lane = threadIdx.x & 63;
   const int chunk = lane & ((1 << a.lcpr) - 1), pl = lane >> a.lcpr;
   const int plw = 64 >> a.lcpr;
   const uint4* wc = gd_w + chunk * 9 * G;
+  GdRed rd;
+  if constexpr (RED) rd.init();
   const uint32_t step = gridDim.x * (blockDim.x >> 6) * plw;
   const int64_t cstep = a.C;
   for (uint32_t it = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * plw + pl; it < a.items; it += step) {
@@ -2569,26 +2646,33 @@ __global__ __launch_bounds__(256) void grouped_direct_kernel(GdArgs a) {
 #pragma unroll
         for (int o = 0; o < 8; ++o) acc[j][o] += f[o];
       }
-      *reinterpret_cast<uint4*>(a.y + off) = f_to_chunk(acc[j], (const bf16_t*)nullptr);
+      const uint4 out = f_to_chunk(acc[j], (const bf16_t*)nullptr);
+      *reinterpret_cast<uint4*>(a.y + off) = out;
+      if constexpr (RED) rd.add(a, gd_tab, chunk, out, off);
     }
   }
+  if constexpr (RED) rd.finish(a, chunk);
 }
 // The data gradient of a STRIDE-2 direct grouped layer (3x3, pad 1): dx[h][w] = sum over the taps
 // with (h + 1 - r) and (w + 1 - s) even of dy[(h + 1 - r) / 2][(w + 1 - s) / 2] * w[tap] -- an even
 // output row takes tap row 1, an odd one rows 0 and 2; likewise columns, so a pixel lane's PL output
 // pixels (from an even w0) read the PL/2 + 1 dy columns w0/2 .. w0/2 + PL/2 of each tap row. Same
 // compact copy as the stride-1 data gradient (mode 1: tap 8 - t holds tap t), same lane layout.
-template <int G, int PL>
+template <int G, int PL, bool RED = false>
 __global__ __launch_bounds__(256) void grouped_dgrad_s2_kernel(GdArgs a) {
   extern __shared__ uint4 gd_w[];
+  __shared__ __attribute__((aligned(16))) float gd_tab[RED ? 3 * kGdRedMaxC : 4];
   const int nw16 = a.C * 9 * G * 2 / 16;
   for (int i = threadIdx.x; i < nw16; i += blockDim.x) gd_w[i] = reinterpret_cast<const uint4*>(a.w)[i];
+  if constexpr (RED) GdRed::load_tab(a, gd_tab);
   __syncthreads();
   constexpr int ND = PL / 2 + 1;  // dy columns per tap row
   const int lane = threadIdx.x & 63;
   const int chunk = lane & ((1 << a.lcpr) - 1), pl = lane >> a.lcpr;
   const int plw = 64 >> a.lcpr;
   const uint4* wc = gd_w + chunk * 9 * G;
+  GdRed rd;
+  if constexpr (RED) rd.init();
   const uint32_t step = gridDim.x * (blockDim.x >> 6) * plw;
   const int64_t cstep = a.C;
   for (uint32_t it = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * plw + pl; it < a.items; it += step) {
@@ -2648,9 +2732,12 @@ __global__ __launch_bounds__(256) void grouped_dgrad_s2_kernel(GdArgs a) {
 #pragma unroll
         for (int o = 0; o < 8; ++o) acc[j][o] += f[o];
       }
-      *reinterpret_cast<uint4*>(a.y + off) = f_to_chunk(acc[j], (const bf16_t*)nullptr);
+      const uint4 out = f_to_chunk(acc[j], (const bf16_t*)nullptr);
+      *reinterpret_cast<uint4*>(a.y + off) = out;
+      if constexpr (RED) rd.add(a, gd_tab, chunk, out, off);
     }
   }
+  if constexpr (RED) rd.finish(a, chunk);
 }
 
 // compact compute copies of a direct grouped convolution (9 taps, G = cpg = kpg channels per group):
@@ -3135,9 +3222,11 @@ int big_tile_cols(const IgemmArgs& a, int64_t xb, int64_t wb) {
   int max_taps = 0;
   for (int z = 0; z < a.ncls; ++z) max_taps = std::max(max_taps, a.cls[z].nr * a.cls[z].ns);
   if (a.gred > 0) {  // grouped (ResNeXt): the 256x64 tile over one RN_GROUP_BLOCK column block, deep reductions
+    // (rn_set_tuning 13 = 2: also the stride-2 data gradients, whose parity classes have <= 4 taps)
     const int nst = max_taps * (int)ceil_div(a.cblk, 64);
+    const int min_nst = g_tune[RN_TUNE_IGEMM_GD] == 2 ? 4 : 8;
     return (big != 1 && big != 5 && RN_GROUP_BLOCK == 64 && !a.in_sc && !a.bias && !g_tune[RN_TUNE_DIAG_IGEMM_L1] &&
-            xb < INT32_MAX && wb < INT32_MAX && max_taps <= 32 && nst >= 8) ? 64 : 0;
+            xb < INT32_MAX && wb < INT32_MAX && max_taps <= 32 && nst >= min_nst) ? 64 : 0;
   }
   if (a.smallc)  // the stem (C = 8): the 256x64 tile in its small-C mode (rn_set_tuning 4 = 1 or 5: never)
     return (big != 1 && big != 5 && a.C == 8 && a.K <= 64 && !a.in_sc && !a.bias && !g_tune[RN_TUNE_DIAG_IGEMM_L1] &&
@@ -3215,15 +3304,22 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
       if (a.bnred) b.mt_max = (int)ceil_div(maxMc, 64);  // BN partials per 64-row wave row
       dim3 grid((unsigned)(ceil_div(maxMc, 256) * b.ntn), 1, a.ncls);
       persist(grid);
+      // block-diagonal grouped tile (GD: the MFMAs of off-diagonal k-steps skipped)
+      const bool gd = m32 && a.gred > 0 && a.gcol == a.gred && a.gcol <= 32 && a.cblk == 64 &&
+                      g_tune[RN_TUNE_IGEMM_GD] != 1;
       if (a.smallc) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, 1>), grid, dim3(256), 0, st, b);
       else if (epi == 1 && a.in_sc)  // (big_tile_cols: C = 64)
         hipLaunchKernelGGL((igemm_big_kernel<64, 2, 1, true, 256, 0, 0, 2>), grid, dim3(256), 0, st, b);
       else if (epi == 0 && a.in_sc)
         hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, 0, 0, 2>), grid, dim3(256), 0, st, b);
+      else if (epi == 1 && gd)
+        hipLaunchKernelGGL((igemm_big_kernel<64, 2, 1, true, 256, 0, 0, 0, 0, 1>), grid, dim3(256), 0, st, b);
+      else if (epi == 2 && gd)
+        hipLaunchKernelGGL((igemm_big_kernel<64, 2, 2, true, 256, 0, 0, 0, 0, 1>), grid, dim3(256), 0, st, b);
       else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 1, true>), grid, dim3(256), 0, st, b);
       else if (epi == 2) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 2, true>), grid, dim3(256), 0, st, b);
       else if (epi == 4) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 4, true>), grid, dim3(256), 0, st, b);
-      else if (m32 && a.gred > 0 && a.gcol == a.gred && a.gcol <= 32 && a.cblk == 64 && g_tune[RN_TUNE_IGEMM_GD] != 1)
+      else if (gd)
         hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true, 256, 0, 0, 0, 0, 1>), grid, dim3(256), 0, st, b);
       else if (m32) hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, true>), grid, dim3(256), 0, st, b);
       else hipLaunchKernelGGL((igemm_big_kernel<64, 2, 0, false>), grid, dim3(256), 0, st, b);
@@ -3408,10 +3504,9 @@ bool gd_direct_ok(const rn_conv_desc* d, int mode) {
   return d && d->grouped_direct == 1 && gd_direct_shape(d, mode);
 }
 
-int gd_launch(const rn_conv_desc* d, int mode, const void* x, const void* w, void* y, const void* add,
-              hipStream_t st) {
-  GdArgs a{};
-  a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.y = (bf16_t*)y; a.add = (const bf16_t*)add;
+// geometry of a direct grouped launch (mode 0 forward, 1 data gradient): fills a's shape fields,
+// returns the workgroups (also the BatchNorm-reduction partials of a RED data gradient)
+int gd_geometry(const rn_conv_desc* d, int mode, GdArgs& a) {
   a.C = d->c;
   if (mode == 0) { a.H = d->h; a.W = d->w; a.P = d->p; a.Q = d->q; a.pad = d->pad_h; }
   else { a.H = d->p; a.W = d->q; a.P = d->h; a.Q = d->w; a.pad = d->r - 1 - d->pad_h; }
@@ -3424,19 +3519,36 @@ int gd_launch(const rn_conv_desc* d, int mode, const void* x, const void* w, voi
   const int PL = s2t ? 8 : cpg == 4 && stride == 1 ? 8 : 4;
   a.qb = (a.Q + PL - 1) / PL;
   const int64_t items = (int64_t)d->n * a.P * a.qb;
-  RN_CHECK_ARG(items < INT32_MAX && (int64_t)d->n * a.H * a.W * a.C < INT32_MAX, "grouped direct: tensor too large");
-  a.items = (uint32_t)items;
-  a.fdQB = make_fastdiv(a.qb); a.fdP = make_fastdiv(a.P);
+  a.items = (uint32_t)std::min<int64_t>(items, UINT32_MAX);
   const int plw = 64 >> lcpr;
   const int64_t want = (items + 4 * plw - 1) / (4 * plw);
-  const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(want, 1024));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(want, 1024));
+}
+
+int gd_launch(const rn_conv_desc* d, int mode, const void* x, const void* w, void* y, const void* add,
+              hipStream_t st, const GdArgs* red = nullptr) {
+  GdArgs a{};
+  if (red) a = *red;  // (data gradient: the BatchNorm reduction fields)
+  a.x = (const bf16_t*)x; a.w = (const bf16_t*)w; a.y = (bf16_t*)y; a.add = (const bf16_t*)add;
+  const int blocks = gd_geometry(d, mode, a);
+  RN_CHECK_ARG((int64_t)d->n * a.P * a.qb < INT32_MAX && (int64_t)d->n * a.H * a.W * a.C < INT32_MAX,
+               "grouped direct: tensor too large");
+  a.fdQB = make_fastdiv(a.qb); a.fdP = make_fastdiv(a.P);
+  const int cpg = d->c / d->groups;
+  const int stride = mode == 0 ? d->stride_h : 1;
+  const bool s2t = mode == 1 && d->stride_h == 2;
   const size_t lds = (size_t)d->c * 9 * cpg * 2;
+  const bool rd = a.bnred != nullptr;
+  RN_CHECK_ARG(!rd || (mode == 1 && d->c <= kGdRedMaxC), "grouped direct BN reduction: data gradient only");
   if (s2t) {
-    if (cpg == 4) hipLaunchKernelGGL((grouped_dgrad_s2_kernel<4, 8>), dim3(blocks), dim3(256), lds, st, a);
+    if (cpg == 4 && rd) hipLaunchKernelGGL((grouped_dgrad_s2_kernel<4, 8, true>), dim3(blocks), dim3(256), lds, st, a);
+    else if (cpg == 4) hipLaunchKernelGGL((grouped_dgrad_s2_kernel<4, 8>), dim3(blocks), dim3(256), lds, st, a);
+    else if (rd) hipLaunchKernelGGL((grouped_dgrad_s2_kernel<8, 8, true>), dim3(blocks), dim3(256), lds, st, a);
     else hipLaunchKernelGGL((grouped_dgrad_s2_kernel<8, 8>), dim3(blocks), dim3(256), lds, st, a);
-  } else if (cpg == 4 && stride == 1)
-    hipLaunchKernelGGL((grouped_direct_kernel<4, 1, 8>), dim3(blocks), dim3(256), lds, st, a);
-  else if (cpg == 4)
+  } else if (cpg == 4 && stride == 1) {
+    if (rd) hipLaunchKernelGGL((grouped_direct_kernel<4, 1, 8, true>), dim3(blocks), dim3(256), lds, st, a);
+    else hipLaunchKernelGGL((grouped_direct_kernel<4, 1, 8>), dim3(blocks), dim3(256), lds, st, a);
+  } else if (cpg == 4)
     hipLaunchKernelGGL((grouped_direct_kernel<4, 2, 4>), dim3(blocks), dim3(256), lds, st, a);
   else
     hipLaunchKernelGGL((grouped_direct_kernel<8, 2, 4>), dim3(blocks), dim3(256), lds, st, a);
@@ -3578,6 +3690,10 @@ int64_t rn_conv_bnstats_blocks(const rn_conv_desc* d) {
 }
 
 int64_t rn_conv_bnred_blocks(const rn_conv_desc* d) {
+  if (gd_direct_ok(d, 1)) {  // one partial per workgroup of the direct kernel
+    GdArgs g{};
+    return gd_geometry(d, 1, g);
+  }
   IgemmArgs a = make_igemm_args(d, 1);
   int maxMc = 0;
   for (int z = 0; z < a.ncls; ++z) maxMc = std::max(maxMc, a.N * a.cls[z].Pc * a.cls[z].Qc);
@@ -3600,8 +3716,13 @@ int rn_conv_bwd_data_bnred_clip(const rn_conv_desc* d, const void* dy, const voi
   RN_CHECK_ARG(d && dy && w_crsk && (dx || (part && !add_src)), "null argument");
   RN_CHECK_ARG(dx || rn_conv_tile(d, 1) >= 128, "a reduction-only dgrad (dx = NULL) needs the 224/256-row tile");
   if (gd_direct_ok(d, 1)) {
-    RN_CHECK_ARG(!part && dx, "grouped direct data gradient: no BatchNorm reduction");
-    return gd_launch(d, 1, dy, w_crsk, dx, add_src, as_stream(stream));
+    RN_CHECK_ARG(dx, "grouped direct data gradient: dx required");
+    if (!part) return gd_launch(d, 1, dy, w_crsk, dx, add_src, as_stream(stream));
+    RN_CHECK_ARG(bn_x && bn_mean && bn_scale && bn_shift, "BN reduction needs x, mean, scale, shift");
+    GdArgs r{};
+    r.bnred = part; r.bn_x = (const bf16_t*)bn_x; r.bn_mean = bn_mean; r.bn_sc = bn_scale; r.bn_sh = bn_shift;
+    r.bn_relu = relu;
+    return gd_launch(d, 1, dy, w_crsk, dx, add_src, as_stream(stream), &r);
   }
   IgemmArgs a = make_igemm_args(d, 1);
   a.x = dy; a.w = w_crsk; a.y = dx; a.add = add_src; a.bias = nullptr;

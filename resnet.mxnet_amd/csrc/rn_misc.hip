@@ -489,6 +489,28 @@ __global__ void quant_codes_kernel(int64_t nchunk, const T* __restrict__ x, T* _
     reinterpret_cast<uint4*>(codes)[i] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
   }
 }
+// the fake-quantized values from the codes: out = code * unit rounded to T -- the same fp32 product
+// the quantizer kernels round (bit-identical to their out), 16 elements per thread
+template <typename T>
+__global__ void quant_expand_kernel(int64_t nchunk, const int8_t* __restrict__ codes, const float* __restrict__ unit_p,
+                                    T* __restrict__ out) {
+  const float unit = *unit_p;
+  constexpr int CE = 16 / sizeof(T);
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nchunk; i += (int64_t)gridDim.x * blockDim.x) {
+    const uint4 cw = reinterpret_cast<const uint4*>(codes)[i];
+    const uint32_t w[4] = {cw.x, cw.y, cw.z, cw.w};
+#pragma unroll
+    for (int h = 0; h < 16 / CE; ++h) {
+      float f[CE];
+#pragma unroll
+      for (int e = 0; e < CE; ++e) {
+        const int j = h * CE + e;
+        f[e] = (float)(int8_t)((w[j >> 2] >> (8 * (j & 3))) & 0xFF) * unit;
+      }
+      reinterpret_cast<uint4*>(out)[i * (16 / CE) + h] = f_to_chunk(f, (const T*)nullptr);
+    }
+  }
+}
 template <typename T>
 __global__ void quant_bwd_kernel(int64_t n, const T* __restrict__ x, const T* __restrict__ dy, T* __restrict__ dx,
                                  const float* __restrict__ minmax, int is_weight, const T* __restrict__ add) {
@@ -648,16 +670,17 @@ __global__ __launch_bounds__(256) void bnq_codes_kernel(const T* __restrict__ x,
         if ((e & 3) == 0) cw[e >> 2] = b;
         else cw[e >> 2] |= b << (8 * (e & 3));
       }
+      if (tg.out[k])  // (null: codes only, the values expanded later by rn_quant_int8_expand)
 #pragma unroll
-      for (int h = 0; h < 16 / CE; ++h) {
-        const uint4 o = f_to_chunk(g + h * CE, (const T*)nullptr);
-        if constexpr (NT) {  // the fake-quantized copy is read only by the weight gradients, later
-          const bnq_u32x4 w = {o.x, o.y, o.z, o.w};
-          __builtin_nontemporal_store(w, reinterpret_cast<bnq_u32x4*>(reinterpret_cast<T*>(tg.out[k]) + off) + h);
-        } else {
-          reinterpret_cast<uint4*>(reinterpret_cast<T*>(tg.out[k]) + off)[h] = o;
+        for (int h = 0; h < 16 / CE; ++h) {
+          const uint4 o = f_to_chunk(g + h * CE, (const T*)nullptr);
+          if constexpr (NT) {  // the fake-quantized copy is read only by the weight gradients, later
+            const bnq_u32x4 w = {o.x, o.y, o.z, o.w};
+            __builtin_nontemporal_store(w, reinterpret_cast<bnq_u32x4*>(reinterpret_cast<T*>(tg.out[k]) + off) + h);
+          } else {
+            reinterpret_cast<uint4*>(reinterpret_cast<T*>(tg.out[k]) + off)[h] = o;
+          }
         }
-      }
       reinterpret_cast<uint4*>(tg.codes[k] + off)[0] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
     }
   }
@@ -1199,7 +1222,7 @@ static int quant_codes_bn(const rn_bn_desc* d, const void* x, const float* scale
   RN_CHECK_ARG(d && x && scale && shift && ws, "null argument");
   RN_CHECK_ARG(d->dtype == RN_BF16 || d->dtype == RN_F32, "bad dtype");
   RN_CHECK_ARG(d->m > 0 && d->c > 0 && d->c % 16 == 0, "bad shape (c must be a multiple of 16)");
-  for (int k = 0; k < NQ; ++k) RN_CHECK_ARG(tg.out[k] && tg.codes[k] && tg.unit[k] && minmax[k], "null argument");
+  for (int k = 0; k < NQ; ++k) RN_CHECK_ARG(tg.codes[k] && tg.unit[k] && minmax[k], "null argument");
   const bool bf = d->dtype == RN_BF16;
   if (d->relu) {
     if (bf) launch_quant_codes_bn<bf16_t, true, NQ>(d, x, scale, shift, tg, minmax, decay, ws, is_train, first_batch, st);
@@ -1232,6 +1255,23 @@ int rn_quant_int8_fwd_codes_bn2(const rn_bn_desc* d, const void* x, const float*
   float* mm[2] = {minmax, minmax2};
   const float decay[2] = {ema_decay, ema_decay2};
   return quant_codes_bn<2>(d, x, scale, shift, tg, mm, decay, ws, is_train, first_batch, as_stream(stream));
+}
+
+int rn_quant_int8_expand(int32_t dtype, int64_t n, const void* codes, const float* unit, void* out,
+                         rn_stream_t stream) {
+  RN_CHECK_ARG(codes && unit && out && n > 0 && n % 16 == 0, "bad arguments (n a multiple of 16)");
+  RN_CHECK_ARG(((uintptr_t)codes & 15) == 0 && ((uintptr_t)out & 15) == 0, "16-byte aligned codes / out");
+  const int64_t nc = n / 16;
+  hipStream_t st = as_stream(stream);
+  if (dtype == RN_BF16)
+    hipLaunchKernelGGL(quant_expand_kernel<bf16_t>, dim3(grid1d(nc)), dim3(256), 0, st, nc, (const int8_t*)codes, unit,
+                       (bf16_t*)out);
+  else if (dtype == RN_F32)
+    hipLaunchKernelGGL(quant_expand_kernel<float>, dim3(grid1d(nc)), dim3(256), 0, st, nc, (const int8_t*)codes, unit,
+                       (float*)out);
+  else
+    RN_CHECK_ARG(false, "bad dtype");
+  return rn_check_launch("quant_int8_expand");
 }
 
 int rn_weight_quant_pack(const rn_wquant_item* items, int32_t count, int32_t dtype, float* ws,

@@ -328,6 +328,24 @@ class Plan:
             op.qsrc = q if op.int8 else None
             if op.int8:
                 q.emit_codes = True
+        # quantizers whose fake-quantized values only int8 convs read (their forwards read the codes):
+        # RN_QUANT_DEFER=1 expands the values from the codes on the weight-gradient stream, just before each
+        # weight gradient that reads them (rn_quant_int8_expand, bit-identical), instead of the forward
+        # writing them. Opt-in: measured slower (C5 24.72 / 24.56 vs 23.78 / 23.91 ms per step: the
+        # quantizer pass saves 0.38 ms of the compute stream, the 52 expansions cost 2.8 ms of the
+        # weight-gradient stream, which then delays the compute stream's tail)
+        users = {}
+        for op in self.ops:
+            for k in ("x", "a", "b", "res", "label"):
+                t = getattr(op, k, None)
+                if t is not None and hasattr(t, "numel"):
+                    users.setdefault(id(t), []).append(op)
+        defer = on and os.environ.get("RN_QUANT_DEFER", "0") == "1"
+        for op in self.ops:
+            if op.kind == "quant":
+                us = users.get(id(op.y), [])
+                op.defer_values = bool(defer and op.emit_codes and us and
+                                       all(u.kind == "conv" and u.int8 and u.qsrc is op for u in us))
 
     def _fuse_bn_apply(self):
         """BatchNorm+ReLU whose output feeds ONLY 1x1 convolutions (act1 -> conv1 / sc, act3 -> conv3
@@ -661,6 +679,7 @@ class Executor:
         if not self.dry_run and os.environ.get("RN_WGRAD_STREAM", "1") == "1":
             self._side_stream = torch.cuda.Stream(device=self.device)
         self._side_idx = set()
+        self._side_pre = set()  # (of _side_idx) SIDE_PRE_CALLS
         self._events = {}
         self.side_enabled = True  # False: the side-stream calls run on the compute stream (serialised timing)
         self._sync_stream()
@@ -829,6 +848,9 @@ class Executor:
                 self._spv2.value = self._side_stream.cuda_stream if self.side_enabled else self._spv.value
 
     WGRAD_CALLS = ("rn_conv_bwd_filter", "rn_conv_bwd_filter_ws", "rn_conv_bwd_filter_x", "rn_stem_conv_wgrad_p4")
+    # side-stream calls that depend on the forward only, not on the backward so far: no fork of their own
+    # (they run while the side stream waits for the next dy), except the first of a step
+    SIDE_PRE_CALLS = ("rn_quant_int8_expand",)
 
     def _route_wgrads(self):
         """Bind the weight-gradient calls of the backward plan to the side stream.
@@ -839,9 +861,11 @@ class Executor:
             return
         ws = self.wgrad_ws.data_ptr() if self.wgrad_ws is not None else None
         for i, (name, fn, args) in enumerate(self._bwd):
-            if name in self.WGRAD_CALLS and args and args[-1] is self._spv:
+            if name in self.WGRAD_CALLS + self.SIDE_PRE_CALLS and args and args[-1] is self._spv:
                 self._bwd[i] = (name, fn, args[:-1] + (self._spv2,))
                 self._side_idx.add(i)
+                if name in self.SIDE_PRE_CALLS:
+                    self._side_pre.add(i)
             elif ws is not None and any(isinstance(a, L.C.c_void_p) and a.value == ws for a in args):
                 raise PlanError("%s uses the weight-gradient slab workspace but is not routed to the side "
                                 "stream" % name)
@@ -905,7 +929,7 @@ class Executor:
                 if op.kind == "bn" and not op.use_global_stats:
                     src = producer.get(id(op.x))
                     if src is not None and src.kind == "conv" and src.y.c % 8 == 0 and src.y.cp == op.x.cp and \
-                            (stats_mode == "2" or self._big_tile(src, 0)):
+                            (stats_mode == "2" or self._big_tile(src, 0) or self._grouped_fuse(src, 0)):
                         src.bnstats = True
                         op.part_src = src
         for op in plan.ops:
@@ -1107,26 +1131,28 @@ class Executor:
                         # + the int8 codes and unit the consumers' int8 forward reads
                         o.codes = self.torch.zeros(o.x.numel, dtype=self.torch.int8, device=self.device)
                         o.unit = self._zeros(1, self.torch.float32)
+                # (deferred values: codes only here, rn_quant_int8_expand before the weight gradient)
+                vout = lambda o: None if o.defer_values else self._p(self.act(o.y))
                 for lst, tr in ((F, 1), (I, 0)):
                     if op.bn_lead is not None:
                         pass  # written by its peer's call
                     elif op.bn_peer is not None:
                         bn, o2 = op.bn_src, op.bn_peer
                         lst.append(self._call("rn_quant_int8_fwd_codes_bn2", L.C.byref(bn.desc),
-                                              self._p(self.act(bn.x)), bn.sc, bn.sh, self._p(self.act(op.y)),
+                                              self._p(self.act(bn.x)), bn.sc, bn.sh, vout(op),
                                               self._p(op.codes), self._p(op.unit), self._ap(q["minmax"]), q["ema"],
-                                              q["nbits"], self._p(self.act(o2.y)), self._p(o2.codes),
+                                              q["nbits"], vout(o2), self._p(o2.codes),
                                               self._p(o2.unit), self._ap(o2.q["minmax"]), o2.q["ema"],
                                               o2.q["nbits"], tr, self._qfirst, qwsp, sp))
                     elif op.bn_src is not None:
                         bn = op.bn_src
                         lst.append(self._call("rn_quant_int8_fwd_codes_bn", L.C.byref(bn.desc),
-                                              self._p(self.act(bn.x)), bn.sc, bn.sh, self._p(self.act(op.y)),
+                                              self._p(self.act(bn.x)), bn.sc, bn.sh, vout(op),
                                               self._p(op.codes), self._p(op.unit), self._ap(q["minmax"]), tr,
                                               q["ema"], self._qfirst, q["nbits"], qwsp, sp))
                     elif op.emit_codes:
                         lst.append(self._call("rn_quant_int8_fwd_codes", self.dtype, op.x.numel,
-                                              self._p(self.act(op.x)), self._p(self.act(op.y)), self._p(op.codes),
+                                              self._p(self.act(op.x)), vout(op), self._p(op.codes),
                                               self._p(op.unit), self._ap(q["minmax"]), 0, tr, q["ema"],
                                               self._qfirst, q["nbits"], qwsp, sp))
                     else:
@@ -1234,6 +1260,19 @@ class Executor:
         x, y = op.x, op.y
         d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad, op.groups)
         return int(self.lib.rn_conv_tile(L.C.byref(d), mode)) >= min_cols
+
+    def _grouped_fuse(self, op, mode):
+        """Does grouped conv `op` carry the BN fusion in its forward (mode 0: the statistics epilogue of
+        the block-diagonal 256x64 tile) / data gradient (mode 1: the BN-backward reduction of that tile
+        or of the direct kernel, rn_conv_bwd_data_bnred)? RN_GROUPED_BN_FUSION=0: neither (A/B)."""
+        if op.kind != "conv" or op.groups <= 1 or self.lib is None or self.dtype != L.RN_BF16 or \
+                os.environ.get("RN_GROUPED_BN_FUSION", "1") != "1":
+            return False
+        x, y = op.x, op.y
+        d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad, op.groups)
+        if mode == 1 and d.grouped_direct == 1:
+            return True
+        return int(self.lib.rn_conv_tile(L.C.byref(d), mode)) == 64
 
     def _conv_fwd_call(self, op, d, xptr, res, sp, stats=True):
         """Conv forward; emits the next BatchNorm's statistics when one consumes y (training), and
@@ -1420,6 +1459,7 @@ class Executor:
             self.wgrad_ws_bytes = max(need + [0])
             if self.wgrad_ws_bytes > 0:
                 self.wgrad_ws = self._zeros(self.wgrad_ws_bytes // 4, self.torch.float32)
+        expanded = set()  # quantizers whose deferred values this plan expands (rn_quant_int8_expand)
         for op in reversed(plan.ops):
             if op.kind == "softmax":
                 gs.has_value.add(id(op.x))  # dlogits written by the forward softmax call
@@ -1460,6 +1500,13 @@ class Executor:
                                                 self._p(self.wgrad_ws) if ws else None,
                                                 self.wgrad_ws_bytes if ws else 0, sp))
                 else:
+                    q = op.qsrc
+                    if q is not None and q.defer_values and id(q) not in expanded:
+                        # the fake-quantized input from its codes, on the weight-gradient stream ahead of
+                        # the wait for dy (routed by _route_wgrads; backward() forks before the first)
+                        expanded.add(id(q))
+                        self._bwd.append(self._call("rn_quant_int8_expand", self.dtype, x.numel, self._p(q.codes),
+                                                    self._p(q.unit), self._p(self.act(x)), sp))
                     self._bwd.append(self._wgrad_call(op.desc, self._p(self.act(x)), self._p(dy), self._gp(op.weight),
                                                       sp))
                 self.param_done_at[op.weight] = len(self._bwd)
@@ -1519,7 +1566,8 @@ class Executor:
                                                 self._ap(op.mean), self._ap(op.var), op.sc, op.sh,
                                                 self._gp(op.gamma), self._gp(op.beta), wsp, sp))
                 elif bwd_fusion and not op.desc.dy2 and w and w[0] == "dgrad" and dy is w[4] and \
-                        op.y.c % 8 == 0 and op.y.c == op.y.cp and (bwd_all or self._big_tile(w[2], 1)) and \
+                        op.y.c % 8 == 0 and op.y.c == op.y.cp and \
+                        (bwd_all or self._big_tile(w[2], 1) or self._grouped_fuse(w[2], 1)) and \
                         (not op.desc.clip or self._big_tile(w[2], 1)):  # (the clip: bf16 LDS-DMA tiles)
                     # the conv dgrad that completes this BN's output gradient also reduces its backward
                     # (sum dz, sum dz*(x - mean)); the BN then needs only finalize + apply
@@ -1735,9 +1783,11 @@ class Executor:
         # hooks: {bwd index -> callable}, e.g. RCCL bucket all-reduce launches; with the wgrad side
         # stream a hook runs on it after a fork, so its collective follows both streams' writes
         hooks = hooks or {}
+        forked = False
         for i, (name, fn, args) in enumerate(self._bwd):
-            if side is not None and i in self._side_idx:
-                self._fork(i)
+            if side is not None and i in self._side_idx and (not forked or i not in self._side_pre):
+                self._fork(i)  # (the first side call of the step waits for the forward too)
+                forked = True
             r = 0 if self.dry_run else fn(*args)
             if r != 0:
                 raise L.RNError("%s: %s" % (name, self.lib.rn_last_error().decode()))

@@ -111,6 +111,7 @@ SIGNATURES = {
     "rn_quant_int8_fwd_codes_bn": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _i32, _f32, _i32, _i32, _P, _P]),
     "rn_quant_int8_fwd_codes_bn2": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _f32, _i32, _P, _P, _P, _P, _f32, _i32,
                                            _i32, _i32, _P, _P]),
+    "rn_quant_int8_expand": (_i32, [_i32, _i64, _P, _P, _P, _P]),
     "rn_weight_quant_pack": (_i32, [_P, _i32, _i32, _P, _P]),
     "rn_quant_int8_bwd": (_i32, [_i32, _i64, _P, _P, _P, _P, _i32, _P, _P]),
     "rn_set_tuning": (_i32, [_i32, _i32]),

@@ -438,7 +438,14 @@ class Checker:
         st, t = self._quant_state(op.q, cur)
         code, val, unit = quant_ref(y, t, float((1 << (int(op.q["nbits"]) - 1)) - 1))
         val = _bf16(val) if self.ex.dtype == 0 else val
-        m = {"state": st, "values": self.mismatch(self.act_nchw(op.y), val)["mismatch"]}
+        if getattr(op, "defer_values", False):
+            # the forward writes codes only: the values are checked where rn_quant_int8_expand writes them
+            if not hasattr(self, "deferred_vals"):
+                self.deferred_vals = {}
+            self.deferred_vals[self.ex.act(op.y).data_ptr()] = (op, val)
+            m = {"state": st}
+        else:
+            m = {"state": st, "values": self.mismatch(self.act_nchw(op.y), val)["mismatch"]}
         if getattr(op, "codes", None) is not None:
             m["codes"] = self.mismatch(self.nchw(op.codes, x.n, x.h, x.w, x.cp, x.c), code)["mismatch"]
             m["unit"] = 0.0 if float(op.unit[0]) == float(unit) else 1.0
@@ -752,6 +759,17 @@ class Checker:
                 ref = ref + state["add"][:n].float()
             self.add("relu_bwd", "relu", self.t(dxp)[:n].float(), ref, BF16_BAR if self.ex.dtype == 0 else F32_BAR)
         return pre, post
+
+    def _h_rn_quant_int8_expand(self, args, state):
+        """A quantizer's deferred fake-quantized values (expanded from its codes on the weight-gradient
+        stream): bit for bit the values the oracle's quantizer gives for the forward's input."""
+        outp = args[4]
+
+        def post():
+            op, val = self.deferred_vals.pop(outp.value)
+            m = {"values": self.mismatch(self.act_nchw(op.y), val)["mismatch"]}
+            self.add_metric("quant_expand", op.q["name"], m, {"values": 0.0})
+        return None, post
 
     def _h_rn_quant_int8_bwd(self, args, state):
         """A Quantization_int8's straight-through backward that is not folded into a BatchNorm (the

@@ -73,7 +73,17 @@ def gpu_quant_values(ex):
             vals[q["name"]] = op.qw.cpu().numpy().reshape(k, r, s_, c).transpose(0, 3, 1, 2)
         if op.kind == "quant":
             t = op.y
-            a = ex.act(t).float().cpu().numpy().reshape(t.n, t.h, t.w, t.cp)[..., :t.c].transpose(0, 3, 1, 2)
+            src = ex.act(t)
+            if getattr(op, "defer_values", False):
+                # (after the forward only the codes exist: the values as the backward expands them)
+                import ctypes as C
+                import torch
+                from rn import lib as L
+                src = torch.empty_like(src)
+                L.call("rn_quant_int8_expand", ex.dtype, src.numel(), C.c_void_p(op.codes.data_ptr()),
+                       C.c_void_p(op.unit.data_ptr()), C.c_void_p(src.data_ptr()),
+                       C.c_void_p(torch.cuda.current_stream().cuda_stream))
+            a = src.float().cpu().numpy().reshape(t.n, t.h, t.w, t.cp)[..., :t.c].transpose(0, 3, 1, 2)
             vals[op.q["name"]] = a
         elif op.kind == "stem" and op.quant:
             # the quantized stem input is the NHWC-8 compute copy conv0 reads

@@ -179,12 +179,19 @@ def test_quant_codes_bn_fused(gpu, dtype, relu, m, c):
     ws = torch.zeros(4096, dtype=torch.float32, device=gpu)
     for train in (1, 0):
         outs = []
-        for fused in (False, True):
+        # (deferred: codes only, then rn_quant_int8_expand -- the int8 graph's weight-gradient stream)
+        for fused in (False, True, "deferred"):
             out = torch.full_like(x, float("nan"))
             codes = torch.zeros(n, dtype=torch.int8, device=gpu)
             unit = torch.zeros(1, dtype=torch.float32, device=gpu)
             mm = torch.tensor([2.5], dtype=torch.float32, device=gpu)
-            if fused:
+            if fused == "deferred":
+                L.call("rn_quant_int8_fwd_codes_bn", C.byref(d), p(x), p(sc), p(sh), None, p(codes), p(unit), p(mm),
+                       train, 0.99, 0, 8, p(ws), stream())
+                torch.cuda.synchronize()
+                assert torch.isnan(out.float()).all()
+                L.call("rn_quant_int8_expand", dtype, n, p(codes), p(unit), p(out), stream())
+            elif fused:
                 L.call("rn_quant_int8_fwd_codes_bn", C.byref(d), p(x), p(sc), p(sh), p(out), p(codes), p(unit), p(mm),
                        train, 0.99, 0, 8, p(ws), stream())
             else:
@@ -193,8 +200,8 @@ def test_quant_codes_bn_fused(gpu, dtype, relu, m, c):
                        0, 8, p(ws), stream())
             outs.append((out, codes, unit, mm))
         torch.cuda.synchronize()
-        for a, b in zip(*outs):
-            assert torch.equal(a, b)
+        for a, b, e in zip(*outs):
+            assert torch.equal(a, b) and torch.equal(a, e)
         assert ws[0].item() == 0.0  # the shared workspace's running max is left zero
         if train:
             yv = y.float()

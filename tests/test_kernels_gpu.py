@@ -536,6 +536,129 @@ def test_grouped_conv_direct(gpu, case):
     assert rel_err(outs[0][0], outs[1][0]) < 4e-3 and rel_err(outs[0][1], outs[1][1]) < 4e-3
 
 
+GBN_CASES = [
+    # n, c, h, w, stride, groups: ResNeXt-50 32x4d conv2 (3x3, pad 1) at small spatial size
+    (2, 128, 9, 9, 1, 32),     # 4 per group: direct data gradient (stride 1)
+    (3, 128, 15, 13, 1, 32),   # ragged pixel lanes
+    (2, 128, 12, 12, 2, 32),   # 4 per group, stride 2: the transposed stride-2 direct data gradient
+    (2, 256, 11, 13, 2, 32),   # 8 per group, stride 2: direct (transposed) data gradient
+    (2, 256, 7, 11, 1, 32),    # 8 per group, stride 1: block-diagonal tile (GD)
+    (2, 512, 6, 7, 1, 32),     # 16 per group: GD tile
+    (1, 1024, 5, 5, 2, 32),    # 32 per group, stride 2: GD tile over parity classes
+]
+
+
+@pytest.fixture(params=[0, 2], ids=["gd_auto", "gd_s2"])
+def gd_tune(request):
+    """rn_set_tuning 13 (block-diagonal grouped tile): 0 auto; 2 also the stride-2 data gradients."""
+    L.call("rn_set_tuning", 13, request.param)
+    yield request.param
+    L.call("rn_set_tuning", 13, 0)
+
+
+@pytest.mark.parametrize("case", GBN_CASES)
+def test_grouped_dgrad_bn_backward_fusion(gpu, case, gd_tune):
+    """The grouped data gradients carrying the BatchNorm(+ReLU) backward reduction of the BN that
+    produced their input (rn_conv_bwd_data_bnred on the direct kernels and on the block-diagonal
+    256x64 tile) + rn_bn_bwd_part == the oracle's grouped dgrad followed by the BN+ReLU backward
+    (symbol/resnext.py:20-25: bn1 -> relu -> grouped conv2); dx as stored is the unfused call's, bit
+    for bit."""
+    n, c, h, w, st, g = case
+    k, r, pd = c, 3, 1
+    rng = np.random.default_rng(21)
+    xb = bf16_round(rng.standard_normal((n, c, h, w)) * 1.5 + 0.3)   # BN input
+    gamma, beta = rng.uniform(0.5, 1.5, c), rng.standard_normal(c) * 0.2
+    a_ref, cache = ops.bn_train_fwd(xb, gamma, beta, 1e-5, False)
+    act = ops.relu_fwd(a_ref)
+    wt = bf16_round(rng.standard_normal((k, c // g, r, r)) / np.sqrt(c // g * r * r))
+    P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+    dy = bf16_round(rng.standard_normal((n, k, P, Q)))
+    prev = bf16_round(rng.standard_normal((n, c, h, w)) * 0.5)
+    dact_ref = ops.conv2d_bwd(act, wt, dy, (st, st), (pd, pd), g)[0] + prev
+    d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd, groups=g)
+    lib = L.load()
+    direct = d.grouped_direct == 1
+    assert direct == (c // g == 4 or (c // g == 8 and st == 2))
+    # (the stride-2 block-diagonal data gradient: 4-tap parity classes, the 128-row kernel by default)
+    assert direct or lib.rn_conv_tile(C.byref(d), 1) == (0 if st == 2 and gd_tune != 2 else 64)
+    wc = torch.zeros(lib.rn_conv_pack_numel(C.byref(d), 1), dtype=torch.bfloat16, device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), None, p(wc), stream())
+    bd = L.BNDesc(dtype=BF16, m=n * h * w, c=c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1)
+    f = lambda a: torch.tensor(np.asarray(a, np.float64), dtype=torch.float32, device=gpu)
+    g_d, b_d, mm, mv = f(gamma), f(beta), f(np.zeros(c)), f(np.ones(c))
+    sm, si, sc, sh = [torch.zeros(c, dtype=torch.float32, device=gpu) for _ in range(4)]
+    ws = torch.zeros(lib.rn_bn_workspace_bytes(C.byref(bd)) // 4 + 16, dtype=torch.float32, device=gpu)
+    xbd = to_nhwc(xb, BF16, gpu)
+    L.call("rn_bn_fwd_train", C.byref(bd), p(xbd), None, p(g_d), p(b_d), p(mm), p(mv), p(sm), p(si), p(sc), p(sh),
+           p(ws), stream())
+    dyd = to_nhwc(dy, BF16, gpu)
+    dact = to_nhwc(prev, BF16, gpu)                      # accumulated in place (add_src = out)
+    plain = to_nhwc(prev, BF16, gpu)
+    nrb = lib.rn_conv_bnred_blocks(C.byref(d))
+    part = torch.full((nrb * c * 2,), float("nan"), dtype=torch.float32, device=gpu)  # every slot written
+    L.call("rn_conv_bwd_data_bnred", C.byref(d), p(dyd), p(wc), p(dact), p(dact), p(xbd), p(sm), p(sc), p(sh), 1,
+           p(part), stream())
+    L.call("rn_conv_bwd_data", C.byref(d), p(dyd), p(wc), p(plain), p(plain), stream())
+    dx = torch.zeros_like(xbd)
+    dg, db = torch.zeros(c, dtype=torch.float32, device=gpu), torch.zeros(c, dtype=torch.float32, device=gpu)
+    L.call("rn_bn_bwd_part", C.byref(bd), p(part), nrb, p(xbd), p(dact), p(dx), None, p(g_d), p(sm), p(si), p(sc),
+           p(sh), p(dg), p(db), p(ws), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dact, plain)
+    assert not torch.isnan(part).any()
+    assert rel_err(from_nhwc(dact, c), dact_ref) < TOL[BF16]
+    dz = ops.relu_bwd(from_nhwc(dact, c), act)           # from the stored gradient, as the kernel reads it
+    dx_ref, dg_ref, db_ref = ops.bn_train_bwd(dz, cache, False)
+    assert rel_err(db.cpu().numpy(), db_ref) < 1e-4
+    assert rel_err(dg.cpu().numpy(), dg_ref) < 1e-4
+    assert rel_err(from_nhwc(dx, c), dx_ref) < 3e-2
+
+
+@pytest.mark.parametrize("case", [c for c in GBN_CASES if c[1] // c[5] >= 8 and not (c[1] // c[5] == 8 and c[4] == 2)])
+def test_grouped_conv_bnstats_epilogue(gpu, case):
+    """BatchNorm statistics from the block-diagonal 256x64 tile's epilogue (rn_conv_fwd_bnstats on a
+    grouped conv, the ResNeXt bn2 input) merged by rn_bn_fwd_train_part == a BatchNorm over the stored
+    grouped conv output."""
+    n, c, h, w, st, g = case
+    k, r, pd = c, 3, 1
+    rng = np.random.default_rng(22)
+    x = bf16_round(rng.standard_normal((n, c, h, w)))
+    wt = bf16_round(rng.standard_normal((k, c // g, r, r)) / np.sqrt(c // g * r * r))
+    P, Q = ops.conv_out_hw(h, w, r, r, (st, st), (pd, pd))
+    res = bf16_round(rng.standard_normal((n, k, P, Q)) + 3.0)  # offset mean: exercises the pivots
+    d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd, groups=g)
+    lib = L.load()
+    assert d.grouped_direct == 0 and lib.rn_conv_tile(C.byref(d), 0) == 64
+    wk = torch.zeros(lib.rn_conv_pack_numel(C.byref(d), 0), dtype=torch.bfloat16, device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), p(wk), None, stream())
+    y = torch.zeros((n, P, Q, k), dtype=torch.bfloat16, device=gpu)
+    plain = torch.zeros_like(y)
+    nblk = lib.rn_conv_bnstats_blocks(C.byref(d))
+    part = torch.zeros(nblk * 3 * k, dtype=torch.float32, device=gpu)
+    xd, rd = to_nhwc(x, BF16, gpu), to_nhwc(res, BF16, gpu)
+    L.call("rn_conv_fwd_bnstats", C.byref(d), p(xd), p(wk), p(y), BF16, p(rd), None, p(part), stream())
+    L.call("rn_conv_fwd", C.byref(d), p(xd), p(wk), p(plain), BF16, p(rd), None, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(y, plain)
+    conv_out = from_nhwc(y, k)
+    assert rel_err(conv_out, ops.conv2d_fwd(x, wt, (st, st), (pd, pd), g) + res) < TOL[BF16]
+    gamma, beta = rng.uniform(0.5, 1.5, k), rng.standard_normal(k) * 0.1
+    _, cache = ops.bn_train_fwd(conv_out, gamma, beta, 1e-5, False)
+    mm_ref, mv_ref = ops.bn_moving_update(np.zeros(k), np.ones(k), cache[3], cache[4], 0.9)
+    bd = L.BNDesc(dtype=BF16, m=n * P * Q, c=k, c_real=k, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1)
+    f = lambda a: torch.tensor(np.asarray(a, np.float64), dtype=torch.float32, device=gpu)
+    g_d, b_d, mm, mv = f(gamma), f(beta), f(np.zeros(k)), f(np.ones(k))
+    sm, si, sc, sh = [torch.zeros(k, dtype=torch.float32, device=gpu) for _ in range(4)]
+    yb = torch.zeros_like(y)
+    ws = torch.zeros(lib.rn_bn_workspace_bytes(C.byref(bd)) // 4 + 16, dtype=torch.float32, device=gpu)
+    L.call("rn_bn_fwd_train_part", C.byref(bd), p(part), nblk, lib.rn_conv_bn_part_rows(C.byref(d), 0), k, p(y),
+           p(yb), p(g_d), p(b_d), p(mm), p(mv), p(sm), p(si), p(sc), p(sh), p(ws), stream())
+    torch.cuda.synchronize()
+    assert rel_err(sm.cpu().numpy(), cache[3]) < 1e-6
+    assert rel_err(mv.cpu().numpy(), mv_ref) < 1e-5
+    assert rel_err(mm.cpu().numpy(), mm_ref) < 1e-5
+
+
 @pytest.mark.parametrize("dtype", [F32, BF16])
 def test_weight_pack_multi(gpu, dtype):
     """rn_conv_weight_pack_multi writes exactly the bytes of one rn_conv_weight_pack per layer: the

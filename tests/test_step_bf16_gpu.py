@@ -224,9 +224,11 @@ def _c4_layerwise(n, image):
     ck = _layerwise(graphs.resnext50_32x4d(), n, image, "bfloat16", warm=1)
     assert not ck.skipped, ck.skipped
     kinds = {r[0] for r in ck.rec}
-    assert {"conv_fwd", "conv_fwd_grouped", "dgrad_grouped", "wgrad_grouped", "wgrad", "bn_apply_add",
+    # (the grouped data gradients carry their BN-backward reduction: direct kernel or block-diagonal tile)
+    assert {"conv_fwd", "conv_fwd_grouped", "dgrad_bnred_grouped", "wgrad_grouped", "wgrad", "bn_apply_add",
             "relu_bwd_bnred", "bn_fwd", "bn_bwd_dx", "bn_bwd_params", "weight_copy"} <= kinds, kinds
     assert sum(1 for r in ck.rec if r[0] == "conv_fwd_grouped") == 16
+    assert sum(1 for r in ck.rec if r[0] in ("dgrad_grouped", "dgrad_bnred_grouped")) == 16
     assert sum(1 for r in ck.rec if r[0] in ("wgrad", "wgrad_grouped")) == 54  # 53 convs + fc1
     assert sum(1 for r in ck.rec if r[0] == "bn_apply_add") == 16
     bad = ck.failures()
@@ -246,7 +248,7 @@ def test_resnet50_int8_full_size_layerwise(gpu):
     _c5_layerwise(256, 224)
 
 
-def _c5_layerwise(n, image):
+def _c5_layerwise(n, image, defer=False):
     from rn import graphs
     ck = _layerwise(graphs.resnet50_int8(), n, image, "bfloat16", warm=1)
     assert not ck.skipped, ck.skipped
@@ -257,6 +259,10 @@ def _c5_layerwise(n, image):
     assert n_i8 == 52, n_i8
     assert sum(1 for r in ck.rec if r[0] == "weight_quant") == 54  # 53 convs + fc1
     assert sum(1 for r in ck.rec if r[0] == "quant") == 54  # 52 int8 inputs + conv0's + fc1's
+    # (RN_QUANT_DEFER=1: the int8 inputs' values deferred to the weight-gradient stream, rn_quant_int8_expand)
+    n_def = sum(1 for op in ck.ex.plan.ops if op.kind == "quant" and op.defer_values)
+    assert n_def == (52 if defer else 0)
+    assert sum(1 for r in ck.rec if r[0] == "quant_expand") == n_def
     assert sum(1 for r in ck.rec if r[0] == "wgrad") == 54
     bad = ck.failures()
     assert not bad, bad[:10]
@@ -285,6 +291,14 @@ def test_resnext50_bf16_layerwise_small(gpu):
 def test_resnet50_int8_layerwise_small(gpu):
     """The C5 per-kernel checks at 8 images of 64x64 (a fast first gate before the full size)."""
     _c5_layerwise(8, 64)
+
+
+def test_resnet50_int8_layerwise_deferred_values(gpu, monkeypatch):
+    """The opt-in deferred fake-quantized values (RN_QUANT_DEFER=1: the quantizers write codes only, the
+    weight-gradient stream expands the values from them before the first weight gradient reading them),
+    per kernel at 8 images of 64x64: the expanded values bit for bit."""
+    monkeypatch.setenv("RN_QUANT_DEFER", "1")
+    _c5_layerwise(8, 64, defer=True)
 
 
 def test_resnet50_fp32_layerwise(gpu):
