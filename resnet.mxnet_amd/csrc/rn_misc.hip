@@ -838,12 +838,36 @@ namespace {
 // gradient only from the outputs (i | i+1) x (j | j+1) -- input row 2i from output row i, row 2i+1
 // from rows i and i+1 -- so each dy / tap-index chunk is read once per block instead of once per
 // covered input pixel (up to 4x). Sums in the generic kernel's order (outputs row-major): bit-identical.
-template <typename T>
-__global__ void maxpool3s2_bwd_kernel(PoolArgs a, const T* __restrict__ dy, const uint8_t* __restrict__ argmax,
-                                      T* __restrict__ dx, const T* __restrict__ add) {
+// RED (bf16, the stem's bn0 -> relu0 -> pool, symbol/resnet.py:94-97): the pool backward completes the
+// BatchNorm+ReLU output gradient, so it also reduces that BN's backward as the conv epilogues do
+// (igemm_big_kernel EPI 2): sum dz, sum dz*(x - mean), dz = dx * relu'(x sc + sh) on the stored dx ->
+// part[block][C][2]. A thread keeps one channel chunk (C / 8 divides the 256-thread block), the lanes
+// of a chunk then the block's waves are summed in a fixed order.
+struct PoolRed {
+  const bf16_t* bn_x;
+  const float *mean, *sc, *sh;
+  float* part;
+  int relu;
+};
+constexpr int kPoolRedMaxC = 256;
+template <typename T, bool RED = false>
+__global__ __launch_bounds__(256) void maxpool3s2_bwd_kernel(PoolArgs a, const T* __restrict__ dy,
+                                                             const uint8_t* __restrict__ argmax, T* __restrict__ dx,
+                                                             const T* __restrict__ add, PoolRed rd) {
   constexpr int CE = 16 / sizeof(T);
   const int cpr = a.c / CE;
   const uint32_t total = (uint32_t)a.n * a.p * a.q * cpr;  // blocks x chunks (P = H/2, Q = W/2)
+  float s1[RED ? 8 : 1], s2[RED ? 8 : 1], r_mu[RED ? 8 : 1], r_sc[RED ? 8 : 1], r_sh[RED ? 8 : 1];
+  if constexpr (RED) {
+    const int c0 = (int)(threadIdx.x % cpr) * 8;  // (the chunk of every i this thread visits)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s1[e] = s2[e] = 0.f;
+      r_mu[e] = rd.mean[c0 + e];
+      r_sc[e] = rd.sc[c0 + e];
+      r_sh[e] = rd.sh[c0 + e];
+    }
+  }
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const uint32_t blk = fdiv(i, a.fd_cpr);
     const int cc = (int)(i - blk * cpr);
@@ -883,15 +907,61 @@ __global__ void maxpool3s2_bwd_kernel(PoolArgs a, const T* __restrict__ dy, cons
         for (int e = 0; e < CE; ++e)
           if ((int)((am4[u] >> (8 * e)) & 0xFF) == tap) acc[e] += g[u][e];
       }
-      reinterpret_cast<uint4*>(dx)[xi] = f_to_chunk(acc, (const T*)nullptr);
+      const uint4 o = f_to_chunk(acc, (const T*)nullptr);
+      reinterpret_cast<uint4*>(dx)[xi] = o;
+      if constexpr (RED) {  // on the stored (rounded) values, as a separate pass would read them
+        float g[8], xv[8];
+        chunk_to_f(o, g, (const bf16_t*)nullptr);
+        chunk_to_f(reinterpret_cast<const uint4*>(rd.bn_x)[xi], xv, (const bf16_t*)nullptr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float dz = (!rd.relu || fmaf(xv[e], r_sc[e], r_sh[e]) > 0.f) ? g[e] : 0.f;
+          s1[e] += dz;
+          s2[e] = fmaf(dz, xv[e] - r_mu[e], s2[e]);
+        }
+      }
     }
   }
+  if constexpr (RED) {
+    __shared__ float red[4][2][kPoolRedMaxC];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int o = cpr; o < 64; o <<= 1)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        s1[e] += __shfl_xor(s1[e], o, 64);
+        s2[e] += __shfl_xor(s2[e], o, 64);
+      }
+    if (lane < cpr)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[wid][0][lane * 8 + e] = s1[e];
+        red[wid][1][lane * 8 + e] = s2[e];
+      }
+    __syncthreads();
+    for (int c = threadIdx.x; c < a.c; c += blockDim.x) {
+      float* dst = rd.part + ((int64_t)blockIdx.x * a.c + c) * 2;
+      dst[0] = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+      dst[1] = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+    }
+  }
+}
+// the 2x2-block form applies (and, bf16 with C / 8 dividing 256 and C <= kPoolRedMaxC, its BN reduction)
+bool maxpool3s2_ok(const rn_pool_desc* d) {
+  return d->type == RN_POOL_MAX && d->r == 3 && d->s == 3 && d->stride_h == 2 && d->stride_w == 2 && d->pad_h == 1 &&
+         d->pad_w == 1 && d->h == 2 * d->p && d->w == 2 * d->q && g_tune[RN_TUNE_POOL_BLOCK_BWD] != 1;
+}
+bool pool_red_ok(const rn_pool_desc* d) {
+  return d && maxpool3s2_ok(d) && d->dtype == RN_BF16 && d->c <= kPoolRedMaxC && 256 % (d->c / 8) == 0;
+}
+int pool_red_blocks(const rn_pool_desc* d) {  // (grid-stride: at most 1024 workgroups, one partial each)
+  return grid1d((int64_t)d->n * d->p * d->q * d->c / 8, 256, 1024);
 }
 }  // namespace
 
 extern "C" {
-int rn_pool_bwd(const rn_pool_desc* d, const void* dy, const uint8_t* argmax, void* dx, const void* add_src,
-                rn_stream_t stream) {
+namespace {
+int pool_bwd(const rn_pool_desc* d, const void* dy, const uint8_t* argmax, void* dx, const void* add_src,
+             const PoolRed* red, rn_stream_t stream) {
   RN_CHECK_ARG(d && dy && dx, "null argument");
   RN_CHECK_ARG(d->type != RN_POOL_MAX || argmax, "max pool backward needs argmax");
   PoolArgs a{d->n, d->h, d->w, d->c, d->r, d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, d->p, d->q, d->type};
@@ -901,20 +971,23 @@ int rn_pool_bwd(const rn_pool_desc* d, const void* dy, const uint8_t* argmax, vo
   RN_CHECK_ARG((int64_t)d->n * d->h * d->w * d->c < INT32_MAX, "pooling tensor exceeds 2^31 elements");
   hipStream_t st = as_stream(stream);
   const int64_t total = (int64_t)d->n * d->h * d->w * d->c / 8;
-  if (d->type == RN_POOL_MAX && d->r == 3 && d->s == 3 && d->stride_h == 2 && d->stride_w == 2 && d->pad_h == 1 &&
-      d->pad_w == 1 && d->h == 2 * d->p && d->w == 2 * d->q && g_tune[RN_TUNE_POOL_BLOCK_BWD] != 1) {
+  if (maxpool3s2_ok(d)) {
     PoolArgs b = a;
     b.fd_a = make_fastdiv(d->q);
     b.fd_b = make_fastdiv(d->p);
     const int64_t nb = (int64_t)d->n * d->p * d->q * d->c / (d->dtype == RN_BF16 ? 8 : 4);
-    if (d->dtype == RN_BF16)
+    if (red && red->part)
+      hipLaunchKernelGGL((maxpool3s2_bwd_kernel<bf16_t, true>), dim3(pool_red_blocks(d)), dim3(256), 0, st, b,
+                         (const bf16_t*)dy, argmax, (bf16_t*)dx, (const bf16_t*)add_src, *red);
+    else if (d->dtype == RN_BF16)
       hipLaunchKernelGGL(maxpool3s2_bwd_kernel<bf16_t>, dim3(grid1d(nb)), dim3(256), 0, st, b, (const bf16_t*)dy,
-                         argmax, (bf16_t*)dx, (const bf16_t*)add_src);
+                         argmax, (bf16_t*)dx, (const bf16_t*)add_src, PoolRed{});
     else
       hipLaunchKernelGGL(maxpool3s2_bwd_kernel<float>, dim3(grid1d(nb)), dim3(256), 0, st, b, (const float*)dy,
-                         argmax, (float*)dx, (const float*)add_src);
+                         argmax, (float*)dx, (const float*)add_src, PoolRed{});
     return rn_check_launch("maxpool3s2_bwd");
   }
+  RN_CHECK_ARG(!(red && red->part), "pool BN reduction: the 3x3 / stride-2 max pool with H = 2P, W = 2Q only");
   if (d->dtype == RN_BF16)
     hipLaunchKernelGGL(pool_bwd_kernel<bf16_t>, dim3(grid1d(total)), dim3(256), 0, st, a, (const bf16_t*)dy,
                        argmax, (bf16_t*)dx, (const bf16_t*)add_src);
@@ -922,6 +995,23 @@ int rn_pool_bwd(const rn_pool_desc* d, const void* dy, const uint8_t* argmax, vo
     hipLaunchKernelGGL(pool_bwd_kernel<float>, dim3(grid1d(total * 2)), dim3(256), 0, st, a, (const float*)dy,
                        argmax, (float*)dx, (const float*)add_src);
   return rn_check_launch("pool_bwd");
+}
+}  // namespace
+
+int rn_pool_bwd(const rn_pool_desc* d, const void* dy, const uint8_t* argmax, void* dx, const void* add_src,
+                rn_stream_t stream) {
+  return pool_bwd(d, dy, argmax, dx, add_src, nullptr, stream);
+}
+
+int64_t rn_pool_bwd_bnred_blocks(const rn_pool_desc* d) { return pool_red_ok(d) ? pool_red_blocks(d) : 0; }
+
+int rn_pool_bwd_bnred(const rn_pool_desc* d, const void* dy, const uint8_t* argmax, void* dx, const void* add_src,
+                      const void* bn_x, const float* bn_mean, const float* bn_scale, const float* bn_shift,
+                      int32_t relu, float* part, rn_stream_t stream) {
+  RN_CHECK_ARG(d && bn_x && bn_mean && bn_scale && bn_shift && part, "null argument");
+  RN_CHECK_ARG(pool_red_ok(d), "pool BN reduction: bf16 3x3 / stride-2 max pool, H = 2P, W = 2Q, C / 8 dividing 256");
+  const PoolRed r{(const bf16_t*)bn_x, bn_mean, bn_scale, bn_shift, part, relu};
+  return pool_bwd(d, dy, argmax, dx, add_src, &r, stream);
 }
 
 int rn_softmax_output(int32_t grad_dtype, int32_t batch, int32_t ncls, int32_t ld, const float* logits,

@@ -1318,11 +1318,14 @@ class Executor:
         if nch <= 1 or not op.p4 or not side or dy is None or op.dfull.n % nch or not self._bwd:
             return 1
         name, _, args = self._bwd[-1]
-        if name != "rn_bn_bwd" or args[3] is None or args[4] is not None:
+        # (rn_bn_bwd_part: the pool backward reduced the BN, rn_pool_bwd_bnred)
+        dx, add = (args[3], args[4]) if name == "rn_bn_bwd" else (args[5], args[6]) if name == "rn_bn_bwd_part" \
+            else (None, None)
+        if dx is None or add is not None:
             return 1
         bn = args[0]._obj
         if bn.dy2 or bn.c != op.dfull.k_pad or bn.m != op.dfull.n * op.dfull.p * op.dfull.q or \
-                args[3].value != self._p(dy).value:
+                dx.value != self._p(dy).value:
             return 1
         return nch
 
@@ -1524,7 +1527,15 @@ class Executor:
                     # stream) starting as soon as its rows are applied: only the last chunk's wgrad
                     # stays on the step's critical path (rn_bn_bwd then reduces + finalizes only)
                     bname, bfn, bargs = self._bwd[-1]
-                    self._bwd[-1] = (bname, bfn, bargs[:3] + (None,) + bargs[4:])
+                    if bname == "rn_bn_bwd":
+                        self._bwd[-1] = (bname, bfn, bargs[:3] + (None,) + bargs[4:])
+                    else:  # rn_bn_bwd_part: finalize only, its coefficients where rn_bn_bwd_apply_rows reads
+                        # them (after the reduction partials of rn_bn_bwd's own layout in the workspace)
+                        bd, part, nrb, xp_, dyp_, dxp_, _, gp_, smp, sip, scp, shp, dgp, dbp, wsp_, _ = bargs
+                        coef = wsp_.value + 4 * 2 * int(self.lib.rn_bn_reduce_blocks(bd)) * bd._obj.c
+                        self._bwd[-1] = self._call("rn_bn_bwd_finalize", bd, part, nrb, gp_, smp, sip, dgp, dbp,
+                                                   L.C.c_void_p((coef + 15) // 16 * 16), sp)
+                        bargs = (bd, xp_, dyp_, dxp_, None, gp_, smp, sip, scp, shp, dgp, dbp, wsp_, sp)
                     d, hp, wp = op.dfull, op.p4[0], op.p4[1]
                     nc = d.n // nch
                     rows = nc * d.p * d.q
@@ -1604,6 +1615,22 @@ class Executor:
                                                     op.bnred_blocks, self._p(self.act(x)), self._p(dy), self._p(out),
                                                     self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc, op.sh,
                                                     self._gp(op.gamma), self._gp(op.beta), wsp, sp))
+                elif bwd_fusion and not op.desc.dy2 and not op.desc.clip and w and w[0] == "pool" and dy is w[4] and \
+                        op.y.c == op.y.cp and self.dtype == BF16 and os.environ.get("RN_POOL_BN_FUSION", "1") == "1" and \
+                        int(self.lib.rn_pool_bwd_bnred_blocks(L.C.byref(w[2].desc))) > 0:
+                    # the max-pool backward that completes this BN's output gradient (the stem's bn0 ->
+                    # relu0 -> pool0) also reduces its backward; the BN then needs only finalize + apply
+                    _, pi, pop, pdy, pout, padd = w
+                    op.bnred_blocks = int(self.lib.rn_pool_bwd_bnred_blocks(L.C.byref(pop.desc)))
+                    op.bnred = self._zeros(op.bnred_blocks * op.y.cp * 2, self.torch.float32)
+                    self._bwd[pi] = self._call("rn_pool_bwd_bnred", L.C.byref(pop.desc), self._p(pdy),
+                                               self._p(pop.argmax), self._p(pout), self._p(padd),
+                                               self._p(self.act(x)), op.sm, op.sc, op.sh, int(op.relu),
+                                               self._p(op.bnred), sp)
+                    self._bwd.append(self._call("rn_bn_bwd_part", L.C.byref(op.desc), self._p(op.bnred),
+                                                op.bnred_blocks, self._p(self.act(x)), self._p(dy), self._p(out),
+                                                self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc, op.sh,
+                                                self._gp(op.gamma), self._gp(op.beta), wsp, sp))
                 elif getattr(op, "pre_part", None) is not None and not op.desc.dy2:
                     # the reduction was done by the residual add's ReLU backward (rn_relu_bwd_bnred)
                     self._bwd.append(self._call("rn_bn_bwd_part", L.C.byref(op.desc), self._p(op.pre_part),
@@ -1663,7 +1690,28 @@ class Executor:
                     # reductions from the same pass (rn_relu_bwd_bnred)
                     bns = [b for b in (getattr(op, "bn_a", None), getattr(op, "bn_b", None))
                            if b is not None and not b.use_global_stats and dy is not None]
-                    if bns and len(bns) == len([b for b in (op.bn_a, op.bn_b) if b is not None]):
+                    w = self._gw.get(id(op.y))
+                    fuse = bool(bns and len(bns) == len([b for b in (op.bn_a, op.bn_b) if b is not None]) and
+                                w and w[0] == "dgrad" and dy is w[4] and self.dtype == BF16 and
+                                op.y.c == op.y.cp and op.y.c % 8 == 0 and w[2].groups == 1 and
+                                os.environ.get("RN_RELU_BNRED_DGRAD", "1") == "1" and
+                                int(self.lib.rn_conv_tile(L.C.byref(w[2].desc), 1)) >= 128)
+                    if fuse:
+                        # the data gradient that completes dL/dy (the next unit's conv1, accumulating the
+                        # shortcut's gradient) stores g = its value * [y > 0] and reduces the BNs itself
+                        # (rn_conv_bwd_data_relu_bnred): dL/dy is never written
+                        _, ci, cop, cdy, cout, cadd = w
+                        nrb = int(self.lib.rn_conv_bnred_blocks(L.C.byref(cop.desc)))
+                        for b in bns:
+                            b.pre_nrb = nrb
+                            b.pre_part = self._zeros(nrb * b.x.cp * 2, self.torch.float32)
+                        b2 = bns[1] if len(bns) == 2 else None
+                        self._bwd[ci] = self._call(
+                            "rn_conv_bwd_data_relu_bnred", L.C.byref(cop.desc), self._p(cdy), self._p(cop.wc),
+                            self._p(gbuf), self._p(cadd), self._p(self.act(op.y)), self._p(self.act(bns[0].x)),
+                            bns[0].sm, self._p(bns[0].pre_part), self._p(self.act(b2.x)) if b2 else None,
+                            b2.sm if b2 else None, self._p(b2.pre_part) if b2 else None, sp)
+                    elif bns and len(bns) == len([b for b in (op.bn_a, op.bn_b) if b is not None]):
                         for b in bns:
                             b.pre_nrb = int(self.lib.rn_bn_reduce_blocks(L.C.byref(b.desc)))
                             b.pre_part = self._zeros(b.pre_nrb * b.x.cp * 2, self.torch.float32)
@@ -1686,6 +1734,7 @@ class Executor:
                     out, add = gs.contribute(x)
                     self._bwd.append(self._call("rn_pool_bwd", L.C.byref(op.desc), self._p(dy), self._p(op.argmax),
                                                 self._p(out), self._p(add), sp))
+                    self._gw[id(x)] = ("pool", len(self._bwd) - 1, op, dy, out, add)
 
     # ------------------------------------------------------------------ update
     def _build_update(self):

@@ -66,6 +66,7 @@ SIGNATURES = {
     "rn_bn_bwd_part": (_i32, [_P, _P, _i64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rn_bn_bwd_finalize": (_i32, [_P, _P, _i64, _P, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_data_bnapply": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P]),
+    "rn_conv_bwd_data_relu_bnred": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_data": (_i32, [_P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_filter": (_i32, [_P, _P, _P, _P, _P]),
     "rn_conv_wgrad_ws_bytes": (_i64, [_P]),
@@ -96,6 +97,8 @@ SIGNATURES = {
     "rn_pool_desc_init": (_i32, [_P]),
     "rn_pool_fwd": (_i32, [_P, _P, _P, _P, _P]),
     "rn_pool_bwd": (_i32, [_P, _P, _P, _P, _P, _P]),
+    "rn_pool_bwd_bnred": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P, _P]),
+    "rn_pool_bwd_bnred_blocks": (_i64, [_P]),
     "rn_softmax_output": (_i32, [_i32, _i32, _i32, _i32, _P, _P, _P, _P, _f32, _P, _P]),
     "rn_col_sum": (_i32, [_i32, _i64, _i32, _i32, _P, _P, _i32, _P]),
     "rn_sgd_mom_update": (_i32, [_i32, _P, _P, _P, _P, _P, _P, _P, _i32, _f32, _P, _f32, _f32, _f32, _P]),

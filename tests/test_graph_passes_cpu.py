@@ -277,7 +277,13 @@ def test_stem_backward_chunked(dry, monkeypatch):
     ex = _bind(sym, shape=(8, 3, 64, 64), precision="bfloat16").executor
     names = _call_names(ex._bwd)
     i = names.index("rn_bn_bwd_apply_rows")
-    assert names[i - 1] == "rn_bn_bwd" and ex._bwd[i - 1][2][3] is None
+    # bn0's reduction done by the max-pool backward (rn_pool_bwd_bnred): finalize only, then the rows
+    assert names[i - 1] == "rn_bn_bwd_finalize" and "rn_pool_bwd_bnred" in names[:i]
+    monkeypatch.setenv("RN_BN_BWD_FUSION", "0")
+    names0 = _call_names(_bind(sym, shape=(8, 3, 64, 64), precision="bfloat16").executor._bwd)
+    i0 = names0.index("rn_bn_bwd_apply_rows")
+    assert names0[i0 - 1] == "rn_bn_bwd" and "rn_pool_bwd_bnred" not in names0
+    monkeypatch.delenv("RN_BN_BWD_FUSION")
     assert names[i:i + 8] == ["rn_bn_bwd_apply_rows", "rn_stem_conv_wgrad_p4"] * 4
     rows = [ex._bwd[i + 2 * j][2][8:10] for j in range(4)]
     m = ex._bwd[i - 1][2][0]._obj.m

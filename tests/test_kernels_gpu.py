@@ -1437,6 +1437,108 @@ def test_maxpool_block_bwd(gpu, dtype, with_add):
     assert rel_err(from_nhwc(out[0], c), dx_ref) < TOL[dtype]
 
 
+@pytest.mark.parametrize("case", [(2, 256, 14, 14, 128, True), (2, 512, 7, 9, 256, False),
+                                  (3, 256, 10, 12, 64, True), (2, 1024, 7, 7, 256, True), (1, 128, 30, 30, 256, False)])
+@pytest.mark.parametrize("with_add", [False, True])
+def test_dgrad_relu_bnred_unit_tail(gpu, case, with_add, big_tiles):
+    """rn_conv_bwd_data_relu_bnred (the post-activation unit tail's backward in the epilogue of the next
+    unit's conv1 data gradient, symbol/resnext.py:41-47) == rn_conv_bwd_data + rn_relu_bwd_bnred: g bit
+    for bit, both BNs' reductions vs the fp64 sums over the stored g."""
+    n, c, h, w, k, two = case
+    rng = np.random.default_rng(45)
+    wt = bf16_round(rng.standard_normal((k, c, 1, 1)) / np.sqrt(c))
+    dy = bf16_round(rng.standard_normal((n, k, h, w)))
+    y = bf16_round(np.maximum(rng.standard_normal((n, c, h, w)), 0))  # the unit's ReLU output (zeros: masked)
+    xa, xb = (bf16_round(rng.standard_normal((n, c, h, w)) + 0.5) for _ in range(2))
+    prev = bf16_round(rng.standard_normal((n, c, h, w)) * 0.5)
+    d = conv_desc(BF16, n, c, h, w, k, 1, 1, 1, 0)
+    lib = L.load()
+    assert lib.rn_conv_tile(C.byref(d), 1) >= 128
+    wc = torch.zeros(d.c * d.k_pad, dtype=torch.bfloat16, device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), None, p(wc), stream())
+    dyd, yd, xad, xbd, prevd = (to_nhwc(v, BF16, gpu) for v in (dy, y, xa, xb, prev))
+    mu_a = torch.tensor(rng.standard_normal(c) * 0.3 + 0.5, dtype=torch.float32, device=gpu)
+    mu_b = torch.tensor(rng.standard_normal(c) * 0.3 + 0.5, dtype=torch.float32, device=gpu)
+    nrb = lib.rn_conv_bnred_blocks(C.byref(d))
+    pa, pb = (torch.full((nrb * c * 2,), float("nan"), dtype=torch.float32, device=gpu) for _ in range(2))
+    g1 = torch.zeros_like(yd)
+    L.call("rn_conv_bwd_data_relu_bnred", C.byref(d), p(dyd), p(wc), p(g1), p(prevd) if with_add else None, p(yd),
+           p(xad), p(mu_a), p(pa), p(xbd) if two else None, p(mu_b) if two else None, p(pb) if two else None,
+           stream())
+    bd = L.BNDesc(dtype=BF16, m=n * h * w, c=c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=0)
+    nrb2 = lib.rn_bn_reduce_blocks(C.byref(bd))
+    qa, qb = (torch.zeros(nrb2 * c * 2, dtype=torch.float32, device=gpu) for _ in range(2))
+    d1 = prevd.clone() if with_add else torch.zeros_like(yd)
+    L.call("rn_conv_bwd_data", C.byref(d), p(dyd), p(wc), p(d1), p(d1) if with_add else None, stream())
+    g2 = torch.zeros_like(yd)
+    L.call("rn_relu_bwd_bnred", C.byref(bd), p(yd), p(d1), p(g2), p(xad), p(mu_a), p(qa), p(xbd) if two else None,
+           p(mu_b) if two else None, p(qb) if two else None, stream())
+    torch.cuda.synchronize()
+    assert torch.equal(g1, g2)
+    assert not torch.isnan(pa).any() and (not two or not torch.isnan(pb).any())
+    gf = g1.double().view(-1, c)
+    for part, x, mu, on in ((pa, xad, mu_a, True), (pb, xbd, mu_b, two)):
+        if not on:
+            continue
+        s = part.view(nrb, c, 2).double().sum(0)
+        xc = x.double().view(-1, c) - mu.double()
+        ref = torch.stack([gf.sum(0), (gf * xc).sum(0)], 1)
+        bound = torch.stack([gf.abs().sum(0), (gf * xc).abs().sum(0)], 1)
+        assert float(((s - ref).abs() / (bound + 1e-30)).max()) < 1e-5
+
+
+@pytest.mark.parametrize("case", [(3, 64, 14, 12), (2, 16, 22, 18), (1, 256, 8, 8), (5, 64, 36, 40)])
+@pytest.mark.parametrize("with_add", [False, True])
+def test_maxpool_bwd_bn_backward_fusion(gpu, case, with_add):
+    """rn_pool_bwd_bnred + rn_bn_bwd_part (the stem's bn0 -> relu0 -> pool0 backward, symbol/resnet.py:
+    94-97, the BN reduction in the pool backward) == rn_pool_bwd (dx bit for bit) followed by the
+    oracle's BatchNorm+ReLU backward on the stored gradient."""
+    n, c, h, w = case
+    rng = np.random.default_rng(44)
+    xb = bf16_round(rng.standard_normal((n, c, h, w)) * 1.5 + 0.3)  # BN input
+    gamma, beta = rng.uniform(0.5, 1.5, c), rng.standard_normal(c) * 0.2
+    a_ref, cache = ops.bn_train_fwd(xb, gamma, beta, 1e-5, False)
+    d = L.PoolDesc(dtype=BF16, n=n, h=h, w=w, c=c, r=3, s=3, stride_h=2, stride_w=2, pad_h=1, pad_w=1,
+                   type=L.RN_POOL_MAX, global_pool=0)
+    L.call("rn_pool_desc_init", C.byref(d))
+    lib = L.load()
+    nrb = lib.rn_pool_bwd_bnred_blocks(C.byref(d))
+    assert nrb > 0
+    bd = L.BNDesc(dtype=BF16, m=n * h * w, c=c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1)
+    f = lambda a: torch.tensor(np.asarray(a, np.float64), dtype=torch.float32, device=gpu)
+    g_d, b_d, mm, mv = f(gamma), f(beta), f(np.zeros(c)), f(np.ones(c))
+    sm, si, sc, sh = [torch.zeros(c, dtype=torch.float32, device=gpu) for _ in range(4)]
+    ws = torch.zeros(lib.rn_bn_workspace_bytes(C.byref(bd)) // 4 + 16, dtype=torch.float32, device=gpu)
+    xbd = to_nhwc(xb, BF16, gpu)
+    act = torch.zeros_like(xbd)
+    L.call("rn_bn_fwd_train", C.byref(bd), p(xbd), p(act), p(g_d), p(b_d), p(mm), p(mv), p(sm), p(si), p(sc), p(sh),
+           p(ws), stream())
+    yd = torch.zeros((n, d.p, d.q, c), dtype=torch.bfloat16, device=gpu)
+    am = torch.zeros(yd.numel(), dtype=torch.uint8, device=gpu)
+    L.call("rn_pool_fwd", C.byref(d), p(act), p(yd), p(am), stream())
+    dyd = to_nhwc(bf16_round(rng.standard_normal((n, c, d.p, d.q))), BF16, gpu)
+    prev = to_nhwc(bf16_round(rng.standard_normal((n, c, h, w)) * 0.5), BF16, gpu)
+    dact = prev.clone() if with_add else torch.zeros_like(xbd)  # (accumulated in place: add_src = out)
+    plain = dact.clone()
+    part = torch.full((nrb * c * 2,), float("nan"), dtype=torch.float32, device=gpu)  # every slot written
+    addp = (lambda t: p(t) if with_add else None)
+    L.call("rn_pool_bwd_bnred", C.byref(d), p(dyd), p(am), p(dact), addp(dact), p(xbd), p(sm), p(sc), p(sh), 1,
+           p(part), stream())
+    L.call("rn_pool_bwd", C.byref(d), p(dyd), p(am), p(plain), addp(plain), stream())
+    dx = torch.zeros_like(xbd)
+    dg, db = torch.zeros(c, dtype=torch.float32, device=gpu), torch.zeros(c, dtype=torch.float32, device=gpu)
+    L.call("rn_bn_bwd_part", C.byref(bd), p(part), nrb, p(xbd), p(dact), p(dx), None, p(g_d), p(sm), p(si), p(sc),
+           p(sh), p(dg), p(db), p(ws), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dact, plain)
+    assert not torch.isnan(part).any()
+    dz = ops.relu_bwd(from_nhwc(dact, c), from_nhwc(act, c))  # the stored gradient, the stored ReLU output
+    dx_ref, dg_ref, db_ref = ops.bn_train_bwd(dz, cache, False)
+    assert rel_err(db.cpu().numpy(), db_ref) < 1e-4
+    assert rel_err(dg.cpu().numpy(), dg_ref) < 1e-4
+    assert rel_err(from_nhwc(dx, c), dx_ref) < 3e-2
+
+
 @pytest.mark.parametrize("case", GCONV_CASES[:4])
 def test_grouped_conv_zero_block_skip(gpu, case):
     """rn_set_tuning 13 / 14: the grouped 64-column tiles skip the MFMAs of their block-diagonal zero

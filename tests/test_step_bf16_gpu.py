@@ -225,8 +225,12 @@ def _c4_layerwise(n, image):
     assert not ck.skipped, ck.skipped
     kinds = {r[0] for r in ck.rec}
     # (the grouped data gradients carry their BN-backward reduction: direct kernel or block-diagonal tile)
+    # (the unit tails' backward in the next unit's conv1 data gradient, rn_conv_bwd_data_relu_bnred; the
+    # last unit's -- its gradient comes from the pooling -- in rn_relu_bwd_bnred)
     assert {"conv_fwd", "conv_fwd_grouped", "dgrad_bnred_grouped", "wgrad_grouped", "wgrad", "bn_apply_add",
-            "relu_bwd_bnred", "bn_fwd", "bn_bwd_dx", "bn_bwd_params", "weight_copy"} <= kinds, kinds
+            "dgrad_relu_bnred", "relu_bwd_bnred", "bn_fwd", "bn_bwd_dx", "bn_bwd_params",
+            "weight_copy"} <= kinds, kinds
+    assert sum(1 for r in ck.rec if r[0] in ("dgrad_relu_bnred", "relu_bwd_bnred")) == 16
     assert sum(1 for r in ck.rec if r[0] == "conv_fwd_grouped") == 16
     assert sum(1 for r in ck.rec if r[0] in ("dgrad_grouped", "dgrad_bnred_grouped")) == 16
     assert sum(1 for r in ck.rec if r[0] in ("wgrad", "wgrad_grouped")) == 54  # 53 convs + fc1

@@ -182,15 +182,16 @@ def test_plan_bn_apply_fusion_opt_in(monkeypatch):
 def test_plan_bn_bwd_fusion_default(monkeypatch):
     """RN_BN_BWD_FUSION: the BN backward reduction rides in the dgrad epilogue that completes the
     BN's output gradient -- by default (1) where that dgrad runs the 256-row tile (41 of 50 here),
-    with 2 on every eligible dgrad (48: bn0 and the final bn1 get theirs from pooling), 0 never."""
+    with 2 on every eligible dgrad (48: bn0 and the final bn1 get theirs from pooling), 0 never; bn0's
+    rides in the stem max-pool's backward (rn_pool_bwd_bnred) unless 0."""
     def counts():
         ex = Executor(Plan(graphs.resnet50(), [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")
         names = [c[0] for c in ex._bwd]
         return names.count("rn_conv_bwd_data_bnred"), names.count("rn_bn_bwd_part"), names.count("rn_bn_bwd")
     monkeypatch.delenv("RN_BN_BWD_FUSION", raising=False)
-    assert counts() == (41, 41, 9)
+    assert counts() == (41, 42, 8)
     monkeypatch.setenv("RN_BN_BWD_FUSION", "2")
-    assert counts() == (48, 48, 2)
+    assert counts() == (48, 49, 1)
     monkeypatch.setenv("RN_BN_BWD_FUSION", "0")
     assert counts() == (0, 0, 50)
 
