@@ -1694,12 +1694,15 @@ class Executor:
                     fuse = bool(bns and len(bns) == len([b for b in (op.bn_a, op.bn_b) if b is not None]) and
                                 w and w[0] == "dgrad" and dy is w[4] and self.dtype == BF16 and
                                 op.y.c == op.y.cp and op.y.c % 8 == 0 and w[2].groups == 1 and
-                                os.environ.get("RN_RELU_BNRED_DGRAD", "1") == "1" and
+                                os.environ.get("RN_RELU_BNRED_DGRAD", "0") == "1" and
                                 int(self.lib.rn_conv_tile(L.C.byref(w[2].desc), 1)) >= 128)
                     if fuse:
                         # the data gradient that completes dL/dy (the next unit's conv1, accumulating the
                         # shortcut's gradient) stores g = its value * [y > 0] and reduces the BNs itself
-                        # (rn_conv_bwd_data_relu_bnred): dL/dy is never written
+                        # (rn_conv_bwd_data_relu_bnred): dL/dy is never written. Opt-in
+                        # (RN_RELU_BNRED_DGRAD=1): measured slower, C4 28.97 / 29.00 vs 28.03 / 27.98 ms
+                        # per step -- the epilogue streams its three extra tensors at ~3.5 TB/s, the
+                        # separate pass at ~5.5 (15 data gradients 6.0 ms vs 2.7 + 2.2 ms)
                         _, ci, cop, cdy, cout, cadd = w
                         nrb = int(self.lib.rn_conv_bnred_blocks(L.C.byref(cop.desc)))
                         for b in bns:

@@ -219,17 +219,18 @@ def test_resnext50_bf16_full_size_layerwise(gpu):
     _c4_layerwise(256, 224)
 
 
-def _c4_layerwise(n, image):
+def _c4_layerwise(n, image, tail_in_dgrad=False):
     from rn import graphs
     ck = _layerwise(graphs.resnext50_32x4d(), n, image, "bfloat16", warm=1)
     assert not ck.skipped, ck.skipped
     kinds = {r[0] for r in ck.rec}
     # (the grouped data gradients carry their BN-backward reduction: direct kernel or block-diagonal tile)
-    # (the unit tails' backward in the next unit's conv1 data gradient, rn_conv_bwd_data_relu_bnred; the
-    # last unit's -- its gradient comes from the pooling -- in rn_relu_bwd_bnred)
+    # (RN_RELU_BNRED_DGRAD=1: the unit tails' backward in the next unit's conv1 data gradient,
+    # rn_conv_bwd_data_relu_bnred; the last unit's -- its gradient comes from the pooling -- and, by
+    # default, every unit's in rn_relu_bwd_bnred)
     assert {"conv_fwd", "conv_fwd_grouped", "dgrad_bnred_grouped", "wgrad_grouped", "wgrad", "bn_apply_add",
-            "dgrad_relu_bnred", "relu_bwd_bnred", "bn_fwd", "bn_bwd_dx", "bn_bwd_params",
-            "weight_copy"} <= kinds, kinds
+            "relu_bwd_bnred", "bn_fwd", "bn_bwd_dx", "bn_bwd_params", "weight_copy"} <= kinds, kinds
+    assert ("dgrad_relu_bnred" in kinds) == tail_in_dgrad, kinds
     assert sum(1 for r in ck.rec if r[0] in ("dgrad_relu_bnred", "relu_bwd_bnred")) == 16
     assert sum(1 for r in ck.rec if r[0] == "conv_fwd_grouped") == 16
     assert sum(1 for r in ck.rec if r[0] in ("dgrad_grouped", "dgrad_bnred_grouped")) == 16
@@ -290,6 +291,13 @@ def test_resnet50_bf16_layerwise_act2_on_load(gpu, monkeypatch):
 def test_resnext50_bf16_layerwise_small(gpu):
     """The C4 per-kernel checks at 8 images of 64x64 (a fast first gate before the full size)."""
     _c4_layerwise(8, 64)
+
+
+def test_resnext50_bf16_layerwise_tail_in_dgrad(gpu, monkeypatch):
+    """The opt-in unit-tail backward in the next unit's conv1 data-gradient epilogue
+    (RN_RELU_BNRED_DGRAD=1, rn_conv_bwd_data_relu_bnred), per kernel at 8 images of 112x112."""
+    monkeypatch.setenv("RN_RELU_BNRED_DGRAD", "1")
+    _c4_layerwise(8, 112, tail_in_dgrad=True)
 
 
 def test_resnet50_int8_layerwise_small(gpu):
