@@ -30,6 +30,13 @@ int chip_cus() {
   }();
   return cus;
 }
+// CUs the weight gradients size their split-M grids for: the chip, scaled by rn_set_tuning 21 (percent;
+// 0 = 100). They share the chip with the data-gradient chain on the other stream, so a smaller grid
+// (fewer slabs to reduce) may cost them nothing
+int wgrad_cus() {
+  const int pct = g_tune[RN_TUNE_WGRAD_SPLIT] > 0 ? g_tune[RN_TUNE_WGRAD_SPLIT] : 100;
+  return std::max(8, chip_cus() * pct / 100);
+}
 
 // ------------------------------------------------------------------------------ igemm
 struct IgemmCls {
@@ -3917,7 +3924,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     g.in_sc = in_scale; g.in_sh = in_shift;
     const int cs = db == 1 ? 64 : 128, ks = db == 1 ? 64 : 32;
     const int slices = (d->c / cs) * (d->k / ks);
-    const int64_t want = std::max<int64_t>(1, chip_cus() / slices);  // (the slab stays ~ CUs x slice)
+    const int64_t want = std::max<int64_t>(1, wgrad_cus() / slices);  // (the slab stays ~ CUs x slice)
     g.ipw = (int)ceil_div(d->n, std::min<int64_t>(d->n, want));
     const int64_t split = ceil_div(d->n, g.ipw);
     if (!launch) return finish(split, "wgrad_dband");
@@ -3948,7 +3955,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     GbArgs g{};
     g.x = (const bf16_t*)x; g.dy = (const bf16_t*)dy; g.N = d->n; g.H = d->h; g.W = d->w; g.C = d->c;
     const int slices = gb == 3 ? 2 : 1;
-    g.ipw = (int)std::max<int64_t>(1, ceil_div((int64_t)d->n * slices, chip_cus()));
+    g.ipw = (int)std::max<int64_t>(1, ceil_div((int64_t)d->n * slices, wgrad_cus()));
     const int64_t split = ceil_div(d->n, g.ipw);
     const int64_t need = split * a.K * (int64_t)a.ldw * 4;  // (a.ldw = 9 * channels per group)
     if (ws_need) *ws_need = need;
@@ -3974,7 +3981,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
       d->c_real == d->c && d->k_pad == d->k && g_tune[RN_TUNE_WGRAD_BAND] != 1 &&
       (int64_t)a.M * (d->k + d->c) * 2 < INT32_MAX) {
     const int64_t mtiles = ceil_div(a.M, 64);
-    const int64_t split = std::min<int64_t>(chip_cus(), std::max<int64_t>(1, mtiles / 4));
+    const int64_t split = std::min<int64_t>(wgrad_cus(), std::max<int64_t>(1, mtiles / 4));
     a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
     const int64_t nsplit = ceil_div(a.M, a.m_per_split);
     if (!launch) return finish(nsplit, "wgrad_stream");
@@ -4036,7 +4043,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     a.nkt = (int)ceil_div(a.K, 128);
     const int64_t tiles = (int64_t)a.nct * a.nkt;
     const int64_t mtiles = ceil_div(a.M, 64);
-    const int64_t target = chip_cus() * (g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU] > 0 ? g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU] : 2);
+    const int64_t target = wgrad_cus() * (g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU] > 0 ? g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU] : 2);
     int64_t split = std::min<int64_t>(std::max<int64_t>(1, target / tiles), std::max<int64_t>(1, mtiles / 8));
     a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
     split = ceil_div(a.M, a.m_per_split);
@@ -4052,7 +4059,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     a.nkt = (int)ceil_div(a.K, bmk);
     const int64_t tiles = (int64_t)a.nct * a.nkt;
     const int64_t mtiles = ceil_div(a.M, 64);
-    int64_t split = std::min<int64_t>(std::max<int64_t>(1, 256 / tiles), std::max<int64_t>(1, mtiles / 4));
+    int64_t split = std::min<int64_t>(std::max<int64_t>(1, wgrad_cus() / tiles), std::max<int64_t>(1, mtiles / 4));
     a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
     split = ceil_div(a.M, a.m_per_split);
     if (!launch) return finish(split, "wgrad_big");
@@ -4080,7 +4087,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
   // variants keep the 64x64 tile's 5.) The chip size is chip_cus(): the device's CU count, cached
   // once per process (rn_conv_wgrad_ws_bytes sizes the slab workspace from this same split at plan
   // time, and the launch agrees with it), 256 on a host without a GPU (plan-only dry runs).
-  const int kSplitCus = chip_cus();
+  const int kSplitCus = wgrad_cus();
   int per_cu = (grouped && a.gdiag) ? 8 : (bmk == 128 && bnc == 128) ? 2 : (bmk == 64 && bnc == 64) ? (in_scale ? 4 : 5) : 3;
   if (g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU] > 0) per_cu = g_tune[RN_TUNE_WGRAD_BLOCKS_PER_CU];
   int64_t want = std::max<int64_t>(1, (int64_t)per_cu * kSplitCus / tiles);

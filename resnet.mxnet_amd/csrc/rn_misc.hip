@@ -633,7 +633,7 @@ template <typename T, bool RELU, int NQ, bool NT = false>
 __global__ __launch_bounds__(256) void bnq_codes_kernel(const T* __restrict__ x, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, int64_t m, int c, int ct,
                                                         int64_t rows_per_block, BnqTargets tg,
-                                                        const float* __restrict__ thr) {
+                                                        const float* __restrict__ thr, int exact_div) {
   float t[NQ], unit[NQ];
 #pragma unroll
   for (int k = 0; k < NQ; ++k) {
@@ -653,18 +653,37 @@ __global__ __launch_bounds__(256) void bnq_codes_kernel(const T* __restrict__ x,
     sc[e] = scale[cb + e];
     sh[e] = shift[cb + e];
   }
+  float inv[NQ];
+#pragma unroll
+  for (int k = 0; k < NQ; ++k) inv[k] = unit[k] > 0.f ? 1.f / unit[k] : 0.f;
   for (int64_t r = r0 + tr; r < r1; r += rl) {
     float f[16];
     bnq_load<T, RELU, NT>(x + r * c + cb, sc, sh, f);
     const int64_t off = r * c + cb;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
-      float g[16];
+      float g[16], tq[16];
       uint32_t cw[4];
+      // the quotient v / unit as v * (1 / unit): within 2^-22 |q| of the IEEE quotient, so the two
+      // round alike unless the product lies that close to a half-integer -- then (rarely: checked per
+      // wave) the exact division, so the codes stay those of round(v / unit) bit for bit (this kernel is
+      // VALU-bound, and the division's ~11 instructions per element were a third of it)
+      uint32_t nearm = exact_div ? 0xFFFFu : 0u;  // (rn_set_tuning 22 = 1: the division everywhere)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        tq[e] = fminf(fmaxf(f[e], -t[k]), t[k]) * inv[k];
+        // (written as !(>) so that a non-finite product -- a unit so small its reciprocal overflows --
+        // takes the exact path too)
+        if (!(fabsf(fabsf(tq[e] - truncf(tq[e])) - 0.5f) > fabsf(tq[e]) * 4.8e-7f)) nearm |= 1u << e;
+      }
+      if (__any(nearm != 0u)) {
+#pragma unroll
+        for (int e = 0; e < 16; ++e)
+          if ((nearm >> e) & 1u) tq[e] = fminf(fmaxf(f[e], -t[k]), t[k]) / unit[k];
+      }
 #pragma unroll
       for (int e = 0; e < 16; ++e) {  // quant_codes_kernel's clip / round / dequantize
-        const float v = fminf(fmaxf(f[e], -t[k]), t[k]);
-        const float q = unit[k] > 0.f ? roundf(v / unit[k]) : 0.f;
+        const float q = unit[k] > 0.f ? roundf(tq[e]) : 0.f;
         g[e] = q * unit[k];
         const uint32_t b = (uint32_t)(uint8_t)(int8_t)(int)q;
         if ((e & 3) == 0) cw[e >> 2] = b;
@@ -773,7 +792,7 @@ __global__ void quant_state_multi_kernel(float* __restrict__ curmax, float* minm
 
 }  // namespace
 
-int g_tune[RN_TUNE_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512, 0, 0, 0, 0, 0, 0, 0, 23, 0, 0};
+int g_tune[RN_TUNE_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512, 0, 0, 0, 0, 0, 0, 0, 23, 0, 0, 0, 0};
 
 extern "C" {
 
@@ -1300,10 +1319,10 @@ static void launch_quant_codes_bn(const rn_bn_desc* d, const void* x, const floa
   const auto g = geo(8);
   if (g_tune[RN_TUNE_BN_NT] & 8)
     hipLaunchKernelGGL((bnq_codes_kernel<T, RELU, NQ, true>), dim3(gx, g.first), dim3(256), 0, st, (const T*)x, scale,
-                       shift, d->m, d->c, ct, g.second, tg, thr);
+                       shift, d->m, d->c, ct, g.second, tg, thr, g_tune[RN_TUNE_QUANT_DIV] == 1 ? 1 : 0);
   else
     hipLaunchKernelGGL((bnq_codes_kernel<T, RELU, NQ>), dim3(gx, g.first), dim3(256), 0, st, (const T*)x, scale,
-                       shift, d->m, d->c, ct, g.second, tg, thr);
+                       shift, d->m, d->c, ct, g.second, tg, thr, g_tune[RN_TUNE_QUANT_DIV] == 1 ? 1 : 0);
 }
 template <int NQ>
 static int quant_codes_bn(const rn_bn_desc* d, const void* x, const float* scale, const float* shift,

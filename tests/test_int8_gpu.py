@@ -209,6 +209,45 @@ def test_quant_codes_bn_fused(gpu, dtype, relu, m, c):
 
 
 @pytest.mark.parametrize("dtype", [F32, BF16])
+def test_quant_codes_bn_ties(gpu, dtype):
+    """The fused quantizer forms the quotient v / unit as v * (1 / unit) and takes the exact division
+    only near a half-integer: with unit = 2^-6 (threshold 127 * 2^-6, inference mode) every input
+    (2k + 1) / 128 is an exact tie, which must round half away from zero as round(v / unit) does --
+    codes and values bit for bit against rn_bn_apply + rn_quant_int8_fwd_codes and numpy."""
+    k = np.arange(-130, 130)
+    vals = (2 * k + 1) / 128.0                       # ties (+ a few past the clip at +-127 * 2^-6)
+    m, c = 64, 16
+    rng = np.random.default_rng(3)
+    x = torch.tensor(rng.choice(vals, size=(m, c)), dtype=tdt(dtype), device=gpu)
+    sc = torch.ones(c, dtype=torch.float32, device=gpu)
+    sh = torch.zeros(c, dtype=torch.float32, device=gpu)
+    d = L.BNDesc(dtype=dtype, m=m, c=c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=0)
+    ws = torch.zeros(4096, dtype=torch.float32, device=gpu)
+    outs = []
+    for fused in (False, True):
+        out = torch.zeros_like(x)
+        codes = torch.zeros(m * c, dtype=torch.int8, device=gpu)
+        unit = torch.zeros(1, dtype=torch.float32, device=gpu)
+        mm = torch.tensor([127 / 64.0], dtype=torch.float32, device=gpu)
+        if fused:
+            L.call("rn_quant_int8_fwd_codes_bn", C.byref(d), p(x), p(sc), p(sh), p(out), p(codes), p(unit), p(mm),
+                   0, 0.99, 0, 8, p(ws), stream())
+        else:
+            y = torch.zeros_like(x)
+            L.call("rn_bn_apply", C.byref(d), p(x), p(y), p(sc), p(sh), stream())
+            L.call("rn_quant_int8_fwd_codes", dtype, m * c, p(y), p(out), p(codes), p(unit), p(mm), 0, 0, 0.99,
+                   0, 8, p(ws), stream())
+        outs.append((out, codes, unit))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert outs[1][2].item() == 1 / 64.0
+    xv = x.double().cpu().numpy()
+    ref = np.sign(xv) * np.floor(np.abs(np.clip(xv, -127 / 64, 127 / 64)) * 64 + 0.5)  # half away from zero
+    np.testing.assert_array_equal(outs[1][1].cpu().numpy().reshape(m, c), ref.astype(np.int8))
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
 @pytest.mark.parametrize("m,c", [(3136, 64), (1001, 48)])
 def test_quant_codes_bn_pair(gpu, dtype, m, c):
     """rn_quant_int8_fwd_codes_bn2 (the two quantizers of one BN output, symbol/resnet_int8.py's first
