@@ -221,6 +221,23 @@ int rn_im2col_nchw_quant(const rn_conv_desc* d, const float* x_nchw, const float
 int rn_stem_quant_clip_grad(const rn_conv_desc* d, const float* x_nchw, const float* scale,
                             const float* shift, const float* minmax, const void* dy, const float* w_q,
                             float* dbeta, rn_stream_t stream);
+/* The same clip gradient as a weight gradient (bf16 NHWC-8 stem image x8, 2 * c_real <= 8): dbeta[c]
+ * -= sum_{k,r,s} w_q[k,r,s,c] * D[k,r,s,c], D = the stem convolution's weight gradient over the clip
+ * mask of channel c (1 where !(-t < x*scale + shift < t) on the fp32 input, t = *minmax).
+ * rn_stem_clip_mask writes the masks into x8's channels c_real .. 2 c_real - 1 (after the forward read
+ * x8; rn_stem_prepare rewrites them to zero next step); rn_stem_clip_wgrad computes the weight
+ * gradient over the real and mask channels into ext (float[k * r * s * 2 c_real], zeroed here),
+ * dw += its real part (ws / ws_bytes: the slab workspace, rn_stem_clip_wgrad_ws_bytes);
+ * rn_stem_clip_dbeta subtracts the mask part's dot product from dbeta (after rn_stem_shift_grad).
+ * rn_stem_clip_supported: 1 where these apply. */
+int32_t rn_stem_clip_supported(const rn_conv_desc* d);
+int rn_stem_clip_mask(const rn_conv_desc* d, const float* x_nchw, const float* scale, const float* shift,
+                      const float* minmax, void* x8, rn_stream_t stream);
+int64_t rn_stem_clip_wgrad_ws_bytes(const rn_conv_desc* d);
+int rn_stem_clip_wgrad(const rn_conv_desc* d, const void* x8, const void* dy, float* dw, float* ext, void* ws,
+                       int64_t ws_bytes, rn_stream_t stream);
+int rn_stem_clip_dbeta(const rn_conv_desc* d, const float* ext, const float* w_q, float* dbeta,
+                       rn_stream_t stream);
 
 /* d(beta) of a BN feeding the stem conv, without the stem dgrad:
  * dbeta[c] += sum_{k,r,s} w[k,r,s,c] * sum_{n,p,q valid(r,s)} dy[n,p,q,k].

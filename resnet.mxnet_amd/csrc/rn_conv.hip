@@ -4461,3 +4461,106 @@ int rn_stem_shift_grad(const rn_conv_desc* d, const void* dy, const float* wm, f
 }
 
 }  // extern "C"
+
+// ---- the int8 stem's clip gradient as a weight gradient (rn_stem_clip_mask / _wgrad / _dbeta)
+// The input quantizer's straight-through clip removes from bn_data's beta gradient the data gradient
+// at every clipped input: sum over clipped (n, c, h, w) of sum_{k,r,s} w[k,r,s,c] dy[n,p,q,k]. That is
+// sum_{k,r,s} w[k,r,s,c] * D[k,r,s,c] with D the weight gradient of the stem convolution over the CLIP
+// MASK of channel c: so the mask goes into the NHWC-8 image's free channels (c_real + c), the stem's
+// weight gradient computes D with the real dW at no extra operand traffic (it reads all 8 channels
+// anyway), and a 3-channel dot product finishes -- on the weight-gradient stream, instead of a gather
+// of 16 dy rows per clipped input on the compute stream at the step's end (stem_clip_grad_kernel).
+namespace {
+__global__ __launch_bounds__(256) void stem_clip_mask_kernel(const float* __restrict__ x, const float* __restrict__ scale,
+                                                             const float* __restrict__ shift,
+                                                             const float* __restrict__ minmax, bf16_t* __restrict__ x8,
+                                                             int64_t npix, int c, int hw) {
+  const float t = *minmax;
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < npix; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t img = i / hw, pix = i - img * hw;
+    uint4 u = reinterpret_cast<const uint4*>(x8)[i];
+    uint32_t w[4] = {u.x, u.y, u.z, u.w};
+    for (int e = 0; e < c; ++e) {
+      const float v = fmaf(x[(img * c + e) * hw + pix], scale[e], shift[e]);
+      const uint32_t m = (v > -t && v < t) ? 0u : 0x3F80u;  // bf16 1.0 where the clip zeroes the gradient
+      const int ch = c + e;
+      w[ch >> 1] = (ch & 1) ? ((w[ch >> 1] & 0x0000FFFFu) | (m << 16)) : ((w[ch >> 1] & 0xFFFF0000u) | m);
+    }
+    reinterpret_cast<uint4*>(x8)[i] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+// dw[k][rs][c] += ext[k][rs][c] for c < c_real (ext: [k][rs][2 c_real], the real channels then the masks)
+__global__ void stem_clip_split_kernel(const float* __restrict__ ext, float* __restrict__ dw, int krs, int c_real) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= krs * c_real) return;
+  const int t = i / c_real, c = i - t * c_real;
+  dw[i] += ext[(int64_t)t * 2 * c_real + c];
+}
+// dbeta[c] -= sum_{k,r,s} w[k][rs][c] * ext[k][rs][c_real + c]: one block per channel, a fixed order
+__global__ __launch_bounds__(256) void stem_clip_dbeta_kernel(const float* __restrict__ ext, const float* __restrict__ w,
+                                                              float* __restrict__ dbeta, int krs, int c_real) {
+  const int c = blockIdx.x;
+  float s = 0.f;
+  for (int t = threadIdx.x; t < krs; t += blockDim.x) s = fmaf(w[(int64_t)t * c_real + c], ext[(int64_t)t * 2 * c_real + c_real + c], s);
+  __shared__ float red[256];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dbeta[c] -= red[0];
+}
+bool stem_clip_ok(const rn_conv_desc* d) {
+  return d && d->dtype == RN_BF16 && d->groups <= 1 && d->c == 8 && d->c_real >= 1 && 2 * d->c_real <= 8;
+}
+rn_conv_desc stem_clip_ext(const rn_conv_desc* d) {  // the same convolution over the real + mask channels
+  rn_conv_desc e = *d;
+  e.c_real = 2 * d->c_real;
+  return e;
+}
+}  // namespace
+
+extern "C" {
+
+int32_t rn_stem_clip_supported(const rn_conv_desc* d) { return stem_clip_ok(d) ? 1 : 0; }
+
+int rn_stem_clip_mask(const rn_conv_desc* d, const float* x, const float* scale, const float* shift,
+                      const float* minmax, void* x8, rn_stream_t stream) {
+  RN_CHECK_ARG(d && x && scale && shift && minmax && x8, "null argument");
+  RN_CHECK_ARG(stem_clip_ok(d), "the clip mask needs the bf16 NHWC-8 stem image with 2 * c_real <= 8");
+  const int64_t npix = (int64_t)d->n * d->h * d->w;
+  hipLaunchKernelGGL(stem_clip_mask_kernel, dim3(grid_for(npix)), dim3(256), 0, as_stream(stream), x, scale, shift,
+                     minmax, (bf16_t*)x8, npix, d->c_real, d->h * d->w);
+  return rn_check_launch("stem_clip_mask");
+}
+
+int64_t rn_stem_clip_wgrad_ws_bytes(const rn_conv_desc* d) {
+  if (!stem_clip_ok(d)) return -1;
+  const rn_conv_desc e = stem_clip_ext(d);
+  return rn_conv_wgrad_ws_bytes(&e);
+}
+
+int rn_stem_clip_wgrad(const rn_conv_desc* d, const void* x8, const void* dy, float* dw, float* ext, void* ws,
+                       int64_t ws_bytes, rn_stream_t stream) {
+  RN_CHECK_ARG(d && x8 && dy && dw && ext, "null argument");
+  RN_CHECK_ARG(stem_clip_ok(d), "the clip weight gradient needs the bf16 NHWC-8 stem image with 2 * c_real <= 8");
+  const rn_conv_desc e = stem_clip_ext(d);
+  const int krs = d->k * d->r * d->s;
+  hipStream_t st = as_stream(stream);
+  if (hipMemsetAsync(ext, 0, sizeof(float) * (size_t)krs * e.c_real, st) != hipSuccess) return rn_check_launch("stem_clip_wgrad");
+  if (rn_conv_bwd_filter_ws(&e, x8, dy, ext, ws, ws_bytes, stream)) return -1;
+  hipLaunchKernelGGL(stem_clip_split_kernel, dim3((krs * d->c_real + 255) / 256), dim3(256), 0, st, ext, dw, krs,
+                     d->c_real);
+  return rn_check_launch("stem_clip_wgrad");
+}
+
+int rn_stem_clip_dbeta(const rn_conv_desc* d, const float* ext, const float* w_q, float* dbeta, rn_stream_t stream) {
+  RN_CHECK_ARG(d && ext && w_q && dbeta, "null argument");
+  RN_CHECK_ARG(stem_clip_ok(d), "the clip gradient needs the bf16 NHWC-8 stem image with 2 * c_real <= 8");
+  hipLaunchKernelGGL(stem_clip_dbeta_kernel, dim3(d->c_real), dim3(256), 0, as_stream(stream), ext, w_q, dbeta,
+                     d->k * d->r * d->s, d->c_real);
+  return rn_check_launch("stem_clip_dbeta");
+}
+
+}  // extern "C"

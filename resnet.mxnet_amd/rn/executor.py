@@ -847,10 +847,18 @@ class Executor:
             if self._side_stream is not None:
                 self._spv2.value = self._side_stream.cuda_stream if self.side_enabled else self._spv.value
 
-    WGRAD_CALLS = ("rn_conv_bwd_filter", "rn_conv_bwd_filter_ws", "rn_conv_bwd_filter_x", "rn_stem_conv_wgrad_p4")
+    WGRAD_CALLS = ("rn_conv_bwd_filter", "rn_conv_bwd_filter_ws", "rn_conv_bwd_filter_x", "rn_stem_conv_wgrad_p4",
+                   "rn_stem_clip_wgrad", "rn_stem_clip_dbeta")
     # side-stream calls that depend on the forward only, not on the backward so far: no fork of their own
     # (they run while the side stream waits for the next dy), except the first of a step
-    SIDE_PRE_CALLS = ("rn_quant_int8_expand",)
+    SIDE_PRE_CALLS = ("rn_quant_int8_expand", "rn_stem_clip_mask")
+
+    def _stem_clip_mask(self, op):
+        """Does the int8 stem's input-quantizer clip gradient ride in its weight gradient (bf16 NHWC-8
+        image, rn_stem_clip_*; RN_STEM_CLIP_MASK=0: the gather kernel rn_stem_quant_clip_grad)?"""
+        return bool(op.kind == "stem" and op.quant and op.bn and self.dtype == BF16 and not op.p4 and
+                    self.lib is not None and os.environ.get("RN_STEM_CLIP_MASK", "1") == "1" and
+                    self.lib.rn_stem_clip_supported(L.C.byref(op.dfull)))
 
     def _route_wgrads(self):
         """Bind the weight-gradient calls of the backward plan to the side stream.
@@ -1459,10 +1467,22 @@ class Executor:
             # (the stem's weight gradient; it needs a slab only in the deterministic mode)
             need += [int(self.lib.rn_conv_wgrad_ws_bytes(L.C.byref(op.dfull))) for op in plan.ops
                      if op.kind == "stem" and not op.p4]
+            need += [int(self.lib.rn_stem_clip_wgrad_ws_bytes(L.C.byref(op.dfull))) for op in plan.ops
+                     if op.kind == "stem" and self._stem_clip_mask(op)]
             self.wgrad_ws_bytes = max(need + [0])
             if self.wgrad_ws_bytes > 0:
                 self.wgrad_ws = self._zeros(self.wgrad_ws_bytes // 4, self.torch.float32)
         expanded = set()  # quantizers whose deferred values this plan expands (rn_quant_int8_expand)
+        for op in plan.ops:
+            if op.kind == "stem" and self._stem_clip_mask(op):
+                # the int8 stem's clip masks into the NHWC-8 image's free channels (rn_stem_clip_mask),
+                # first on the weight-gradient stream: its clip gradient then rides in the stem's weight
+                # gradient (rn_stem_clip_wgrad / rn_stem_clip_dbeta) instead of a gather at the step's end
+                _, _, sc, sh = op.bn_ptrs
+                op.clip_ext = self._zeros(op.dfull.k * op.dfull.r * op.dfull.s * 2 * op.dfull.c_real,
+                                          self.torch.float32)
+                self._bwd.append(self._call("rn_stem_clip_mask", L.C.byref(op.dfull), self._in_ptr, sc, sh,
+                                            self._ap(op.quant["minmax"]), self._p(op.x8), sp))
         for op in reversed(plan.ops):
             if op.kind == "softmax":
                 gs.has_value.add(id(op.x))  # dlogits written by the forward softmax call
@@ -1553,13 +1573,22 @@ class Executor:
                 elif op.p4:
                     self._bwd.append(self._call("rn_stem_conv_wgrad_p4", L.C.byref(op.dfull), self._p(op.x8),
                                                 self._p(dy), self._gp(op.weight), op.p4[0], op.p4[1], sp))
+                elif self._stem_clip_mask(op):
+                    ws = self.wgrad_ws is not None
+                    self._bwd.append(self._call("rn_stem_clip_wgrad", L.C.byref(op.dfull), self._p(op.x8),
+                                                self._p(dy), self._gp(op.weight), self._p(op.clip_ext),
+                                                self._p(self.wgrad_ws) if ws else None,
+                                                self.wgrad_ws_bytes if ws else 0, sp))
                 else:
                     self._bwd.append(self._wgrad_call(op.dfull, self._p(op.x8), self._p(dy), self._gp(op.weight), sp))
                 self.param_done_at[op.weight] = len(self._bwd)
                 if op.bn:
                     self._bwd.append(self._call("rn_stem_shift_grad", L.C.byref(op.dfull), self._p(dy),
                                                 op.wsrc, self._gp(op.bn["beta"]), self._p(self.stem_ws), sp))
-                    if op.quant:
+                    if op.quant and self._stem_clip_mask(op):
+                        self._bwd.append(self._call("rn_stem_clip_dbeta", L.C.byref(op.dfull), self._p(op.clip_ext),
+                                                    op.wsrc, self._gp(op.bn["beta"]), sp))
+                    elif op.quant:
                         _, _, sc, sh = op.bn_ptrs
                         self._bwd.append(self._call("rn_stem_quant_clip_grad", L.C.byref(op.dfull),
                                                     self._in_ptr, sc, sh, self._ap(op.quant["minmax"]),

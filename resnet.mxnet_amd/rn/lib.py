@@ -85,6 +85,11 @@ SIGNATURES = {
     "rn_im2col_nchw": (_i32, [_P, _P, _P, _P, _P, _i32, _P]),
     "rn_im2col_nchw_quant": (_i32, [_P, _P, _P, _P, _P, _i32, _f32, _i32, _i32, _P, _P, _i32, _P]),
     "rn_stem_quant_clip_grad": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
+    "rn_stem_clip_supported": (_i32, [_P]),
+    "rn_stem_clip_mask": (_i32, [_P, _P, _P, _P, _P, _P, _P]),
+    "rn_stem_clip_wgrad_ws_bytes": (_i64, [_P]),
+    "rn_stem_clip_wgrad": (_i32, [_P, _P, _P, _P, _P, _P, _i64, _P]),
+    "rn_stem_clip_dbeta": (_i32, [_P, _P, _P, _P, _P]),
     "rn_stem_shift_grad": (_i32, [_P, _P, _P, _P, _P, _P]),
     "rn_bn_workspace_bytes": (_i64, [_P]),
     "rn_bn_fwd_train": (_i32, [_P] * 13),

@@ -893,9 +893,33 @@ class Checker:
         conv0's data gradient (fix_gamma BatchNorm), from the weights conv0 ran with. With an input
         quantizer the clip gradient that follows completes it (checked there)."""
         d, dyp, wmp, dbp = args[0]._obj, args[1], args[2], args[3]
-        if any(nm == "rn_stem_quant_clip_grad" for nm, _, _ in self.ex._bwd):
+        if any(nm in ("rn_stem_quant_clip_grad", "rn_stem_clip_dbeta") for nm, _, _ in self.ex._bwd):
             return None, (lambda: None)
         return None, (lambda: self._stem_dbeta(d, dyp, wmp, dbp))
+
+    def _h_rn_stem_clip_mask(self, args, state):
+        return None, (lambda: None)  # (its masks: checked through the clip gradient they produce)
+
+    def _h_rn_stem_clip_wgrad(self, args, state):
+        """The int8 stem's weight gradient over the real and clip-mask channels: dW (real channels) vs the
+        oracle's; the mask part is checked through bn_data's beta gradient (rn_stem_clip_dbeta)."""
+        self._stem_dy = args[2]
+        return self._wgrad(args, state)
+
+    def _h_rn_stem_clip_dbeta(self, args, state):
+        """rn_stem_shift_grad + rn_stem_clip_wgrad's mask part + this == the clipped beta gradient of
+        _h_rn_stem_quant_clip_grad, with the same bars."""
+        d, wmp, dbp = args[0]._obj, args[2], args[3]
+        op = [o for o in self.ex.plan.ops if o.kind == "stem"][0]
+
+        def post():
+            x = op.x
+            data = self.ex._in_bufs[self.ex._in_idx].view(x.n, x.c, x.h, x.w).float()
+            sc, sh = op.bnbuf[16:16 + x.c], op.bnbuf[24:24 + x.c]
+            v = _fma(data, sc.view(1, -1, 1, 1), sh.view(1, -1, 1, 1))
+            t = self.aux_val(self.ex._ap(op.quant["minmax"]))
+            self._stem_dbeta(d, self._stem_dy, wmp, dbp, clip=((v > -t) & (v < t)).double())
+        return None, post
 
     def _h_rn_stem_quant_clip_grad(self, args, state):
         """rn_stem_shift_grad + this: dbeta[c] = sum of conv0's data gradient over the unclipped inputs,

@@ -760,6 +760,61 @@ def test_stem_quant(gpu, h, w):
     assert rel_err(dbeta.cpu().numpy(), dbeta_ref) < 1e-4
 
 
+@pytest.mark.parametrize("n,h,w,k", [(2, 20, 18, 64), (3, 32, 30, 64), (2, 19, 17, 32)])
+def test_stem_clip_as_weight_gradient(gpu, n, h, w, k):
+    """The int8 stem's clip gradient through its weight gradient (rn_stem_clip_mask / _wgrad / _dbeta:
+    the clip masks in the NHWC-8 image's free channels, their weight gradient dotted with the weights)
+    == rn_stem_quant_clip_grad's gather, and the real channels' dW == rn_conv_bwd_filter_ws on the
+    unmasked image; the masks themselves vs numpy."""
+    c, r, st, pd = 3, 7, 2, 3
+    rng = np.random.default_rng(46)
+    x = rng.uniform(-1, 1, (n, c, h, w)).astype(np.float32)
+    scale = np.array([1.5, 0.5, 2.0], dtype=np.float32)
+    shift = np.array([0.1, -0.2, 0.3], dtype=np.float32)
+    t = np.float32(1.1)                                  # clips part of the affine image
+    aff = x * scale[None, :, None, None] + shift[None, :, None, None]
+    mask_ref = ~((aff > -t) & (aff < t))
+    assert mask_ref.sum() > 20
+    dfull = conv_desc(BF16, n, 8, h, w, k, r, r, st, pd, c_real=c)
+    lib = L.load()
+    assert lib.rn_stem_clip_supported(C.byref(dfull)) == 1
+    x8h = np.zeros((n, h, w, 8), dtype=np.float32)
+    x8h[..., :c] = bf16_round(np.clip(aff, -t, t)).transpose(0, 2, 3, 1)   # (a stand-in for the quantized input)
+    x8 = torch.tensor(x8h, dtype=torch.bfloat16, device=gpu).contiguous()
+    x8_plain = x8.clone()
+    P, Q = dfull.p, dfull.q
+    dyd = to_nhwc(bf16_round(rng.standard_normal((n, k, P, Q))), BF16, gpu)
+    wq = ops.quant_int8_weight(rng.standard_normal((k, c, r, r)) * 0.1)[0]
+    master = _master_krsc(wq, gpu)
+    xd = torch.from_numpy(x).to(gpu)
+    sc, sh = torch.tensor(scale, device=gpu), torch.tensor(shift, device=gpu)
+    minmax = torch.tensor([float(t)], dtype=torch.float32, device=gpu)
+    sws = torch.zeros(P * Q * pad8(k) + P * r * k + k * r * r, dtype=torch.float32, device=gpu)
+    # the gather route
+    wsb = max(lib.rn_conv_wgrad_ws_bytes(C.byref(dfull)), lib.rn_stem_clip_wgrad_ws_bytes(C.byref(dfull)), 16)
+    ws = torch.zeros(wsb // 4 + 4, dtype=torch.float32, device=gpu)
+    dw_ref = torch.zeros(k * r * r * c, dtype=torch.float32, device=gpu)
+    L.call("rn_conv_bwd_filter_ws", C.byref(dfull), p(x8_plain), p(dyd), p(dw_ref), p(ws), wsb, stream())
+    dbeta_ref = torch.zeros(c, dtype=torch.float32, device=gpu)
+    L.call("rn_stem_shift_grad", C.byref(dfull), p(dyd), p(master), p(dbeta_ref), p(sws), stream())
+    L.call("rn_stem_quant_clip_grad", C.byref(dfull), p(xd), p(sc), p(sh), p(minmax), p(dyd), p(master),
+           p(dbeta_ref), stream())
+    # the weight-gradient route
+    L.call("rn_stem_clip_mask", C.byref(dfull), p(xd), p(sc), p(sh), p(minmax), p(x8), stream())
+    dw = torch.full((k * r * r * c,), 0.25, dtype=torch.float32, device=gpu)  # (accumulated into)
+    ext = torch.full((k * r * r * 2 * c,), float("nan"), dtype=torch.float32, device=gpu)
+    L.call("rn_stem_clip_wgrad", C.byref(dfull), p(x8), p(dyd), p(dw), p(ext), p(ws), wsb, stream())
+    dbeta = torch.zeros(c, dtype=torch.float32, device=gpu)
+    L.call("rn_stem_shift_grad", C.byref(dfull), p(dyd), p(master), p(dbeta), p(sws), stream())
+    L.call("rn_stem_clip_dbeta", C.byref(dfull), p(ext), p(master), p(dbeta), stream())
+    torch.cuda.synchronize()
+    x8f = x8.float().cpu().numpy()
+    assert np.array_equal(x8f[..., :c], x8h[..., :c]) and not x8f[..., 2 * c:].any()
+    assert np.array_equal(x8f[..., c:2 * c] == 1.0, mask_ref.transpose(0, 2, 3, 1))
+    assert rel_err(dw.cpu().numpy() - 0.25, dw_ref.cpu().numpy()) < 1e-5
+    assert rel_err(dbeta.cpu().numpy(), dbeta_ref.cpu().numpy()) < 1e-4
+
+
 @pytest.fixture(params=[(0, 0, 512), (0, 0, 8), (1, 0, 0), (1, 1, 512)],
                 ids=["rows224", "rows224_persist8", "rows256_mfma32", "rows256_mfma16"])
 def tile_variant(request):

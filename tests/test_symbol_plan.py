@@ -147,7 +147,16 @@ def test_plan_int8_quantization(monkeypatch):
     # 16 of the 17 activation quantizers read a BN+ReLU output only quantizers read -- one (8 BNs) or
     # two (the 4 units' act1: conv1 and the shortcut): their straight-through backwards fold into that
     # BN's backward (rn_bn_desc.clip, + clip2 / dy2); fc1's stays. RN_QUANT_BWD_FOLD=0 keeps all 17
-    assert names.count("rn_quant_int8_bwd") == 1 and names.count("rn_stem_quant_clip_grad") == 1
+    assert names.count("rn_quant_int8_bwd") == 1 and names.count("rn_stem_quant_clip_grad") == 0
+    # the stem input quantizer's clip gradient rides in the stem's weight gradient (bf16): the masks
+    # first (side stream), the mask channels' weight gradient, its dot product after the shift gradient
+    assert names[0] == "rn_stem_clip_mask" and names.count("rn_stem_clip_wgrad") == 1
+    assert names.index("rn_stem_shift_grad") < names.index("rn_stem_clip_dbeta")
+    monkeypatch.setenv("RN_STEM_CLIP_MASK", "0")
+    n0 = [c[0] for c in Executor(Plan(graphs.resnet_int8([1, 1, 1, 1], 4, [64, 256, 512, 1024, 2048], 16),
+                                      [("data", (2, 3, 64, 64))], [("softmax_label", (2,))]), "cpu")._bwd]
+    assert n0.count("rn_stem_quant_clip_grad") == 1 and "rn_stem_clip_mask" not in n0
+    monkeypatch.delenv("RN_STEM_CLIP_MASK")
     assert sum(1 for op in ex.plan.ops if op.kind == "bn" and op.desc.clip) == 12
     assert sum(1 for op in ex.plan.ops if op.kind == "bn" and op.desc.dy2 and op.desc.clip2) == 4
     monkeypatch.setenv("RN_QUANT_BWD_FOLD", "0")
