@@ -8,7 +8,9 @@ seeded U(-1,1) data, random labels), bf16 activations/weights with fp32 master w
 gradients and BN statistics. Inputs are resident in HBM before the timed region.
 
 Rank 0 prints ONE JSON line (contract in the task statement), including
-  roofline     : the dominant kernel family (most time per step) -- algorithmic FLOP per launch
+  roofline     : the dominant kernel family (most time per step in a serialised calibration step,
+                 among the compute stream's families when the weight gradients run overlapped on
+                 the side stream; every family's time is listed) -- algorithmic FLOP per launch
                  / average launch duration from HIP events around every launch of that family
                  (eager mode: inside the timed region; HIP-graph mode: in one eager step right
                  after it, graph nodes carry no timing events), vs the dense bf16 MFMA peak
@@ -444,7 +446,12 @@ def main():
         step()
     torch.cuda.synchronize()
     fams = calibrate_families(torch, ex, mod)
-    dom = max(fams, key=lambda f: fams[f][0])
+    # the dominant family of the step's critical path: with the side stream on, the weight gradients
+    # run overlapped with the data-gradient chain (sized for half the chip, rn_set_tuning 21), so the
+    # roofline line follows the compute stream's largest family; all families stay listed below
+    side = bool(getattr(ex, "_side_idx", None)) and ex.side_enabled
+    crit = [f for f in fams if not (side and f.startswith("wgrad"))] or list(fams)
+    dom = max(crit, key=lambda f: fams[f][0])
     solo_ms = fams[dom][0] / max(fams[dom][1], 1)
     timer = FamilyTimer(torch, ex, dom)
     # auto: one HIP graph on a single GPU -- unless the executor runs its weight gradients on a side
@@ -569,6 +576,8 @@ def main():
                 workload, a.batch, a.image, a.image), "model": model_name, "global_batch": a.batch * world,
                 "seq_len": None, "parallelism": "dp%d" % world, "per_gpu_images_per_sec": round(value / world, 2)},
             "roofline": {"bound": bound, "kernel": dom, "launches_per_step": len(timer.idx),
+                         "dominant_rule": "most kernel time per step on the compute (critical-path) stream" if side
+                         else "most kernel time per step",
                          "achieved": round(achieved, 2), "peak": peak, "unit": unit,
                          "frac": round(achieved / peak, 4),
                          "traffic": round(traffic) if traffic else None, "traffic_unit": "HBM bytes/launch",
