@@ -613,6 +613,7 @@ const char* rn_last_error(void);
  *      the data-gradient stream (measured, ResNet-50 at batch 256: 100 % 20.83 / 20.80 ms per step,
  *      75 % 20.74, 50 % 20.09 / 20.04, 25 % 23.85). Set before the workspaces are sized
  *      (rn_conv_wgrad_ws_bytes),
+ * 23 = the same percent for the grouped image-band weight gradients only (0 = key 21's),
  * 22 = 1: the BatchNorm-folded int8 quantizers (rn_quant_int8_fwd_codes_bn[2]) form every quotient
  *      v / unit by division (default 0: v * (1 / unit), the division only where that product lies
  *      within 2^-21 |v / unit| of a half-integer -- the same codes bit for bit, fewer instructions). */

@@ -3956,7 +3956,10 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     GbArgs g{};
     g.x = (const bf16_t*)x; g.dy = (const bf16_t*)dy; g.N = d->n; g.H = d->h; g.W = d->w; g.C = d->c;
     const int slices = gb == 3 ? 2 : 1;
-    g.ipw = (int)std::max<int64_t>(1, ceil_div((int64_t)d->n * slices, wgrad_cus()));
+    // (rn_set_tuning 23: these kernels' own percent of the chip, 0 = key 21's)
+    const int gcus = g_tune[RN_TUNE_GBAND_SPLIT] > 0 ? std::max(8, chip_cus() * g_tune[RN_TUNE_GBAND_SPLIT] / 100)
+                                                   : wgrad_cus();
+    g.ipw = (int)std::max<int64_t>(1, ceil_div((int64_t)d->n * slices, gcus));
     const int64_t split = ceil_div(d->n, g.ipw);
     const int64_t need = split * a.K * (int64_t)a.ldw * 4;  // (a.ldw = 9 * channels per group)
     if (ws_need) *ws_need = need;
