@@ -421,11 +421,12 @@ def main():
     pinned = mx.io.DataBatch(data=[mx.nd.array(data, ctx=mx.Context("cpu_pinned", 0))],
                              label=[mx.nd.array(label, ctx=mx.Context("cpu_pinned", 0))])
 
-    # the data-gradient chain on a high-priority stream when the weight gradients run beside it
-    # (RN_MAIN_PRIORITY=0: the default stream): the hardware then prefers the chain's workgroups
-    # and the side stream fills what is left
+    # RN_MAIN_PRIORITY=1: the data-gradient chain on a high-priority stream when the weight
+    # gradients run beside it, so the hardware prefers the chain's workgroups. Off by default: with
+    # the weight gradients' grids sized for part of the chip (rn_set_tuning 21) equal priorities
+    # measure faster (profiles/r04/priority: C2 -0.7 %, C4 -1.7 %, C5 -0.6 %)
     main_stream = None
-    if getattr(ex, "_side_stream", None) is not None and os.environ.get("RN_MAIN_PRIORITY", "1") == "1":
+    if getattr(ex, "_side_stream", None) is not None and os.environ.get("RN_MAIN_PRIORITY", "0") == "1":
         lo, hi = torch.cuda.Stream.priority_range()
         main_stream = torch.cuda.Stream(priority=min(lo, hi))
         torch.cuda.synchronize()

@@ -31,9 +31,10 @@ int chip_cus() {
   return cus;
 }
 // CUs the weight gradients size their split-M grids for: the chip, scaled by rn_set_tuning 21 (percent,
-// default 50; 0 = 100). They share the chip with the data-gradient chain on the other stream: half the
+// default 45; 0 = 100). They share the chip with the data-gradient chain on the other stream: half the
 // splits halve the partial slabs written and reduced, and the data gradients keep more of the CUs
-// (ResNet-50: 20.83 -> 20.09 ms per step; a quarter starves the weight gradients: 23.85)
+// (ResNet-50: 100 % 20.83, 50 % 20.09 ms per step, 45 % 0.8 % below 50; a quarter starves the weight
+// gradients: 23.85)
 int wgrad_cus() {
   const int pct = g_tune[RN_TUNE_WGRAD_SPLIT] > 0 ? g_tune[RN_TUNE_WGRAD_SPLIT] : 100;
   return std::max(8, chip_cus() * pct / 100);

@@ -92,7 +92,8 @@ class BucketAllReducer:
     def timing_summary(self, world):
         """Overlap of the bucket all-reduces with the backward over the recorded steps (call after a
         device synchronize): exposed_ms = end of the backward -> last bucket done (the communication
-        the backward did not hide), per-bucket launch offsets from the backward's start, and the
+        the backward did not hide), the last step's per-bucket launch offsets from its backward's start
+        (compare with backward_ms_last, that step's backward; the steps vary), and the
         algorithmic bus bandwidth 2(n-1)/n x bytes over the window first launch -> last done (a
         lower bound: the window includes waiting for gradients)."""
         if not self.records:
@@ -115,6 +116,6 @@ class BucketAllReducer:
         mean = lambda v: sum(v) / len(v)  # noqa: E731
         return {"steps_timed": len(exp), "exposed_ms": round(mean(exp), 3), "exposed_ms_max": round(max(exp), 3),
                 "backward_ms": round(mean(bwd), 3), "comm_window_ms": round(mean(win), 3),
-                "bucket_launch_offsets_ms": offs[-1],
+                "bucket_launch_offsets_ms": offs[-1], "backward_ms_last": round(bwd[-1], 3),
                 "bus_gbs": round(2.0 * (world - 1) / world * nbytes / (mean(win) * 1e-3) / 1e9, 2),
                 "bytes_per_step": int(nbytes)}

@@ -77,7 +77,8 @@ def test_bench_gpus2_runs_two_ranks(gpu):
         assert key in ar, key
     assert ar["steps_timed"] == 3 and len(ar["bucket_launch_offsets_ms"]) == ar["buckets"]
     offs = ar["bucket_launch_offsets_ms"]
-    assert offs == sorted(offs) and offs[0] < ar["backward_ms"]  # the first bucket leaves during the backward
+    # the first bucket leaves during the backward (the same step's: two ranks sharing one GPU vary a lot)
+    assert offs == sorted(offs) and offs[0] < ar["backward_ms_last"]
     assert ar["exposed_ms"] >= 0 and ar["bus_gbs"] > 0
     assert out["allreduce"]["launch"].startswith("one process per GPU (bench.py --gpus")
     assert abs(out["config"]["per_gpu_images_per_sec"] * 2 - out["value"]) < 0.05 * out["value"]
