@@ -166,6 +166,18 @@ int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, flo
 int64_t rn_conv_wgrad_ws_bytes(const rn_conv_desc* d);
 int rn_conv_bwd_filter_ws(const rn_conv_desc* d, const void* x, const void* dy, float* dw, void* ws,
                           int64_t ws_bytes, rn_stream_t stream);
+/* The weight gradient of an int8 convolution (symbol/resnet_int8.py: Quantization_int8 on the data, then
+ * Convolution; MXNet's backward multiplies dy by the fake-quantized values x = unit * code) from the
+ * input's int8 codes (x_codes: NHWC, c channels, as rn_quant_int8_fwd_codes* write them) and its unit
+ * (x_unit: one fp32, device): dw += *x_unit * sum dy * code -- the codes widened to bf16 exactly, the
+ * unit applied once per tile, so the bf16 fake-quantized values need not exist. The 128 / 256-column
+ * LDS-DMA tiles only: rn_conv_wgrad_i8_supported(d) = 1 where this applies (bf16, dense, c % 16 == 0,
+ * c_real == c, > 64 output channels and columns); ws as rn_conv_bwd_filter_ws, sized by
+ * rn_conv_wgrad_i8_ws_bytes(d) (-1 where unsupported). */
+int32_t rn_conv_wgrad_i8_supported(const rn_conv_desc* d);
+int64_t rn_conv_wgrad_i8_ws_bytes(const rn_conv_desc* d);
+int rn_conv_bwd_filter_i8(const rn_conv_desc* d, const void* x_codes, const float* x_unit, const void* dy, float* dw,
+                          void* ws, int64_t ws_bytes, rn_stream_t stream);
 /* rn_conv_bwd_filter_ws over the same BN+ReLU-on-load input as rn_conv_fwd_x (x = the BatchNorm
  * input; the 1x1 convolutions run the LDS-DMA tiles with the transform on their B fragments). */
 int rn_conv_bwd_filter_x(const rn_conv_desc* d, const void* x, const void* dy, float* dw, const float* in_scale,

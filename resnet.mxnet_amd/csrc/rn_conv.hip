@@ -663,6 +663,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(IgemmArgs p) {
 // buffers, NBUF-1 K-tiles in flight, one counted vmcnt + barrier per 64-deep K-tile. The epilogue
 // stages each wave's accumulators through LDS in two 64-row halves and writes 16-byte row chunks.
 typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v2i __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ v4i make_rsrc(const void* base, uint32_t bytes) {
   const uint64_t a = (uint64_t)base;
@@ -1447,12 +1448,31 @@ struct WgradArgs {
                               // (no atomics; wgrad_slab_reduce_kernel sums the splits into dw)
   const float* in_sc;         // nullable: BN+ReLU applied to the gathered x while staging
   const float* in_sh;
+  const float* xunit;         // (wgrad_big_kernel I8X) x holds int8 codes: dW = unit * sum dy * code
   FastDiv fdQ, fdPQ, fdC, fdS;  // fdC divides by cblk (dense: C)
 };
 
 // 16-byte chunk swizzle of an LDS image whose rows are read 4-at-a-time by
 // ds_read_b64_tr_b16 (rows 8g+4h+q): keeps the 8 rows of a 32-lane half on distinct slots.
 __device__ __forceinline__ int swz_tr(int row) { return 2 * ((row & 3) | (((row >> 3) & 1) << 2)); }
+// (int8 B images, read 8 rows per ds_read_b64_tr_b8: rows 8 g .. 8 g + 7 on 8 distinct chunks)
+__device__ __forceinline__ int swz_tr8(int row) { return row & 7; }
+// 8 int8 codes (two dwords, bytes in row order) -> 8 bf16 of the same integers (exact): bias to unsigned,
+// the byte conversions, minus the bias, then the fp32 high halves
+__device__ __forceinline__ v8s i8x8_to_bf16(v2i v) {
+  uint32_t o[4];
+#pragma unroll
+  for (int w = 0; w < 2; ++w) {
+    const uint32_t u = (uint32_t)v[w] ^ 0x80808080u;
+    const float f0 = (float)(u & 0xFFu) - 128.f, f1 = (float)((u >> 8) & 0xFFu) - 128.f;
+    const float f2 = (float)((u >> 16) & 0xFFu) - 128.f, f3 = (float)(u >> 24) - 128.f;
+    o[2 * w] = __builtin_amdgcn_perm(__float_as_uint(f1), __float_as_uint(f0), 0x07060302u);
+    o[2 * w + 1] = __builtin_amdgcn_perm(__float_as_uint(f3), __float_as_uint(f2), 0x07060302u);
+  }
+  v8s r;
+  __builtin_memcpy(&r, o, 16);
+  return r;
+}
 
 template <typename T, int BMK, int BNC, bool XF = false, bool GW = false>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
@@ -1732,11 +1752,18 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 // their transposed read. A lane's B fragment j holds one output column (= input channel) for the
 // whole kernel, so its scale / shift are two registers; max(x*sc + sh, 0) rounded to bf16 as
 // bn_apply_kernel does.
-template <int BMK, int NBUF, int BNC = 256, int XF = 0>
+// I8X: x holds the int8 codes of an activation Quantization_int8 (symbol/resnet_int8.py; the input of an
+// int8 convolution, whose fake-quantized values x = unit * code the weight gradient multiplies): the B
+// image holds the bytes (16 channels per 16-byte chunk, half the LDS and HBM bytes), read with
+// ds_read_b64_tr_b8 -- lane i of a 16-lane group gets column i of an 8-row x 16-byte block, lane l
+// supplying row l / 2, bytes 8 (l % 2).. -- and widened to bf16 (exact: |code| <= 127); dW = unit *
+// sum dy * code, the unit applied once in the epilogue.
+template <int BMK, int NBUF, int BNC = 256, int XF = 0, int I8X = 0>
 __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(WgradArgs p) {
-  constexpr int CE = 8, BKM = 64;
+  static_assert(!(XF && I8X), "int8 input: no input transform");
+  constexpr int CE = I8X ? 16 : 8, BKM = 64, XES = I8X ? 1 : 2;  // B chunk channels, B bytes per element
   constexpr int NWC = BNC / 64, NW = 2 * NWC;              // waves along the columns, waves
-  constexpr int A_CPR = BMK / 8, B_CPR = BNC / 8;      // 16-byte chunks per LDS row
+  constexpr int A_CPR = BMK / 8, B_CPR = BNC * XES / 16;  // 16-byte chunks per LDS row
   constexpr int A_RPI = 64 / A_CPR, B_RPI = 64 / B_CPR;  // rows per 1 KiB DMA instruction
   constexpr int AR = BKM / A_RPI / NW, BR = BKM / B_RPI / NW;  // DMA instructions per wave per M-tile
   constexpr int LPT = AR + BR;
@@ -1772,7 +1799,7 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
   for (int j = 0; j < BR; ++j) {
     b_row[j] = (wid * BR + j) * B_RPI + lane / B_CPR;
     const int slot = lane % B_CPR;
-    const int col = n0 + 8 * (slot ^ (swz_tr(b_row[j]) & (B_CPR - 1)));
+    const int col = n0 + CE * (slot ^ ((I8X ? swz_tr8(b_row[j]) : swz_tr(b_row[j])) & (B_CPR - 1)));
     if (col < p.ncol_load && p.p4) {  // chunk = taps (r, s), (r, s + 1) of the padded image
       b_ch[j] = 0;
       b_h[j] = col >> 5;
@@ -1815,7 +1842,7 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
       const int hin = pp * p.sh + b_h[j];
       const int win = qq * p.sw + b_w[j];
       const bool ok = b_ch[j] >= 0 && m < mend && (unsigned)hin < (unsigned)p.H && (unsigned)win < (unsigned)p.W;
-      const uint32_t off = (uint32_t)(((n * p.H + hin) * p.W + win) * p.C + b_ch[j]) * 2u;
+      const uint32_t off = (uint32_t)(((n * p.H + hin) * p.W + win) * p.C + b_ch[j]) * (uint32_t)XES;
       dma16_global(ok ? (const void*)(xb + off) : (const void*)zb, lds_b + la + j * 1024);
     }
   };
@@ -1841,11 +1868,22 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
     const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
     {
       v8s af[MI], bfv[NI];
+      if constexpr (I8X) {  // rows 8 g .. 8 g + 7 of the slab in one transposed byte read per fragment
+        const int row = slab * 32 + 8 * g + (li >> 1);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int cb = wn * 64 + j * 16 + 8 * (li & 1);  // byte column
+          const int byte = row * (B_CPR * 16) + (((cb >> 4) ^ (swz_tr8(row) & (B_CPR - 1))) << 4) + (cb & 15);
+          const v2i v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)(Bb + byte));
+          bfv[j] = i8x8_to_bf16(v);
+        }
+      }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int row = slab * 32 + 8 * g + 4 * h + q;
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
+          if constexpr (I8X) break;
           const int col = wn * 64 + j * 16 + 4 * pp;
           const int byte = row * (B_CPR * 16) + ((((col * 2) >> 4) ^ (swz_tr(row) & (B_CPR - 1))) << 4) + ((col * 2) & 15);
           v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(Bb + byte));
@@ -1894,6 +1932,13 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
   // D[row = k][col] -> fp32 atomic add into dw (dense, unpadded: ldw = ncol); padded channels (the
   // stem's 3 of 8) keep c < creal
   if (kRnDiag && p.diag_noepi) return;  // diagnostic (rn_set_tuning 6): no dW epilogue (wrong results)
+  if constexpr (I8X) {  // dW = unit * sum dy * code
+    const float u = *p.xunit;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] *= u;
+  }
   const bool padded = p.creal != p.C;
   if (p.slab && !padded) {  // plain stores of this split's partial tile (rows of 16 columns: 64-byte segments)
     float* dst = p.slab + (int64_t)zs * p.K * p.ldw;
@@ -3844,16 +3889,21 @@ int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, 
 namespace {
 // The weight-gradient kernel choice for d. launch == false: only *ws_need (bytes of split-M partial
 // slabs the chosen kernel stores when given a workspace; 0 = it adds into dw with atomics).
+// xunit != NULL: x holds int8 codes, dW = *xunit * sum dy * code (the 128 / 256-column LDS-DMA tiles only:
+// wgrad_i8_ok)
 int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* dw, const float* in_scale,
                    const float* in_shift, float* ws, int64_t ws_bytes, int64_t* ws_need, bool launch,
-                   hipStream_t st) {
+                   hipStream_t st, const float* xunit = nullptr, bool i8 = false) {
   if (ws_need) *ws_need = 0;
   RN_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "in_scale / in_shift must both be set");
   RN_CHECK_ARG(!in_scale || d->groups == 1, "input transform on a grouped conv");
+  RN_CHECK_ARG(!i8 || (!in_scale && d->dtype == RN_BF16 && d->groups <= 1 && d->c_real == d->c && d->c % 16 == 0),
+               "int8 input codes: bf16 dy, dense, whole 16-channel chunks, no input transform");
 
   WgradArgs a{};
   a.x = x; a.dy = dy; a.dw = dw;
   a.in_sc = in_scale; a.in_sh = in_shift;
+  a.xunit = xunit;
   a.N = d->n; a.H = d->h; a.W = d->w; a.C = d->c; a.P = d->p; a.Q = d->q; a.K = d->k;
   a.ldy = d->k_pad; a.R = d->r; a.S = d->s; a.sh = d->stride_h; a.sw = d->stride_w;
   a.ph = d->pad_h; a.pw = d->pad_w;
@@ -3918,7 +3968,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
   // rn_set_tuning 19 = 2 is needed to run them)
   const int db = (d->c == 64 && d->w <= 62) ? 1 : g_tune[RN_TUNE_WGRAD_BAND] != 2 ? 0 :
                  (d->c == 128 && d->w <= 30) ? 2 : ((d->c == 256 || d->c == 512) && d->w <= 14) ? 3 : 0;
-  if (d->dtype == RN_BF16 && !grouped && db && d->r == 3 && d->s == 3 && d->stride_h == 1 &&
+  if (!i8 && d->dtype == RN_BF16 && !grouped && db && d->r == 3 && d->s == 3 && d->stride_h == 1 &&
       d->stride_w == 1 && d->pad_h == 1 && d->pad_w == 1 && d->c_real == d->c && d->k == d->c &&
       d->k_pad == d->k && g_tune[RN_TUNE_WGRAD_BAND] != 1 && (int64_t)d->n * d->h * d->w * d->c < INT32_MAX) {
     DbArgs g{};
@@ -3982,7 +4032,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
   // streaming pass over M per workgroup (wgrad_stream_kernel; rn_set_tuning 19 = 1: off)
   const bool one = d->r == 1 && d->s == 1 && d->stride_h == 1 && d->stride_w == 1 && d->pad_h == 0 && d->pad_w == 0;
   auto pw2 = [](int v) { return v == 64 || v == 128 || v == 256; };
-  if (d->dtype == RN_BF16 && !grouped && one && pw2(d->k) && pw2(d->c) && d->k * d->c <= 32768 &&
+  if (!i8 && d->dtype == RN_BF16 && !grouped && one && pw2(d->k) && pw2(d->c) && d->k * d->c <= 32768 &&
       d->c_real == d->c && d->k_pad == d->k && g_tune[RN_TUNE_WGRAD_BAND] != 1 &&
       (int64_t)a.M * (d->k + d->c) * 2 < INT32_MAX) {
     const int64_t mtiles = ceil_div(a.M, 64);
@@ -4013,7 +4063,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
   // small-M layers (stage 3-4).
   // (default for the stem's padded channels, c_real < c = 8; rn_set_tuning 5 = 4 for every 64-channel layer)
   const bool stem_dma = d->c_real < d->c && d->c == 8 && g_tune[RN_TUNE_WGRAD_BIG] != 3;
-  if (d->dtype == RN_BF16 && !grouped && !in_scale && (d->c_real == d->c || stem_dma) && a.K <= 64 &&
+  if (!i8 && d->dtype == RN_BF16 && !grouped && !in_scale && (d->c_real == d->c || stem_dma) && a.K <= 64 &&
       a.ncol_load > 64 && (g_tune[RN_TUNE_WGRAD_BIG] == 4 || stem_dma) &&
       (int64_t)d->n * d->h * d->w * d->c < INT32_MAX && (int64_t)a.M * a.ldy < INT32_MAX) {
     // 64 x 128 LDS-DMA tiles for the 64-channel layers (4 waves, 3 buffers, two workgroups per CU)
@@ -4055,6 +4105,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     if (!launch) return finish(split, "wgrad_dma128");
     if (!use_slab(split)) return -1;
     if (in_scale) hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128, 1>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
+    else if (i8) hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128, 0, 1>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
     return finish(split, "wgrad_dma128");
   }
@@ -4073,9 +4124,16 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     if (in_scale) {
       if (bmk == 256) hipLaunchKernelGGL((wgrad_big_kernel<256, 2, 256, 1>), grid, dim3(512), 0, st, a);
       else hipLaunchKernelGGL((wgrad_big_kernel<128, 3, 256, 1>), grid, dim3(512), 0, st, a);
+    } else if (i8) {
+      if (bmk == 256) hipLaunchKernelGGL((wgrad_big_kernel<256, 2, 256, 0, 1>), grid, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((wgrad_big_kernel<128, 3, 256, 0, 1>), grid, dim3(512), 0, st, a);
     } else if (bmk == 256) hipLaunchKernelGGL((wgrad_big_kernel<256, 2>), grid, dim3(512), 0, st, a);
     else hipLaunchKernelGGL((wgrad_big_kernel<128, 3>), grid, dim3(512), 0, st, a);
     return finish(split, "wgrad_big");
+  }
+  if (i8) {  // (a plan-time query, launch == false, sets no error)
+    if (launch) rn_set_error("int8 input codes: no weight-gradient kernel for this shape (rn_conv_wgrad_i8_supported)");
+    return -1;
   }
   // 64-wide tiles where K or the column count is <= 64 (stage-1 layers): a 128 tile would spend
   // half (or three quarters) of its MFMAs on zero rows / columns
@@ -4162,6 +4220,33 @@ int rn_conv_bwd_filter_ws(const rn_conv_desc* d, const void* x, const void* dy, 
 
 int rn_conv_bwd_filter(const rn_conv_desc* d, const void* x, const void* dy, float* dw, rn_stream_t stream) {
   return rn_conv_bwd_filter_x(d, x, dy, dw, nullptr, nullptr, nullptr, 0, stream);
+}
+
+int32_t rn_conv_wgrad_i8_supported(const rn_conv_desc* d) {
+  if (!d || d->dtype != RN_BF16 || d->groups > 1 || d->c_real != d->c || d->c % 16 != 0) return 0;
+  int64_t need = 0;
+  const int r = wgrad_dispatch(d, nullptr, nullptr, nullptr, nullptr, nullptr, reinterpret_cast<float*>(16), INT64_MAX,
+                               &need, false, nullptr, nullptr, true);
+  return r == 0 && need > 0 ? 1 : 0;
+}
+
+int64_t rn_conv_wgrad_i8_ws_bytes(const rn_conv_desc* d) {
+  if (!rn_conv_wgrad_i8_supported(d)) return -1;
+  int64_t need = 0;
+  if (wgrad_dispatch(d, nullptr, nullptr, nullptr, nullptr, nullptr, reinterpret_cast<float*>(16), INT64_MAX, &need,
+                     false, nullptr, nullptr, true))
+    return -1;
+  return need;
+}
+
+int rn_conv_bwd_filter_i8(const rn_conv_desc* d, const void* x_codes, const float* x_unit, const void* dy, float* dw,
+                          void* ws, int64_t ws_bytes, rn_stream_t stream) {
+  RN_CHECK_ARG(d && x_codes && x_unit && dy && dw, "null argument");
+  RN_CHECK_ARG(ws_bytes >= 0 && (ws || ws_bytes == 0), "bad workspace");
+  RN_CHECK_ARG(((uintptr_t)ws & 15) == 0, "workspace must be 16-byte aligned");
+  RN_CHECK_ARG(rn_conv_wgrad_i8_supported(d), "int8 input codes: unsupported shape (rn_conv_wgrad_i8_supported)");
+  return wgrad_dispatch(d, x_codes, dy, dw, nullptr, nullptr, reinterpret_cast<float*>(ws), ws_bytes, nullptr, true,
+                        as_stream(stream), x_unit, true);
 }
 
 // ---------------------------------------------------------------- stem over the padded NHWC4 image

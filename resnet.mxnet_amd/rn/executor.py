@@ -344,6 +344,8 @@ class Plan:
         for op in self.ops:
             if op.kind == "quant":
                 us = users.get(id(op.y), [])
+                op.value_users = us
+                op.codes_wgrad = False  # (the executor decides: _codes_wgrad)
                 op.defer_values = bool(defer and op.emit_codes and us and
                                        all(u.kind == "conv" and u.int8 and u.qsrc is op for u in us))
 
@@ -847,8 +849,8 @@ class Executor:
             if self._side_stream is not None:
                 self._spv2.value = self._side_stream.cuda_stream if self.side_enabled else self._spv.value
 
-    WGRAD_CALLS = ("rn_conv_bwd_filter", "rn_conv_bwd_filter_ws", "rn_conv_bwd_filter_x", "rn_stem_conv_wgrad_p4",
-                   "rn_stem_clip_wgrad", "rn_stem_clip_dbeta")
+    WGRAD_CALLS = ("rn_conv_bwd_filter", "rn_conv_bwd_filter_ws", "rn_conv_bwd_filter_x", "rn_conv_bwd_filter_i8",
+                   "rn_stem_conv_wgrad_p4", "rn_stem_clip_wgrad", "rn_stem_clip_dbeta")
     # side-stream calls that depend on the forward only, not on the backward so far: no fork of their own
     # (they run while the side stream waits for the next dy), except the first of a step
     SIDE_PRE_CALLS = ("rn_quant_int8_expand", "rn_stem_clip_mask")
@@ -904,12 +906,33 @@ class Executor:
         L.check(self.lib.rn_conv_desc_init(L.C.byref(d)), "rn_conv_desc_init")
         return d
 
+    def _codes_wgrad(self, plan):
+        """Quantizers whose fake-quantized values only int8 convolutions read, each of whose weight
+        gradients takes the int8 codes instead (rn_conv_bwd_filter_i8: dW = unit * sum dy * code, the
+        128 / 256-column tiles, every ResNet-50 layer past stage 1): the forward writes the codes only,
+        and the bf16 values -- 2 of the pass's 5 bytes per element -- are never written or read
+        (RN_QUANT_CODES_WGRAD=0: values + bf16 weight gradients)."""
+        on = os.environ.get("RN_QUANT_CODES_WGRAD", "1") == "1" and self.dtype == L.RN_BF16
+        for op in plan.ops:
+            if op.kind != "quant":
+                continue
+            us = getattr(op, "value_users", [])
+            ok = on and op.emit_codes and not op.defer_values and bool(us) and \
+                all(u.kind == "conv" and u.int8 and u.qsrc is op for u in us)
+            if ok:
+                for u in us:
+                    x, y = u.x, u.y
+                    d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, u.kernel, u.stride, u.pad, u.groups)
+                    ok = ok and int(self.lib.rn_conv_wgrad_i8_supported(L.C.byref(d))) == 1
+            op.codes_wgrad = bool(ok)
+
     # ------------------------------------------------------------------ forward
     def _build_forward(self):
         plan = self.plan
         sp = self._sp()
         ws_bytes = 64
         self._descs = []  # keep ctypes structs alive
+        self._codes_wgrad(plan)
         self.packs = []   # weight pack calls (bind time / set_params)
         # every weight quantizer in one rn_weight_quant_pack (RN_WQUANT_BATCH=0: three calls per weight)
         self._wq_batch = os.environ.get("RN_WQUANT_BATCH", "1") == "1"
@@ -1139,8 +1162,9 @@ class Executor:
                         # + the int8 codes and unit the consumers' int8 forward reads
                         o.codes = self.torch.zeros(o.x.numel, dtype=self.torch.int8, device=self.device)
                         o.unit = self._zeros(1, self.torch.float32)
-                # (deferred values: codes only here, rn_quant_int8_expand before the weight gradient)
-                vout = lambda o: None if o.defer_values else self._p(self.act(o.y))
+                # (deferred values: codes only here, rn_quant_int8_expand before the weight gradient;
+                # codes_wgrad: codes only, the weight gradients multiply them)
+                vout = lambda o: None if (o.defer_values or o.codes_wgrad) else self._p(self.act(o.y))
                 for lst, tr in ((F, 1), (I, 0)):
                     if op.bn_lead is not None:
                         pass  # written by its peer's call
@@ -1469,6 +1493,8 @@ class Executor:
                      if op.kind == "stem" and not op.p4]
             need += [int(self.lib.rn_stem_clip_wgrad_ws_bytes(L.C.byref(op.dfull))) for op in plan.ops
                      if op.kind == "stem" and self._stem_clip_mask(op)]
+            need += [int(self.lib.rn_conv_wgrad_i8_ws_bytes(L.C.byref(op.desc))) for op in plan.ops
+                     if op.kind == "conv" and getattr(op, "qsrc", None) is not None and op.qsrc.codes_wgrad]
             self.wgrad_ws_bytes = max(need + [0])
             if self.wgrad_ws_bytes > 0:
                 self.wgrad_ws = self._zeros(self.wgrad_ws_bytes // 4, self.torch.float32)
@@ -1520,6 +1546,12 @@ class Executor:
                     ws = self.wgrad_ws is not None and int(self.lib.rn_conv_wgrad_ws_bytes(L.C.byref(op.desc))) > 0
                     self._bwd.append(self._call("rn_conv_bwd_filter_x", L.C.byref(op.desc), self._p(self.act(op.xf.x)),
                                                 self._p(dy), self._gp(op.weight), op.xf.sc, op.xf.sh,
+                                                self._p(self.wgrad_ws) if ws else None,
+                                                self.wgrad_ws_bytes if ws else 0, sp))
+                elif getattr(op, "qsrc", None) is not None and op.qsrc.codes_wgrad:  # the input's codes, x its unit
+                    q, ws = op.qsrc, self.wgrad_ws is not None
+                    self._bwd.append(self._call("rn_conv_bwd_filter_i8", L.C.byref(op.desc), self._p(q.codes),
+                                                self._p(q.unit), self._p(dy), self._gp(op.weight),
                                                 self._p(self.wgrad_ws) if ws else None,
                                                 self.wgrad_ws_bytes if ws else 0, sp))
                 else:

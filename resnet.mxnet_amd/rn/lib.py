@@ -71,6 +71,9 @@ SIGNATURES = {
     "rn_conv_bwd_filter": (_i32, [_P, _P, _P, _P, _P]),
     "rn_conv_wgrad_ws_bytes": (_i64, [_P]),
     "rn_conv_bwd_filter_ws": (_i32, [_P, _P, _P, _P, _P, _i64, _P]),
+    "rn_conv_wgrad_i8_supported": (_i32, [_P]),
+    "rn_conv_wgrad_i8_ws_bytes": (_i64, [_P]),
+    "rn_conv_bwd_filter_i8": (_i32, [_P, _P, _P, _P, _P, _P, _i64, _P]),
     "rn_conv_weight_numel": (_i64, [_P]),
     "rn_conv_pack_numel": (_i64, [_P, _i32]),
     "rn_conv_weight_pack": (_i32, [_P, _P, _P, _P, _P]),

@@ -444,6 +444,8 @@ class Checker:
                 self.deferred_vals = {}
             self.deferred_vals[self.ex.act(op.y).data_ptr()] = (op, val)
             m = {"state": st}
+        elif getattr(op, "codes_wgrad", False):  # codes only: the weight gradients multiply them (unit * code)
+            m = {"state": st}
         else:
             m = {"state": st, "values": self.mismatch(self.act_nchw(op.y), val)["mismatch"]}
         if getattr(op, "codes", None) is not None:
@@ -610,7 +612,7 @@ class Checker:
             self._bn_bwd_check(op, _bf16(g).double(), state.get("add"), dxp)
         return (self._snap(addp, state, "add") if addp is not None else None), post
 
-    def _wgrad(self, args, state, xf=False, p4=False):
+    def _wgrad(self, args, state, xf=False, p4=False, xval=None):
         d = args[0]._obj
         xp, dyp, dwp = args[1], args[2], args[3]
         name = self.grad_name(dwp)
@@ -626,7 +628,9 @@ class Checker:
                 ref, rab = ref_wgrad(x, dy, (d.r, d.s), (d.stride_h, d.stride_w), (0, 0), with_abs=True)
                 ref, rab = ref[:, :d.c_real], rab[:, :d.c_real]
             else:
-                if xf:
+                if xval is not None:
+                    x = xval()
+                elif xf:
                     x = self.bn_relu_input(self.bn_by_sm_x[xp.value])
                 else:
                     x = self.nchw(self.t(xp), n, d.h, d.w, d.c, d.c_real)
@@ -652,6 +656,19 @@ class Checker:
         if not hasattr(self, "bn_by_sm_x"):
             self.bn_by_sm_x = {self.ex.act(op.x).data_ptr(): op for op in self.ex.plan.ops if op.kind == "bn"}
         return self._wgrad(args, state, xf=True)
+
+    def _h_rn_conv_bwd_filter_i8(self, args, state):
+        """The weight gradient of an int8 conv from its input's codes (rn_conv_bwd_filter_i8): against the
+        oracle on x = unit * code (the codes themselves are checked bit for bit at the quantizer)."""
+        d = args[0]._obj
+        cp_, up_ = args[1], args[2]
+        q = {o.codes.data_ptr(): o for o in self.ex.plan.ops
+             if o.kind == "quant" and getattr(o, "codes", None) is not None}[cp_.value]
+        assert q.unit.data_ptr() == up_.value
+
+        def xval():
+            return self.nchw(q.codes, d.n, d.h, d.w, d.c, d.c_real) * float(q.unit[0])  # (fp32, as the values)
+        return self._wgrad((args[0], None, args[3], args[4]), state, xval=xval)
 
     def _h_rn_stem_conv_wgrad_p4(self, args, state):
         d = args[0]._obj

@@ -74,8 +74,8 @@ def gpu_quant_values(ex):
         if op.kind == "quant":
             t = op.y
             src = ex.act(t)
-            if getattr(op, "defer_values", False):
-                # (after the forward only the codes exist: the values as the backward expands them)
+            if getattr(op, "defer_values", False) or getattr(op, "codes_wgrad", False):
+                # (after the forward only the codes exist: the values as rn_quant_int8_expand gives them)
                 import ctypes as C
                 import torch
                 from rn import lib as L

@@ -1786,3 +1786,62 @@ def test_wgrad_grouped_image_bands(gpu, case):
     cond = np.abs(outs[0] - dw_ref) / (dw_abs + 1e-30)
     assert cond.max() < 2e-6, cond.max()
     assert np.abs(outs[0] - outs[2]).max() <= 1e-5 * np.abs(dw_abs).max()
+
+
+@pytest.mark.parametrize("case", [
+    (3, 128, 9, 11, 128, 1, 1, 0),    # 128 columns: the 128 x 128 tile (wgrad_big_kernel<128, 2, 128>), ragged M
+    (2, 256, 14, 14, 512, 1, 1, 0),   # 256-column tiles, 256-row k tiles
+    (2, 512, 7, 9, 128, 1, 1, 0),     # 256-column tiles, 128-row k tiles
+    (2, 256, 14, 14, 1024, 1, 2, 0),  # the stride-2 shortcut
+    (3, 128, 13, 10, 128, 3, 1, 1),   # a 3x3 gather with halo (9 x 128 columns)
+    (2, 256, 15, 14, 256, 3, 2, 1),   # a stage's first 3x3, stride 2, odd rows
+    (2, 48, 9, 9, 192, 3, 1, 1),      # 3 16-channel chunks per tap, k past the last 128-row tile
+])
+def test_wgrad_int8_codes(gpu, case):
+    """rn_conv_bwd_filter_i8: the weight gradient of an int8 convolution from its input's int8 codes
+    (symbol/resnet_int8.py: MXNet multiplies dy by the fake-quantized values unit * code): the codes
+    staged as bytes, read with the transposed byte reads and widened to bf16, the unit applied once.
+    Against the fp64 oracle of dy and unit * code (fp32 accumulation of exact products, one rounding of
+    the unit: 2e-6 of the sum of the terms' magnitudes), bit-identical run to run (split slabs)."""
+    n, c, h, w, k, r, st, pd = case
+    rng = np.random.default_rng(12)
+    codes = rng.integers(-127, 128, size=(n, c, h, w)).astype(np.int8)
+    codes[0, :, 0, :] = 127   # the extremes
+    codes[-1, :, -1, :] = -127
+    unit = np.float32(0.0137)
+    x = codes.astype(np.float64) * float(unit)
+    ho, wo = (h + 2 * pd - r) // st + 1, (w + 2 * pd - r) // st + 1
+    dy = bf16_round(rng.standard_normal((n, k, ho, wo)))
+    _, dw_ref = ops.conv2d_bwd(x, np.zeros((k, c, r, r)), dy, (st, st), (pd, pd))
+    dw_abs = ops.conv2d_bwd(np.abs(x), np.zeros((k, c, r, r)), np.abs(dy), (st, st), (pd, pd))[1]
+    d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd)
+    lib = L.load()
+    assert lib.rn_conv_wgrad_i8_supported(C.byref(d)) == 1
+    need = lib.rn_conv_wgrad_i8_ws_bytes(C.byref(d))
+    assert need >= k * r * r * c * 4
+    ws = torch.full((need // 4 + 4,), float("nan"), dtype=torch.float32, device=gpu)
+    xd = torch.from_numpy(np.ascontiguousarray(codes.transpose(0, 2, 3, 1))).to(gpu)
+    ud = torch.tensor([unit], dtype=torch.float32, device=gpu)
+    dyd = to_nhwc(dy, BF16, gpu)
+    outs = []
+    for _ in range(2):
+        dw = torch.zeros(k * r * r * c, dtype=torch.float32, device=gpu)
+        L.call("rn_conv_bwd_filter_i8", C.byref(d), p(xd), p(ud), p(dyd), p(dw), p(ws), need, stream())
+        torch.cuda.synchronize()
+        outs.append(dw.cpu().numpy().reshape(k, r, r, c).transpose(0, 3, 1, 2).astype(np.float64))
+    assert np.array_equal(outs[0], outs[1])
+    cond = np.abs(outs[0] - dw_ref) / (dw_abs + 1e-30)
+    assert cond.max() < 2e-6, cond.max()
+
+
+def test_wgrad_int8_codes_unsupported(gpu):
+    """Shapes the int8-codes weight gradient does not cover (<= 64 output channels: stage 1's streaming
+    and band kernels; channels not in 16-byte chunks) report 0 and the call fails with an error, never a
+    launch."""
+    lib = L.load()
+    for n, c, h, w, k, r, st, pd in ((2, 256, 8, 8, 64, 1, 1, 0), (2, 64, 8, 8, 64, 3, 1, 1), (2, 24, 8, 8, 128, 3, 1, 1)):
+        d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd)
+        assert lib.rn_conv_wgrad_i8_supported(C.byref(d)) == 0
+        assert lib.rn_conv_wgrad_i8_ws_bytes(C.byref(d)) == -1
+        dummy = torch.zeros(16, dtype=torch.float32, device=gpu)
+        assert lib.rn_conv_bwd_filter_i8(C.byref(d), p(dummy), p(dummy), p(dummy), p(dummy), None, 0, stream()) != 0
