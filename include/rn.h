@@ -248,6 +248,12 @@ int rn_stem_clip_mask(const rn_conv_desc* d, const float* x_nchw, const float* s
 int64_t rn_stem_clip_wgrad_ws_bytes(const rn_conv_desc* d);
 int rn_stem_clip_wgrad(const rn_conv_desc* d, const void* x8, const void* dy, float* dw, float* ext, void* ws,
                        int64_t ws_bytes, rn_stream_t stream);
+/* rn_stem_clip_wgrad over one image chunk (d, x8, dy: the chunk's descriptor and rows): ext is zeroed by
+ * the first chunk (first = 1), every chunk adds its weight gradient into ext, and the last (last = 1)
+ * adds the real part into dw -- so each chunk's gradient starts as soon as its rows of the stem's
+ * BatchNorm backward are applied (rn_bn_bwd_apply_rows), on the weight-gradient stream. */
+int rn_stem_clip_wgrad_chunk(const rn_conv_desc* d, const void* x8, const void* dy, float* dw, float* ext, void* ws,
+                             int64_t ws_bytes, int32_t first, int32_t last, rn_stream_t stream);
 int rn_stem_clip_dbeta(const rn_conv_desc* d, const float* ext, const float* w_q, float* dbeta,
                        rn_stream_t stream);
 

@@ -4631,18 +4631,25 @@ int64_t rn_stem_clip_wgrad_ws_bytes(const rn_conv_desc* d) {
   return rn_conv_wgrad_ws_bytes(&e);
 }
 
-int rn_stem_clip_wgrad(const rn_conv_desc* d, const void* x8, const void* dy, float* dw, float* ext, void* ws,
-                       int64_t ws_bytes, rn_stream_t stream) {
+int rn_stem_clip_wgrad_chunk(const rn_conv_desc* d, const void* x8, const void* dy, float* dw, float* ext, void* ws,
+                             int64_t ws_bytes, int32_t first, int32_t last, rn_stream_t stream) {
   RN_CHECK_ARG(d && x8 && dy && dw && ext, "null argument");
   RN_CHECK_ARG(stem_clip_ok(d), "the clip weight gradient needs the bf16 NHWC-8 stem image with 2 * c_real <= 8");
   const rn_conv_desc e = stem_clip_ext(d);
   const int krs = d->k * d->r * d->s;
   hipStream_t st = as_stream(stream);
-  if (hipMemsetAsync(ext, 0, sizeof(float) * (size_t)krs * e.c_real, st) != hipSuccess) return rn_check_launch("stem_clip_wgrad");
-  if (rn_conv_bwd_filter_ws(&e, x8, dy, ext, ws, ws_bytes, stream)) return -1;
+  if (first && hipMemsetAsync(ext, 0, sizeof(float) * (size_t)krs * e.c_real, st) != hipSuccess)
+    return rn_check_launch("stem_clip_wgrad");
+  if (rn_conv_bwd_filter_ws(&e, x8, dy, ext, ws, ws_bytes, stream)) return -1;  // (adds into ext)
+  if (!last) return 0;
   hipLaunchKernelGGL(stem_clip_split_kernel, dim3((krs * d->c_real + 255) / 256), dim3(256), 0, st, ext, dw, krs,
                      d->c_real);
   return rn_check_launch("stem_clip_wgrad");
+}
+
+int rn_stem_clip_wgrad(const rn_conv_desc* d, const void* x8, const void* dy, float* dw, float* ext, void* ws,
+                       int64_t ws_bytes, rn_stream_t stream) {
+  return rn_stem_clip_wgrad_chunk(d, x8, dy, dw, ext, ws, ws_bytes, 1, 1, stream);
 }
 
 int rn_stem_clip_dbeta(const rn_conv_desc* d, const float* ext, const float* w_q, float* dbeta, rn_stream_t stream) {

@@ -850,7 +850,7 @@ class Executor:
                 self._spv2.value = self._side_stream.cuda_stream if self.side_enabled else self._spv.value
 
     WGRAD_CALLS = ("rn_conv_bwd_filter", "rn_conv_bwd_filter_ws", "rn_conv_bwd_filter_x", "rn_conv_bwd_filter_i8",
-                   "rn_stem_conv_wgrad_p4", "rn_stem_clip_wgrad", "rn_stem_clip_dbeta")
+                   "rn_stem_conv_wgrad_p4", "rn_stem_clip_wgrad", "rn_stem_clip_wgrad_chunk", "rn_stem_clip_dbeta")
     # side-stream calls that depend on the forward only, not on the backward so far: no fork of their own
     # (they run while the side stream waits for the next dy), except the first of a step
     SIDE_PRE_CALLS = ("rn_quant_int8_expand", "rn_stem_clip_mask")
@@ -1343,11 +1343,13 @@ class Executor:
 
     def _stem_chunks(self, op, dy):
         """Image chunks of the stem's BN-backward apply + weight gradient (RN_STEM_CHUNKS, default 4;
-        1 = one rn_bn_bwd and one wgrad): the NHWC4 stem with a side stream, whose output gradient is
-        the dx of the rn_bn_bwd call just emitted (no add operand, no paired gradient)."""
+        1 = one rn_bn_bwd and one wgrad): the NHWC4 stem, or the int8 stem's NHWC-8 image with the clip
+        masks (rn_stem_clip_wgrad_chunk), with a side stream, whose output gradient is the dx of the
+        rn_bn_bwd call just emitted (no add operand, no paired gradient)."""
         nch = int(os.environ.get("RN_STEM_CHUNKS", "4"))
         side = self._side_stream is not None or (self.dry_run and os.environ.get("RN_WGRAD_STREAM", "1") == "1")
-        if nch <= 1 or not op.p4 or not side or dy is None or op.dfull.n % nch or not self._bwd:
+        if nch <= 1 or not (op.p4 or self._stem_clip_mask(op)) or not side or dy is None or op.dfull.n % nch or \
+                not self._bwd:
             return 1
         name, _, args = self._bwd[-1]
         # (rn_bn_bwd_part: the pool backward reduced the BN, rn_pool_bwd_bnred)
@@ -1588,7 +1590,7 @@ class Executor:
                         self._bwd[-1] = self._call("rn_bn_bwd_finalize", bd, part, nrb, gp_, smp, sip, dgp, dbp,
                                                    L.C.c_void_p((coef + 15) // 16 * 16), sp)
                         bargs = (bd, xp_, dyp_, dxp_, None, gp_, smp, sip, scp, shp, dgp, dbp, wsp_, sp)
-                    d, hp, wp = op.dfull, op.p4[0], op.p4[1]
+                    d = op.dfull
                     nc = d.n // nch
                     rows = nc * d.p * d.q
                     for i in range(nch):
@@ -1597,11 +1599,20 @@ class Executor:
                         self._descs.append(dc)
                         self._bwd.append(self._call("rn_bn_bwd_apply_rows", bargs[0], bargs[1], bargs[2], bargs[3],
                                                     None, bargs[8], bargs[9], bargs[12], i * rows, rows, sp))
-                        self._bwd.append(self._call(
-                            "rn_stem_conv_wgrad_p4", L.C.byref(dc),
-                            L.C.c_void_p(op.x8.data_ptr() + i * nc * hp * wp * 4 * 2),
-                            L.C.c_void_p(self._p(dy).value + i * rows * d.k_pad * 2), self._gp(op.weight), hp, wp,
-                            sp))
+                        dyc = L.C.c_void_p(self._p(dy).value + i * rows * d.k_pad * 2)
+                        if op.p4:
+                            hp, wp = op.p4
+                            self._bwd.append(self._call(
+                                "rn_stem_conv_wgrad_p4", L.C.byref(dc),
+                                L.C.c_void_p(op.x8.data_ptr() + i * nc * hp * wp * 4 * 2), dyc, self._gp(op.weight),
+                                hp, wp, sp))
+                        else:  # the int8 stem: NHWC-8 chunks, clip masks in channels c_real..
+                            ws = self.wgrad_ws is not None
+                            self._bwd.append(self._call(
+                                "rn_stem_clip_wgrad_chunk", L.C.byref(dc),
+                                L.C.c_void_p(op.x8.data_ptr() + i * nc * d.h * d.w * 8 * 2), dyc, self._gp(op.weight),
+                                self._p(op.clip_ext), self._p(self.wgrad_ws) if ws else None,
+                                self.wgrad_ws_bytes if ws else 0, int(i == 0), int(i == nch - 1), sp))
                 elif op.p4:
                     self._bwd.append(self._call("rn_stem_conv_wgrad_p4", L.C.byref(op.dfull), self._p(op.x8),
                                                 self._p(dy), self._gp(op.weight), op.p4[0], op.p4[1], sp))

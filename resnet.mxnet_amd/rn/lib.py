@@ -92,6 +92,7 @@ SIGNATURES = {
     "rn_stem_clip_mask": (_i32, [_P, _P, _P, _P, _P, _P, _P]),
     "rn_stem_clip_wgrad_ws_bytes": (_i64, [_P]),
     "rn_stem_clip_wgrad": (_i32, [_P, _P, _P, _P, _P, _P, _i64, _P]),
+    "rn_stem_clip_wgrad_chunk": (_i32, [_P, _P, _P, _P, _P, _P, _i64, _i32, _i32, _P]),
     "rn_stem_clip_dbeta": (_i32, [_P, _P, _P, _P, _P]),
     "rn_stem_shift_grad": (_i32, [_P, _P, _P, _P, _P, _P]),
     "rn_bn_workspace_bytes": (_i64, [_P]),

@@ -923,6 +923,19 @@ class Checker:
         self._stem_dy = args[2]
         return self._wgrad(args, state)
 
+    def _h_rn_stem_clip_wgrad_chunk(self, args, state):
+        """The same over image chunks (executor._stem_chunks): dW is complete after the last chunk, checked
+        there against the whole batch."""
+        d = args[0]._obj
+        op = [o for o in self.ex.plan.ops if o.kind == "stem"][0]
+        i = (args[1].value - op.x8.data_ptr()) // (d.n * d.h * d.w * 8 * 2)
+        if not args[8]:
+            return None, (lambda: None)
+        dy0 = types.SimpleNamespace(value=args[2].value - i * d.n * d.p * d.q * d.k_pad * 2)
+        full = (types.SimpleNamespace(_obj=op.dfull), types.SimpleNamespace(value=op.x8.data_ptr()), dy0, args[3])
+        self._stem_dy = dy0
+        return self._wgrad(full, state)
+
     def _h_rn_stem_clip_dbeta(self, args, state):
         """rn_stem_shift_grad + rn_stem_clip_wgrad's mask part + this == the clipped beta gradient of
         _h_rn_stem_quant_clip_grad, with the same bars."""

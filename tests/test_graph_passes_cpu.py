@@ -305,3 +305,22 @@ def test_stem_backward_chunked(dry, monkeypatch):
     monkeypatch.setenv("RN_STEM_CHUNKS", "1")
     names1 = _call_names(_bind(sym, shape=(8, 3, 64, 64), precision="bfloat16").executor._bwd)
     assert "rn_bn_bwd_apply_rows" not in names1 and names1.count("rn_stem_conv_wgrad_p4") == 1
+
+
+def test_int8_stem_backward_chunked(dry, monkeypatch):
+    """The int8 stem (NHWC-8 image with the clip masks): the same per-chunk BN apply rows, each chunk's
+    weight gradient over the real + mask channels (rn_stem_clip_wgrad_chunk: the first zeroes the
+    extended gradient, the last adds the real part into dW), then the clip's dbeta after the shift grad."""
+    sym = graphs.resnet_int8(*R50_SMALL.values())
+    ex = _bind(sym, shape=(8, 3, 64, 64), precision="bfloat16").executor
+    names = _call_names(ex._bwd)
+    i = names.index("rn_bn_bwd_apply_rows")
+    assert names[i:i + 8] == ["rn_bn_bwd_apply_rows", "rn_stem_clip_wgrad_chunk"] * 4
+    flags = [tuple(ex._bwd[i + 2 * j + 1][2][7:9]) for j in range(4)]
+    assert flags == [(1, 0), (0, 0), (0, 0), (0, 1)]
+    assert sum(ex._bwd[i + 2 * j + 1][2][0]._obj.n for j in range(4)) == 8
+    assert names.index("rn_stem_shift_grad") < names.index("rn_stem_clip_dbeta")
+    assert "rn_stem_clip_wgrad" not in names
+    monkeypatch.setenv("RN_STEM_CHUNKS", "1")
+    names1 = _call_names(_bind(sym, shape=(8, 3, 64, 64), precision="bfloat16").executor._bwd)
+    assert "rn_stem_clip_wgrad_chunk" not in names1 and names1.count("rn_stem_clip_wgrad") == 1
