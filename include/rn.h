@@ -170,10 +170,11 @@ int rn_conv_bwd_filter_ws(const rn_conv_desc* d, const void* x, const void* dy, 
  * Convolution; MXNet's backward multiplies dy by the fake-quantized values x = unit * code) from the
  * input's int8 codes (x_codes: NHWC, c channels, as rn_quant_int8_fwd_codes* write them) and its unit
  * (x_unit: one fp32, device): dw += *x_unit * sum dy * code -- the codes widened to bf16 exactly, the
- * unit applied once per tile, so the bf16 fake-quantized values need not exist. The 128 / 256-column
- * LDS-DMA tiles only: rn_conv_wgrad_i8_supported(d) = 1 where this applies (bf16, dense, c % 16 == 0,
- * c_real == c, > 64 output channels and columns); ws as rn_conv_bwd_filter_ws, sized by
- * rn_conv_wgrad_i8_ws_bytes(d) (-1 where unsupported). */
+ * unit applied once per tile, so the bf16 fake-quantized values need not exist. On the streaming
+ * 1x1 kernel and the 128 / 256-column LDS-DMA tiles: rn_conv_wgrad_i8_supported(d) = 1 where this applies
+ * (bf16, dense, c % 16 == 0, c_real == c; a 1x1 stride-1 conv with K, C in {64, 128, 256}, K x C <= 32768,
+ * or > 64 output channels and columns -- not stage 1's 3x3 image-band shape); ws as rn_conv_bwd_filter_ws,
+ * sized by rn_conv_wgrad_i8_ws_bytes(d) (-1 where unsupported). */
 int32_t rn_conv_wgrad_i8_supported(const rn_conv_desc* d);
 int64_t rn_conv_wgrad_i8_ws_bytes(const rn_conv_desc* d);
 int rn_conv_bwd_filter_i8(const rn_conv_desc* d, const void* x_codes, const float* x_unit, const void* dy, float* dw,

@@ -2332,7 +2332,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_gband_kernel(GbArgs p) {
 // (the tiled kernels re-read one operand per output tile and ran at 3 TB/s, 2-3x this shape's memory
 // time); the split partials go to the slab (wgrad_slab_reduce_kernel). XF: the producing
 // BatchNorm+ReLU applied to the x fragments after their transposed read, as wgrad_big_kernel XF.
-// 8 waves, wave (wk, wc) owns MI x NI 16x16 blocks of dW.
+// 8 waves, wave (wk, wc) owns MI x NI 16x16 blocks of dW. I8X: x holds int8 codes, staged and read as
+// wgrad_big_kernel I8X (the unit applied in the epilogue).
 constexpr int stream_wk(int kb, int cb) {  // waves along K (of 8) minimizing the wave's A + B fragments
   int best = 0, cost = 1 << 30;
   for (int wk = 1; wk <= 8; wk *= 2) {
@@ -2342,14 +2343,17 @@ constexpr int stream_wk(int kb, int cb) {  // waves along K (of 8) minimizing th
   }
   return best;
 }
-template <int K, int C, int XF, int NBUF>
+template <int K, int C, int XF, int NBUF, int I8X = 0>
 __global__ __launch_bounds__(512, 1) void wgrad_stream_kernel(WgradArgs p) {
-  constexpr int BKM = 64;
-  constexpr int A_CPR = K / 8, B_CPR = C / 8;              // 16-byte chunks per LDS row
+  static_assert(!(XF && I8X), "int8 input: no input transform");
+  constexpr int BKM = 64, XES = I8X ? 1 : 2, CEB = 16 / XES;   // B bytes per element, channels per chunk
+  constexpr int A_CPR = K / 8, B_CPR = C / CEB;            // 16-byte chunks per LDS row
   constexpr int A_RPI = 64 / A_CPR, B_RPI = 64 / B_CPR;    // rows per 1 KiB DMA instruction
   constexpr int A_INS = BKM / A_RPI, B_INS = BKM / B_RPI;  // instructions per M-tile
-  static_assert((A_INS + B_INS) % 8 == 0, "DMA pieces per wave");
-  constexpr int LPT = (A_INS + B_INS) / 8;
+  constexpr int TOT = A_INS + B_INS;
+  // DMA pieces per wave: every wave issues LPT (the same count, for the vmcnt waits); past TOT a wave
+  // re-issues the last piece (the same bytes to the same LDS chunk)
+  constexpr int LPT = (TOT + 7) / 8;
   constexpr int KB = K / 16, CB = C / 16;
   constexpr int WK = stream_wk(KB, CB), WC = 8 / WK;  // (the split with the fewest fragment reads)
   constexpr int MI = KB / WK, NI = CB / WC;
@@ -2368,12 +2372,13 @@ __global__ __launch_bounds__(512, 1) void wgrad_stream_kernel(WgradArgs p) {
   bool d_isa[LPT];
 #pragma unroll
   for (int j = 0; j < LPT; ++j) {
-    const int piece = wid * LPT + j;
+    const int piece = min(wid * LPT + j, TOT - 1);
     d_isa[j] = piece < A_INS;
     const int cpr = d_isa[j] ? A_CPR : B_CPR;
     const int row = d_isa[j] ? piece * A_RPI + lane / A_CPR : (piece - A_INS) * B_RPI + lane / B_CPR;
     d_row[j] = row;
-    d_col[j] = 8 * ((lane % cpr) ^ (swz_tr(row) & (cpr - 1)));
+    d_col[j] = d_isa[j] ? 8 * ((lane % cpr) ^ (swz_tr(row) & (cpr - 1)))
+                        : CEB * ((lane % cpr) ^ ((I8X ? swz_tr8(row) : swz_tr(row)) & (cpr - 1)));
   }
   const char* __restrict__ dyb = reinterpret_cast<const char*>(p.dy);
   const char* __restrict__ xb = reinterpret_cast<const char*>(p.x);
@@ -2382,10 +2387,10 @@ __global__ __launch_bounds__(512, 1) void wgrad_stream_kernel(WgradArgs p) {
   auto issue = [&](int mb, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < LPT; ++j) {
-      const int piece = wid * LPT + j;
+      const int piece = min(wid * LPT + j, TOT - 1);
       const int m = mb + d_row[j];
       const bool ok = m < mend;
-      const uint32_t off = d_isa[j] ? (uint32_t)(m * p.ldy + d_col[j]) * 2u : (uint32_t)(m * p.C + d_col[j]) * 2u;
+      const uint32_t off = d_isa[j] ? (uint32_t)(m * p.ldy + d_col[j]) * 2u : (uint32_t)(m * p.C + d_col[j]) * (uint32_t)XES;
       const char* src = d_isa[j] ? dyb + off : xb + off;
       const uint32_t la = lds0 + buf * (kStage * 16) +
                           (d_isa[j] ? piece * 1024 : A_SZ * 16 + (piece - A_INS) * 1024);
@@ -2427,11 +2432,22 @@ __global__ __launch_bounds__(512, 1) void wgrad_stream_kernel(WgradArgs p) {
         }
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
+          if constexpr (I8X) break;
           const int col = (wc * NI + j) * 16 + 4 * pp;
           const int byte = row * (B_CPR * 16) + ((((col * 2) >> 4) ^ (swz_tr(row) & (B_CPR - 1))) << 4) + ((col * 2) & 15);
           const v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(Bb + byte));
 #pragma unroll
           for (int e = 0; e < 4; ++e) bfv[j][4 * h + e] = v[e];
+        }
+      }
+      if constexpr (I8X) {  // rows 8 g .. 8 g + 7 of the slab, one transposed byte read per fragment
+        const int row = slab * 32 + 8 * g + (li >> 1);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int cb = (wc * NI + j) * 16 + 8 * (li & 1);
+          const int byte = row * (B_CPR * 16) + (((cb >> 4) ^ (swz_tr8(row) & (B_CPR - 1))) << 4) + (cb & 15);
+          const v2i v = __builtin_amdgcn_ds_read_tr8_b64_v2i32((__attribute__((address_space(3))) v2i*)(Bb + byte));
+          bfv[j] = i8x8_to_bf16(v);
         }
       }
       if constexpr (XF) {  // (rows past the M range: their dy rows are zero)
@@ -2459,6 +2475,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_stream_kernel(WgradArgs p) {
     compute(t % NBUF);
   }
   wait_vmcnt<0>();
+  const float us = I8X ? *p.xunit : 1.f;  // (I8X: dW = unit * sum dy * code)
   float* dst = p.slab + (int64_t)zs * K * C;
 #pragma unroll
   for (int i = 0; i < MI; ++i)
@@ -2466,7 +2483,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_stream_kernel(WgradArgs p) {
     for (int e = 0; e < 4; ++e) {
       const int k = (wk * MI + i) * 16 + (lane >> 4) * 4 + e;
 #pragma unroll
-      for (int j = 0; j < NI; ++j) dst[(int64_t)k * C + (wc * NI + j) * 16 + (lane & 15)] = acc[i][j][e];
+      for (int j = 0; j < NI; ++j) dst[(int64_t)k * C + (wc * NI + j) * 16 + (lane & 15)] = I8X ? acc[i][j][e] * us : acc[i][j][e];
     }
 }
 
@@ -3889,8 +3906,8 @@ int rn_conv_bwd_data(const rn_conv_desc* d, const void* dy, const void* w_crsk, 
 namespace {
 // The weight-gradient kernel choice for d. launch == false: only *ws_need (bytes of split-M partial
 // slabs the chosen kernel stores when given a workspace; 0 = it adds into dw with atomics).
-// xunit != NULL: x holds int8 codes, dW = *xunit * sum dy * code (the 128 / 256-column LDS-DMA tiles only:
-// wgrad_i8_ok)
+// i8: x holds int8 codes, dW = *xunit * sum dy * code (the streaming kernel and the 128 / 256-column
+// LDS-DMA tiles only: rn_conv_wgrad_i8_supported)
 int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* dw, const float* in_scale,
                    const float* in_shift, float* ws, int64_t ws_bytes, int64_t* ws_need, bool launch,
                    hipStream_t st, const float* xunit = nullptr, bool i8 = false) {
@@ -4032,7 +4049,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
   // streaming pass over M per workgroup (wgrad_stream_kernel; rn_set_tuning 19 = 1: off)
   const bool one = d->r == 1 && d->s == 1 && d->stride_h == 1 && d->stride_w == 1 && d->pad_h == 0 && d->pad_w == 0;
   auto pw2 = [](int v) { return v == 64 || v == 128 || v == 256; };
-  if (!i8 && d->dtype == RN_BF16 && !grouped && one && pw2(d->k) && pw2(d->c) && d->k * d->c <= 32768 &&
+  if (d->dtype == RN_BF16 && !grouped && one && pw2(d->k) && pw2(d->c) && d->k * d->c <= 32768 &&
       d->c_real == d->c && d->k_pad == d->k && g_tune[RN_TUNE_WGRAD_BAND] != 1 &&
       (int64_t)a.M * (d->k + d->c) * 2 < INT32_MAX) {
     const int64_t mtiles = ceil_div(a.M, 64);
@@ -4047,6 +4064,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
 #define RN_STREAM(KK, CC)                                                                         \
   if (d->k == KK && d->c == CC) {                                                                 \
     if (t) hipLaunchKernelGGL((wgrad_stream_kernel<KK, CC, 1, 3>), grid, dim3(512), 0, st, a);    \
+    else if (i8) hipLaunchKernelGGL((wgrad_stream_kernel<KK, CC, 0, 3, 1>), grid, dim3(512), 0, st, a); \
     else hipLaunchKernelGGL((wgrad_stream_kernel<KK, CC, 0, 3>), grid, dim3(512), 0, st, a);      \
   }
       RN_STREAM(64, 64) RN_STREAM(64, 128) RN_STREAM(64, 256) RN_STREAM(128, 64) RN_STREAM(128, 128)

@@ -909,7 +909,8 @@ class Executor:
     def _codes_wgrad(self, plan):
         """Quantizers whose fake-quantized values only int8 convolutions read, each of whose weight
         gradients takes the int8 codes instead (rn_conv_bwd_filter_i8: dW = unit * sum dy * code, the
-        128 / 256-column tiles, every ResNet-50 layer past stage 1): the forward writes the codes only,
+        streaming and 128 / 256-column kernels, every ResNet-50 layer but stage 1's 3x3): the forward
+        writes the codes only,
         and the bf16 values -- 2 of the pass's 5 bytes per element -- are never written or read
         (RN_QUANT_CODES_WGRAD=0: values + bf16 weight gradients)."""
         on = os.environ.get("RN_QUANT_CODES_WGRAD", "1") == "1" and self.dtype == L.RN_BF16

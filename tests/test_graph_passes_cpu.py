@@ -199,13 +199,14 @@ def test_int8_forward_plan(dry, monkeypatch):
     ex = _bind(graphs.resnet_int8(*R50_SMALL.values()), shape).executor
     assert not any(op.defer_values for op in ex.plan.ops if op.kind == "quant")
     assert "rn_quant_int8_expand" not in _call_names(ex._bwd)
-    # default (bf16): the quantizers of stages 2-4 (every conv with > 64 output channels) write codes only
-    # and their convs' weight gradients multiply the codes (rn_conv_bwd_filter_i8, on the side stream)
+    # default (bf16): the quantizers whose convs' weight gradients take codes (all but stage 1's act2, whose
+    # conv2 runs the image-band kernel) write codes only (rn_conv_bwd_filter_i8, on the side stream)
     ex = _bind(graphs.resnet_int8(*R50_SMALL.values()), shape, precision="bfloat16").executor
     cw = [op for op in ex.plan.ops if op.kind == "quant" and op.codes_wgrad]
     bn = _call_names(ex._bwd)
-    assert len(cw) == 42 and bn.count("rn_conv_bwd_filter_i8") == 42
-    assert all(op.qsrc.codes_wgrad == (op.name.split("_")[0] != "stage1") for op in ex.plan.ops if op.kind == "conv")
+    assert len(cw) == 49 and bn.count("rn_conv_bwd_filter_i8") == 49
+    assert all(op.qsrc.codes_wgrad == (not (op.name.startswith("stage1") and op.name.endswith("conv2")))
+               for op in ex.plan.ops if op.kind == "conv")
     assert "rn_conv_bwd_filter_i8" in ex.WGRAD_CALLS  # (routed to the side stream by name, _route_wgrads)
     monkeypatch.setenv("RN_QUANT_CODES_WGRAD", "0")
     ex = _bind(graphs.resnet_int8(*R50_SMALL.values()), shape, precision="bfloat16").executor

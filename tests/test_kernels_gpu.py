@@ -1789,7 +1789,11 @@ def test_wgrad_grouped_image_bands(gpu, case):
 
 
 @pytest.mark.parametrize("case", [
-    (3, 128, 9, 11, 128, 1, 1, 0),    # 128 columns: the 128 x 128 tile (wgrad_big_kernel<128, 2, 128>), ragged M
+    (3, 128, 9, 11, 128, 1, 2, 0),    # 128 columns, stride 2: the 128 x 128 tile (wgrad_big_kernel<128, 2, 128>)
+    (3, 64, 13, 11, 64, 1, 1, 0),     # the streaming kernel (wgrad_stream_kernel<64, 64>), ragged M
+    (2, 64, 9, 9, 256, 1, 1, 0),      # streaming, stage 1's conv3 / shortcut shape
+    (2, 256, 9, 10, 64, 1, 1, 0),     # streaming, stage 1's conv1 shape
+    (2, 256, 5, 7, 128, 1, 1, 0),     # streaming, stage 2's first conv1
     (2, 256, 14, 14, 512, 1, 1, 0),   # 256-column tiles, 256-row k tiles
     (2, 512, 7, 9, 128, 1, 1, 0),     # 256-column tiles, 128-row k tiles
     (2, 256, 14, 14, 1024, 1, 2, 0),  # the stride-2 shortcut
@@ -1835,11 +1839,11 @@ def test_wgrad_int8_codes(gpu, case):
 
 
 def test_wgrad_int8_codes_unsupported(gpu):
-    """Shapes the int8-codes weight gradient does not cover (<= 64 output channels: stage 1's streaming
-    and band kernels; channels not in 16-byte chunks) report 0 and the call fails with an error, never a
-    launch."""
+    """Shapes the int8-codes weight gradient does not cover (<= 64 output channels off the streaming
+    kernel, stage 1's 3x3 image-band kernel; channels not in 16-byte chunks) report 0 and the call fails
+    with an error, never a launch."""
     lib = L.load()
-    for n, c, h, w, k, r, st, pd in ((2, 256, 8, 8, 64, 1, 1, 0), (2, 64, 8, 8, 64, 3, 1, 1), (2, 24, 8, 8, 128, 3, 1, 1)):
+    for n, c, h, w, k, r, st, pd in ((2, 256, 8, 8, 64, 1, 2, 0), (2, 64, 8, 8, 64, 3, 1, 1), (2, 24, 8, 8, 128, 3, 1, 1)):
         d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd)
         assert lib.rn_conv_wgrad_i8_supported(C.byref(d)) == 0
         assert lib.rn_conv_wgrad_i8_ws_bytes(C.byref(d)) == -1

@@ -268,11 +268,11 @@ def _c5_layerwise(n, image, defer=False):
     n_def = sum(1 for op in ck.ex.plan.ops if op.kind == "quant" and op.defer_values)
     assert n_def == (52 if defer else 0)
     assert sum(1 for r in ck.rec if r[0] == "quant_expand") == n_def
-    # (default: the quantizers of stages 2-4, whose convs all have > 64 output channels, write codes only
-    # and their weight gradients multiply the codes, rn_conv_bwd_filter_i8)
+    # (default: the quantizers but stage 1's act2 write codes only and their weight gradients multiply
+    # the codes, rn_conv_bwd_filter_i8)
     n_cw = sum(1 for op in ck.ex.plan.ops if op.kind == "quant" and op.codes_wgrad)
-    assert n_cw == (0 if defer else 42), n_cw
-    assert ck.covered.get("rn_conv_bwd_filter_i8", 0) == (0 if defer else 42)  # one per quantizer
+    assert n_cw == (0 if defer else 49), n_cw
+    assert ck.covered.get("rn_conv_bwd_filter_i8", 0) == (0 if defer else 49)  # one per quantizer
     assert sum(1 for r in ck.rec if r[0] == "wgrad") == 54
     bad = ck.failures()
     assert not bad, bad[:10]

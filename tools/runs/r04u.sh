@@ -1,0 +1,8 @@
+# int8-codes weight gradients on the streaming kernel too (stage 1): tests, C5 layerwise, A/B pairs
+b() { echo "200 env $1 python bench.py --model resnet50_int8 --no-cpu-baseline --pcie-steps 0 > gpurun_out/r04u_$2.log 2>&1"; }
+tools/gpu_steps.sh \
+ "300 python -u -m pytest tests/test_kernels_gpu.py -x -q -k 'int8_codes or wgrad_stream' --timeout 120 --timeout-method thread > gpurun_out/r04u_kt.log 2>&1" \
+ "600 python -u -m pytest tests/test_step_bf16_gpu.py -x -q -k 'int8' --timeout 500 --timeout-method thread > gpurun_out/r04u_lw.log 2>&1" \
+ "$(b RN_X=0 n1)" "$(b RN_QUANT_CODES_WGRAD=0 o1)" "$(b RN_X=0 n2)" "$(b RN_QUANT_CODES_WGRAD=0 o2)"
+tail -n2 gpurun_out/r04u_kt.log; tail -n2 gpurun_out/r04u_lw.log
+for f in n1 o1 n2 o2; do echo -n "$f "; tail -n1 gpurun_out/r04u_$f.log | grep -o '"ms_per_step": [0-9.]*'; done
