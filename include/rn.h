@@ -115,6 +115,16 @@ int rn_conv_bwd_data_bnred_clip(const rn_conv_desc* d, const void* dy, const voi
                                 const void* add_src, const void* bn_x, const float* bn_mean, const float* bn_scale,
                                 const float* bn_shift, int32_t relu, const float* clip, float* part,
                                 rn_stream_t stream);
+/* A stage-first unit's act1 read by two Quantization_int8 (symbol/resnet_int8.py: conv1's and the
+ * shortcut's, each with its own threshold): the later of the two data gradients writes dx = bf16(
+ * [y < *clip] * bf16(its gradient) + [y < *clip2] * other), y = bf16(bn_x * scale + shift) -- both
+ * straight-through clips, as rn_bn_bwd forms them from rn_bn_desc.dy / dy2 -- and reduces the BN+ReLU
+ * backward from it (part, as rn_conv_bwd_data_bnred); the BN then runs rn_bn_bwd_part on dx with no clip.
+ * other: the first quantizer's stored gradient (read only). bf16, dense, an LDS-DMA tile. */
+int rn_conv_bwd_data_bnred_clip2(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
+                                 const void* other, const void* bn_x, const float* bn_mean, const float* bn_scale,
+                                 const float* bn_shift, const float* clip, const float* clip2, float* part,
+                                 rn_stream_t stream);
 /* The post-activation unit tail's backward (symbol/resnext.py:41-47 / resnet_cifar: y = relu(bn3(conv3)
  * [+ bn_sc(sc)] + shortcut)) in the epilogue of the data gradient that completes dL/dy: this call
  * stores g = round(conv_transpose(dy, w) + add_src) * [y > 0] (add_src nullable; the value

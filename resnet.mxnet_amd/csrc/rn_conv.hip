@@ -94,6 +94,7 @@ struct IgemmArgs {
   const float* bn_coef;
   // dgrad only, nullable: a folded Quantization_int8 straight-through clip on the BN output (rn_bn_desc.clip)
   const float* bn_clip;
+  const float* bn_clip2;  // (EPI 4) nullable: a quantizer pair -- add is the other quantizer's gradient (below)
   // dgrad only, nullable (igemm_big_kernel EPIX 6, rn_conv_bwd_data_relu_bnred): the post-activation unit
   // tail's backward in the epilogue -- the stored value is g = round(dgrad + add) * [rr_y > 0] (the ReLU
   // after the residual add), reduced for the BatchNorm whose input is bn_x (mean bn_mean, -> bnred) and
@@ -1168,6 +1169,12 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
   }
   const bf16_t* __restrict__ bxg = reinterpret_cast<const bf16_t*>(p.bn_x);
   const float clipt = CLIP ? *p.bn_clip : 0.f;  // (EPI 4: a folded quantizer clip)
+  // (EPI 4, a quantizer pair: the two quantizers of one BN+ReLU output, symbol/resnet_int8.py's stage-first
+  // units. This dgrad's own gradient takes clip 1, the add operand -- the other quantizer's stored gradient
+  // -- clip 2; the stored value is their clipped sum, rounded once, as rn_bn.hip's relu_clip2_dz forms
+  // it, and the reduction reads it with the ReLU mask only)
+  const bool qpair = CLIP && p.bn_clip2 != nullptr;
+  const float clipt2 = qpair ? *p.bn_clip2 : 0.f;
 #pragma unroll
   for (int h = 0; h < NCH; ++h) {
     constexpr int kLast = WM - 64 * (NCH - 1);  // rows of the last chunk (48 for 112-row waves)
@@ -1264,6 +1271,16 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
             if (ag) w += a[e];
             v[e] = w;
           }
+        } else if (CLIP && qpair) {  // c1 * bf16(own) + c2 * add, c = [bf16(BN output) < t]
+          float a[8], xv[8];
+          chunk_to_f(addv[k][0], a, (const bf16_t*)nullptr);
+          chunk_to_f(xpre[XP ? k : 0], xv, (const bf16_t*)nullptr);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float y = to_f(from_f<bf16_t>(fmaf(xv[e], r_sc[e], r_sh[e])));
+            const float own = to_f(from_f<bf16_t>(v[e]));
+            v[e] = (y < clipt ? own : 0.f) + (y < clipt2 ? a[e] : 0.f);
+          }
         } else if (ag) {
           float a[8];
 #pragma unroll
@@ -1328,7 +1345,7 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
             for (int e = 0; e < 8; ++e) {
               float dz = (!p.bn_relu || fmaf(xv[e], r_sc[e], r_sh[e]) > 0.f) ? g[e] : 0.f;
               if constexpr (CLIP)  // the quantizer's straight-through clip on the stored BN output
-                if (!(to_f(from_f<bf16_t>(fmaf(xv[e], r_sc[e], r_sh[e]))) < clipt)) dz = 0.f;
+                if (!qpair && !(to_f(from_f<bf16_t>(fmaf(xv[e], r_sc[e], r_sh[e]))) < clipt)) dz = 0.f;
               s1[e] += dz;
               s2[e] = fmaf(dz, xv[e] - r_mu[e], s2[e]);
             }
@@ -3864,6 +3881,23 @@ int rn_conv_bwd_data_bnred_clip(const rn_conv_desc* d, const void* dy, const voi
   hipStream_t st = as_stream(stream);
   if (d->dtype == RN_BF16) return launch_igemm<bf16_t, bf16_t>(a, st);
   return launch_igemm<float, float>(a, st);
+}
+
+int rn_conv_bwd_data_bnred_clip2(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
+                                 const void* other, const void* bn_x, const float* bn_mean, const float* bn_scale,
+                                 const float* bn_shift, const float* clip, const float* clip2, float* part,
+                                 rn_stream_t stream) {
+  RN_CHECK_ARG(d && dy && w_crsk && dx && other && bn_x && bn_mean && bn_scale && bn_shift && clip && clip2 && part,
+               "null argument");
+  RN_CHECK_ARG(d->dtype == RN_BF16 && d->groups <= 1 && d->c % 8 == 0 && d->c == d->c_real && rn_conv_tile(d, 1) >= 64,
+               "a quantizer pair's clips fold into a bf16 BN+ReLU reduction on an LDS-DMA tile");
+  IgemmArgs a = make_igemm_args(d, 1);
+  a.x = dy; a.w = w_crsk; a.y = dx; a.add = other; a.bias = nullptr;
+  int maxMc = 0;
+  for (int z = 0; z < a.ncls; ++z) maxMc = std::max(maxMc, a.N * a.cls[z].Pc * a.cls[z].Qc);
+  a.bnred = part; a.bn_x = bn_x; a.bn_mean = bn_mean; a.bn_sc = bn_scale; a.bn_sh = bn_shift;
+  a.bn_relu = 1; a.bn_clip = clip; a.bn_clip2 = clip2; a.mt_max = (int)ceil_div(maxMc, 128);
+  return launch_igemm<bf16_t, bf16_t>(a, as_stream(stream));
 }
 
 int rn_conv_bwd_data_relu_bnred(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* g,

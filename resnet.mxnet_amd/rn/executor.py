@@ -1466,6 +1466,8 @@ class Executor:
             if op.kind == "bn":
                 op.qpair = False
                 op.qorder = []  # the folded quantizers in backward order (their gradients' pending order)
+                op.qwriters = []  # (a pair) the last writer of each one's gradient (self._gw entries)
+                op.pair_fused = None
         for bn, qs in groups.values():
             if len(qs) == 1:
                 bn.desc.clip = self._ap(qs[0].q["minmax"]).value  # (the threshold the forward just updated)
@@ -1483,6 +1485,10 @@ class Executor:
         # BN backward applied by a recomputed cheap dgrad (rn_conv_bwd_data_bnapply), opt-in
         # (RN_BN_BWD_RECOMPUTE=1): bit-identical, but measured 22.18 vs 21.45 ms per step
         recompute = os.environ.get("RN_BN_BWD_RECOMPUTE", "0") == "1"
+        # a quantizer pair's clips and BN reduction in the later data gradient's epilogue
+        # (rn_conv_bwd_data_bnred_clip2), opt-in (RN_QUANT_PAIR_FUSION=1): parity-green but measured
+        # neutral (C5 22.68 / 22.69 vs 22.69 / 22.68 ms) -- default rn_bn_bwd with dy / dy2
+        pair_fusion = bwd_fusion and os.environ.get("RN_QUANT_PAIR_FUSION", "0") == "1"
         # one workspace for the weight gradients' split-M partial tiles (rn_conv_bwd_filter_ws),
         # sized for the largest layer. Shared safely because every call using it is a weight-gradient
         # call, and those all run in plan order on ONE stream (the side stream when it is on:
@@ -1527,6 +1533,19 @@ class Executor:
                 if len(pend) == 2:
                     op.desc.clip2 = self._ap(op.qorder[1].q["minmax"]).value
                     op.desc.dy2 = self._p(pend[1]).value
+                    ws_ = op.qwriters
+                    ok = pair_fusion and self.dtype == BF16 and op.relu and op.y.c % 8 == 0 and \
+                        op.y.c == op.y.cp and len(ws_) == 2 and \
+                        all(w and w[0] == "dgrad" and w[5] is None and w[4] is b for w, b in zip(ws_, pend))
+                    if ok:
+                        late = 0 if ws_[0][1] > ws_[1][1] else 1
+                        lw = ws_[late]
+                        ok = lw[2].desc.groups <= 1 and int(self.lib.rn_conv_tile(L.C.byref(lw[2].desc), 1)) >= 64
+                    if ok:
+                        # the later dgrad stores both clipped gradients' sum and reduces the BN from it
+                        op.pair_fused = (lw, ws_[1 - late], op.qorder[late], op.qorder[1 - late])
+                        dy = lw[4]
+                        op.desc.clip = op.desc.clip2 = op.desc.dy2 = 0
             else:
                 dy = gs.read(op.y) if op.kind != "softmax" else None
             if dy is None:
@@ -1649,6 +1668,19 @@ class Executor:
                                                 self._p(dy), self._p(out), self._p(add), self._pp(op.gamma),
                                                 self._ap(op.mean), self._ap(op.var), op.sc, op.sh,
                                                 self._gp(op.gamma), self._gp(op.beta), wsp, sp))
+                elif op.pair_fused is not None:
+                    lw, ew, lq, eq = op.pair_fused
+                    _, ci, cop, cdy, cout, _ = lw
+                    op.bnred_blocks = int(self.lib.rn_conv_bnred_blocks(L.C.byref(cop.desc)))
+                    op.bnred = self._zeros(op.bnred_blocks * op.y.cp * 2, self.torch.float32)
+                    self._bwd[ci] = self._call("rn_conv_bwd_data_bnred_clip2", L.C.byref(cop.desc), self._p(cdy),
+                                               self._p(cop.wc), self._p(cout), self._p(ew[4]), self._p(self.act(x)),
+                                               op.sm, op.sc, op.sh, self._ap(lq.q["minmax"]),
+                                               self._ap(eq.q["minmax"]), self._p(op.bnred), sp)
+                    self._bwd.append(self._call("rn_bn_bwd_part", L.C.byref(op.desc), self._p(op.bnred),
+                                                op.bnred_blocks, self._p(self.act(x)), self._p(dy), self._p(out),
+                                                self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc, op.sh,
+                                                self._gp(op.gamma), self._gp(op.beta), wsp, sp))
                 elif bwd_fusion and not op.desc.dy2 and w and w[0] == "dgrad" and dy is w[4] and \
                         op.y.c % 8 == 0 and op.y.c == op.y.cp and \
                         (bwd_all or self._big_tile(w[2], 1) or self._grouped_fuse(w[2], 1)) and \
@@ -1739,6 +1771,7 @@ class Executor:
                     bn = folds[id(op)]
                     bn.qorder.append(op)
                     if bn.qpair:
+                        bn.qwriters.append(self._gw.get(id(op.y)))
                         self._gw[id(op.x)] = ("other",)
                     elif id(op.y) in self._gw:
                         self._gw[id(op.x)] = self._gw[id(op.y)]

@@ -62,6 +62,7 @@ SIGNATURES = {
     "rn_relu_bwd_bnred": (_i32, [_P] * 11),
     "rn_conv_bwd_data_bnred": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P, _P]),
     "rn_conv_bwd_data_bnred_clip": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P, _P, _P]),
+    "rn_conv_bwd_data_bnred_clip2": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bnred_blocks": (_i64, [_P]),
     "rn_bn_bwd_part": (_i32, [_P, _P, _i64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rn_bn_bwd_finalize": (_i32, [_P, _P, _i64, _P, _P, _P, _P, _P, _P, _P]),

@@ -593,6 +593,33 @@ class Checker:
         # (its reduction carries the folded quantizer clip: checked through the BN backward it feeds)
         return self._dgrad(args, state, bnred=True)
 
+    def _h_rn_conv_bwd_data_bnred_clip2(self, args, state):
+        """A quantizer pair's later data gradient: dx = [y < t1] * its dgrad + [y < t2] * the other
+        quantizer's stored gradient, y = bf16(BN output) (clip_grad_quantization_int8.py's STE of each, as
+        rn_bn_bwd's relu_clip2_dz sums them) -- vs the fp32 dgrad of the device's dy (its BN reduction:
+        checked through the BN backward it feeds)."""
+        d = args[0]._obj
+        dyp, wcp, dxp, otp, xp, c1p, c2p = args[1], args[2], args[3], args[4], args[5], args[9], args[10]
+        op = self.wc_op[wcp.value]
+        if not hasattr(self, "bn_by_sm_x"):
+            self.bn_by_sm_x = {self.ex.act(o.x).data_ptr(): o for o in self.ex.plan.ops if o.kind == "bn"}
+        bn = self.bn_by_sm_x[xp.value]
+        snap = self._snap(otp, state, "other")
+
+        def post():
+            n = d.n
+            dy = self.nchw(self.t(dyp), n, d.p, d.q, d.k_pad, d.k)
+            w = self.w_from_crsk(op.wc, d)
+            g = ref_dgrad(dy, w, (d.h, d.w), (d.stride_h, d.stride_w), (d.pad_h, d.pad_w))
+            _, _, sc, sh = self.bn_coefs(bn)
+            c = d.c_real
+            y = _bf16(_fma(self.act_nchw(bn.x), sc[:c].view(1, c, 1, 1), sh[:c].view(1, c, 1, 1)))
+            other = self.nchw(state["other"], n, d.h, d.w, d.c, d.c_real)
+            ref = g * (y < self.aux_val(c1p)) + other * (y < self.aux_val(c2p))
+            dev = self.nchw(self.t(dxp), n, d.h, d.w, d.c, d.c_real)
+            self.add("dgrad_bnred_clip2", op.name, dev, ref, BF16_BAR)
+        return snap, post
+
     def _h_rn_bn_bwd_finalize(self, args, state):
         return None, (lambda: None)  # (dgamma / dbeta: checked after rn_conv_bwd_data_bnapply)
 

@@ -276,6 +276,7 @@ def _c5_layerwise(n, image, defer=False):
     assert sum(1 for r in ck.rec if r[0] == "wgrad") == 54
     bad = ck.failures()
     assert not bad, bad[:10]
+    return ck
 
 
 def test_resnet50_bf16_layerwise_act2_on_load(gpu, monkeypatch):
@@ -308,6 +309,15 @@ def test_resnext50_bf16_layerwise_tail_in_dgrad(gpu, monkeypatch):
 def test_resnet50_int8_layerwise_small(gpu):
     """The C5 per-kernel checks at 8 images of 64x64 (a fast first gate before the full size)."""
     _c5_layerwise(8, 64)
+
+
+def test_resnet50_int8_layerwise_pair_fusion(gpu, monkeypatch):
+    """The opt-in quantizer-pair fusion (RN_QUANT_PAIR_FUSION=1: the stage-first units' two act1
+    quantizers' clips and the BN reduction in the later data gradient's epilogue,
+    rn_conv_bwd_data_bnred_clip2), per kernel at 8 images of 112x112."""
+    monkeypatch.setenv("RN_QUANT_PAIR_FUSION", "1")
+    ck = _c5_layerwise(8, 112)
+    assert ck.covered.get("rn_conv_bwd_data_bnred_clip2", 0) == 3
 
 
 def test_resnet50_int8_layerwise_deferred_values(gpu, monkeypatch):
