@@ -662,32 +662,41 @@ __global__ __launch_bounds__(256) void bnq_codes_kernel(const T* __restrict__ x,
     const int64_t off = r * c + cb;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
-      float g[16], tq[16];
+      float g[16], tq[16], sm[16];
       uint32_t cw[4];
       // the quotient v / unit as v * (1 / unit): within 2^-22 |q| of the IEEE quotient, so the two
       // round alike unless the product lies that close to a half-integer -- then (rarely: checked per
       // wave) the exact division, so the codes stay those of round(v / unit) bit for bit (this kernel is
-      // VALU-bound, and the division's ~11 instructions per element were a third of it)
+      // VALU-bound, and the division's ~11 instructions per element were a third of it).
+      // Rounding: sm = tq + 1.5 * 2^23 rounds tq to the nearest integer (ties to even) in the low
+      // mantissa bits -- the code's byte is sm's low byte, the integer sm - 1.5 * 2^23. That equals
+      // roundf's (ties away) wherever tq is not within the near-half tolerance below, whose elements
+      // take roundf of the exact quotient instead: |tq - rne(tq)| = 0.5 - |frac(tq) - 0.5|, so the test
+      // is the same one, exactly
+      constexpr float kMagic = 12582912.f;
       uint32_t nearm = exact_div ? 0xFFFFu : 0u;  // (rn_set_tuning 22 = 1: the division everywhere)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         tq[e] = fminf(fmaxf(f[e], -t[k]), t[k]) * inv[k];
+        sm[e] = tq[e] + kMagic;
+        const float d = fabsf(tq[e] - (sm[e] - kMagic));
         // (written as !(>) so that a non-finite product -- a unit so small its reciprocal overflows --
         // takes the exact path too)
-        if (!(fabsf(fabsf(tq[e] - truncf(tq[e])) - 0.5f) > fabsf(tq[e]) * 4.8e-7f)) nearm |= 1u << e;
+        if (!(0.5f - d > fabsf(tq[e]) * 4.8e-7f)) nearm |= 1u << e;
       }
       if (__any(nearm != 0u)) {
 #pragma unroll
         for (int e = 0; e < 16; ++e)
-          if ((nearm >> e) & 1u) tq[e] = fminf(fmaxf(f[e], -t[k]), t[k]) / unit[k];
+          if ((nearm >> e) & 1u)
+            sm[e] = (unit[k] > 0.f ? roundf(fminf(fmaxf(f[e], -t[k]), t[k]) / unit[k]) : 0.f) + kMagic;
       }
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {  // quant_codes_kernel's clip / round / dequantize
-        const float q = unit[k] > 0.f ? roundf(tq[e]) : 0.f;
-        g[e] = q * unit[k];
-        const uint32_t b = (uint32_t)(uint8_t)(int8_t)(int)q;
-        if ((e & 3) == 0) cw[e >> 2] = b;
-        else cw[e >> 2] |= b << (8 * (e & 3));
+      for (int e = 0; e < 16; e += 4) {  // quant_codes_kernel's clip / round / dequantize
+        const uint32_t lo = __builtin_amdgcn_perm(__float_as_uint(sm[e + 1]), __float_as_uint(sm[e]), 0x0c0c0400u);
+        const uint32_t hi = __builtin_amdgcn_perm(__float_as_uint(sm[e + 3]), __float_as_uint(sm[e + 2]), 0x0c0c0400u);
+        cw[e >> 2] = lo | (hi << 16);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) g[e + u] = (sm[e + u] - kMagic) * unit[k];
       }
       if (tg.out[k])  // (null: codes only, the values expanded later by rn_quant_int8_expand)
 #pragma unroll
