@@ -677,12 +677,20 @@ __global__ __launch_bounds__(256) void bnq_codes_kernel(const T* __restrict__ x,
       uint32_t nearm = exact_div ? 0xFFFFu : 0u;  // (rn_set_tuning 22 = 1: the division everywhere)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        tq[e] = fminf(fmaxf(f[e], -t[k]), t[k]) * inv[k];
-        sm[e] = tq[e] + kMagic;
-        const float d = fabsf(tq[e] - (sm[e] - kMagic));
-        // (written as !(>) so that a non-finite product -- a unit so small its reciprocal overflows --
-        // takes the exact path too)
-        if (!(0.5f - d > fabsf(tq[e]) * 4.8e-7f)) nearm |= 1u << e;
+        if constexpr (RELU) {  // (f >= 0, t >= 0: the clip is min(f, t), a select; tq >= 0)
+          tq[e] = (f[e] < t[k] ? f[e] : t[k]) * inv[k];
+          sm[e] = tq[e] + kMagic;
+          // (the same test as below up to the rounding of its right-hand side, which the tolerance's 2x
+          // margin over the reciprocal's error absorbs; a non-finite product fails the < and is exact)
+          if (!(fabsf(tq[e] - (sm[e] - kMagic)) < fmaf(-4.8e-7f, tq[e], 0.5f))) nearm |= 1u << e;
+        } else {
+          tq[e] = fminf(fmaxf(f[e], -t[k]), t[k]) * inv[k];
+          sm[e] = tq[e] + kMagic;
+          const float d = fabsf(tq[e] - (sm[e] - kMagic));
+          // (written as !(>) so that a non-finite product -- a unit so small its reciprocal overflows --
+          // takes the exact path too)
+          if (!(0.5f - d > fabsf(tq[e]) * 4.8e-7f)) nearm |= 1u << e;
+        }
       }
       if (__any(nearm != 0u)) {
 #pragma unroll
