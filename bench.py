@@ -69,23 +69,28 @@ def conv_call_bytes(ex, name, args):
 PMC_ROUNDS = ("r04", "r03")  # newest first: the committed PMC summary of the latest round that has one
 
 
-def pmc_json_path():
+def pmc_json_path(model="resnet50"):
+    """The committed PMC summary of this model's bench (profiles/<round>/pmc_hbm_bytes_per_launch_<model>.json;
+    the unsuffixed file is ResNet-50's): another model's per-launch bytes are not this one's."""
     env = os.environ.get("RN_PMC_JSON")
     if env:
         return env
     for r in PMC_ROUNDS:
-        p = os.path.join(REPO, "profiles", r, "pmc_hbm_bytes_per_launch.json")
-        if os.path.exists(p):
-            return p
+        names = ["pmc_hbm_bytes_per_launch_%s.json" % model] + (["pmc_hbm_bytes_per_launch.json"]
+                                                                if model == "resnet50" else [])
+        for nm in names:
+            p = os.path.join(REPO, "profiles", r, nm)
+            if os.path.exists(p):
+                return p
     return None
 
 
-def pmc_traffic(family, path=None):
+def pmc_traffic(family, path=None, model="resnet50"):
     """HBM bytes per launch of `family` from the committed rocprofv3 PMC summary (tools/pmc_bench.sh +
     tools/pmc_summary.py: FETCH_SIZE doubled per the gfx950 correction, plus WRITE_SIZE). The summary
     nests the families under "hbm" (with "sq" and "last_step_hbm_bytes" beside it); a flat
     {family: record} file (round 2) is read too."""
-    path = path or pmc_json_path()
+    path = path or pmc_json_path(model)
     if not path:
         return None, None
     try:
@@ -553,7 +558,7 @@ def main():
         flops_step = ex.plan.train_flops()
         per_launch_flops = timer.flops / max(1, len(timer.idx))
         avg_ms = fam_ms / max(fam_n, 1)
-        traffic, traffic_src = pmc_traffic(dom)
+        traffic, traffic_src = pmc_traffic(dom, model=a.model)
         alg_bytes = timer.bytes / max(1, len(timer.idx))
         # which roofline binds this family: its algorithmic FLOP per algorithmic byte vs the ridge
         intensity = per_launch_flops / max(alg_bytes, 1.0)

@@ -140,3 +140,7 @@ def test_pmc_traffic_reads_the_committed_summary(tmp_path):
     nested = tmp_path / "nested.json"
     nested.write_text(json.dumps({"hbm": {"fam": {"hbm_bytes": 7.0}}, "sq": {}, "last_step_hbm_bytes": 1.0}))
     assert bench.pmc_traffic("fam", str(nested))[0] == 7.0
+    # another model reads its own summary, never ResNet-50's
+    for m in ("resnext50", "resnet50_int8"):
+        p = bench.pmc_json_path(m)
+        assert p is None or p.endswith("pmc_hbm_bytes_per_launch_%s.json" % m), p
