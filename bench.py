@@ -8,14 +8,15 @@ seeded U(-1,1) data, random labels), bf16 activations/weights with fp32 master w
 gradients and BN statistics. Inputs are resident in HBM before the timed region.
 
 Rank 0 prints ONE JSON line (contract in the task statement), including
-  roofline     : the dominant kernel family (most time per step in a serialised calibration step,
-                 among the compute stream's families when the weight gradients run overlapped on
-                 the side stream; every family's time is listed) -- algorithmic FLOP per launch
-                 / average launch duration from HIP events around every launch of that family
-                 (eager mode: inside the timed region; HIP-graph mode: in one eager step right
-                 after it, graph nodes carry no timing events), vs the dense bf16 MFMA peak
-  roofline     : "bound" from the family's algorithmic FLOP/byte vs the 312.5 FLOP/B ridge (2.5 PF
-                 bf16 / 8 TB/s); both the MFMA and the HBM fraction are reported
+  roofline     : the dominant kernel family (most kernel time per step in a serialised calibration
+                 step; every family's time is listed) -- algorithmic FLOP and bytes per launch /
+                 average launch duration from HIP events around every launch of that family on the
+                 stream it runs on (eager mode: inside the timed region; HIP-graph mode: in one eager
+                 step right after it, graph nodes carry no timing events); "bound" from the family's
+                 algorithmic FLOP/byte vs the 312.5 FLOP/B ridge (2.5 PF bf16 / 8 TB/s), both the MFMA
+                 and the HBM fraction reported
+  critical_path: the same record for the compute stream's largest family (the data-gradient chain that
+                 sets the step while the weight gradients run overlapped on the side stream)
   pcie_inclusive: the same step fed the iterator's pinned host batch every step (not `value`)
   cpu_baseline : torch-CPU fp32 (oneDNN) restatement of the same step (oracle/torch_cpu.py,
                  "port") on every host core, batch 32 (rank 0, N=1 only)
@@ -205,6 +206,38 @@ def calibrate_families(torch, ex, mod):
     return out
 
 
+def family_roofline(family, timer, calib, model="resnet50"):
+    """Roofline record of one kernel family: algorithmic FLOP and bytes per launch over the average launch
+    duration from the HIP events of the timed region (`avg_launch_ms`, sharing the CUs with whatever runs
+    beside it) and from the serialised calibration step (`solo_*`: the kernel alone)."""
+    launches = max(1, len(timer.idx))
+    fam_ms, fam_n = timer.result()
+    avg_ms = fam_ms / max(fam_n, 1)
+    solo_ms = calib[0] / max(calib[1], 1)
+    flops = timer.flops / launches
+    alg_bytes = timer.bytes / launches
+    traffic, traffic_src = pmc_traffic(family, model=model)
+    intensity = flops / max(alg_bytes, 1.0)  # algorithmic FLOP per byte vs the ridge: which roofline binds
+    bound = "mfma" if intensity >= RIDGE else "hbm"
+    tflops = flops / (avg_ms * 1e-3) / 1e12
+    gbs = alg_bytes / (avg_ms * 1e-3) / 1e9
+    achieved, peak, unit = (tflops, PEAK_BF16_TFLOPS, "TFLOP/s") if bound == "mfma" else (gbs, PEAK_HBM_GBS, "GB/s")
+    solo_tf = flops / (solo_ms * 1e-3) / 1e12
+    solo_gbs = alg_bytes / (solo_ms * 1e-3) / 1e9
+    return {"bound": bound, "kernel": family, "launches_per_step": len(timer.idx),
+            "achieved": round(achieved, 2), "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
+            "traffic": round(traffic) if traffic else None, "traffic_unit": "HBM bytes/launch",
+            "traffic_source": traffic_src, "algorithmic_bytes": round(alg_bytes), "flops_per_launch": round(flops),
+            "intensity_flop_per_byte": round(intensity, 1), "ridge_flop_per_byte": round(RIDGE, 1),
+            # both rooflines of the family, whichever binds
+            "mfma_achieved_tflops": round(tflops, 2), "mfma_frac": round(tflops / PEAK_BF16_TFLOPS, 4),
+            "hbm_achieved_gbs": round(gbs, 1), "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
+            "avg_launch_ms": round(avg_ms, 4),
+            # the same launches in the serialised calibration step (nothing sharing the CUs)
+            "solo_avg_launch_ms": round(solo_ms, 4), "solo_mfma_frac": round(solo_tf / PEAK_BF16_TFLOPS, 4),
+            "solo_hbm_frac": round(solo_gbs / PEAK_HBM_GBS, 4)}
+
+
 def cpu_baseline(batch=32, steps=2, image=224):
     """SURVEY.md 8d / BASELINE.md 3: the reference's MXNet CPU executor cannot run here, so its
     closest analogue -- torch-CPU fp32 functional ops (oneDNN, MXNet's MKL-DNN counterpart) on every
@@ -339,6 +372,9 @@ def launch_ranks(n, argv, cmd=None):
         print("bench.py: launcher got signal %d; stopping every rank" % e.args[0], file=sys.stderr)
         rc = 128 + e.args[0]
     finally:
+        # a second TERM / INT during the cleanup must not abort it before every rank is killed and reaped
+        for s in old:
+            signal.signal(s, signal.SIG_IGN)
         stop_live()
         for s, h in old.items():
             signal.signal(s, h)
@@ -452,14 +488,18 @@ def main():
         step()
     torch.cuda.synchronize()
     fams = calibrate_families(torch, ex, mod)
-    # the dominant family of the step's critical path: with the side stream on, the weight gradients
-    # run overlapped with the data-gradient chain (sized for half the chip, rn_set_tuning 21), so the
-    # roofline line follows the compute stream's largest family; all families stay listed below
+    # roofline.kernel: the family with the most kernel time per step (serialised calibration step), as the
+    # contract says -- with the side stream on that is the weight-gradient family. critical_path: the
+    # compute (data-gradient) stream's largest family, which sets the step when the weight gradients
+    # run overlapped beside it (rn_set_tuning 21 sizes them for part of the chip); both are timed with
+    # HIP events on the stream each launch runs on, every family's time is listed
     side = bool(getattr(ex, "_side_idx", None)) and ex.side_enabled
-    crit = [f for f in fams if not (side and f.startswith("wgrad"))] or list(fams)
-    dom = max(crit, key=lambda f: fams[f][0])
-    solo_ms = fams[dom][0] / max(fams[dom][1], 1)
-    timer = FamilyTimer(torch, ex, dom)
+    dom = max(fams, key=lambda f: fams[f][0])
+    crit_fams = [f for f in fams if not (side and f.startswith("wgrad"))] or list(fams)
+    crit = max(crit_fams, key=lambda f: fams[f][0])
+    timers = {dom: FamilyTimer(torch, ex, dom)}
+    if crit != dom:
+        timers[crit] = FamilyTimer(torch, ex, crit)
     # auto: one HIP graph on a single GPU -- unless the executor runs its weight gradients on a side
     # stream: the graph replay serialises the two branches, eager launches overlap them (measured
     # 22.30 vs 22.93 ms per step for the graph with everything on one stream)
@@ -487,7 +527,8 @@ def main():
         torch.cuda.synchronize()
         run = replay
     else:
-        timer.wrap()  # HIP events around every launch of the dominant family, inside the timed region
+        for t in timers.values():  # HIP events around every launch of the reported families, in the timed region
+            t.wrap()
         run = step
 
     reducer = mod._reducer
@@ -516,15 +557,16 @@ def main():
     if use_graph:
         # graph nodes cannot carry timing events: time the family's launches in one eager step
         # run directly after the timed region (same kernels and shapes as the replayed graph)
-        timer.wrap()
+        for t in timers.values():
+            t.wrap()
         step()
         torch.cuda.synchronize()
-    timer.unwrap()
+    for t in timers.values():
+        t.unwrap()
     if world > 1:
         t = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    fam_ms, fam_n = timer.result()
     # PCIe-inclusive rate (never `value`): the solver's own loop feeds the iterator's pinned host
     # batch every step (core/solver.py:115, data/imagenet.py:17-18) -- copied H2D on the copy
     # stream, double-buffered, overlapping the previous step
@@ -556,19 +598,7 @@ def main():
         value = imgs / elapsed
         ms_step = elapsed / a.steps * 1e3
         flops_step = ex.plan.train_flops()
-        per_launch_flops = timer.flops / max(1, len(timer.idx))
-        avg_ms = fam_ms / max(fam_n, 1)
-        traffic, traffic_src = pmc_traffic(dom, model=a.model)
-        alg_bytes = timer.bytes / max(1, len(timer.idx))
-        # which roofline binds this family: its algorithmic FLOP per algorithmic byte vs the ridge
-        intensity = per_launch_flops / max(alg_bytes, 1.0)
-        bound = "mfma" if intensity >= RIDGE else "hbm"
-        tflops = per_launch_flops / (avg_ms * 1e-3) / 1e12
-        gbs = alg_bytes / (avg_ms * 1e-3) / 1e9
-        achieved, peak, unit = (tflops, PEAK_BF16_TFLOPS, "TFLOP/s") if bound == "mfma" else \
-            (gbs, PEAK_HBM_GBS, "GB/s")
-        solo_tf = per_launch_flops / (solo_ms * 1e-3) / 1e12
-        solo_gbs = alg_bytes / (solo_ms * 1e-3) / 1e9
+        roof = {f: family_roofline(f, t, fams[f], model=a.model) for f, t in timers.items()}
         out = {
             "metric": MODEL_METRIC[a.model], "value": round(value, 2), "unit": "images/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
@@ -581,28 +611,15 @@ def main():
             "config": {"workload": "%s train step, batch %d/GPU, %dx%d" % (
                 workload, a.batch, a.image, a.image), "model": model_name, "global_batch": a.batch * world,
                 "seq_len": None, "parallelism": "dp%d" % world, "per_gpu_images_per_sec": round(value / world, 2)},
-            "roofline": {"bound": bound, "kernel": dom, "launches_per_step": len(timer.idx),
-                         "dominant_rule": "most kernel time per step on the compute (critical-path) stream" if side
-                         else "most kernel time per step",
-                         "achieved": round(achieved, 2), "peak": peak, "unit": unit,
-                         "frac": round(achieved / peak, 4),
-                         "traffic": round(traffic) if traffic else None, "traffic_unit": "HBM bytes/launch",
-                         "traffic_source": traffic_src, "algorithmic_bytes": round(alg_bytes),
-                         "flops_per_launch": round(per_launch_flops),
-                         "intensity_flop_per_byte": round(intensity, 1), "ridge_flop_per_byte": round(RIDGE, 1),
-                         # both rooflines of the family, whichever binds
-                         "mfma_achieved_tflops": round(tflops, 2), "mfma_frac": round(tflops / PEAK_BF16_TFLOPS, 4),
-                         "hbm_achieved_gbs": round(gbs, 1), "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
-                         "avg_launch_ms": round(avg_ms, 4),
-                         # the same launches in the serialised calibration step (no weight gradient
-                         # sharing the CUs): the kernel's own rate
-                         "solo_avg_launch_ms": round(solo_ms, 4),
-                         "solo_mfma_frac": round(solo_tf / PEAK_BF16_TFLOPS, 4),
-                         "solo_hbm_frac": round(solo_gbs / PEAK_HBM_GBS, 4),
-                         "concurrent_streams": 2 if (ex._side_idx and ex.side_enabled) else 1,
-                         "step_tflops": round(flops_step / (ms_step * 1e-3) / 1e12, 2),
-                         "step_frac": round(flops_step / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
-                         "families_ms_per_step": {f: round(v[0], 3) for f, v in fams.items()}},
+            "roofline": dict(roof[dom], dominant_rule="most kernel time per step (serialised calibration step)",
+                             concurrent_streams=2 if (ex._side_idx and ex.side_enabled) else 1,
+                             step_tflops=round(flops_step / (ms_step * 1e-3) / 1e12, 2),
+                             step_frac=round(flops_step / (ms_step * 1e-3) / 1e12 / PEAK_BF16_TFLOPS, 4),
+                             families_ms_per_step={f: round(v[0], 3) for f, v in fams.items()}),
+            # the compute stream's largest family: the step's critical path while the weight gradients
+            # run overlapped on the side stream (the same record as roofline's; equal to it with one stream)
+            "critical_path": dict(roof[crit], rule="most kernel time per step among the compute stream's "
+                                                   "families" if side else "one stream: the dominant family"),
             "outputs_finite": finite,
             "hip_graph": bool(use_graph),
             "inputs": "pinned host batch copied every step (PCIe-inclusive)" if a.host_input else

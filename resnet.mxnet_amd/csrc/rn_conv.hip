@@ -4087,7 +4087,11 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
       d->c_real == d->c && d->k_pad == d->k && g_tune[RN_TUNE_WGRAD_BAND] != 1 &&
       (int64_t)a.M * (d->k + d->c) * 2 < INT32_MAX) {
     const int64_t mtiles = ceil_div(a.M, 64);
-    const int64_t split = std::min<int64_t>(wgrad_cus(), std::max<int64_t>(1, mtiles / 4));
+    int64_t split = std::min<int64_t>(wgrad_cus(), std::max<int64_t>(1, mtiles / 4));
+    // (at launch: no more splits than the workspace holds -- rn_set_tuning 21 may have changed since the
+    // plan sized it, and the int8-codes form has no other kernel to fall back to)
+    const int64_t slab1 = (int64_t)a.K * a.ldw * 4;
+    if (launch && ws && ws_bytes >= slab1) split = std::min<int64_t>(split, ws_bytes / slab1);
     a.m_per_split = (int)(ceil_div(mtiles, split) * 64);
     const int64_t nsplit = ceil_div(a.M, a.m_per_split);
     if (!launch) return finish(nsplit, "wgrad_stream");

@@ -642,6 +642,11 @@ class _GradState:
         key = id(t)
         buf = self.ex.grad_buf(t)
         if key in self.has_value:
+            # another contribution lands in a buffer that already holds one: the previous writer's fused
+            # BN reduction (self.ex._gw, pool / dgrad) saw a partial gradient. A fusing writer re-registers
+            # itself after its call (its output then includes this add operand); any other writer leaves
+            # the entry "other", so the BN backward runs its own reduction
+            self.ex._gw[key] = ("other",)
             return buf, buf
         self.has_value.add(key)
         pend = self.pending.get(key)
@@ -680,6 +685,9 @@ class Executor:
         self._side_stream = None
         if not self.dry_run and os.environ.get("RN_WGRAD_STREAM", "1") == "1":
             self._side_stream = torch.cuda.Stream(device=self.device)
+        # the weight gradients' split-M grids: part of the chip when they overlap the data-gradient chain,
+        # all of it when they run serialised (before the plan sizes its workspace from the same key)
+        L.set_wgrad_split(os.environ.get("RN_WGRAD_STREAM", "1") == "1")
         self._side_idx = set()
         self._side_pre = set()  # (of _side_idx) SIDE_PRE_CALLS
         self._events = {}
@@ -700,6 +708,10 @@ class Executor:
         self._route_wgrads()
         self._build_update()
         self.bucket_bytes = bucket_bytes
+        # the trailing bucket (RN_TAIL_BUCKET_MB, default 5 MB): the parameters at the flat buffer's end --
+        # the stem's and the first stage's, whose gradients the backward completes last -- get a bucket of
+        # their own, so that only this small one is exposed after the backward's last kernel
+        self.tail_bucket_bytes = int(float(os.environ.get("RN_TAIL_BUCKET_MB", "5")) * (1 << 20))
         self.num_update = 0
 
     # ------------------------------------------------------------------ buffers
@@ -2024,18 +2036,34 @@ class Executor:
 
     # ------------------------------------------------------------------ gradient buckets
     def buckets(self):
-        """[(start, end, last_bwd_index)] over the flat grad buffer, ~bucket_bytes each."""
+        """[(start, end, last_bwd_index)] over the flat grad buffer: ~bucket_bytes each, except the trailing
+        bucket -- the longest suffix of the parameter order (the earliest layers, whose gradients are final
+        last) within tail_bucket_bytes -- which stands alone so that little is left to sum once the backward
+        has ended (core/solver.py:116-121: the kvstore push of the last gradients)."""
         out = []
+        order = list(self.param_order)
+        sizes = [int(np.prod(self.param_shape[nm])) for nm in order]
+        tail_at = len(order)
+        tb = getattr(self, "tail_bucket_bytes", 0)
+        acc = 0
+        while tail_at > 0 and (acc + sizes[tail_at - 1]) * 4 <= tb:
+            tail_at -= 1
+            acc += sizes[tail_at]
+        if tail_at == 0 or acc == 0:
+            tail_at = len(order)  # (everything within the tail size, or nothing fits: the plain plan)
         cur_start, cur_end, cur_last = None, None, 0
-        for nm in self.param_order:
+        for k, nm in enumerate(order):
             o = self.param_off[nm]
-            n = int(np.prod(self.param_shape[nm]))
+            n = sizes[k]
             last = self.param_done_at.get(nm, len(self._bwd))
+            if k == tail_at and cur_start is not None:  # close the head before the trailing bucket
+                out.append((cur_start, o, cur_last))
+                cur_start = None
             if cur_start is None:
                 cur_start, cur_end, cur_last = o, o + n, last
             else:
                 cur_end, cur_last = o + n, max(cur_last, last)
-            if (cur_end - cur_start) * 4 >= self.bucket_bytes:
+            if k < tail_at and (cur_end - cur_start) * 4 >= self.bucket_bytes:
                 out.append((cur_start, cur_end, cur_last))
                 cur_start = None
         if cur_start is not None:

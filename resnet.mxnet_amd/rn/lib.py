@@ -176,7 +176,22 @@ def load(auto_build=True):
     for kv in filter(None, os.environ.get("RN_TUNE", "").split(",")):
         k, v = kv.split("=")
         check(lib.rn_set_tuning(int(k), int(v)), "rn_set_tuning")
+        USER_TUNED.add(int(k))
     return lib
+
+
+USER_TUNED = set()  # rn_set_tuning keys fixed by RN_TUNE: the executor leaves them alone
+WGRAD_SPLIT_OVERLAPPED = 45  # rn_set_tuning 21 with the weight gradients on the side stream (percent of the chip)
+
+
+def set_wgrad_split(overlapped):
+    """rn_set_tuning 21 -- the share of the chip the split-M weight gradients size their grids for -- by how
+    the executor runs them: 45 % beside the data-gradient chain on the side stream (measured, DESIGN.md
+    round 4), the whole chip when they run serialised on the compute stream (RN_WGRAD_STREAM=0). An
+    RN_TUNE=21=... override wins. Launches clamp their split to the workspace the plan sized."""
+    lib = load()
+    if 21 not in USER_TUNED:
+        check(lib.rn_set_tuning(21, WGRAD_SPLIT_OVERLAPPED if overlapped else 100), "rn_set_tuning")
 
 
 def check(ret, what=""):

@@ -86,3 +86,30 @@ def test_slab_workspace_only_on_weight_gradient_calls():
     users = [name for name, fn, args in ex._bwd + ex._fwd_train
              if any(isinstance(a, C.c_void_p) and a.value == ws for a in args)]
     assert users and all(u in Executor.WGRAD_CALLS for u in users), users
+
+
+def test_trailing_bucket_is_small_and_last():
+    """the parameters whose gradients the backward completes last (the stem and the
+    first stage, at the flat buffer's end) form a trailing bucket of their own within
+    RN_TAIL_BUCKET_MB (5 MB), so only it can be exposed after the stem's weight gradient; the other
+    buckets keep ~25 MB and every bucket still launches after its last writer (test above)."""
+    ex = Executor(Plan(graphs.resnet50(), [("data", (2, 3, 64, 64))], [("softmax_label", (2,))],
+                       dtype="bfloat16"), "cpu")
+    ex.bucket_bytes = 25 << 20
+    b = ex.buckets()
+    s, e, launch = b[-1]
+    assert (e - s) * 4 <= 5 << 20
+    names = [n for n in ex.param_order if s <= ex.param_off[n] < e]
+    assert any(n.startswith("conv0") for n in names) and any(n.startswith("stage1_") for n in names)
+    assert not any(n.startswith(("stage3_", "stage4_", "fc1")) for n in names)
+    # the trailing bucket follows the stem's weight gradient: it launches with the backward's last calls
+    assert launch >= ex.param_done_at["conv0_weight"]
+    # the bucket before it is a head bucket: it ends where the trailing one starts, and it launches earlier
+    assert b[-2][1] == s and b[-2][2] <= launch
+    # head buckets: ~25 MB each (the last head bucket may be shorter)
+    for hs, he, _ in b[:-2]:
+        assert (he - hs) * 4 >= 25 << 20
+    # a tail size of 0 restores the plain ~25 MB plan
+    ex.tail_bucket_bytes = 0
+    plain = ex.buckets()
+    assert plain[-1][1] == ex.nparam and len(plain) == len(b) - 1
