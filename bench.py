@@ -32,6 +32,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 for _p in (REPO, os.path.join(REPO, "resnet.mxnet_amd")):
     if _p not in sys.path:
         sys.path.insert(0, _p)
+import rn  # noqa: E402,F401  (before any HIP call: rn sets the process's hardware-queue count, rn/__init__.py)
 
 METRIC = "images/sec/GPU ResNet-50 224px bf16 bs256; 1→8 GPU scaling"
 # the other BASELINE configs (C4, C5) are reported under their own names, never as the headline metric
@@ -433,7 +434,8 @@ def main():
     force_ar = world == 1 and os.environ.get("RN_BENCH_ALLREDUCE", "0") == "1"
     if force_ar:
         dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%s" % os.environ.get("MASTER_PORT", "29511"),
-                                rank=0, world_size=1, device_id=torch.device("cuda", local))
+                                rank=0, world_size=1, device_id=torch.device("cuda", local),
+                                **rdist.nccl_pg_kwargs())
 
     sym = {"resnet50": graphs.resnet50, "resnext50": graphs.resnext50_32x4d,
            "resnet50_int8": graphs.resnet50_int8}[a.model]()

@@ -23,8 +23,21 @@ def init_from_env(backend=None):
     kw = {}
     if backend == "nccl":
         kw["device_id"] = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        kw.update(nccl_pg_kwargs())
     dist.init_process_group(backend=backend, rank=int(os.environ["RANK"]), world_size=ws, **kw)
     return True
+
+
+def nccl_pg_kwargs():
+    """RN_NCCL_HIPRIO=1: RCCL's streams from torch's high-priority pool (ProcessGroupNCCL.Options
+    is_high_priority_stream), i.e. hardware queues apart from the normal-priority compute and weight-gradient
+    streams (A/B knob)."""
+    if os.environ.get("RN_NCCL_HIPRIO", "0") != "1":
+        return {}
+    import torch.distributed as dist
+    opts = dist.ProcessGroupNCCL.Options()
+    opts.is_high_priority_stream = True
+    return {"pg_options": opts}
 
 
 class BucketAllReducer:

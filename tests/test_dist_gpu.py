@@ -121,6 +121,9 @@ def _run(graph, precision, mode, bucket_mb):
     q = ctx.Queue()
     port = _free_port()
     os.environ["RN_BUCKET_MB"] = str(bucket_mb)  # inherited by the spawned ranks
+    # two ranks on one GPU: HIP's 4 hardware queues each (8 per process oversubscribe the queue slots)
+    os.environ["RN_HW_QUEUES"] = "4"
+    os.environ["GPU_MAX_HW_QUEUES"] = "4"
     procs = [ctx.Process(target=_worker, args=(r, 2, port, graph, precision, mode, q)) for r in range(2)]
     for p in procs:
         p.start()
