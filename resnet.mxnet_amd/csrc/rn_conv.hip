@@ -2360,6 +2360,15 @@ constexpr int stream_wk(int kb, int cb) {  // waves along K (of 8) minimizing th
   }
   return best;
 }
+// The stream kernel's LDS swizzle: swz_tr, except for 8-chunk (128-byte, 64-channel) rows. A transposed
+// 64-bit read's 32-lane group covers rows 8 g + 4 h + q (g = 0, 1; q = 0..3) at two chunks each; with
+// 128-byte rows a row's bank half is row & 1, and swz_tr & 7 = 2 q drops g, so rows r and r + 8 hit the
+// same banks (2-way: PMC 0.288 of the kernel's LDS cycles were conflicts on ResNet-50's 64-channel
+// layers, profiles/r04/pmc_summary_resnet50_final.txt). Here the chunk pair of a row is 2 ((q >> 1) | 2 g):
+// with q & 1 picking the bank half, the 8 rows x 2 chunks cover 16 distinct 16-byte bank groups.
+__device__ __forceinline__ int swz_st(int row, int cpr) {
+  return cpr == 8 ? 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) : swz_tr(row);
+}
 template <int K, int C, int XF, int NBUF, int I8X = 0>
 __global__ __launch_bounds__(512, 1) void wgrad_stream_kernel(WgradArgs p) {
   static_assert(!(XF && I8X), "int8 input: no input transform");
@@ -2394,8 +2403,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_stream_kernel(WgradArgs p) {
     const int cpr = d_isa[j] ? A_CPR : B_CPR;
     const int row = d_isa[j] ? piece * A_RPI + lane / A_CPR : (piece - A_INS) * B_RPI + lane / B_CPR;
     d_row[j] = row;
-    d_col[j] = d_isa[j] ? 8 * ((lane % cpr) ^ (swz_tr(row) & (cpr - 1)))
-                        : CEB * ((lane % cpr) ^ ((I8X ? swz_tr8(row) : swz_tr(row)) & (cpr - 1)));
+    d_col[j] = d_isa[j] ? 8 * ((lane % cpr) ^ (swz_st(row, cpr) & (cpr - 1)))
+                        : CEB * ((lane % cpr) ^ ((I8X ? swz_tr8(row) : swz_st(row, cpr)) & (cpr - 1)));
   }
   const char* __restrict__ dyb = reinterpret_cast<const char*>(p.dy);
   const char* __restrict__ xb = reinterpret_cast<const char*>(p.x);
@@ -2442,7 +2451,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_stream_kernel(WgradArgs p) {
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const int col = (wk * MI + i) * 16 + 4 * pp;
-          const int byte = row * (A_CPR * 16) + ((((col * 2) >> 4) ^ (swz_tr(row) & (A_CPR - 1))) << 4) + ((col * 2) & 15);
+          const int byte = row * (A_CPR * 16) + ((((col * 2) >> 4) ^ (swz_st(row, A_CPR) & (A_CPR - 1))) << 4) + ((col * 2) & 15);
           const v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(Ab + byte));
 #pragma unroll
           for (int e = 0; e < 4; ++e) af[i][4 * h + e] = v[e];
@@ -2451,7 +2460,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_stream_kernel(WgradArgs p) {
         for (int j = 0; j < NI; ++j) {
           if constexpr (I8X) break;
           const int col = (wc * NI + j) * 16 + 4 * pp;
-          const int byte = row * (B_CPR * 16) + ((((col * 2) >> 4) ^ (swz_tr(row) & (B_CPR - 1))) << 4) + ((col * 2) & 15);
+          const int byte = row * (B_CPR * 16) + ((((col * 2) >> 4) ^ (swz_st(row, B_CPR) & (B_CPR - 1))) << 4) + ((col * 2) & 15);
           const v4s v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(Bb + byte));
 #pragma unroll
           for (int e = 0; e < 4; ++e) bfv[j][4 * h + e] = v[e];
@@ -2647,6 +2656,13 @@ struct GdArgs {
   int bn_relu;
 };
 constexpr int kGdRedMaxC = 512;  // (gd_direct_shape: C / 8 divides 64)
+// LDS stride of one 8-channel chunk's weights, [tap][G] 16-byte rows plus one pad row: the lanes of a
+// ds_read_b128 group read 16 different chunks at the same tap, and an unpadded stride of 9 G rows
+// (144 / 288 dwords = 16 / 32 mod 64 banks) put 4 / 8 of them on the same banks (PMC: 0.78 / 0.85 of
+// the LDS cycles were bank conflicts, profiles/r04/pmc_summary_resnext50.txt); 9 G + 1 rows = 148 / 292
+// dwords step 20 / 36 banks, 5 c / 9 c mod 16 distinct over 16 chunks: conflict-free
+template <int G>
+constexpr int kGdWStride = 9 * G + 1;
 
 // RED: one lane's stored output chunk into its BatchNorm-backward sums (channels chunk*8 .. +7). The
 // per-channel mean / scale / shift sit in an LDS table (tab[3][C], loaded before the kernel's first
@@ -2717,14 +2733,15 @@ __global__ __launch_bounds__(256) void grouped_direct_kernel(GdArgs a) {
   extern __shared__ uint4 gd_w[];
   __shared__ __attribute__((aligned(16))) float gd_tab[RED ? 3 * kGdRedMaxC : 4];
   const int nw16 = a.C * 9 * G * 2 / 16;
-  for (int i = threadIdx.x; i < nw16; i += blockDim.x) gd_w[i] = reinterpret_cast<const uint4*>(a.w)[i];
+  for (int i = threadIdx.x; i < nw16; i += blockDim.x)
+    gd_w[i / (9 * G) * kGdWStride<G> + i % (9 * G)] = reinterpret_cast<const uint4*>(a.w)[i];
   if constexpr (RED) GdRed::load_tab(a, gd_tab);
   __syncthreads();
   constexpr int NC = (PL - 1) * ST + 3;
   const int lane = threadIdx.x & 63;
   const int chunk = lane & ((1 << a.lcpr) - 1), pl = lane >> a.lcpr;
   const int plw = 64 >> a.lcpr;
-  const uint4* wc = gd_w + chunk * 9 * G;
+  const uint4* wc = gd_w + chunk * kGdWStride<G>;
   GdRed rd;
   if constexpr (RED) rd.init();
   const uint32_t step = gridDim.x * (blockDim.x >> 6) * plw;
@@ -2804,14 +2821,15 @@ __global__ __launch_bounds__(256) void grouped_dgrad_s2_kernel(GdArgs a) {
   extern __shared__ uint4 gd_w[];
   __shared__ __attribute__((aligned(16))) float gd_tab[RED ? 3 * kGdRedMaxC : 4];
   const int nw16 = a.C * 9 * G * 2 / 16;
-  for (int i = threadIdx.x; i < nw16; i += blockDim.x) gd_w[i] = reinterpret_cast<const uint4*>(a.w)[i];
+  for (int i = threadIdx.x; i < nw16; i += blockDim.x)
+    gd_w[i / (9 * G) * kGdWStride<G> + i % (9 * G)] = reinterpret_cast<const uint4*>(a.w)[i];
   if constexpr (RED) GdRed::load_tab(a, gd_tab);
   __syncthreads();
   constexpr int ND = PL / 2 + 1;  // dy columns per tap row
   const int lane = threadIdx.x & 63;
   const int chunk = lane & ((1 << a.lcpr) - 1), pl = lane >> a.lcpr;
   const int plw = 64 >> a.lcpr;
-  const uint4* wc = gd_w + chunk * 9 * G;
+  const uint4* wc = gd_w + chunk * kGdWStride<G>;
   GdRed rd;
   if constexpr (RED) rd.init();
   const uint32_t step = gridDim.x * (blockDim.x >> 6) * plw;
@@ -3637,7 +3655,7 @@ bool gd_direct_shape(const rn_conv_desc* d, int mode) {
   const int cpg = d->c / d->groups;
   if (d->c != d->c_real || d->k != d->c || d->k_pad != d->k || d->c % d->groups || (cpg != 4 && cpg != 8)) return false;
   if (d->r != 3 || d->s != 3 || d->pad_h != 1 || d->pad_w != 1 || d->stride_h != d->stride_w) return false;
-  if (d->c % 8 || 64 % (d->c / 8) || (int64_t)d->c * 9 * cpg * 2 > 64 * 1024) return false;
+  if (d->c % 8 || 64 % (d->c / 8) || (int64_t)(d->c / 8) * (9 * cpg + 1) * 16 > 64 * 1024) return false;
   if (cpg == 8) return (mode == 0 || mode == 1) && d->stride_h == 2;  // (stride 1: the MFMA tile wins)
   return (mode == 0 || mode == 1) && (d->stride_h == 1 || d->stride_h == 2);
 }
@@ -3681,7 +3699,7 @@ int gd_launch(const rn_conv_desc* d, int mode, const void* x, const void* w, voi
   const int cpg = d->c / d->groups;
   const int stride = mode == 0 ? d->stride_h : 1;
   const bool s2t = mode == 1 && d->stride_h == 2;
-  const size_t lds = (size_t)d->c * 9 * cpg * 2;
+  const size_t lds = (size_t)(d->c / 8) * (9 * cpg + 1) * 16;  // (kGdWStride: one pad row per chunk)
   const bool rd = a.bnred != nullptr;
   RN_CHECK_ARG(!rd || (mode == 1 && d->c <= kGdRedMaxC), "grouped direct BN reduction: data gradient only");
   if (s2t) {

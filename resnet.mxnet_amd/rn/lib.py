@@ -9,7 +9,7 @@ import os
 from .build import LIB_PATH as _BUILT_LIB, build, needs_build
 
 # RN_LIB_PATH: load another build of the library (A/B of two builds in one GPU call); default the in-tree one
-LIB_PATH = os.environ.get("RN_LIB_PATH", _BUILT_LIB)
+LIB_PATH = os.environ.get("RN_LIB_PATH") or _BUILT_LIB
 
 RN_BF16 = 0
 RN_F32 = 1
