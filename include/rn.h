@@ -599,8 +599,8 @@ const char* rn_last_error(void);
  * 10 = igemm 256-row-family persistent grid: workgroups (a multiple of 8) that walk the tiles of a
  *      larger grid, so one tile's output stores drain while the next tile loads (default 512; 0 = one
  *      tile per workgroup),
- * 11 = the 4-wave one-buffer 224x128 conv tile, two workgroups per CU (0 auto: one-K-tile forward
- *      1x1 layers of >= 1024 tiles; 1 off; 2 every 1x1 pad-0 conv),
+ * 11 = the 4-wave one-buffer 224x128 conv tile, two workgroups per CU (0 auto: forward 1x1 layers of
+ *      >= 1024 tiles; 1 off; 2 every 1x1 pad-0 conv; 3 one-K-tile forward layers only, the round-4 rule),
  * 12 = 3x3 / stride-2 max-pool backward over 2x2 input blocks (0 = on where H = 2P, W = 2Q; 1 = the
  *      per-pixel gather),
  * 13 = grouped convolutions with equal channels in and out per group (<= 32): skip the MFMAs of the

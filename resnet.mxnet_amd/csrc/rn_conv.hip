@@ -3356,9 +3356,11 @@ IgemmArgs make_igemm_args(const rn_conv_desc* d, int mode) {
 }
 
 // The 4-wave one-buffer 224x128 tile (igemm_big_kernel W4, two workgroups per CU) for these
-// arguments? rn_set_tuning 11: 0 auto (forward 1x1, pad 0, ONE K-tile, >= 1024 tiles: the stage-1
-// conv3 / shortcut layers, 230 -> 215 us; measured no better on the 2-K-tile and dgrad layers,
-// DESIGN.md 3), 1 never, 2 every eligible 1x1 pad-0 layer, fwd and dgrad (tests).
+// arguments? rn_set_tuning 11: 0 auto (forward 1x1, pad 0, >= 1024 tiles: the stage-1 conv3 / shortcut
+// layers, 230 -> 215 us; since round 5 also the deeper ones -- stage-2 unit-1 conv1 163 -> 131 us,
+// stage-3 unit-1 conv1 83 -> 77 us in isolation, ResNet-50 20.45 / 20.44 -> 20.42 / 20.40 ms per step;
+// the data gradients and the grids under 1024 tiles measured no better or slower), 1 never,
+// 2 every eligible 1x1 pad-0 layer, fwd and dgrad (tests), 3 the round-4 rule (one K-tile only).
 bool w4_tile(const IgemmArgs& a) {
   const int mode = g_tune[RN_TUNE_IGEMM_W4];
   if (mode == 1 || g_tune[RN_TUNE_IGEMM_ROWS] == 1 || a.ncls != 1 || a.gred > 0 || a.smallc || a.bias || a.K <= 64)
@@ -3368,7 +3370,8 @@ bool w4_tile(const IgemmArgs& a) {
   if (a.in_sc && a.C > kXfMaxCW4) return false;
   if (mode == 2) return true;
   const int64_t tiles = ceil_div((int64_t)a.N * c.Pc * c.Qc, 224) * ceil_div(a.K, 128);
-  return a.hinc > 0 && ceil_div(a.cblk, 64) == 1 && tiles >= 1024;
+  if (mode == 3) return a.hinc > 0 && ceil_div(a.cblk, 64) == 1 && tiles >= 1024;  // (round-4 rule: one K-tile)
+  return a.hinc > 0 && tiles >= 1024;
 }
 
 // Columns of the 256-row tile launch_igemm runs for these arguments (bf16 in and out), 0 for the

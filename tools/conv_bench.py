@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--graph", default="resnet50")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--only", default="fwd,dgrad,wgrad")
+    ap.add_argument("--only", default="fwd,dgrad,wgrad", help="modes among fwd, dgrad, wgrad, dgbn (dgrad + BN reduction)")
     ap.add_argument("--filter", default="")
     ap.add_argument("--cold", action="store_true", help="evict L2/MALL (write 512 MB) before every timed call")
     a = ap.parse_args()
@@ -64,16 +64,23 @@ def main():
         P = lambda t: C.c_void_p(t.data_ptr())
         ws_bytes = int(lib.rn_conv_wgrad_ws_bytes(C.byref(d)))  # split-M slab workspace, as the executor uses
         ws = torch.empty(max(ws_bytes, 16) // 4, device=dev)
+        bnv = torch.rand(cp, device=dev) * 0.5 + 0.5
+        bnpart = torch.empty(int(lib.rn_conv_bnred_blocks(C.byref(d))) * cp * 2 + 16, device=dev)
         L.check(lib.rn_conv_weight_pack(C.byref(d), P(wm), P(wk), P(wc), st), "pack")
         calls = {
             "fwd": lambda: lib.rn_conv_fwd(C.byref(d), P(x), P(wk), P(y), L.RN_BF16, P(yv) if res else None, None, st),
             "dgrad": lambda: lib.rn_conv_bwd_data(C.byref(d), P(yv), P(wc), P(dx), None, st),
             "wgrad": lambda: lib.rn_conv_bwd_filter_ws(C.byref(d), P(x), P(yv), P(dw), P(ws), ws_bytes, st),
+            # the data gradient with the BatchNorm-backward reduction of its output in the epilogue (EPI 2,
+            # how the step runs it): bn_x = the dgrad output's shape
+            "dgbn": lambda: lib.rn_conv_bwd_data_bnred(C.byref(d), P(yv), P(wc), P(dx), None, P(x), P(bnv), P(bnv),
+                                                       P(bnv), 1, P(bnpart), st),
         }
         flops = 2.0 * n * d.p * d.q * k * (c // g) * kern[0] * kern[1]
         # algorithmic HBM bytes (bf16): x + w + y (+ residual for fwd); per-mode roofline time
         xb, yb, wb = 2.0 * n * h * w * c, 2.0 * n * d.p * d.q * k, 2.0 * k * kern[0] * kern[1] * (c // g)
-        algb = {"fwd": xb + wb + yb * (2 if res else 1), "dgrad": yb + wb + xb, "wgrad": xb + yb + 2 * wb}
+        algb = {"fwd": xb + wb + yb * (2 if res else 1), "dgrad": yb + wb + xb, "wgrad": xb + yb + 2 * wb,
+                "dgbn": yb + wb + 2 * xb}
         row = "%-26s %3d %-22s %-5s" % (name[:26], cnt, "%dx%dx%d>%d k%d s%d" % (h, w, c, k, kern[0], stride[0]),
                                        "g%d" % g if g > 1 else ("+res" if res else ""))
         for m in modes:
