@@ -1,5 +1,5 @@
 # A/B of the executor's stream placement (RN_SIDE_STREAM, RN_MAIN_STREAM, RN_MAIN_PRIORITY) with the
-# all-reduce hooks on / off (RN_BENCH_ALLREDUCE); usage: bash tools/runs/r05c_streams.sh TAG "VAR=V ..." ...
+# all-reduce hooks on / off (RN_BENCH_ALLREDUCE); usage: bash tools/runs/env_ab.sh TAG "VAR=V ..." ...
 set -o pipefail
 tag=$1; shift
 i=0

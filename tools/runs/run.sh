@@ -9,6 +9,8 @@
 #   bench            the default bench line (C2, with the CPU baselines)
 #   c2 | c4 | c5     the C2 / C4 / C5 bench lines without the CPU baselines
 #   c2@K=V[,K=V]     the C2 bench line with RN_TUNE overrides (A/B of a tuning key), same for c4@ / c5@
+#   c2%VAR=V[,VAR=V] the C2 bench line under environment variables (A/B of an RN_* knob), same for c4% / c5%
+#   lib:MODEL        the MODEL bench line with experiments/librn_base.so (RN_LIB_PATH: A/B of two builds)
 #   prof[:model][@K=V] rocprofv3 --kernel-trace --stats of a 5-step bench (+ step breakdown, stream use),
 #                    optionally with RN_TUNE overrides
 #   pmc[:model]      rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE, SQ group) of a 3-step bench
@@ -26,6 +28,10 @@ for s in "$@"; do
     c2|c4|c5) steps+=("200 python bench.py --model $(model_of $s) --no-cpu-baseline --pcie-steps 0 > gpurun_out/${tag}_${s}.log 2>&1");;
     c2@*|c4@*|c5@*) m=${s%%@*}; kv=${s#*@}; lab=$(echo "$kv" | tr '=,' '__')
       steps+=("200 env RN_TUNE=$kv python bench.py --model $(model_of $m) --no-cpu-baseline --pcie-steps 0 > gpurun_out/${tag}_${m}_${lab}.log 2>&1");;
+    c2%*|c4%*|c5%*) m=${s%%\%*}; kv=${s#*%}; lab=$(echo "$kv" | tr '=,' '__')
+      steps+=("200 env $(echo "$kv" | tr ',' ' ') python bench.py --model $(model_of $m) --no-cpu-baseline --pcie-steps 0 > gpurun_out/${tag}_${m}_${lab}.log 2>&1");;
+    lib:*) m=${s#lib:}
+      steps+=("200 env RN_LIB_PATH=experiments/librn_base.so python bench.py --model $(model_of $m) --no-cpu-baseline --pcie-steps 0 > gpurun_out/${tag}_${m}_base.log 2>&1");;
     prof|prof:*|prof@*|prof:*@*) spec=${s#prof}; kv=""; [[ "$spec" == *@* ]] && kv=${spec#*@} && spec=${spec%%@*}
       m=$(model_of "${spec#:}"); lab=${m}$( [ -n "$kv" ] && echo "_$(echo "$kv" | tr '=,' '__')" )
       steps+=("300 env RN_TUNE=$kv bash tools/prof_bench.sh ${tag}_${lab} --model $m --steps 5 --warmup 2 --no-cpu-baseline --pcie-steps 0 > gpurun_out/${tag}_prof_${lab}.log 2>&1");;
