@@ -17,6 +17,7 @@ Rank 0 prints ONE JSON line (contract in the task statement), including
                  and the HBM fraction reported
   critical_path: the same record for the compute stream's largest family (the data-gradient chain that
                  sets the step while the weight gradients run overlapped on the side stream)
+  weight_gradients: the same record for the weight-gradient family (side stream)
   pcie_inclusive: the same step fed the iterator's pinned host batch every step (not `value`)
   cpu_baseline : torch-CPU fp32 (oneDNN) restatement of the same step (oracle/torch_cpu.py,
                  "port") on every host core, batch 32 (rank 0, N=1 only)
@@ -191,8 +192,9 @@ def calibrate_families(torch, ex, mod):
                 fams[f] = FamilyTimer(torch, ex, f)
     for t in fams.values():
         t.wrap()
-    # one serialised step (the weight gradients on the compute stream too): each family's solo
-    # launch durations, which choose the dominant family and give its solo roofline fraction
+    # one serialised step (the weight gradients on the compute stream too, with the whole chip's split-M
+    # grids as RN_WGRAD_STREAM=0 runs them): each family's solo launch durations, which choose the dominant
+    # family and give its solo roofline fraction
     ex.side_enabled = False
     mod.forward(None, is_train=True)
     mod.backward()
@@ -499,9 +501,11 @@ def main():
     dom = max(fams, key=lambda f: fams[f][0])
     crit_fams = [f for f in fams if not (side and f.startswith("wgrad"))] or list(fams)
     crit = max(crit_fams, key=lambda f: fams[f][0])
+    wg = next((f for f in fams if f.startswith("wgrad")), None)  # the weight-gradient family (side stream)
     timers = {dom: FamilyTimer(torch, ex, dom)}
-    if crit != dom:
-        timers[crit] = FamilyTimer(torch, ex, crit)
+    for f in (crit, wg):
+        if f is not None and f not in timers:
+            timers[f] = FamilyTimer(torch, ex, f)
     # auto: one HIP graph on a single GPU -- unless the executor runs its weight gradients on a side
     # stream: the graph replay serialises the two branches, eager launches overlap them (measured
     # 22.30 vs 22.93 ms per step for the graph with everything on one stream)
@@ -622,6 +626,9 @@ def main():
             # run overlapped on the side stream (the same record as roofline's; equal to it with one stream)
             "critical_path": dict(roof[crit], rule="most kernel time per step among the compute stream's "
                                                    "families" if side else "one stream: the dominant family"),
+            # the weight gradients (the side stream's family: in-step with part of the chip's grids beside the
+            # data-gradient chain, solo = the serialised calibration step on the whole chip)
+            "weight_gradients": roof.get(wg),
             "outputs_finite": finite,
             "hip_graph": bool(use_graph),
             "inputs": "pinned host batch copied every step (PCIe-inclusive)" if a.host_input else

@@ -691,7 +691,7 @@ class Executor:
         self._side_idx = set()
         self._side_pre = set()  # (of _side_idx) SIDE_PRE_CALLS
         self._events = {}
-        self.side_enabled = True  # False: the side-stream calls run on the compute stream (serialised timing)
+        self._side_enabled = True  # False: the side-stream calls run on the compute stream (serialised timing)
         self._sync_stream()
         self._acts = {}
         self._grads = {}
@@ -713,6 +713,20 @@ class Executor:
         # their own, so that only this small one is exposed after the backward's last kernel
         self.tail_bucket_bytes = int(float(os.environ.get("RN_TAIL_BUCKET_MB", "5")) * (1 << 20))
         self.num_update = 0
+
+    @property
+    def side_enabled(self):
+        return self._side_enabled
+
+    @side_enabled.setter
+    def side_enabled(self, on):
+        """False: the weight gradients run on the compute stream, serialised (bench.py's calibration step),
+        with the whole chip's split-M grids -- as RN_WGRAD_STREAM=0 runs them (lib.set_wgrad_split; the
+        workspace is sized for both)."""
+        on = bool(on)
+        if on != self._side_enabled and self._side_stream is not None:
+            L.set_wgrad_split(on)
+        self._side_enabled = on
 
     # ------------------------------------------------------------------ buffers
     def _zeros(self, numel, dtype):
@@ -1507,16 +1521,25 @@ class Executor:
         # _route_wgrads enforces this)
         self.wgrad_ws, self.wgrad_ws_bytes = None, 0
         if os.environ.get("RN_WGRAD_SLAB", "1") == "1":
-            need = [int(self.lib.rn_conv_wgrad_ws_bytes(L.C.byref(op.desc))) for op in plan.ops
-                    if op.kind in ("conv", "fc") and getattr(op, "desc", None) is not None]
-            # (the stem's weight gradient; it needs a slab only in the deterministic mode)
-            need += [int(self.lib.rn_conv_wgrad_ws_bytes(L.C.byref(op.dfull))) for op in plan.ops
-                     if op.kind == "stem" and not op.p4]
-            need += [int(self.lib.rn_stem_clip_wgrad_ws_bytes(L.C.byref(op.dfull))) for op in plan.ops
-                     if op.kind == "stem" and self._stem_clip_mask(op)]
-            need += [int(self.lib.rn_conv_wgrad_i8_ws_bytes(L.C.byref(op.desc))) for op in plan.ops
-                     if op.kind == "conv" and getattr(op, "qsrc", None) is not None and op.qsrc.codes_wgrad]
-            self.wgrad_ws_bytes = max(need + [0])
+            def need_now():
+                need = [int(self.lib.rn_conv_wgrad_ws_bytes(L.C.byref(op.desc))) for op in plan.ops
+                        if op.kind in ("conv", "fc") and getattr(op, "desc", None) is not None]
+                # (the stem's weight gradient; it needs a slab only in the deterministic mode)
+                need += [int(self.lib.rn_conv_wgrad_ws_bytes(L.C.byref(op.dfull))) for op in plan.ops
+                         if op.kind == "stem" and not op.p4]
+                need += [int(self.lib.rn_stem_clip_wgrad_ws_bytes(L.C.byref(op.dfull))) for op in plan.ops
+                         if op.kind == "stem" and self._stem_clip_mask(op)]
+                need += [int(self.lib.rn_conv_wgrad_i8_ws_bytes(L.C.byref(op.desc))) for op in plan.ops
+                         if op.kind == "conv" and getattr(op, "qsrc", None) is not None and op.qsrc.codes_wgrad]
+                return max(need + [0])
+            # sized for both weight-gradient grids: the overlapped one (part of the chip) and the whole
+            # chip, which a serialised step (side_enabled False: bench.py's calibration) runs with
+            overlapped = os.environ.get("RN_WGRAD_STREAM", "1") == "1"
+            self.wgrad_ws_bytes = need_now()
+            if overlapped:
+                L.set_wgrad_split(False)
+                self.wgrad_ws_bytes = max(self.wgrad_ws_bytes, need_now())
+                L.set_wgrad_split(True)
             if self.wgrad_ws_bytes > 0:
                 self.wgrad_ws = self._zeros(self.wgrad_ws_bytes // 4, self.torch.float32)
         expanded = set()  # quantizers whose deferred values this plan expands (rn_quant_int8_expand)

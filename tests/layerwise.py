@@ -931,15 +931,21 @@ class Checker:
         dev = self.ex.gview(name)[:d.c_real].double()
         # dbeta[c] sums ~n h w data-gradient terms that cancel to 1e-3 .. 1e-7 of their magnitudes (cancel =
         # sum |terms| / |sum|: 7e3 .. 3e6 measured at 256 x 224^2), so its relative (fro) error is fp32
-        # summation noise times that factor -- informational. The bars: cond (|dev - ref| over the sum of
-        # the magnitudes, the summation bound) and err_terms (|dev - ref| in units of the mean |term|: a
-        # clip mask flipped at one input moves its channel by about one term; measured 2e-5 .. 2e-2)
+        # summation noise times that factor -- informational: any change of summation order moves it by a
+        # random factor of that size. The int8 stem's four image chunks (rn_stem_clip_wgrad_chunk: each
+        # chunk's clip-mask weight gradient, then the chunks' dot products added in chunk order) changed the
+        # order, and the relative error with it (2.75e-4 -> 3.36e-3), while the error
+        # stayed ~1e3 x under the fp32 summation bound (cond 7e-10: an fp32 tree over 1.3e7 terms may
+        # reach ~24 x 6e-8 = 1.4e-6 of sum |terms|). The bars: cond (|dev - ref| over the sum of the
+        # magnitudes, the summation bound) and err_terms (|dev - ref| in units of the mean |term|: a clip
+        # mask flipped at one input moves its channel by about one term; measured 2e-5 .. 1.6e-2, the bar
+        # three times the largest)
         nterm = float(d.n * d.h * d.w)
         self.add_metric("stem_dbeta", name, {"cond": float(((dev - ref).abs() / rab).max()),
                                              "fro": _fro(dev, ref),
                                              "cancel": float((rab / (ref.abs() + 1e-300)).max()),
                                              "err_terms": float(((dev - ref).abs() / (rab / nterm)).max())},
-                        {"cond": 2e-6, "err_terms": 0.5})
+                        {"cond": 2e-6, "err_terms": 0.05})
 
     def _h_rn_stem_shift_grad(self, args, state):
         """bn_data's beta gradient without the stem's data gradient: dbeta[c] = sum over the image of
