@@ -184,14 +184,15 @@ USER_TUNED = set()  # rn_set_tuning keys fixed by RN_TUNE: the executor leaves t
 WGRAD_SPLIT_OVERLAPPED = 45  # rn_set_tuning 21 with the weight gradients on the side stream (percent of the chip)
 
 
-def set_wgrad_split(overlapped):
+def set_wgrad_split(overlapped, pct=None):
     """rn_set_tuning 21 -- the share of the chip the split-M weight gradients size their grids for -- by how
-    the executor runs them: 45 % beside the data-gradient chain on the side stream (measured, DESIGN.md
-    round 4), the whole chip when they run serialised on the compute stream (RN_WGRAD_STREAM=0). An
-    RN_TUNE=21=... override wins. Launches clamp their split to the workspace the plan sized."""
+    the executor runs them: `pct` (default 45 %) beside the data-gradient chain on the side stream
+    (measured, DESIGN.md rounds 4-5), the whole chip when they run serialised on the compute stream
+    (RN_WGRAD_STREAM=0). An RN_TUNE=21=... override wins. Launches clamp their split to the workspace the
+    plan sized."""
     lib = load()
     if 21 not in USER_TUNED:
-        check(lib.rn_set_tuning(21, WGRAD_SPLIT_OVERLAPPED if overlapped else 100), "rn_set_tuning")
+        check(lib.rn_set_tuning(21, (pct or WGRAD_SPLIT_OVERLAPPED) if overlapped else 100), "rn_set_tuning")
 
 
 def check(ret, what=""):
