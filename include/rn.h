@@ -125,18 +125,6 @@ int rn_conv_bwd_data_bnred_clip2(const rn_conv_desc* d, const void* dy, const vo
                                  const void* other, const void* bn_x, const float* bn_mean, const float* bn_scale,
                                  const float* bn_shift, const float* clip, const float* clip2, float* part,
                                  rn_stream_t stream);
-/* The post-activation unit tail's backward (symbol/resnext.py:41-47 / resnet_cifar: y = relu(bn3(conv3)
- * [+ bn_sc(sc)] + shortcut)) in the epilogue of the data gradient that completes dL/dy: this call
- * stores g = round(conv_transpose(dy, w) + add_src) * [y > 0] (add_src nullable; the value
- * rn_conv_bwd_data then rn_relu_bwd_bnred would store, bit for bit -- the un-masked gradient is never
- * written) and reduces, as rn_relu_bwd_bnred does, part[rn_conv_bnred_blocks(d)][c][2] = per block
- * (sum g, sum g*(bn_x - bn_mean)) for the BN whose input is bn_x, and part2 likewise for a second BN
- * (bn_x2 / bn_mean2 / part2 all NULL or all set); rn_bn_bwd_part finishes each BN. bf16, dense, c a
- * multiple of 8 with c == c_real, the 224-row tile (rn_conv_tile(d, 1) >= 128). */
-int rn_conv_bwd_data_relu_bnred(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* g,
-                                const void* add_src, const void* y, const void* bn_x, const float* bn_mean,
-                                float* part, const void* bn_x2, const float* bn_mean2, float* part2,
-                                rn_stream_t stream);
 /* The BatchNorm(+ReLU) backward of the BN whose output gradient this convolution's data gradient is,
  * APPLIED in the epilogue to the recomputed gradient: dx = A (dz - mean(dz)) - A2 (x - mean)
  * (+ add_src), dz = g relu'(x scale + shift) (relu != 0), g = conv_transpose(dy, w) rounded as

@@ -95,14 +95,6 @@ struct IgemmArgs {
   // dgrad only, nullable: a folded Quantization_int8 straight-through clip on the BN output (rn_bn_desc.clip)
   const float* bn_clip;
   const float* bn_clip2;  // (EPI 4) nullable: a quantizer pair -- add is the other quantizer's gradient (below)
-  // dgrad only, nullable (igemm_big_kernel EPIX 6, rn_conv_bwd_data_relu_bnred): the post-activation unit
-  // tail's backward in the epilogue -- the stored value is g = round(dgrad + add) * [rr_y > 0] (the ReLU
-  // after the residual add), reduced for the BatchNorm whose input is bn_x (mean bn_mean, -> bnred) and
-  // for a second one (the projection shortcut's BN: bn_x2 / bn_mean2 -> bnred2, nullable)
-  const void* rr_y;
-  const void* bn_x2;
-  const float* bn_mean2;
-  float* bnred2;
   // int8 forward (igemm_big_kernel Q8): per-tensor quantization units of the int8 codes in x and w
   // (Quantization_int8: value = code * unit); the int32 accumulators are scaled by their product
   const float* qunit_x;
@@ -763,10 +755,9 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 template <int BN, int NBUF, int EPIX = 0, bool M32 = false, int BM = 256, int SC = 0, int Q8 = 0, int XF = 0, int W4 = 0,
           int GD = 0>
 __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1) void igemm_big_kernel(IgemmArgs p) {
-  constexpr int EPI = EPIX == 4 || EPIX == 6 ? 2 : EPIX == 5 ? 1 : EPIX;
+  constexpr int EPI = EPIX == 4 ? 2 : EPIX == 5 ? 1 : EPIX;
   constexpr bool CLIP = EPIX == 4;
   constexpr bool MM = EPIX == 5;  // EPI 1 + the per-block extremes of the stored output (p.stats_mm)
-  constexpr bool RR = EPIX == 6;  // EPI 2 of the post-activation unit tail: ReLU mask from rr_y, 1-2 BNs
   constexpr int ES = Q8 ? 1 : 2;                 // operand bytes per element
   constexpr int BMA = 256, CE = 16 / ES, BKE = 128 / ES;
   using OutT = typename std::conditional<Q8 == 2, float, bf16_t>::type;
@@ -831,10 +822,6 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
           const int64_t o = ((int64_t)(blockIdx.z * p.mt_max + PR * mtile + hh) * p.ldo + col) * 2;
           p.bnred[o] = 0.f;
           p.bnred[o + 1] = 0.f;
-          if (RR && p.bnred2) {
-            p.bnred2[o] = 0.f;
-            p.bnred2[o + 1] = 0.f;
-          }
         }
       }
     continue;
@@ -1148,11 +1135,7 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
 #pragma unroll
   for (int e = 0; e < NS; ++e) {
     s1[e] = s2[e] = piv[e] = r_mu[e] = r_sc[e] = r_sh[e] = 0.f;
-    if constexpr (RR) {  // (RR: r_mu / r_sc hold the two BNs' means; the ReLU mask comes from rr_y)
-      const bool okc = col0 + e < p.K;
-      r_mu[e] = okc ? p.bn_mean[col0 + e] : 0.f;
-      r_sc[e] = okc && p.bn_mean2 ? p.bn_mean2[col0 + e] : 0.f;
-    } else if constexpr (EPI == 2 || EPI == 3) {
+    if constexpr (EPI == 2 || EPI == 3) {
       const bool okc = col0 + e < p.K;
       r_sc[e] = okc ? p.bn_sc[col0 + e] : 0.f;
       r_sh[e] = okc ? p.bn_sh[col0 + e] : 0.f;
@@ -1183,7 +1166,6 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
     uint4 addv[CPR][AW];
     constexpr bool XP = EPI == 2 || EPI == 3;
     uint4 xpre[XP ? CPR : 1];  // BN input at the same positions (EPI 2 / 3), loaded with the residual
-    uint4 ypre[RR ? CPR : 1], x2pre[RR ? CPR : 1];  // (RR) the ReLU output, the second BN's input
 #pragma unroll
     for (int k = 0; k < CPR; ++k) {
       const int r = lane / CPR + (64 / CPR) * k;
@@ -1192,7 +1174,6 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
 #pragma unroll
       for (int u = 0; u < AW; ++u) addv[k][u] = make_uint4(0, 0, 0, 0);
       if constexpr (XP) xpre[k] = make_uint4(0, 0, 0, 0);
-      if constexpr (RR) ypre[k] = x2pre[k] = make_uint4(0, 0, 0, 0);
       if (m < Mc && col0 < p.K && r < rows_h) {
         const int n = fdiv(m, cl.fdPQ);
         const int rem = m - n * cl.Pc * cl.Qc;
@@ -1204,11 +1185,6 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
           for (int u = 0; u < AW; ++u) addv[k][u] = reinterpret_cast<const uint4*>(ag + off[k])[u];
         if constexpr (XP)
           if (col0 + 8 <= p.K) xpre[k] = *reinterpret_cast<const uint4*>(bxg + off[k]);
-        if constexpr (RR)
-          if (col0 + 8 <= p.K) {
-            ypre[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(p.rr_y) + off[k]);
-            if (p.bn_x2) x2pre[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(p.bn_x2) + off[k]);
-          }
       }
     }
     // Each wave stages through its own LDS region, so the epilogue needs no block barrier -- a wave's
@@ -1291,14 +1267,6 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
         uint4 out[AW];
 #pragma unroll
         for (int u = 0; u < AW; ++u) out[u] = f_to_chunk(v + u * (8 / AW), (const OutT*)nullptr);
-        if constexpr (RR) {  // g = the rounded gradient where the unit's ReLU passed, else +0 (exact)
-          float g[8], yv[8];
-          chunk_to_f(out[0], g, (const bf16_t*)nullptr);
-          chunk_to_f(ypre[k], yv, (const bf16_t*)nullptr);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) g[e] = yv[e] > 0.f ? g[e] : 0.f;
-          out[0] = f_to_chunk(g, (const bf16_t*)nullptr);
-        }
         if (yg && (!(kRnDiag && (p.sched & 32)) || (out[0].x & 0xFFFF) == 0x7FC1))  // (EPI 2 may only reduce;
                                                                                   // diagnostic bit 32: no stores)
         {
@@ -1328,16 +1296,6 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
             if (want_mm)
 #pragma unroll
               for (int e = 0; e < NM; ++e) mxv[e] = fmaxf(mxv[e], sgn[e] * g[e]);
-          } else if constexpr (RR) {  // (piv holds the second BN's sum dz * (x2 - mean2))
-            float xv[8], x2[8];
-            chunk_to_f(xpre[k], xv, (const bf16_t*)nullptr);
-            chunk_to_f(x2pre[k], x2, (const bf16_t*)nullptr);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              s1[e] += g[e];
-              s2[e] = fmaf(g[e], xv[e] - r_mu[e], s2[e]);
-              piv[e] = fmaf(g[e], x2[e] - r_sc[e], piv[e]);
-            }
           } else {
             float xv[8];
             chunk_to_f(xpre[XP ? k : 0], xv, (const bf16_t*)nullptr);
@@ -1369,7 +1327,6 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
       for (int e = 0; e < 8; ++e) {
         s1[e] += __shfl_xor(s1[e], o, 64);
         s2[e] += __shfl_xor(s2[e], o, 64);
-        if constexpr (RR) piv[e] += __shfl_xor(piv[e], o, 64);
       }
     if (want_mm)
 #pragma unroll
@@ -1388,9 +1345,6 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
         if (want_mm)
 #pragma unroll
           for (int e = 0; e < NM; ++e) xch[lane * 32 + 16 + e] = mxv[e];
-        if constexpr (RR)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) xch[lane * 32 + 24 + e] = piv[e];
       }
       __syncthreads();
       if (wm == 0 && lane < CPR) {
@@ -1402,9 +1356,6 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
         if (want_mm)
 #pragma unroll
           for (int e = 0; e < NM; ++e) mxv[e] = fmaxf(mxv[e], xch[lane * 32 + 16 + e]);
-        if constexpr (RR)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) piv[e] += xch[lane * 32 + 24 + e];
       }
     }
     if (lane < CPR && (!PAIR || wm == 0)) {
@@ -1429,10 +1380,6 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
           const int64_t o = ((int64_t)(blockIdx.z * p.mt_max + blk) * p.ldo + col) * 2;
           p.bnred[o] = (rows_ok && okc) ? s1[e] : 0.f;
           p.bnred[o + 1] = (rows_ok && okc) ? s2[e] : 0.f;
-          if (RR && p.bnred2) {
-            p.bnred2[o] = (rows_ok && okc) ? s1[e] : 0.f;
-            p.bnred2[o + 1] = (rows_ok && okc) ? piv[e] : 0.f;
-          }
         }
       }
     }
@@ -3448,9 +3395,9 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   const bool dma = g_tune[RN_TUNE_IGEMM_DMA] > 0 && !a.in_sc && !b.diag_l1 && xb < INT32_MAX && wb < INT32_MAX &&
                    max_taps <= 64;
   if constexpr (std::is_same<T, bf16_t>::value && std::is_same<OutT, bf16_t>::value) {
-    const int epi = a.stats ? 1 : a.bnred ? (a.rr_y ? 6 : a.bn_clip ? 4 : 2) : a.bn_coef ? 3 : 0;
+    const int epi = a.stats ? 1 : a.bnred ? (a.bn_clip ? 4 : 2) : a.bn_coef ? 3 : 0;
     const int bn = big_tile_cols(a, xb, wb);
-    RN_CHECK_ARG((epi != 3 || bn >= 128) && (epi != 4 || bn >= 64) && (epi != 6 || bn >= 128),
+    RN_CHECK_ARG((epi != 3 || bn >= 128) && (epi != 4 || bn >= 64),
                  "this dgrad epilogue needs an LDS-DMA tile");
     const bool m32 = g_tune[RN_TUNE_IGEMM_MFMA] != 1;
     // persistent tiles (rn_set_tuning 10 = workgroups, a multiple of 8): only where the grid is larger
@@ -3500,7 +3447,6 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
   else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 1, M, R>), grid, dim3(512), 0, st, b);   \
   else if (epi == 2) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 2, M, R>), grid, dim3(512), 0, st, b);   \
   else if (epi == 3) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 3, M, R>), grid, dim3(512), 0, st, b);   \
-  else if (epi == 6) hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 6, M, R>), grid, dim3(512), 0, st, b);   \
   else hipLaunchKernelGGL((igemm_big_kernel<BNV, NB, 4, M, R>), grid, dim3(512), 0, st, b);
       if (bn == 128 && bm == 224 && w4_tile(a)) {  // two 4-wave workgroups per CU
         dim3 g4((unsigned)(ceil_div(maxMc, 224) * b.ntn), 1, 1);
@@ -3517,7 +3463,6 @@ int launch_igemm(const IgemmArgs& a, hipStream_t st) {
         else if (epi == 1) hipLaunchKernelGGL((igemm_big_kernel<128, 1, 1, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
         else if (epi == 2) hipLaunchKernelGGL((igemm_big_kernel<128, 1, 2, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
         else if (epi == 3) hipLaunchKernelGGL((igemm_big_kernel<128, 1, 3, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
-        else if (epi == 6) hipLaunchKernelGGL((igemm_big_kernel<128, 1, 6, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
         else hipLaunchKernelGGL((igemm_big_kernel<128, 1, 4, false, 224, 0, 0, 0, 1>), g4, dim3(256), 0, st, b);
         return rn_check_launch("igemm_big_w4");
       }
@@ -3918,24 +3863,6 @@ int rn_conv_bwd_data_bnred_clip2(const rn_conv_desc* d, const void* dy, const vo
   for (int z = 0; z < a.ncls; ++z) maxMc = std::max(maxMc, a.N * a.cls[z].Pc * a.cls[z].Qc);
   a.bnred = part; a.bn_x = bn_x; a.bn_mean = bn_mean; a.bn_sc = bn_scale; a.bn_sh = bn_shift;
   a.bn_relu = 1; a.bn_clip = clip; a.bn_clip2 = clip2; a.mt_max = (int)ceil_div(maxMc, 128);
-  return launch_igemm<bf16_t, bf16_t>(a, as_stream(stream));
-}
-
-int rn_conv_bwd_data_relu_bnred(const rn_conv_desc* d, const void* dy, const void* w_crsk, void* g,
-                                const void* add_src, const void* y, const void* bn_x, const float* bn_mean,
-                                float* part, const void* bn_x2, const float* bn_mean2, float* part2,
-                                rn_stream_t stream) {
-  RN_CHECK_ARG(d && dy && w_crsk && g && y && bn_x && bn_mean && part, "null argument");
-  RN_CHECK_ARG(!bn_x2 == !bn_mean2 && !bn_x2 == !part2, "the second BatchNorm: bn_x2, bn_mean2, part2 together");
-  RN_CHECK_ARG(d->dtype == RN_BF16 && d->groups <= 1 && d->c == d->c_real && d->c % 8 == 0 && rn_conv_tile(d, 1) >= 128,
-               "the unit-tail epilogue: bf16, dense, whole 8-channel chunks, a 224-row LDS-DMA data-gradient tile");
-  IgemmArgs a = make_igemm_args(d, 1);
-  a.x = dy; a.w = w_crsk; a.y = g; a.add = add_src; a.bias = nullptr;
-  int maxMc = 0;
-  for (int z = 0; z < a.ncls; ++z) maxMc = std::max(maxMc, a.N * a.cls[z].Pc * a.cls[z].Qc);
-  a.bnred = part; a.bn_x = bn_x; a.bn_mean = bn_mean; a.bn_relu = 0;
-  a.rr_y = y; a.bn_x2 = bn_x2; a.bn_mean2 = bn_mean2; a.bnred2 = part2;
-  a.mt_max = (int)ceil_div(maxMc, 128);
   return launch_igemm<bf16_t, bf16_t>(a, as_stream(stream));
 }
 

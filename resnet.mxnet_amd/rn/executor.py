@@ -328,26 +328,19 @@ class Plan:
             op.qsrc = q if op.int8 else None
             if op.int8:
                 q.emit_codes = True
-        # quantizers whose fake-quantized values only int8 convs read (their forwards read the codes):
-        # RN_QUANT_DEFER=1 expands the values from the codes on the weight-gradient stream, just before each
-        # weight gradient that reads them (rn_quant_int8_expand, bit-identical), instead of the forward
-        # writing them. Opt-in: measured slower (C5 24.72 / 24.56 vs 23.78 / 23.91 ms per step: the
-        # quantizer pass saves 0.38 ms of the compute stream, the 52 expansions cost 2.8 ms of the
-        # weight-gradient stream, which then delays the compute stream's tail)
+        # (round 4's opt-in RN_QUANT_DEFER -- the values expanded from the codes on the weight-gradient stream
+        # by rn_quant_int8_expand -- measured 4 % slower on C5 and was removed in round 5; the weight gradients
+        # multiply the codes instead, codes_wgrad)
         users = {}
         for op in self.ops:
             for k in ("x", "a", "b", "res", "label"):
                 t = getattr(op, k, None)
                 if t is not None and hasattr(t, "numel"):
                     users.setdefault(id(t), []).append(op)
-        defer = on and os.environ.get("RN_QUANT_DEFER", "0") == "1"
         for op in self.ops:
             if op.kind == "quant":
-                us = users.get(id(op.y), [])
-                op.value_users = us
+                op.value_users = users.get(id(op.y), [])
                 op.codes_wgrad = False  # (the executor decides: _codes_wgrad)
-                op.defer_values = bool(defer and op.emit_codes and us and
-                                       all(u.kind == "conv" and u.int8 and u.qsrc is op for u in us))
 
     def _fuse_bn_apply(self):
         """BatchNorm+ReLU whose output feeds ONLY 1x1 convolutions (act1 -> conv1 / sc, act3 -> conv3
@@ -881,7 +874,7 @@ class Executor:
                    "rn_stem_conv_wgrad_p4", "rn_stem_clip_wgrad", "rn_stem_clip_wgrad_chunk", "rn_stem_clip_dbeta")
     # side-stream calls that depend on the forward only, not on the backward so far: no fork of their own
     # (they run while the side stream waits for the next dy), except the first of a step
-    SIDE_PRE_CALLS = ("rn_quant_int8_expand", "rn_stem_clip_mask")
+    SIDE_PRE_CALLS = ("rn_stem_clip_mask",)
 
     def _stem_clip_mask(self, op):
         """Does the int8 stem's input-quantizer clip gradient ride in its weight gradient (bf16 NHWC-8
@@ -946,7 +939,7 @@ class Executor:
             if op.kind != "quant":
                 continue
             us = getattr(op, "value_users", [])
-            ok = on and op.emit_codes and not op.defer_values and bool(us) and \
+            ok = on and op.emit_codes and bool(us) and \
                 all(u.kind == "conv" and u.int8 and u.qsrc is op for u in us)
             if ok:
                 for u in us:
@@ -1191,9 +1184,8 @@ class Executor:
                         # + the int8 codes and unit the consumers' int8 forward reads
                         o.codes = self.torch.zeros(o.x.numel, dtype=self.torch.int8, device=self.device)
                         o.unit = self._zeros(1, self.torch.float32)
-                # (deferred values: codes only here, rn_quant_int8_expand before the weight gradient;
-                # codes_wgrad: codes only, the weight gradients multiply them)
-                vout = lambda o: None if (o.defer_values or o.codes_wgrad) else self._p(self.act(o.y))
+                # (codes_wgrad: codes only, the weight gradients multiply them)
+                vout = lambda o: None if o.codes_wgrad else self._p(self.act(o.y))
                 for lst, tr in ((F, 1), (I, 0)):
                     if op.bn_lead is not None:
                         pass  # written by its peer's call
@@ -1544,7 +1536,6 @@ class Executor:
                 L.set_wgrad_split(True, self.wgrad_split_pct)
             if self.wgrad_ws_bytes > 0:
                 self.wgrad_ws = self._zeros(self.wgrad_ws_bytes // 4, self.torch.float32)
-        expanded = set()  # quantizers whose deferred values this plan expands (rn_quant_int8_expand)
         for op in plan.ops:
             if op.kind == "stem" and self._stem_clip_mask(op):
                 # the int8 stem's clip masks into the NHWC-8 image's free channels (rn_stem_clip_mask),
@@ -1614,13 +1605,6 @@ class Executor:
                                                 self._p(self.wgrad_ws) if ws else None,
                                                 self.wgrad_ws_bytes if ws else 0, sp))
                 else:
-                    q = op.qsrc
-                    if q is not None and q.defer_values and id(q) not in expanded:
-                        # the fake-quantized input from its codes, on the weight-gradient stream ahead of
-                        # the wait for dy (routed by _route_wgrads; backward() forks before the first)
-                        expanded.add(id(q))
-                        self._bwd.append(self._call("rn_quant_int8_expand", self.dtype, x.numel, self._p(q.codes),
-                                                    self._p(q.unit), self._p(self.act(x)), sp))
                     self._bwd.append(self._wgrad_call(op.desc, self._p(self.act(x)), self._p(dy), self._gp(op.weight),
                                                       sp))
                 self.param_done_at[op.weight] = len(self._bwd)
@@ -1833,31 +1817,10 @@ class Executor:
                     # reductions from the same pass (rn_relu_bwd_bnred)
                     bns = [b for b in (getattr(op, "bn_a", None), getattr(op, "bn_b", None))
                            if b is not None and not b.use_global_stats and dy is not None]
-                    w = self._gw.get(id(op.y))
-                    fuse = bool(bns and len(bns) == len([b for b in (op.bn_a, op.bn_b) if b is not None]) and
-                                w and w[0] == "dgrad" and dy is w[4] and self.dtype == BF16 and
-                                op.y.c == op.y.cp and op.y.c % 8 == 0 and w[2].groups == 1 and
-                                os.environ.get("RN_RELU_BNRED_DGRAD", "0") == "1" and
-                                int(self.lib.rn_conv_tile(L.C.byref(w[2].desc), 1)) >= 128)
-                    if fuse:
-                        # the data gradient that completes dL/dy (the next unit's conv1, accumulating the
-                        # shortcut's gradient) stores g = its value * [y > 0] and reduces the BNs itself
-                        # (rn_conv_bwd_data_relu_bnred): dL/dy is never written. Opt-in
-                        # (RN_RELU_BNRED_DGRAD=1): measured slower, C4 28.97 / 29.00 vs 28.03 / 27.98 ms
-                        # per step -- the epilogue streams its three extra tensors at ~3.5 TB/s, the
-                        # separate pass at ~5.5 (15 data gradients 6.0 ms vs 2.7 + 2.2 ms)
-                        _, ci, cop, cdy, cout, cadd = w
-                        nrb = int(self.lib.rn_conv_bnred_blocks(L.C.byref(cop.desc)))
-                        for b in bns:
-                            b.pre_nrb = nrb
-                            b.pre_part = self._zeros(nrb * b.x.cp * 2, self.torch.float32)
-                        b2 = bns[1] if len(bns) == 2 else None
-                        self._bwd[ci] = self._call(
-                            "rn_conv_bwd_data_relu_bnred", L.C.byref(cop.desc), self._p(cdy), self._p(cop.wc),
-                            self._p(gbuf), self._p(cadd), self._p(self.act(op.y)), self._p(self.act(bns[0].x)),
-                            bns[0].sm, self._p(bns[0].pre_part), self._p(self.act(b2.x)) if b2 else None,
-                            b2.sm if b2 else None, self._p(b2.pre_part) if b2 else None, sp)
-                    elif bns and len(bns) == len([b for b in (op.bn_a, op.bn_b) if b is not None]):
+                    # (round 4's opt-in RN_RELU_BNRED_DGRAD -- this pass in the next unit's conv1 data-gradient
+                    # epilogue -- measured 3 % slower on C4 and was removed in round 5: the epilogue streamed
+                    # its extra tensors at ~3.5 TB/s, this pass runs at ~5.5)
+                    if bns and len(bns) == len([b for b in (op.bn_a, op.bn_b) if b is not None]):
                         for b in bns:
                             b.pre_nrb = int(self.lib.rn_bn_reduce_blocks(L.C.byref(b.desc)))
                             b.pre_part = self._zeros(b.pre_nrb * b.x.cp * 2, self.torch.float32)

@@ -67,7 +67,6 @@ SIGNATURES = {
     "rn_bn_bwd_part": (_i32, [_P, _P, _i64, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rn_bn_bwd_finalize": (_i32, [_P, _P, _i64, _P, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_data_bnapply": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _i32, _P]),
-    "rn_conv_bwd_data_relu_bnred": (_i32, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_data": (_i32, [_P, _P, _P, _P, _P, _P]),
     "rn_conv_bwd_filter": (_i32, [_P, _P, _P, _P, _P]),
     "rn_conv_wgrad_ws_bytes": (_i64, [_P]),

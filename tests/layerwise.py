@@ -568,27 +568,6 @@ class Checker:
             return None, (lambda: None)  # are checked through dgamma / dbeta / dx of the apply below
         return self._dgrad(args, state, bnred=True)
 
-    def _h_rn_conv_bwd_data_relu_bnred(self, args, state):
-        """The data gradient carrying the post-activation unit tail's backward: g = its value (+ add),
-        rounded as rn_conv_bwd_data stores it, times [y > 0] -- vs the fp32 dgrad of the device's dy (its
-        BN reductions: checked through the BN backwards they feed)."""
-        d = args[0]._obj
-        dyp, wcp, gp, addp, yp = args[1], args[2], args[3], args[4], args[5]
-        op = self.wc_op[wcp.value]
-
-        def post():
-            n = d.n
-            dy = self.nchw(self.t(dyp), n, d.p, d.q, d.k_pad, d.k)
-            w = self.w_from_crsk(op.wc, d)
-            ref = ref_dgrad(dy, w, (d.h, d.w), (d.stride_h, d.stride_w), (d.pad_h, d.pad_w))
-            if state.get("add") is not None:
-                ref = ref + self.nchw(state["add"], n, d.h, d.w, d.c, d.c_real)
-            y = self.nchw(self.t(yp), n, d.h, d.w, d.c, d.c_real)
-            ref = ref * (y > 0)
-            dev = self.nchw(self.t(gp), n, d.h, d.w, d.c, d.c_real)
-            self.add("dgrad_relu_bnred", op.name, dev, ref, BF16_BAR)
-        return (self._snap(addp, state, "add") if addp is not None else None), post
-
     def _h_rn_conv_bwd_data_bnred_clip(self, args, state):
         # (its reduction carries the folded quantizer clip: checked through the BN backward it feeds)
         return self._dgrad(args, state, bnred=True)

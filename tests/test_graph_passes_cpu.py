@@ -150,8 +150,6 @@ def test_int8_forward_plan(dry, monkeypatch):
     fed by the quantizer's codes (rn_quant_int8_fwd_codes); the stem (quantizer folded into its
     im2col) and fc1 stay on the fake-quant path; RN_INT8_MFMA=0 turns it off."""
     shape = (2, 3, 64, 64)
-    # (with the opt-in deferred values, RN_QUANT_DEFER=1; default off, checked at the end)
-    monkeypatch.setenv("RN_QUANT_DEFER", "1")
     # npair: BNs whose output two quantizers read (resnet_int8's first units: conv1 and the shortcut
     # each quantize act1; attach_quantize_node shares one quantizer per tensor)
     for sym, nconv, npair in ((graphs.resnet_int8(*R50_SMALL.values()), 52, 4),
@@ -182,22 +180,13 @@ def test_int8_forward_plan(dry, monkeypatch):
             assert nbn + nbn2 == sum(op.bn_src is not None for op in qops) > 0
             assert nbn2 == sum(op.bn_peer is not None for op in qops) == npair
             assert all(op.bn_src.apply_in_quant and op.bn_src.y is op.x for op in qops if op.bn_src is not None)
-            # the int8 convs' inputs: codes only in the forward, the values expanded once per quantizer on
-            # the weight-gradient stream, each just before the first weight gradient reading them
-            src = {id(c.qsrc) for c in convs}
-            assert sum(op.defer_values for op in qops) == len(src)
-            bn = _call_names(ex._bwd)
-            assert bn.count("rn_quant_int8_expand") == len(src)
-            for i, nm in enumerate(bn):
-                if nm == "rn_quant_int8_expand":
-                    assert bn[i + 1] in ex.WGRAD_CALLS
+            # (no value expansion in the plan: round 4's opt-in deferred values were removed in round 5)
+            assert "rn_quant_int8_expand" not in _call_names(ex._bwd)
             # every weight quantizer (+ the int8 convs' codes and data-gradient copies) in one batched call
             packs = _call_names(ex.packs)
             assert packs[0] == "rn_weight_quant_pack" and "rn_conv_weight_pack_i8" not in packs
             assert len(ex._wq_ops) >= nconv and sum(op.int8 for op in ex._wq_ops if op.kind == "conv") == nconv
-    monkeypatch.delenv("RN_QUANT_DEFER")
     ex = _bind(graphs.resnet_int8(*R50_SMALL.values()), shape).executor
-    assert not any(op.defer_values for op in ex.plan.ops if op.kind == "quant")
     assert "rn_quant_int8_expand" not in _call_names(ex._bwd)
     # default (bf16): the quantizers whose convs' weight gradients take codes (all but stage 1's act2, whose
     # conv2 runs the image-band kernel) write codes only (rn_conv_bwd_filter_i8, on the side stream)

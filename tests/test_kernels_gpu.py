@@ -1492,56 +1492,6 @@ def test_maxpool_block_bwd(gpu, dtype, with_add):
     assert rel_err(from_nhwc(out[0], c), dx_ref) < TOL[dtype]
 
 
-@pytest.mark.parametrize("case", [(2, 256, 14, 14, 128, True), (2, 512, 7, 9, 256, False),
-                                  (3, 256, 10, 12, 64, True), (2, 1024, 7, 7, 256, True), (1, 128, 30, 30, 256, False)])
-@pytest.mark.parametrize("with_add", [False, True])
-def test_dgrad_relu_bnred_unit_tail(gpu, case, with_add, big_tiles):
-    """rn_conv_bwd_data_relu_bnred (the post-activation unit tail's backward in the epilogue of the next
-    unit's conv1 data gradient, symbol/resnext.py:41-47) == rn_conv_bwd_data + rn_relu_bwd_bnred: g bit
-    for bit, both BNs' reductions vs the fp64 sums over the stored g."""
-    n, c, h, w, k, two = case
-    rng = np.random.default_rng(45)
-    wt = bf16_round(rng.standard_normal((k, c, 1, 1)) / np.sqrt(c))
-    dy = bf16_round(rng.standard_normal((n, k, h, w)))
-    y = bf16_round(np.maximum(rng.standard_normal((n, c, h, w)), 0))  # the unit's ReLU output (zeros: masked)
-    xa, xb = (bf16_round(rng.standard_normal((n, c, h, w)) + 0.5) for _ in range(2))
-    prev = bf16_round(rng.standard_normal((n, c, h, w)) * 0.5)
-    d = conv_desc(BF16, n, c, h, w, k, 1, 1, 1, 0)
-    lib = L.load()
-    assert lib.rn_conv_tile(C.byref(d), 1) >= 128
-    wc = torch.zeros(d.c * d.k_pad, dtype=torch.bfloat16, device=gpu)
-    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), None, p(wc), stream())
-    dyd, yd, xad, xbd, prevd = (to_nhwc(v, BF16, gpu) for v in (dy, y, xa, xb, prev))
-    mu_a = torch.tensor(rng.standard_normal(c) * 0.3 + 0.5, dtype=torch.float32, device=gpu)
-    mu_b = torch.tensor(rng.standard_normal(c) * 0.3 + 0.5, dtype=torch.float32, device=gpu)
-    nrb = lib.rn_conv_bnred_blocks(C.byref(d))
-    pa, pb = (torch.full((nrb * c * 2,), float("nan"), dtype=torch.float32, device=gpu) for _ in range(2))
-    g1 = torch.zeros_like(yd)
-    L.call("rn_conv_bwd_data_relu_bnred", C.byref(d), p(dyd), p(wc), p(g1), p(prevd) if with_add else None, p(yd),
-           p(xad), p(mu_a), p(pa), p(xbd) if two else None, p(mu_b) if two else None, p(pb) if two else None,
-           stream())
-    bd = L.BNDesc(dtype=BF16, m=n * h * w, c=c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=0)
-    nrb2 = lib.rn_bn_reduce_blocks(C.byref(bd))
-    qa, qb = (torch.zeros(nrb2 * c * 2, dtype=torch.float32, device=gpu) for _ in range(2))
-    d1 = prevd.clone() if with_add else torch.zeros_like(yd)
-    L.call("rn_conv_bwd_data", C.byref(d), p(dyd), p(wc), p(d1), p(d1) if with_add else None, stream())
-    g2 = torch.zeros_like(yd)
-    L.call("rn_relu_bwd_bnred", C.byref(bd), p(yd), p(d1), p(g2), p(xad), p(mu_a), p(qa), p(xbd) if two else None,
-           p(mu_b) if two else None, p(qb) if two else None, stream())
-    torch.cuda.synchronize()
-    assert torch.equal(g1, g2)
-    assert not torch.isnan(pa).any() and (not two or not torch.isnan(pb).any())
-    gf = g1.double().view(-1, c)
-    for part, x, mu, on in ((pa, xad, mu_a, True), (pb, xbd, mu_b, two)):
-        if not on:
-            continue
-        s = part.view(nrb, c, 2).double().sum(0)
-        xc = x.double().view(-1, c) - mu.double()
-        ref = torch.stack([gf.sum(0), (gf * xc).sum(0)], 1)
-        bound = torch.stack([gf.abs().sum(0), (gf * xc).abs().sum(0)], 1)
-        assert float(((s - ref).abs() / (bound + 1e-30)).max()) < 1e-5
-
-
 @pytest.mark.parametrize("case", [(3, 64, 14, 12), (2, 16, 22, 18), (1, 256, 8, 8), (5, 64, 36, 40)])
 @pytest.mark.parametrize("with_add", [False, True])
 def test_maxpool_bwd_bn_backward_fusion(gpu, case, with_add):

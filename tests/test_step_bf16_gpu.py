@@ -219,19 +219,16 @@ def test_resnext50_bf16_full_size_layerwise(gpu):
     _c4_layerwise(256, 224)
 
 
-def _c4_layerwise(n, image, tail_in_dgrad=False):
+def _c4_layerwise(n, image):
     from rn import graphs
     ck = _layerwise(graphs.resnext50_32x4d(), n, image, "bfloat16", warm=1)
     assert not ck.skipped, ck.skipped
     kinds = {r[0] for r in ck.rec}
     # (the grouped data gradients carry their BN-backward reduction: direct kernel or block-diagonal tile)
-    # (RN_RELU_BNRED_DGRAD=1: the unit tails' backward in the next unit's conv1 data gradient,
-    # rn_conv_bwd_data_relu_bnred; the last unit's -- its gradient comes from the pooling -- and, by
-    # default, every unit's in rn_relu_bwd_bnred)
+    # (every unit tail's backward in rn_relu_bwd_bnred)
     assert {"conv_fwd", "conv_fwd_grouped", "dgrad_bnred_grouped", "wgrad_grouped", "wgrad", "bn_apply_add",
             "relu_bwd_bnred", "bn_fwd", "bn_bwd_dx", "bn_bwd_params", "weight_copy"} <= kinds, kinds
-    assert ("dgrad_relu_bnred" in kinds) == tail_in_dgrad, kinds
-    assert sum(1 for r in ck.rec if r[0] in ("dgrad_relu_bnred", "relu_bwd_bnred")) == 16
+    assert sum(1 for r in ck.rec if r[0] == "relu_bwd_bnred") == 16
     assert sum(1 for r in ck.rec if r[0] == "conv_fwd_grouped") == 16
     assert sum(1 for r in ck.rec if r[0] in ("dgrad_grouped", "dgrad_bnred_grouped")) == 16
     assert sum(1 for r in ck.rec if r[0] in ("wgrad", "wgrad_grouped")) == 54  # 53 convs + fc1
@@ -253,7 +250,7 @@ def test_resnet50_int8_full_size_layerwise(gpu):
     _c5_layerwise(256, 224)
 
 
-def _c5_layerwise(n, image, defer=False):
+def _c5_layerwise(n, image):
     from rn import graphs
     ck = _layerwise(graphs.resnet50_int8(), n, image, "bfloat16", warm=1)
     assert not ck.skipped, ck.skipped
@@ -264,15 +261,12 @@ def _c5_layerwise(n, image, defer=False):
     assert n_i8 == 52, n_i8
     assert sum(1 for r in ck.rec if r[0] == "weight_quant") == 54  # 53 convs + fc1
     assert sum(1 for r in ck.rec if r[0] == "quant") == 54  # 52 int8 inputs + conv0's + fc1's
-    # (RN_QUANT_DEFER=1: the int8 inputs' values deferred to the weight-gradient stream, rn_quant_int8_expand)
-    n_def = sum(1 for op in ck.ex.plan.ops if op.kind == "quant" and op.defer_values)
-    assert n_def == (52 if defer else 0)
-    assert sum(1 for r in ck.rec if r[0] == "quant_expand") == n_def
+    assert sum(1 for r in ck.rec if r[0] == "quant_expand") == 0
     # (default: the quantizers but stage 1's act2 write codes only and their weight gradients multiply
     # the codes, rn_conv_bwd_filter_i8)
     n_cw = sum(1 for op in ck.ex.plan.ops if op.kind == "quant" and op.codes_wgrad)
-    assert n_cw == (0 if defer else 49), n_cw
-    assert ck.covered.get("rn_conv_bwd_filter_i8", 0) == (0 if defer else 49)  # one per quantizer
+    assert n_cw == 49, n_cw
+    assert ck.covered.get("rn_conv_bwd_filter_i8", 0) == 49  # one per quantizer
     assert sum(1 for r in ck.rec if r[0] == "wgrad") == 54
     bad = ck.failures()
     assert not bad, bad[:10]
@@ -299,13 +293,6 @@ def test_resnext50_bf16_layerwise_small(gpu):
     _c4_layerwise(8, 64)
 
 
-def test_resnext50_bf16_layerwise_tail_in_dgrad(gpu, monkeypatch):
-    """The opt-in unit-tail backward in the next unit's conv1 data-gradient epilogue
-    (RN_RELU_BNRED_DGRAD=1, rn_conv_bwd_data_relu_bnred), per kernel at 8 images of 112x112."""
-    monkeypatch.setenv("RN_RELU_BNRED_DGRAD", "1")
-    _c4_layerwise(8, 112, tail_in_dgrad=True)
-
-
 def test_resnet50_int8_layerwise_small(gpu):
     """The C5 per-kernel checks at 8 images of 64x64 (a fast first gate before the full size)."""
     _c5_layerwise(8, 64)
@@ -318,14 +305,6 @@ def test_resnet50_int8_layerwise_pair_fusion(gpu, monkeypatch):
     monkeypatch.setenv("RN_QUANT_PAIR_FUSION", "1")
     ck = _c5_layerwise(8, 112)
     assert ck.covered.get("rn_conv_bwd_data_bnred_clip2", 0) == 3
-
-
-def test_resnet50_int8_layerwise_deferred_values(gpu, monkeypatch):
-    """The opt-in deferred fake-quantized values (RN_QUANT_DEFER=1: the quantizers write codes only, the
-    weight-gradient stream expands the values from them before the first weight gradient reading them),
-    per kernel at 8 images of 64x64: the expanded values bit for bit."""
-    monkeypatch.setenv("RN_QUANT_DEFER", "1")
-    _c5_layerwise(8, 64, defer=True)
 
 
 def test_resnet50_fp32_layerwise(gpu):
