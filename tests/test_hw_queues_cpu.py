@@ -1,0 +1,36 @@
+"""rn/__init__.py raises HIP's hardware-queue count before the process's first HIP call (profiles/r05/streams:
+with HIP's 4 queues the RCCL process group's pool streams moved the weight-gradient stream onto the compute
+stream's queue and the two branches of the backward ran serialised, 25.8 vs 20.4 ms per step). Each case
+imports rn in a fresh interpreter with a given environment and reads GPU_MAX_HW_QUEUES back."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _queues(**env):
+    e = {k: v for k, v in os.environ.items()
+         if k not in ("GPU_MAX_HW_QUEUES", "RN_HW_QUEUES", "RN_DIST_BACKEND", "WORLD_SIZE")}
+    e.update(env)
+    code = ("import os, sys; sys.path.insert(0, %r); import rn; print(os.environ.get('GPU_MAX_HW_QUEUES'))"
+            % os.path.join(REPO, "resnet.mxnet_amd"))
+    r = subprocess.run([sys.executable, "-c", code], env=e, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return r.stdout.strip()
+
+
+@pytest.mark.parametrize("env,want", [
+    ({}, "8"),                                                      # one process per GPU: 8 queues
+    ({"GPU_MAX_HW_QUEUES": "4"}, "8"),                              # HIP's default raised
+    ({"GPU_MAX_HW_QUEUES": "16"}, "16"),                            # a larger setting is kept
+    ({"RN_HW_QUEUES": "6"}, "6"),                                   # explicit count
+    ({"RN_HW_QUEUES": "64"}, "None"),                               # beyond 32: left alone
+    ({"RN_DIST_BACKEND": "gloo", "WORLD_SIZE": "2"}, "4"),          # ranks sharing one GPU (rehearsal)
+    ({"RN_DIST_BACKEND": "gloo", "WORLD_SIZE": "2", "GPU_MAX_HW_QUEUES": "8"}, "4"),
+    ({"RN_DIST_BACKEND": "nccl", "WORLD_SIZE": "8"}, "8"),          # one rank per GPU over RCCL
+])
+def test_hardware_queue_count(env, want):
+    assert _queues(**env) == want
