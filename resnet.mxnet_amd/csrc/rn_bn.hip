@@ -313,6 +313,100 @@ __global__ __launch_bounds__(256) void bn_fwd_finalize_part_kernel(const double*
   }
 }
 
+// bn_part_merge_kernel + bn_fwd_finalize_part_kernel in ONE launch where the partials form at most 4
+// merge groups (nblk <= 4 * kPartGroup: the stage-3/4 layers' 224-row conv tiles, ResNet-50 at batch 256).
+// A block takes 16 channels; thread (group g, sub v, channel) forms the merge kernel's sub-sum v of group g
+// (its 16 interleaved blocks -- every load of it in flight at once, as there), the four sub-sums of a group
+// are added in sub order, then the finalize kernel's walk over the groups in group order: outputs
+// bit-identical to the two launches, one launch and one kernel boundary fewer on the forward chain
+__global__ __launch_bounds__(256) void bn_fwd_merge_finalize_kernel(
+    const float* __restrict__ part, int nblk, int64_t m, int rows_blk, int ld, int c, int c_real, float eps,
+    float momentum, int fix_gamma, const float* __restrict__ gamma, const float* __restrict__ beta,
+    float* moving_mean, float* moving_var, float* save_mean, float* save_invstd, float* scale, float* shift) {
+  const int cl = threadIdx.x & 15, ch = blockIdx.x * 16 + cl;
+  const int g = threadIdx.x >> 6, v = (threadIdx.x >> 4) & 3;
+  const int ngrp = (nblk + kPartGroup - 1) / kPartGroup;
+  __shared__ double sub[3][4][4][16];  // [s1, s2, n][group][sub][channel]
+  __shared__ double piv[4][16];
+  if (ch < c && g < ngrp) {
+    const int b0 = g * kPartGroup, b1 = min(nblk, b0 + kPartGroup);
+    const double q = part[(int64_t)b0 * 3 * ld + 2 * ld + ch];
+    constexpr int kPer = kPartGroup / 4;
+    float va[kPer], vs[kPer], vp[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int b = b0 + v + 4 * u;
+      const float* pb = part + (int64_t)min(b, b1 - 1) * 3 * ld + ch;
+      va[u] = pb[0];
+      vs[u] = pb[ld];
+      vp[u] = pb[2 * ld];
+    }
+    double s1 = 0.0, s2 = 0.0, n = 0.0;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+      const int b = b0 + v + 4 * u;
+      if (b >= b1) break;
+      const double nb = (double)min<int64_t>(rows_blk, m - (int64_t)b * rows_blk);
+      const double d = (double)vp[u] - q;
+      const double a = va[u];
+      s1 += a + nb * d;
+      s2 += (double)vs[u] + 2.0 * d * a + nb * d * d;
+      n += nb;
+    }
+    sub[0][g][v][cl] = s1;
+    sub[1][g][v][cl] = s2;
+    sub[2][g][v][cl] = n;
+    if (v == 0) piv[g][cl] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x >= 16 || ch >= c) return;
+  // per group: the merge kernel's sub sums in order; then the finalize kernel's per-sub terms (sub = group
+  // here, each walking one group) added in group order
+  const double q0 = piv[0][cl];
+  double t1[4], t2[4];
+#pragma unroll
+  for (int gg = 0; gg < 4; ++gg) {
+    t1[gg] = t2[gg] = 0.0;
+    if (gg >= ngrp) continue;
+    double a = sub[0][gg][0][cl], s = sub[1][gg][0][cl], nb = sub[2][gg][0][cl];
+#pragma unroll
+    for (int vv = 1; vv < 4; ++vv) {
+      a += sub[0][gg][vv][cl];
+      s += sub[1][gg][vv][cl];
+      nb += sub[2][gg][vv][cl];
+    }
+    const double d = piv[gg][cl] - q0;
+    t1[gg] += a + nb * d;
+    t2[gg] += s + 2.0 * d * a + nb * d * d;
+  }
+  double s1 = t1[0], s2 = t2[0];
+#pragma unroll
+  for (int gg = 1; gg < 4; ++gg) {
+    s1 += t1[gg];
+    s2 += t2[gg];
+  }
+  if (ch >= c_real) {
+    scale[ch] = 0.f;
+    shift[ch] = 0.f;
+    return;
+  }
+  const double md = s1 / (double)m;
+  const double mean = q0 + md;
+  double var = s2 / (double)m - md * md;
+  if (var < 0) var = 0;
+  const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float gm = fix_gamma ? 1.f : gamma[ch];
+  const float sc = gm * invstd;
+  scale[ch] = sc;
+  shift[ch] = beta[ch] - (float)mean * sc;
+  save_mean[ch] = (float)mean;
+  save_invstd[ch] = invstd;
+  if (moving_mean) {
+    moving_mean[ch] = moving_mean[ch] * momentum + (float)mean * (1.f - momentum);
+    moving_var[ch] = moving_var[ch] * momentum + (float)var * (1.f - momentum);
+  }
+}
+
 // ---- stem input (bn_data over the NCHW fp32 `data`, symbol/resnet.py:90): statistics straight from
 // the NCHW planes, then one pass writing the normalised NHWC-8 compute copy for conv0.
 // part[b][c][2]: shifted sums over images [b*ipb, (b+1)*ipb) of channel c, pivot x[0][c][0][0].
@@ -855,11 +949,17 @@ int rn_bn_fwd_train_part(const rn_bn_desc* d, const float* part, int64_t nblk, i
   hipStream_t st = as_stream(stream);
   const int ngrp = (int)ceil_div(nblk, kPartGroup);
   double* part2 = reinterpret_cast<double*>(ws);
-  hipLaunchKernelGGL(bn_part_merge_kernel, dim3((d->c + 63) / 64, ngrp), dim3(256), 0, st, part, (int)nblk, d->m,
-                     rows_blk, ld, d->c, part2);
-  hipLaunchKernelGGL(bn_fwd_finalize_part_kernel, dim3((d->c + 63) / 64), dim3(256), 0, st, part2, ngrp, d->m, d->c,
-                     d->c_real, d->eps, d->momentum, d->fix_gamma, gamma, beta, moving_mean, moving_var, save_mean,
-                     save_invstd, scale, shift);
+  if (ngrp <= 4 && g_tune[RN_TUNE_BN_MERGE] != 1) {  // (rn_set_tuning 24 = 1: the two launches everywhere)
+    hipLaunchKernelGGL(bn_fwd_merge_finalize_kernel, dim3((d->c + 15) / 16), dim3(256), 0, st, part, (int)nblk,
+                       d->m, rows_blk, ld, d->c, d->c_real, d->eps, d->momentum, d->fix_gamma, gamma, beta,
+                       moving_mean, moving_var, save_mean, save_invstd, scale, shift);
+  } else {
+    hipLaunchKernelGGL(bn_part_merge_kernel, dim3((d->c + 63) / 64, ngrp), dim3(256), 0, st, part, (int)nblk, d->m,
+                       rows_blk, ld, d->c, part2);
+    hipLaunchKernelGGL(bn_fwd_finalize_part_kernel, dim3((d->c + 63) / 64), dim3(256), 0, st, part2, ngrp, d->m,
+                       d->c, d->c_real, d->eps, d->momentum, d->fix_gamma, gamma, beta, moving_mean, moving_var,
+                       save_mean, save_invstd, scale, shift);
+  }
   if (rn_check_launch("bn_fwd_finalize_part")) return -1;
   if (!y) return 0;
   RN_CHECK_ARG(x != nullptr, "null x");

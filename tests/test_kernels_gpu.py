@@ -659,6 +659,47 @@ def test_grouped_conv_bnstats_epilogue(gpu, case):
     assert rel_err(mm.cpu().numpy(), mm_ref) < 1e-5
 
 
+@pytest.mark.parametrize("nblk,rows,c", [(56, 224, 512), (224, 224, 256), (224, 224, 1024), (1, 224, 64),
+                                          (65, 128, 72), (256, 64, 136), (257, 64, 64), (3584, 224, 64)])
+def test_bn_fwd_merge_finalize_one_launch(gpu, nblk, rows, c):
+    """rn_bn_fwd_train_part merges the conv epilogue's BatchNorm partials and finalizes in ONE launch where
+    they form at most 4 merge groups (nblk <= 256): every output (scale, shift, saved mean / invstd,
+    moving statistics) bit for bit that of the two-launch merge + finalize (rn_set_tuning 24 = 1), on
+    partials with an offset mean and ragged last blocks; beyond 4 groups the call takes the two launches."""
+    lib = L.load()
+    rng = np.random.default_rng(31 + nblk)
+    m = nblk * rows - rows // 3  # (a ragged last block)
+    ld = c + 8
+    part = np.zeros((nblk, 3, ld), np.float32)
+    nb = np.minimum(rows, m - np.arange(nblk) * rows).astype(np.float64)
+    piv = rng.standard_normal((nblk, c)) * 0.5 + 3.0
+    part[:, 2, :c] = piv
+    part[:, 0, :c] = rng.standard_normal((nblk, c)) * np.sqrt(nb)[:, None]
+    part[:, 1, :c] = (rng.uniform(0.5, 1.5, (nblk, c)) * nb[:, None]).astype(np.float32)
+    bd = L.BNDesc(dtype=BF16, m=m, c=c, c_real=c - (8 if c % 64 else 0), eps=1e-5, momentum=0.9, fix_gamma=0, relu=1)
+    f = lambda a: torch.tensor(np.asarray(a, np.float64), dtype=torch.float32, device=gpu)
+    pd = f(part.reshape(-1))
+    gamma, beta = f(rng.uniform(0.5, 1.5, c)), f(rng.standard_normal(c) * 0.1)
+    ws = torch.zeros(lib.rn_bn_workspace_bytes(C.byref(bd)) // 4 + 16 + nblk * 8 * c, dtype=torch.float32, device=gpu)
+    outs = []
+    for mode in (0, 1):
+        L.call("rn_set_tuning", 24, mode)
+        mm, mv = f(rng.standard_normal(c) * 0 + 0.25), f(np.ones(c))
+        sm, si, sc, sh = [torch.full((c,), 7.0, dtype=torch.float32, device=gpu) for _ in range(4)]
+        L.call("rn_bn_fwd_train_part", C.byref(bd), p(pd), nblk, rows, ld, None, None, p(gamma), p(beta), p(mm),
+               p(mv), p(sm), p(si), p(sc), p(sh), p(ws), stream())
+        torch.cuda.synchronize()
+        outs.append([t.clone() for t in (sm, si, sc, sh, mm, mv)])
+    L.call("rn_set_tuning", 24, 0)
+    for a, b in zip(*outs):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    # and the merged mean is the batch mean of the partials' rows
+    mean = (piv + part[:, 0, :c] / nb[:, None]) * nb[:, None]
+    ref = mean.sum(0) / nb.sum()
+    nreal = bd.c_real
+    assert np.abs(outs[0][0].cpu().numpy()[:nreal] - ref[:nreal]).max() < 1e-4
+
+
 @pytest.mark.parametrize("dtype", [F32, BF16])
 def test_weight_pack_multi(gpu, dtype):
     """rn_conv_weight_pack_multi writes exactly the bytes of one rn_conv_weight_pack per layer: the
