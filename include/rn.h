@@ -581,7 +581,9 @@ const char* rn_last_error(void);
  *     LDS-DMA tiles, measured slower; 3 = the register-staged kernel only),
  * 6 = diagnostic build only: wgrad skips its dW epilogue (wrong results; isolates the atomic adds),
  * 7 = diagnostic build only: igemm 256-row tile schedule experiments (bit mask; 0 = default; bits 4,
- *     8, 16, 32 drop waits / DMAs / the epilogue / the stores: wrong results),
+ *     8, 16, 32, 64, 128, 256, 512 drop waits / DMAs / the epilogue / the stores / the epilogue's LDS
+ *     staging writes (16x16 tiles) / its BatchNorm partial math / its loads / its staging reads: wrong
+ *     results),
  * 8 = igemm 256-row tile MFMA shape (0 = 32x32x16, 1 = 16x16x32),
  * 9 = igemm 224-row tiles for the 256/128-column tiles (0 = on, 1 = 256 rows),
  * 10 = igemm 256-row-family persistent grid: workgroups (a multiple of 8) that walk the tiles of a

@@ -1180,11 +1180,12 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
         const int ii = fdiv(rem, cl.fdQ);
         const int jj = rem - ii * cl.Qc;
         off[k] = ((int64_t)(n * p.P + cl.a + p.ostep_h * ii) * p.Q + cl.b + p.ostep_w * jj) * p.ldo + col0;
-        if (ag && col0 + 8 <= p.K)
+        const bool eld = !(kRnDiag && (p.sched & 256));  // (diagnostic bit 256: no epilogue loads)
+        if (ag && col0 + 8 <= p.K && eld)
 #pragma unroll
           for (int u = 0; u < AW; ++u) addv[k][u] = reinterpret_cast<const uint4*>(ag + off[k])[u];
         if constexpr (XP)
-          if (col0 + 8 <= p.K) xpre[k] = *reinterpret_cast<const uint4*>(bxg + off[k]);
+          if (col0 + 8 <= p.K && eld) xpre[k] = *reinterpret_cast<const uint4*>(bxg + off[k]);
       }
     }
     // Each wave stages through its own LDS region, so the epilogue needs no block barrier -- a wave's
@@ -1203,6 +1204,13 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
           for (int e = 0; e < 16; ++e)
             ep[(i * 32 + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5)) * EP_LD + j * 32 + (lane & 31)] =
                 acc[h * 2 + i][j][e];
+    } else if (kRnDiag && (p.sched & 64)) {  // diagnostic (rn_set_tuning 7 bit 64): no staging writes (the
+                                           // accumulators kept live, the staged values stale: wrong results)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (h * 4 + i < MI)
+#pragma unroll
+          for (int j = 0; j < NI; ++j) asm volatile("" ::"v"(acc[h * 4 + i][j]));
     } else {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -1230,8 +1238,13 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
       if (off[k] < 0) continue;
       const int r = lane / CPR + (64 / CPR) * k;
       float v[8];
-      *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(ep + r * EP_LD + cc * 8);
-      *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(ep + r * EP_LD + cc * 8 + 4);
+      if (kRnDiag && (p.sched & 512)) {  // (diagnostic bit 512: no staging reads -- stale values)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = (float)(r + e);
+      } else {
+        *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(ep + r * EP_LD + cc * 8);
+        *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(ep + r * EP_LD + cc * 8 + 4);
+      }
       if (col0 + 8 <= p.K) {
         if constexpr (EPI == 3) {
           // the BatchNorm(+ReLU) backward applied to the gradient as rn_conv_bwd_data would store it,
@@ -1282,7 +1295,9 @@ __global__ __launch_bounds__(BN == 64 || W4 ? 256 : 512, BN == 64 || W4 ? 2 : 1)
             for (int u = 0; u < AW; ++u) reinterpret_cast<uint4*>(yg + off[k])[u] = out[u];
           }
         }
-        if constexpr (EPI == 1 || EPI == 2) {  // on the stored (rounded) values, as a separate pass would read them
+        if (EPI != 1 && EPI != 2) {
+        } else if (kRnDiag && (p.sched & 128)) {  // diagnostic (bit 128): no BatchNorm partial math (wrong results)
+        } else if constexpr (EPI == 1 || EPI == 2) {  // on the stored (rounded) values, as a separate pass would read them
           float g[8];
 #pragma unroll
           for (int u = 0; u < AW; ++u) chunk_to_f(out[u], g + u * (8 / AW), (const OutT*)nullptr);
