@@ -636,6 +636,8 @@ const char* rn_last_error(void);
  * 23 = the same percent for the grouped image-band weight gradients only (0 = key 21's),
  * 24 = 1: rn_bn_fwd_train_part always merges and finalizes in two launches (default 0: one launch where
  *      the partials form at most 4 merge groups, bit-identical),
+ * 25 = 1: the weight-gradient slab reduction always runs its general kernel (default 0: one thread per
+ *      16-byte column with every split in flight where there are <= 16 splits; the same sums),
  * 22 = 1: the BatchNorm-folded int8 quantizers (rn_quant_int8_fwd_codes_bn[2]) form every quotient
  *      v / unit by division (default 0: v * (1 / unit), the division only where that product lies
  *      within 2^-21 |v / unit| of a half-integer -- the same codes bit for bit, fewer instructions). */

@@ -2525,6 +2525,32 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __r
   }
 }
 
+// The same sum for at most 16 splits (the split-M grids sized for 45 % of the chip give 1-16): one
+// thread per float4 column, every split's load in flight at once, added in split order onto dw --
+// the value wgrad_slab_reduce_kernel stores (its 16 group sums are then the splits themselves and
+// zeros; the one trailing + 0 reproduces its sign of a zero sum). The general kernel left 15/16 of its
+// threads idle at these split counts.
+__global__ __launch_bounds__(256) void wgrad_slab_reduce_few_kernel(const float* __restrict__ slab, int nsplit,
+                                                                    int64_t n4, float* __restrict__ dw) {
+  const int64_t col = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (col >= n4) return;
+  const float4* __restrict__ s4 = reinterpret_cast<const float4*>(slab);
+  float4 v[16];
+#pragma unroll
+  for (int z = 0; z < 16; ++z)
+    if (z < nsplit) v[z] = s4[(int64_t)z * n4 + col];
+  float4 t = reinterpret_cast<const float4*>(dw)[col];
+#pragma unroll
+  for (int z = 0; z < 16; ++z)
+    if (z < nsplit) {
+      t.x += v[z].x; t.y += v[z].y; t.z += v[z].z; t.w += v[z].w;
+    }
+  if (nsplit < 16) {
+    t.x += 0.f; t.y += 0.f; t.z += 0.f; t.w += 0.f;
+  }
+  reinterpret_cast<float4*>(dw)[col] = t;
+}
+
 // ------------------------------------------------------------------------------ helpers
 template <typename T>
 __global__ void pack_krsc_kernel(const float* __restrict__ wm, T* __restrict__ out, int K, int RS,
@@ -3260,6 +3286,15 @@ int slab_reduce_blocks(int64_t n) {
   if (n & 3) return grid_for(n);
   return (int)std::max<int64_t>(1, (n / 4 + 15) / 16);
 }
+// dw[i] += sum_z slab[z][i]: the few-split kernel for <= 16 splits of whole 16-byte chunks (rn_set_tuning 25
+// = 1: the general kernel always)
+void launch_slab_reduce(const float* slab, int split, int64_t n, float* dw, hipStream_t st) {
+  if (split <= 16 && (n & 3) == 0 && g_tune[RN_TUNE_SLAB_FEW] != 1)
+    hipLaunchKernelGGL(wgrad_slab_reduce_few_kernel, dim3((unsigned)std::max<int64_t>(1, (n / 4 + 255) / 256)), dim3(256),
+                       0, st, slab, split, n / 4, dw);
+  else
+    hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3(slab_reduce_blocks(n)), dim3(256), 0, st, slab, split, n, dw);
+}
 
 // Build igemm args for fwd (mode 0) or dgrad (mode 1).
 // fwd : gathered = x (N,H,W,C), out = y (N,P,Q,K), B = w_krsc [K][R][S][C]
@@ -3972,7 +4007,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     if (rn_check_launch(what)) return -1;
     if (a.slab) {
       const int64_t n = (int64_t)a.K * a.ldw;
-      hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3(slab_reduce_blocks(n)), dim3(256), 0, st, a.slab, (int)split, n, dw);
+      launch_slab_reduce(a.slab, (int)split, n, dw, st);
       return rn_check_launch("wgrad_slab_reduce");
     }
     return 0;
@@ -4049,7 +4084,7 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
       else hipLaunchKernelGGL((wgrad_gband_kernel<256, 16, 16, 2, 2>), grid, dim3(512), 0, st, g);
       if (rn_check_launch("wgrad_gband")) return -1;
       const int64_t n = (int64_t)a.K * a.ldw;
-      hipLaunchKernelGGL(wgrad_slab_reduce_kernel, dim3(slab_reduce_blocks(n)), dim3(256), 0, st, a.slab, (int)split, n, dw);
+      launch_slab_reduce(a.slab, (int)split, n, dw, st);
       return rn_check_launch("wgrad_slab_reduce");
     }
     if (ws_need) *ws_need = 0;

@@ -114,3 +114,41 @@ def test_resnet50_fp32_deterministic_unreplayed(gpu, deterministic):
     assert med(e_dev) <= max(1e-4, 4 * med(e32))
     assert max(e_dev.values()) <= max(1e-4, 4 * max(e32.values()))
     assert max_rel(r1["prob"][0], ref["prob"][0]) <= max(1e-4, 4 * max_rel(r32["prob"][0], ref["prob"][0]))
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("case", [
+    (8, 64, 28, 28, 128, 3, 1, 1, 1),
+    (16, 256, 14, 14, 512, 1, 2, 0, 1),
+    (4, 3, 32, 32, 64, 7, 2, 3, 1),
+    (4, 128, 14, 14, 128, 3, 1, 1, 32),
+    (32, 2048, 1, 1, 1000, 1, 1, 0, 1),
+    (64, 64, 56, 56, 64, 1, 1, 0, 1),      # many splits (> 16: the general kernel in both modes)
+])
+def test_slab_reduce_few_splits_bitwise(gpu, deterministic, dtype, case):
+    """rn_set_tuning 25: the few-split slab reduction (one thread per 16-byte column, <= 16 splits)
+    stores exactly the general kernel's sums (dw accumulated into: += onto a nonzero start)."""
+    n, c, h, w, k, r, st, pd, g = case
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal((n, c, h, w))
+    d = conv_desc(dtype, n, c, h, w, k, r, r, st, pd, groups=g)
+    dy = rng.standard_normal((n, k, d.p, d.q))
+    if dtype == BF16:
+        x, dy = bf16_round(x), bf16_round(dy)
+    lib = L.load()
+    need = int(lib.rn_conv_wgrad_ws_bytes(C.byref(d)))
+    ws = torch.empty(need // 4, dtype=torch.float32, device=gpu)
+    xd, dyd = to_nhwc(x, dtype, gpu), to_nhwc(dy, dtype, gpu)
+    start = torch.tensor(rng.standard_normal(k * r * r * (c // g)), dtype=torch.float32, device=gpu)
+    outs = []
+    try:
+        for mode in (1, 0):
+            L.call("rn_set_tuning", 25, mode)
+            dw = start.clone()
+            ws.fill_(float("nan"))
+            L.call("rn_conv_bwd_filter_ws", C.byref(d), p(xd), p(dyd), p(dw), p(ws), need, stream())
+            outs.append(dw)
+        torch.cuda.synchronize()
+    finally:
+        L.call("rn_set_tuning", 25, 0)
+    assert torch.equal(outs[0], outs[1])
