@@ -638,6 +638,8 @@ const char* rn_last_error(void);
  *      the partials form at most 4 merge groups, bit-identical),
  * 25 = 1: the weight-gradient slab reduction always runs its general kernel (default 0: one thread per
  *      16-byte column with every split in flight where there are <= 16 splits; the same sums),
+ * 26 = 1: the 3x3 / stride-1 / pad-1 64 -> 64 convolutions (forward, data gradient) on the implicit-GEMM
+ *      tile (default 0: conv3x3c64_band_kernel, image bands and the nine taps' weights in LDS),
  * 22 = 1: the BatchNorm-folded int8 quantizers (rn_quant_int8_fwd_codes_bn[2]) form every quotient
  *      v / unit by division (default 0: v * (1 / unit), the division only where that product lies
  *      within 2^-21 |v / unit| of a half-integer -- the same codes bit for bit, fewer instructions). */

@@ -3676,6 +3676,125 @@ bool gd_direct_ok(const rn_conv_desc* d, int mode) {
   return d && d->grouped_direct == 1 && gd_direct_shape(d, mode);
 }
 
+// ---- 3x3 / stride 1 / pad 1 convolution of 64 channels into 64 over image bands in LDS (ResNet-50
+// stage 1's conv2 forward and data gradient, symbol/resnet.py:24-27; rn_set_tuning 26 = 1: off). The implicit
+// GEMM DMAs every input element once per tap (nine 64-channel K-tiles from L2); here a persistent
+// workgroup keeps all nine taps' weights in LDS (72 KB, [tap][out][in]) and double-buffers bands of
+// four input rows (the two output rows and their halo, 64 pixel slots per row: the halo columns and
+// rows outside the image zero-filled by the DMA), so each input element is loaded about twice and
+// every tap reads it from LDS. Seven waves: wave w owns 16-pixel block w of the band's 2 W <= 112 pixels,
+// all 64 output channels (four 16x16 blocks: per (tap, k-step) 5 fragment reads for 4 MFMAs, the next
+// step's reads issued before this step's MFMAs); the MFMA operands are swapped so a lane's accumulator
+// holds four consecutive channels of one pixel (one 8-byte store per block). Data gradient (FLIP): dy
+// through the CRSK copy with the taps mirrored, dx[p] = sum dy[p + t - 1] w[8 - t]. ResNet-50 stage 1
+// (tools/conv_bench.py): forward 105.9 -> 66.2 us, data gradient 115.3 -> 80.7 us; step 20.25 -> 20.03 ms.
+struct BandArgs {
+  const void* x;  // [N][H][W][64] bf16
+  const void* w;  // [64][9][64] bf16: out, tap, in
+  void* y;        // [N][H][W][64] bf16
+  int N, H, W, hb, nbands, x_bytes, y_bytes;
+};
+constexpr int kBandBytes = 4 * 64 * 128;  // one band buffer: 4 rows x 64 pixel slots x 64 channels
+template <int FLIP>
+__global__ __launch_bounds__(448, 1) void conv3x3c64_band_kernel(BandArgs p) {
+  __shared__ __attribute__((aligned(16))) uint4 smem[(2 * kBandBytes + 9 * 64 * 128) / 16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;  // 7 waves: wave w = pixel block w
+  const v4i rs_x = make_rsrc(p.x, (uint32_t)p.x_bytes);
+  const v4i rs_w = make_rsrc(p.w, 64 * 9 * 64 * 2);
+  const __amdgpu_buffer_rsrc_t rs_y = __builtin_amdgcn_make_buffer_rsrc(p.y, (short)0, p.y_bytes, 0x00020000);
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  constexpr uint32_t kW = 2 * kBandBytes;  // weights after the two band buffers
+  // the weights: 576 rows (tap, out) x 8 chunks, chunk phys of row r holding in-channel chunk phys ^ (r & 7);
+  // 72 pieces over waves 0-5
+  if (wid < 6) {
+#pragma unroll
+    for (int j = 0; j < 12; ++j) {
+      const int ins = wid * 12 + j, chunk = ins * 64 + lane;
+      const int row = chunk >> 3, tap = row >> 6, o = row & 63;
+      const int logical = (chunk & 7) ^ (row & 7);
+      dma16_asm(rs_w, lds0 + kW + ins * 1024, (uint32_t)(((o * 9 + (FLIP ? 8 - tap : tap)) * 64 + logical * 8) * 2));
+    }
+  }
+  // band b -> buffer bb (32 pieces over waves 0-3): slot (row br, column bc) holds input row h0 - 1 + br,
+  // column bc - 1
+  auto issue_band = [&](int b, int bb) __attribute__((always_inline)) {
+    if (wid >= 4) return;
+    const int n = b / p.hb, h0 = (b - n * p.hb) * 2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ins = wid * 8 + j, chunk = ins * 64 + lane;
+      const int pix = chunk >> 3, br = pix >> 6, bc = pix & 63;
+      const int h = h0 - 1 + br, wc = bc - 1;
+      const int logical = (chunk & 7) ^ (pix & 7);
+      const bool ok = (unsigned)h < (unsigned)p.H && (unsigned)wc < (unsigned)p.W;
+      dma16_asm(rs_x, lds0 + bb * kBandBytes + ins * 1024,
+                ok ? (uint32_t)((((n * p.H + h) * p.W + wc) * 64 + logical * 8) * 2) : kOob);
+    }
+  };
+  // this lane's output pixel wid * 16 + (lane & 15) = (orow, ocol); for tap (r, s) its input sits in slot
+  // (orow + r, ocol + s), at byte ab[s] + r * 8192 (+ 64 for k-step 1); weight block j at wbj[j] + tap * 8192
+  const int q = lane >> 4, c = lane & 15;
+  const int pp = wid * 16 + c;
+  const int orow = pp >= p.W ? 1 : 0, ocol = pp - orow * p.W;
+  int ab[3], wbj[4];
+#pragma unroll
+  for (int sx = 0; sx < 3; ++sx) {
+    const int col = min(ocol + sx, 63);
+    ab[sx] = orow * 8192 + col * 128 + ((q ^ (col & 7)) << 4);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int o = j * 16 + c;
+    wbj[j] = (int)kW + o * 128 + ((q ^ (o & 7)) << 4);
+  }
+  const char* lds = reinterpret_cast<const char*>(smem);
+  int it = 0;
+  int b = blockIdx.x;
+  if (b < p.nbands) issue_band(b, 0);
+  for (; b < p.nbands; b += gridDim.x, ++it) {
+    const int bb = it & 1;
+    if (it == 0) wait_vmcnt<0>();
+    else wait_vmcnt<4>();  // (the previous band's 4 stores may stay in flight)
+    __syncthreads();       // the band has landed for every wave; every wave is done with the other buffer
+    if (b + (int)gridDim.x < p.nbands) issue_band(b + gridDim.x, bb ^ 1);
+    v4f acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = v4f{0.f, 0.f, 0.f, 0.f};
+    const int boff = bb * kBandBytes;
+    // 18 steps (tap, k-step), each 5 fragment reads (1 pixel block, 4 weight blocks) for 4 MFMAs; step i + 1's
+    // reads are issued before step i's MFMAs
+    uint4 fa[2], fb[2][4];
+    auto ld = [&](int step, int slot) __attribute__((always_inline)) {
+      const int t = step >> 1, ks = step & 1, r = t / 3, sx = t % 3;
+      fa[slot] = *reinterpret_cast<const uint4*>(lds + boff + ((ab[sx] + r * 8192) ^ (ks * 64)));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[slot][j] = *reinterpret_cast<const uint4*>(lds + ((wbj[j] + t * 8192) ^ (ks * 64)));
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int step = 0; step < 18; ++step) {
+      if (step + 1 < 18) ld(step + 1, (step + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);  // (hipcc otherwise sinks every read next to its MFMA)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        mfma_slab<bf16_t>(acc[j], fb[step & 1][j], fa[step & 1]);  // (swapped: lane = pixel, 4 channels)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int n = b / p.hb, h0 = (b - n * p.hb) * 2;
+    const int h = h0 + orow;
+    const bool ok = pp < 2 * p.W && h < p.H;
+    const int obase = (((n * p.H + h) * p.W + ocol) * 64 + 4 * q) * 2;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t lo = (uint32_t)f2bf(acc[j][0]) | ((uint32_t)f2bf(acc[j][1]) << 16);
+      const uint32_t hi = (uint32_t)f2bf(acc[j][2]) | ((uint32_t)f2bf(acc[j][3]) << 16);
+      const uint32_t voff = ok ? (uint32_t)(obase + j * 32) : 0x80000000u;
+      typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+      __builtin_amdgcn_raw_buffer_store_b64(u32x2{lo, hi}, rs_y, voff, 0, 0);
+    }
+  }
+}
+
 // geometry of a direct grouped launch (mode 0 forward, 1 data gradient): fills a's shape fields,
 // returns the workgroups (also the BatchNorm-reduction partials of a RED data gradient)
 int gd_geometry(const rn_conv_desc* d, int mode, GdArgs& a) {
@@ -3725,6 +3844,23 @@ int gd_launch(const rn_conv_desc* d, int mode, const void* x, const void* w, voi
   else
     hipLaunchKernelGGL((grouped_direct_kernel<8, 2, 4>), dim3(blocks), dim3(256), lds, st, a);
   return rn_check_launch(mode == 0 ? "grouped_direct_fwd" : "grouped_direct_dgrad");
+}
+
+// conv3x3c64_band_kernel for these arguments? (rn_set_tuning 26 = 1: never -- the implicit-GEMM tile)
+bool band_ok(const rn_conv_desc* d) {
+  return g_tune[RN_TUNE_CONV_BAND] != 1 && d->dtype == RN_BF16 && d->groups <= 1 && d->r == 3 && d->s == 3 &&
+         d->stride_h == 1 && d->stride_w == 1 && d->pad_h == 1 && d->pad_w == 1 && d->c == 64 && d->c_real == 64 &&
+         d->k == 64 && d->k_pad == 64 && d->w <= 56 && (int64_t)d->n * d->h * d->w * 64 * 2 < INT32_MAX;
+}
+int band_launch(const rn_conv_desc* d, const void* x, const void* w, void* y, int flip, hipStream_t st) {
+  BandArgs a{};
+  a.x = x; a.w = w; a.y = y;
+  a.N = d->n; a.H = d->h; a.W = d->w; a.hb = (d->h + 1) / 2; a.nbands = d->n * a.hb;
+  a.x_bytes = a.y_bytes = d->n * d->h * d->w * 64 * 2;
+  const dim3 grid((unsigned)std::min(a.nbands, chip_cus()));
+  if (flip) hipLaunchKernelGGL(conv3x3c64_band_kernel<1>, grid, dim3(448), 0, st, a);
+  else hipLaunchKernelGGL(conv3x3c64_band_kernel<0>, grid, dim3(448), 0, st, a);
+  return rn_check_launch("conv3x3c64_band");
 }
 
 }  // namespace
@@ -3787,6 +3923,8 @@ int rn_conv_fwd_x(const rn_conv_desc* d, const void* x, const void* w, void* y, 
     RN_CHECK_ARG(!bias && !part && y_dtype == RN_BF16, "grouped direct forward: no bias / statistics, bf16 output");
     return gd_launch(d, 0, x, w, y, add_src, as_stream(stream));
   }
+  if (band_ok(d) && !add_src && !bias && !part && !in_scale && y_dtype == RN_BF16)
+    return band_launch(d, x, w, y, 0, as_stream(stream));
   IgemmArgs a = make_igemm_args(d, 0);
   a.x = x; a.w = w; a.y = y; a.add = add_src; a.bias = bias; a.stats = part;
   a.in_sc = in_scale; a.in_sh = in_shift;
@@ -3896,6 +4034,7 @@ int rn_conv_bwd_data_bnred_clip(const rn_conv_desc* d, const void* dy, const voi
     r.bn_relu = relu;
     return gd_launch(d, 1, dy, w_crsk, dx, add_src, as_stream(stream), &r);
   }
+  if (band_ok(d) && !part && !add_src && !clip && dx) return band_launch(d, dy, w_crsk, dx, 1, as_stream(stream));
   IgemmArgs a = make_igemm_args(d, 1);
   a.x = dy; a.w = w_crsk; a.y = dx; a.add = add_src; a.bias = nullptr;
   if (part) {

@@ -1840,3 +1840,48 @@ def test_wgrad_int8_codes_unsupported(gpu):
         assert lib.rn_conv_wgrad_i8_ws_bytes(C.byref(d)) == -1
         dummy = torch.zeros(16, dtype=torch.float32, device=gpu)
         assert lib.rn_conv_bwd_filter_i8(C.byref(d), p(dummy), p(dummy), p(dummy), p(dummy), None, 0, stream()) != 0
+
+
+@pytest.mark.parametrize("persist", [0, 1])
+@pytest.mark.parametrize("case", [
+    (3, 64, 56, 56, 64, 3, 1, 1),    # stage 1's conv2 (several bands per workgroup)
+    (5, 64, 9, 13, 64, 3, 1, 1),     # odd rows: the last band has one output row
+    (1, 64, 7, 7, 64, 3, 1, 1),      # fewer pixels than one band's blocks
+    (2, 64, 20, 56, 64, 3, 1, 1),    # the widest row
+])
+def test_conv3x3_band(gpu, case, persist):
+    """conv3x3c64_band_kernel (image bands in LDS, all nine taps' weights resident; the default for a
+    3x3 / stride-1 / pad-1 64 -> 64 convolution, rn_set_tuning 26 = 1 the implicit-GEMM tile) for the
+    forward and the data gradient, against the fp32 reference and the implicit-GEMM tile. persist = 1: a
+    batch large enough that every workgroup walks several bands (the double-buffered band loads)."""
+    n, c, h, w, k, r, st, pd = case
+    if persist:
+        n = 40
+    x, wt = _conv_data((n, c, h, w, k, r, st, pd), 23)
+    x, wt = bf16_round(x), bf16_round(wt)
+    dy = bf16_round(np.random.default_rng(24).standard_normal((n, k, h, w)))
+    ref = ops.conv2d_fwd(x, wt, (st, st), (pd, pd))
+    dx_ref, _ = ops.conv2d_bwd(x, wt, dy, (st, st), (pd, pd))
+    d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd)
+    wk = torch.zeros(k * r * r * d.c, dtype=torch.bfloat16, device=gpu)
+    wc = torch.zeros(d.c * r * r * d.k_pad, dtype=torch.bfloat16, device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), p(wk), p(wc), stream())
+    xd, dyd = to_nhwc(x, BF16, gpu), to_nhwc(dy, BF16, gpu)
+    outs = []
+    try:
+        for mode in (0, 1):
+            L.call("rn_set_tuning", 26, mode)
+            y = torch.full((n, h, w, 64), float("nan"), dtype=torch.bfloat16, device=gpu)
+            dx = torch.full((n, h, w, 64), float("nan"), dtype=torch.bfloat16, device=gpu)
+            L.call("rn_conv_fwd", C.byref(d), p(xd), p(wk), p(y), BF16, None, None, stream())
+            L.call("rn_conv_bwd_data", C.byref(d), p(dyd), p(wc), p(dx), None, stream())
+            torch.cuda.synchronize()
+            outs.append((y, dx))
+    finally:
+        L.call("rn_set_tuning", 26, 0)
+    for y, dx in outs:
+        assert not torch.isnan(y).any() and not torch.isnan(dx).any()
+        assert rel_err(from_nhwc(y, k), ref) < TOL[BF16]
+        assert rel_err(from_nhwc(dx, c), dx_ref) < TOL[BF16]
+    assert rel_err(from_nhwc(outs[1][0], k), from_nhwc(outs[0][0], k)) < 1e-2
+    assert rel_err(from_nhwc(outs[1][1], c), from_nhwc(outs[0][1], c)) < 1e-2
