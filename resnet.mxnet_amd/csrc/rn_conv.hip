@@ -3689,15 +3689,18 @@ bool gd_direct_ok(const rn_conv_desc* d, int mode) {
 // through the CRSK copy with the taps mirrored, dx[p] = sum dy[p + t - 1] w[8 - t]. ResNet-50 stage 1
 // (tools/conv_bench.py): forward 105.9 -> 66.2 us, data gradient 115.3 -> 80.7 us; step 20.25 -> 20.03 ms.
 struct BandArgs {
+  const float *in_sc, *in_sh;  // (XF) the producing BatchNorm+ReLU, applied to the landed band
   const void* x;  // [N][H][W][64] bf16
   const void* w;  // [64][9][64] bf16: out, tap, in
   void* y;        // [N][H][W][64] bf16
   int N, H, W, hb, nbands, x_bytes, y_bytes;
 };
 constexpr int kBandBytes = 4 * 64 * 128;  // one band buffer: 4 rows x 64 pixel slots x 64 channels
-template <int FLIP>
+template <int FLIP, int XF = 0>
 __global__ __launch_bounds__(448, 1) void conv3x3c64_band_kernel(BandArgs p) {
+  static_assert(!(FLIP && XF), "the input transform is a forward one");
   __shared__ __attribute__((aligned(16))) uint4 smem[(2 * kBandBytes + 9 * 64 * 128) / 16];
+  __shared__ __attribute__((aligned(16))) float xtab[XF ? 128 : 4];  // (XF) scale[64], shift[64]
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;  // 7 waves: wave w = pixel block w
   const v4i rs_x = make_rsrc(p.x, (uint32_t)p.x_bytes);
   const v4i rs_w = make_rsrc(p.w, 64 * 9 * 64 * 2);
@@ -3748,6 +3751,12 @@ __global__ __launch_bounds__(448, 1) void conv3x3c64_band_kernel(BandArgs p) {
     wbj[j] = (int)kW + o * 128 + ((q ^ (o & 7)) << 4);
   }
   const char* lds = reinterpret_cast<const char*>(smem);
+  if constexpr (XF) {
+    if (tid < 64) {
+      xtab[tid] = p.in_sc[tid];
+      xtab[64 + tid] = p.in_sh[tid];
+    }
+  }
   int it = 0;
   int b = blockIdx.x;
   if (b < p.nbands) issue_band(b, 0);
@@ -3756,6 +3765,23 @@ __global__ __launch_bounds__(448, 1) void conv3x3c64_band_kernel(BandArgs p) {
     if (it == 0) wait_vmcnt<0>();
     else wait_vmcnt<4>();  // (the previous band's 4 stores may stay in flight)
     __syncthreads();       // the band has landed for every wave; every wave is done with the other buffer
+    if constexpr (XF) {
+      // max(x * sc + sh, 0) rounded to bf16 in place, as bn_apply_kernel stores it; the zero halo (the
+      // convolution pads the activation) stays zero
+      const int n = b / p.hb, h0 = (b - n * p.hb) * 2;
+      uint4* band = smem + bb * (kBandBytes / 16);
+      for (int i = tid; i < kBandBytes / 16; i += 448) {
+        const int pix = i >> 3, br = pix >> 6, bc = pix & 63;
+        if ((unsigned)(h0 - 1 + br) >= (unsigned)p.H || (unsigned)(bc - 1) >= (unsigned)p.W) continue;
+        const int ch = ((i & 7) ^ (pix & 7)) * 8;
+        float f[8];
+        chunk_to_f(band[i], f, (const bf16_t*)nullptr);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], xtab[ch + e], xtab[64 + ch + e]), 0.f);
+        band[i] = f_to_chunk(f, (const bf16_t*)nullptr);
+      }
+      __syncthreads();
+    }
     if (b + (int)gridDim.x < p.nbands) issue_band(b + gridDim.x, bb ^ 1);
     v4f acc[4];
 #pragma unroll
@@ -3852,13 +3878,15 @@ bool band_ok(const rn_conv_desc* d) {
          d->stride_h == 1 && d->stride_w == 1 && d->pad_h == 1 && d->pad_w == 1 && d->c == 64 && d->c_real == 64 &&
          d->k == 64 && d->k_pad == 64 && d->w <= 56 && (int64_t)d->n * d->h * d->w * 64 * 2 < INT32_MAX;
 }
-int band_launch(const rn_conv_desc* d, const void* x, const void* w, void* y, int flip, hipStream_t st) {
+int band_launch(const rn_conv_desc* d, const void* x, const void* w, void* y, int flip, hipStream_t st,
+                const float* in_sc = nullptr, const float* in_sh = nullptr) {
   BandArgs a{};
-  a.x = x; a.w = w; a.y = y;
+  a.x = x; a.w = w; a.y = y; a.in_sc = in_sc; a.in_sh = in_sh;
   a.N = d->n; a.H = d->h; a.W = d->w; a.hb = (d->h + 1) / 2; a.nbands = d->n * a.hb;
   a.x_bytes = a.y_bytes = d->n * d->h * d->w * 64 * 2;
   const dim3 grid((unsigned)std::min(a.nbands, chip_cus()));
   if (flip) hipLaunchKernelGGL(conv3x3c64_band_kernel<1>, grid, dim3(448), 0, st, a);
+  else if (in_sc) hipLaunchKernelGGL((conv3x3c64_band_kernel<0, 1>), grid, dim3(448), 0, st, a);
   else hipLaunchKernelGGL(conv3x3c64_band_kernel<0>, grid, dim3(448), 0, st, a);
   return rn_check_launch("conv3x3c64_band");
 }
@@ -3923,8 +3951,8 @@ int rn_conv_fwd_x(const rn_conv_desc* d, const void* x, const void* w, void* y, 
     RN_CHECK_ARG(!bias && !part && y_dtype == RN_BF16, "grouped direct forward: no bias / statistics, bf16 output");
     return gd_launch(d, 0, x, w, y, add_src, as_stream(stream));
   }
-  if (band_ok(d) && !add_src && !bias && !part && !in_scale && y_dtype == RN_BF16)
-    return band_launch(d, x, w, y, 0, as_stream(stream));
+  if (band_ok(d) && !add_src && !bias && !part && y_dtype == RN_BF16)
+    return band_launch(d, x, w, y, 0, as_stream(stream), in_scale, in_shift);
   IgemmArgs a = make_igemm_args(d, 0);
   a.x = x; a.w = w; a.y = y; a.add = add_src; a.bias = bias; a.stats = part;
   a.in_sc = in_scale; a.in_sh = in_shift;

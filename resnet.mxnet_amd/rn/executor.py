@@ -368,9 +368,10 @@ class Plan:
         # the 3x3 stride-1 consumers too (act2 -> conv2, symbol/resnet.py:19-21) where the weight gradient
         # is the image-band kernel (stage 1: C = K = 64), which transforms its staged x images in place;
         # the forward's 64-column tile applies it on load from a register table (bf16).
-        # Opt-in (RN_BN_APPLY_FUSION_3X3=1): measured 0.6 % slower per step (two alternating pairs, r04d:
-        # the per-K-tile transform of the 3x3 forward costs more than the act2 pass it saves); stages 2-4
-        # too, on the 224-row tiles and the band weight gradients, 4 % slower (r04c).
+        # Opt-in (RN_BN_APPLY_FUSION_3X3=1). Round 4 measured the 64-column tile's per-K-tile transform 0.6 %
+        # slower per step, and stages 2-4 on the 224-row tiles and the band weight gradients 4 % slower
+        # (r04c); with round 5's image-band forward (conv3x3c64_band_kernel transforms each landed band once
+        # in LDS) it measures equal (20.04 / 20.03 / 20.01 vs 20.05 / 20.01 / 20.02 ms), so act2 stays written.
         band3 = self.dtype == BF16 and os.environ.get("RN_BN_APPLY_FUSION_3X3", "0") == "1"
 
         def xf_ok(u):
@@ -380,7 +381,7 @@ class Plan:
                 return True
             c, k, w = u.x.c, u.y.c, u.x.w
             return (band3 and tuple(u.kernel) == (3, 3) and tuple(u.stride) == (1, 1) and tuple(u.pad) == (1, 1)
-                    and c == k and u.x.cp == c and u.y.cp == k and c == 64 and w <= 62)
+                    and c == k and u.x.cp == c and u.y.cp == k and c == 64 and w <= 56)
         for bn in self.ops:
             if bn.kind != "bn" or not bn.relu or id(bn.y) in out_ids:
                 continue

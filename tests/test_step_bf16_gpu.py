@@ -275,8 +275,8 @@ def _c5_layerwise(n, image):
 
 def test_resnet50_bf16_layerwise_act2_on_load(gpu, monkeypatch):
     """The opt-in act2 fusion (RN_BN_APPLY_FUSION_3X3=1: stage 1's bn2+ReLU applied on load by conv2's
-    64-column forward tile and its image-band weight gradient, act2 never written), per kernel at 8 images
-    of 112x112 with the C2 bars."""
+    image-band forward and its image-band weight gradient, act2 never written), per kernel at 8 images of
+    112x112 with the C2 bars."""
     from rn import graphs
     monkeypatch.setenv("RN_BN_APPLY_FUSION_3X3", "1")
     ck = _layerwise(graphs.resnet50(), 8, 112, "bfloat16")
