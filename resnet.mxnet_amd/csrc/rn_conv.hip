@@ -3680,14 +3680,14 @@ bool gd_direct_ok(const rn_conv_desc* d, int mode) {
 // stage 1's conv2 forward and data gradient, symbol/resnet.py:24-27; rn_set_tuning 26 = 1: off). The implicit
 // GEMM DMAs every input element once per tap (nine 64-channel K-tiles from L2); here a persistent
 // workgroup keeps all nine taps' weights in LDS (72 KB, [tap][out][in]) and double-buffers bands of
-// four input rows (the two output rows and their halo, 64 pixel slots per row: the halo columns and
-// rows outside the image zero-filled by the DMA), so each input element is loaded about twice and
-// every tap reads it from LDS. Seven waves: wave w owns 16-pixel block w of the band's 2 W <= 112 pixels,
-// all 64 output channels (four 16x16 blocks: per (tap, k-step) 5 fragment reads for 4 MFMAs, the next
-// step's reads issued before this step's MFMAs); the MFMA operands are swapped so a lane's accumulator
-// holds four consecutive channels of one pixel (one 8-byte store per block). Data gradient (FLIP): dy
-// through the CRSK copy with the taps mirrored, dx[p] = sum dy[p + t - 1] w[8 - t]. ResNet-50 stage 1
-// (tools/conv_bench.py): forward 105.9 -> 66.2 us, data gradient 115.3 -> 80.7 us; step 20.25 -> 20.03 ms.
+// six input rows (four output rows and their halo, 58 pixel slots per row: the halo columns and rows
+// outside the image zero-filled by the DMA; 44 KB each, 160 KB in all), so each input element is loaded
+// 1.5 times and every tap reads it from LDS. Seven waves: wave w owns 16-pixel blocks 2w, 2w + 1 of the
+// band's 4 W <= 224 pixels, all 64 output channels (per (tap, k-step) 6 fragment reads for 8 MFMAs, the
+// next step's reads issued before this step's MFMAs); the MFMA operands are swapped so a lane's
+// accumulator holds four consecutive channels of one pixel (one 8-byte store per block). Data gradient
+// (FLIP): dy through the CRSK copy with the taps mirrored, dx[p] = sum dy[p + t - 1] w[8 - t]. ResNet-50
+// stage 1 (tools/conv_bench.py, same box): forward 113.7 -> 63.7 us, data gradient 123.4 -> 77.9 us.
 struct BandArgs {
   const float *in_sc, *in_sh;  // (XF) the producing BatchNorm+ReLU, applied to the landed band
   const void* x;  // [N][H][W][64] bf16
@@ -3695,13 +3695,15 @@ struct BandArgs {
   void* y;        // [N][H][W][64] bf16
   int N, H, W, hb, nbands, x_bytes, y_bytes;
 };
-constexpr int kBandBytes = 4 * 64 * 128;  // one band buffer: 4 rows x 64 pixel slots x 64 channels
+constexpr int kBandSlots = 58;                     // pixel slots per band row (W + 2 halo columns, W <= 56)
+constexpr int kBandRows = 6;                       // 4 output rows + the halo rows
+constexpr int kBandChunks = 2816;                  // 16-byte chunks per buffer (6 x 58 x 8 = 2784, rounded
+constexpr int kBandBytes = kBandChunks * 16;       // up to whole 64-lane DMA instructions: 44)
 template <int FLIP, int XF = 0>
 __global__ __launch_bounds__(448, 1) void conv3x3c64_band_kernel(BandArgs p) {
   static_assert(!(FLIP && XF), "the input transform is a forward one");
-  __shared__ __attribute__((aligned(16))) uint4 smem[(2 * kBandBytes + 9 * 64 * 128) / 16];
-  __shared__ __attribute__((aligned(16))) float xtab[XF ? 128 : 4];  // (XF) scale[64], shift[64]
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;  // 7 waves: wave w = pixel block w
+  __shared__ __attribute__((aligned(16))) uint4 smem[(2 * kBandBytes + 9 * 64 * 128) / 16];  // = 160 KB
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;  // 7 waves: wave w = pixel blocks 2w, 2w + 1
   const v4i rs_x = make_rsrc(p.x, (uint32_t)p.x_bytes);
   const v4i rs_w = make_rsrc(p.w, 64 * 9 * 64 * 2);
   const __amdgpu_buffer_rsrc_t rs_y = __builtin_amdgcn_make_buffer_rsrc(p.y, (short)0, p.y_bytes, 0x00020000);
@@ -3718,81 +3720,86 @@ __global__ __launch_bounds__(448, 1) void conv3x3c64_band_kernel(BandArgs p) {
       dma16_asm(rs_w, lds0 + kW + ins * 1024, (uint32_t)(((o * 9 + (FLIP ? 8 - tap : tap)) * 64 + logical * 8) * 2));
     }
   }
-  // band b -> buffer bb (32 pieces over waves 0-3): slot (row br, column bc) holds input row h0 - 1 + br,
-  // column bc - 1
+  // band b -> buffer bb (44 pieces over waves 0-3): slot (row br, column bc) holds input row h0 - 1 + br,
+  // column bc - 1, its chunk phys holding channel chunk phys ^ (slot & 7)
   auto issue_band = [&](int b, int bb) __attribute__((always_inline)) {
     if (wid >= 4) return;
-    const int n = b / p.hb, h0 = (b - n * p.hb) * 2;
+    const int n = b / p.hb, h0 = (b - n * p.hb) * 4;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int ins = wid * 8 + j, chunk = ins * 64 + lane;
-      const int pix = chunk >> 3, br = pix >> 6, bc = pix & 63;
+    for (int j = 0; j < 11; ++j) {
+      const int ins = wid * 11 + j, chunk = ins * 64 + lane;
+      const int pix = chunk >> 3, br = pix / kBandSlots, bc = pix - br * kBandSlots;
       const int h = h0 - 1 + br, wc = bc - 1;
       const int logical = (chunk & 7) ^ (pix & 7);
-      const bool ok = (unsigned)h < (unsigned)p.H && (unsigned)wc < (unsigned)p.W;
+      const bool ok = br < kBandRows && (unsigned)h < (unsigned)p.H && (unsigned)wc < (unsigned)p.W;
       dma16_asm(rs_x, lds0 + bb * kBandBytes + ins * 1024,
                 ok ? (uint32_t)((((n * p.H + h) * p.W + wc) * 64 + logical * 8) * 2) : kOob);
     }
   };
-  // this lane's output pixel wid * 16 + (lane & 15) = (orow, ocol); for tap (r, s) its input sits in slot
-  // (orow + r, ocol + s), at byte ab[s] + r * 8192 (+ 64 for k-step 1); weight block j at wbj[j] + tap * 8192
+  // this lane's output pixels bk * 16 + (lane & 15) (bk = 2 wid + i) = (orow, ocol); for tap (r, s) the
+  // input sits in slot (orow + r) * 58 + ocol + s, at byte ab[i][r][s] (+ 64 for k-step 1); weight block j
+  // at wbj[j] + tap * 8192
   const int q = lane >> 4, c = lane & 15;
-  const int pp = wid * 16 + c;
-  const int orow = pp >= p.W ? 1 : 0, ocol = pp - orow * p.W;
-  int ab[3], wbj[4];
+  int ab[2][3][3], orow[2], ocol[2], pp[2];
 #pragma unroll
-  for (int sx = 0; sx < 3; ++sx) {
-    const int col = min(ocol + sx, 63);
-    ab[sx] = orow * 8192 + col * 128 + ((q ^ (col & 7)) << 4);
+  for (int i = 0; i < 2; ++i) {
+    pp[i] = (2 * wid + i) * 16 + c;
+    orow[i] = min(pp[i] / p.W, 3);
+    ocol[i] = pp[i] - orow[i] * p.W;
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int sx = 0; sx < 3; ++sx) {
+        const int slot = min((orow[i] + r) * kBandSlots + min(ocol[i] + sx, kBandSlots - 1), kBandRows * kBandSlots - 1);
+        ab[i][r][sx] = slot * 128 + ((q ^ (slot & 7)) << 4);
+      }
   }
+  int wbj[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int o = j * 16 + c;
     wbj[j] = (int)kW + o * 128 + ((q ^ (o & 7)) << 4);
   }
   const char* lds = reinterpret_cast<const char*>(smem);
-  if constexpr (XF) {
-    if (tid < 64) {
-      xtab[tid] = p.in_sc[tid];
-      xtab[64 + tid] = p.in_sh[tid];
-    }
-  }
   int it = 0;
   int b = blockIdx.x;
   if (b < p.nbands) issue_band(b, 0);
   for (; b < p.nbands; b += gridDim.x, ++it) {
     const int bb = it & 1;
     if (it == 0) wait_vmcnt<0>();
-    else wait_vmcnt<4>();  // (the previous band's 4 stores may stay in flight)
+    else wait_vmcnt<8>();  // (the previous band's 8 stores may stay in flight)
     __syncthreads();       // the band has landed for every wave; every wave is done with the other buffer
+    const int n = b / p.hb, h0 = (b - n * p.hb) * 4;
     if constexpr (XF) {
       // max(x * sc + sh, 0) rounded to bf16 in place, as bn_apply_kernel stores it; the zero halo (the
       // convolution pads the activation) stays zero
-      const int n = b / p.hb, h0 = (b - n * p.hb) * 2;
       uint4* band = smem + bb * (kBandBytes / 16);
-      for (int i = tid; i < kBandBytes / 16; i += 448) {
-        const int pix = i >> 3, br = pix >> 6, bc = pix & 63;
+      for (int i = tid; i < kBandRows * kBandSlots * 8; i += 448) {
+        const int pix = i >> 3, br = pix / kBandSlots, bc = pix - br * kBandSlots;
         if ((unsigned)(h0 - 1 + br) >= (unsigned)p.H || (unsigned)(bc - 1) >= (unsigned)p.W) continue;
         const int ch = ((i & 7) ^ (pix & 7)) * 8;
         float f[8];
         chunk_to_f(band[i], f, (const bf16_t*)nullptr);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], xtab[ch + e], xtab[64 + ch + e]), 0.f);
+        for (int e = 0; e < 8; ++e) f[e] = fmaxf(fmaf(f[e], p.in_sc[ch + e], p.in_sh[ch + e]), 0.f);
         band[i] = f_to_chunk(f, (const bf16_t*)nullptr);
       }
       __syncthreads();
     }
     if (b + (int)gridDim.x < p.nbands) issue_band(b + gridDim.x, bb ^ 1);
-    v4f acc[4];
+    v4f acc[2][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = v4f{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
     const int boff = bb * kBandBytes;
-    // 18 steps (tap, k-step), each 5 fragment reads (1 pixel block, 4 weight blocks) for 4 MFMAs; step i + 1's
+    // 18 steps (tap, k-step), each 6 fragment reads (2 pixel blocks, 4 weight blocks) for 8 MFMAs; step i + 1's
     // reads are issued before step i's MFMAs
-    uint4 fa[2], fb[2][4];
+    uint4 fa[2][2], fb[2][4];
     auto ld = [&](int step, int slot) __attribute__((always_inline)) {
       const int t = step >> 1, ks = step & 1, r = t / 3, sx = t % 3;
-      fa[slot] = *reinterpret_cast<const uint4*>(lds + boff + ((ab[sx] + r * 8192) ^ (ks * 64)));
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[slot][i] = *reinterpret_cast<const uint4*>(lds + boff + (ab[i][r][sx] ^ (ks * 64)));
 #pragma unroll
       for (int j = 0; j < 4; ++j) fb[slot][j] = *reinterpret_cast<const uint4*>(lds + ((wbj[j] + t * 8192) ^ (ks * 64)));
     };
@@ -3802,21 +3809,25 @@ __global__ __launch_bounds__(448, 1) void conv3x3c64_band_kernel(BandArgs p) {
       if (step + 1 < 18) ld(step + 1, (step + 1) & 1);
       __builtin_amdgcn_sched_barrier(0);  // (hipcc otherwise sinks every read next to its MFMA)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        mfma_slab<bf16_t>(acc[j], fb[step & 1][j], fa[step & 1]);  // (swapped: lane = pixel, 4 channels)
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          mfma_slab<bf16_t>(acc[i][j], fb[step & 1][j], fa[step & 1][i]);  // (swapped: lane = pixel, 4 channels)
       __builtin_amdgcn_sched_barrier(0);
     }
-    const int n = b / p.hb, h0 = (b - n * p.hb) * 2;
-    const int h = h0 + orow;
-    const bool ok = pp < 2 * p.W && h < p.H;
-    const int obase = (((n * p.H + h) * p.W + ocol) * 64 + 4 * q) * 2;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t lo = (uint32_t)f2bf(acc[j][0]) | ((uint32_t)f2bf(acc[j][1]) << 16);
-      const uint32_t hi = (uint32_t)f2bf(acc[j][2]) | ((uint32_t)f2bf(acc[j][3]) << 16);
-      const uint32_t voff = ok ? (uint32_t)(obase + j * 32) : 0x80000000u;
-      typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-      __builtin_amdgcn_raw_buffer_store_b64(u32x2{lo, hi}, rs_y, voff, 0, 0);
+    for (int i = 0; i < 2; ++i) {
+      const int h = h0 + orow[i];
+      const bool ok = pp[i] < 4 * p.W && h < p.H;
+      const int obase = (((n * p.H + h) * p.W + ocol[i]) * 64 + 4 * q) * 2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t lo = (uint32_t)f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
+        const uint32_t hi = (uint32_t)f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
+        const uint32_t voff = ok ? (uint32_t)(obase + j * 32) : 0x80000000u;
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{lo, hi}, rs_y, voff, 0, 0);
+      }
     }
   }
 }
@@ -3882,7 +3893,7 @@ int band_launch(const rn_conv_desc* d, const void* x, const void* w, void* y, in
                 const float* in_sc = nullptr, const float* in_sh = nullptr) {
   BandArgs a{};
   a.x = x; a.w = w; a.y = y; a.in_sc = in_sc; a.in_sh = in_sh;
-  a.N = d->n; a.H = d->h; a.W = d->w; a.hb = (d->h + 1) / 2; a.nbands = d->n * a.hb;
+  a.N = d->n; a.H = d->h; a.W = d->w; a.hb = (d->h + 3) / 4; a.nbands = d->n * a.hb;
   a.x_bytes = a.y_bytes = d->n * d->h * d->w * 64 * 2;
   const dim3 grid((unsigned)std::min(a.nbands, chip_cus()));
   if (flip) hipLaunchKernelGGL(conv3x3c64_band_kernel<1>, grid, dim3(448), 0, st, a);
