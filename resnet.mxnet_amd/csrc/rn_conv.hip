@@ -3832,6 +3832,126 @@ __global__ __launch_bounds__(448, 1) void conv3x3c64_band_kernel(BandArgs p) {
   }
 }
 
+// The int8 forward of the same layer (symbol/resnet_int8.py: the quantized stage-1 conv2): x and the
+// weights as int8 codes (64-byte pixel slots, one 16x16x64 i8 MFMA k-step per tap), y = unit_x * unit_w *
+// the exact int32 sums (igemm_big_kernel Q8's epilogue, so bit-identical to it). 80 KB of LDS: two
+// workgroups per CU. 64-byte slots: chunk phys of slot s holds channel chunk phys ^ ((s >> 1) & 3).
+constexpr int kBand8Chunks = 1408;  // 6 x 58 x 4 = 1392, rounded up to 22 whole 64-lane DMA instructions
+constexpr int kBand8Bytes = kBand8Chunks * 16;
+struct Band8Args {
+  const void* x;  // [N][H][W][64] int8 codes
+  const void* w;  // [64][9][64] int8 codes
+  void* y;        // [N][H][W][64] bf16
+  const float *ux, *uw;
+  int N, H, W, hb, nbands, x_bytes, y_bytes;
+};
+__global__ __launch_bounds__(448, 2) void conv3x3c64_band_i8_kernel(Band8Args p) {
+  __shared__ __attribute__((aligned(16))) uint4 smem[(2 * kBand8Bytes + 9 * 64 * 64) / 16];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const v4i rs_x = make_rsrc(p.x, (uint32_t)p.x_bytes);
+  const v4i rs_w = make_rsrc(p.w, 64 * 9 * 64);
+  const __amdgpu_buffer_rsrc_t rs_y = __builtin_amdgcn_make_buffer_rsrc(p.y, (short)0, p.y_bytes, 0x00020000);
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  constexpr uint32_t kW = 2 * kBand8Bytes;
+  if (wid < 6) {  // 576 rows (tap, out) x 4 chunks = 36 pieces over waves 0-5
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int ins = wid * 6 + j, chunk = ins * 64 + lane;
+      const int row = chunk >> 2, tap = row >> 6, o = row & 63;
+      const int logical = (chunk & 3) ^ ((row >> 1) & 3);
+      dma16_asm(rs_w, lds0 + kW + ins * 1024, (uint32_t)((o * 9 + tap) * 64 + logical * 16));
+    }
+  }
+  auto issue_band = [&](int b, int bb) __attribute__((always_inline)) {
+    if (wid >= 2) return;  // 22 pieces over waves 0-1
+    const int n = b / p.hb, h0 = (b - n * p.hb) * 4;
+#pragma unroll
+    for (int j = 0; j < 11; ++j) {
+      const int ins = wid * 11 + j, chunk = ins * 64 + lane;
+      const int pix = chunk >> 2, br = pix / kBandSlots, bc = pix - br * kBandSlots;
+      const int h = h0 - 1 + br, wc = bc - 1;
+      const int logical = (chunk & 3) ^ ((pix >> 1) & 3);
+      const bool ok = br < kBandRows && (unsigned)h < (unsigned)p.H && (unsigned)wc < (unsigned)p.W;
+      dma16_asm(rs_x, lds0 + bb * kBand8Bytes + ins * 1024,
+                ok ? (uint32_t)(((n * p.H + h) * p.W + wc) * 64 + logical * 16) : kOob);
+    }
+  };
+  const int q = lane >> 4, c = lane & 15;
+  int ab[2][9], orow[2], ocol[2], pp[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    pp[i] = (2 * wid + i) * 16 + c;
+    orow[i] = min(pp[i] / p.W, 3);
+    ocol[i] = pp[i] - orow[i] * p.W;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int slot = min((orow[i] + t / 3) * kBandSlots + min(ocol[i] + t % 3, kBandSlots - 1), kBandRows * kBandSlots - 1);
+      ab[i][t] = slot * 64 + ((q ^ ((slot >> 1) & 3)) << 4);
+    }
+  }
+  int wbj[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int o = j * 16 + c;
+    wbj[j] = (int)kW + o * 64 + ((q ^ ((o >> 1) & 3)) << 4);  // + tap * 4096
+  }
+  const float qs = *p.ux * *p.uw;
+  const char* lds = reinterpret_cast<const char*>(smem);
+  int it = 0;
+  int b = blockIdx.x;
+  if (b < p.nbands) issue_band(b, 0);
+  for (; b < p.nbands; b += gridDim.x, ++it) {
+    const int bb = it & 1;
+    if (it == 0) wait_vmcnt<0>();
+    else wait_vmcnt<8>();
+    __syncthreads();
+    if (b + (int)gridDim.x < p.nbands) issue_band(b + gridDim.x, bb ^ 1);
+    v4i acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = v4i{0, 0, 0, 0};
+    const int boff = bb * kBand8Bytes;
+    uint4 fa[2][2], fb[2][4];
+    auto ld = [&](int t, int slot) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) fa[slot][i] = *reinterpret_cast<const uint4*>(lds + boff + ab[i][t]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[slot][j] = *reinterpret_cast<const uint4*>(lds + wbj[j] + t * 4096);
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      if (t + 1 < 9) ld(t + 1, (t + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint4 a8 = fb[t & 1][j], b8 = fa[t & 1][i];
+          acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(*reinterpret_cast<const v4i*>(&a8),
+                                                             *reinterpret_cast<const v4i*>(&b8), acc[i][j], 0, 0, 0);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int n = b / p.hb, h0 = (b - n * p.hb) * 4;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int h = h0 + orow[i];
+      const bool ok = pp[i] < 4 * p.W && h < p.H;
+      const int obase = (((n * p.H + h) * p.W + ocol[i]) * 64 + 4 * q) * 2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t lo = (uint32_t)f2bf((float)acc[i][j][0] * qs) | ((uint32_t)f2bf((float)acc[i][j][1] * qs) << 16);
+        const uint32_t hi = (uint32_t)f2bf((float)acc[i][j][2] * qs) | ((uint32_t)f2bf((float)acc[i][j][3] * qs) << 16);
+        const uint32_t voff = ok ? (uint32_t)(obase + j * 32) : 0x80000000u;
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{lo, hi}, rs_y, voff, 0, 0);
+      }
+    }
+  }
+}
+
 // geometry of a direct grouped launch (mode 0 forward, 1 data gradient): fills a's shape fields,
 // returns the workgroups (also the BatchNorm-reduction partials of a RED data gradient)
 int gd_geometry(const rn_conv_desc* d, int mode, GdArgs& a) {
@@ -3992,6 +4112,16 @@ int rn_conv_fwd_i8_mm(const rn_conv_desc* d, const void* x_codes, const void* w_
   RN_CHECK_ARG(d->groups <= 1, "int8 convolution is dense");
   RN_CHECK_ARG(y_dtype == RN_BF16 || y_dtype == RN_F32, "bad output dtype");
   RN_CHECK_ARG(!part || d->k % 8 == 0, "BatchNorm statistics need whole 8-channel chunks");
+  if (band_ok(d) && !add_src && !part && !part_mm && y_dtype == RN_BF16) {  // (image bands, int8 codes)
+    Band8Args b{};
+    b.x = x_codes; b.w = w_codes; b.y = y; b.ux = x_unit; b.uw = w_unit;
+    b.N = d->n; b.H = d->h; b.W = d->w; b.hb = (d->h + 3) / 4; b.nbands = d->n * b.hb;
+    b.x_bytes = d->n * d->h * d->w * 64;
+    b.y_bytes = d->n * d->h * d->w * 64 * 2;
+    const dim3 grid((unsigned)std::min(b.nbands, 2 * chip_cus()));
+    hipLaunchKernelGGL(conv3x3c64_band_i8_kernel, grid, dim3(448), 0, as_stream(stream), b);
+    return rn_check_launch("conv3x3c64_band_i8");
+  }
   IgemmArgs a = make_igemm_args(d, 0);
   a.smallc = 0;
   a.x = x_codes; a.w = w_codes; a.y = y; a.add = add_src; a.bias = nullptr; a.stats = part; a.stats_mm = part_mm;

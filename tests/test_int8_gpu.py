@@ -503,3 +503,28 @@ def test_weight_quant_pack_batched_multistep(gpu, monkeypatch):
         np.testing.assert_array_equal(m1[k], m0[k], err_msg=k)
     for a, b in zip(p1, p0):
         np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.parametrize("case", [
+    (3, 64, 56, 56, 64, 3, 1, 1),      # the quantized stage-1 conv2 (several bands per workgroup)
+    (5, 64, 9, 13, 64, 3, 1, 1),       # a last band of one output row
+    (1, 64, 7, 7, 64, 3, 1, 1),        # fewer pixels than one band
+    (40, 64, 20, 56, 64, 3, 1, 1),     # the widest row, many bands per workgroup
+])
+def test_int8_conv3x3_band(gpu, case):
+    """conv3x3c64_band_i8_kernel (the int8 image-band forward of a 3x3 / stride-1 / pad-1 64 -> 64
+    layer, default; rn_set_tuning 26 = 1 the int8 implicit-GEMM tile): exact integer sums (f32 path of the
+    tile vs the oracle) and the bf16 output bit-identical to the tile's, both scaling the same int32 sums."""
+    n, c, h, w, k, r, st, pd = case
+    ux, uw = 0.0123, 0.00071
+    outs = []
+    try:
+        for mode in (0, 1):
+            L.call("rn_set_tuning", 26, mode)
+            _, y, exact = _run(gpu, case, BF16, ux, uw)
+            outs.append(y)
+    finally:
+        L.call("rn_set_tuning", 26, 0)
+    np.testing.assert_array_equal(outs[0], outs[1])
+    ref = exact * (np.float64(np.float32(ux)) * np.float64(np.float32(uw)))
+    assert rel_err(outs[0], ref) < 2 ** -8
