@@ -1978,6 +1978,15 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
 // and ran at 6x these layers' memory time. 8 waves, wave (wk, wc) owns KB_W x CB_W 16-channel block
 // pairs over all 9 taps (18 accumulators). Each workgroup stores its partial dW slice into the slab
 // [split][K][9][C]; the split reduction pass sums them (deterministic order).
+// The stream and band weight-gradient kernels' LDS swizzle: swz_tr, except for 8-chunk (128-byte, 64-channel) rows. A transposed
+// 64-bit read's 32-lane group covers rows 8 g + 4 h + q (g = 0, 1; q = 0..3) at two chunks each; with
+// 128-byte rows a row's bank half is row & 1, and swz_tr & 7 = 2 q drops g, so rows r and r + 8 hit the
+// same banks (2-way: PMC 0.288 of the kernel's LDS cycles were conflicts on ResNet-50's 64-channel
+// layers, profiles/r04/pmc_summary_resnet50_final.txt). Here the chunk pair of a row is 2 ((q >> 1) | 2 g):
+// with q & 1 picking the bank half, the 8 rows x 2 chunks cover 16 distinct 16-byte bank groups.
+__device__ __forceinline__ int swz_st(int row, int cpr) {
+  return cpr == 8 ? 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) : swz_tr(row);
+}
 struct DbArgs {
   const bf16_t* x;   // [N][H][W][C]
   const bf16_t* dy;  // [N][H][W][K]
@@ -2040,7 +2049,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_dband_kernel(DbArgs p) {
     const int px = isx ? piece * S::XPPI + lane / XCPR : (piece - S::XINS) * S::DPPI + lane / DCPR;
     dr[j] = isx ? px / WP : -1 - px / WP;  // (dy pieces: -1 - row)
     dc[j] = px % WP;
-    dch[j] = (isx ? c0 : k0) + 8 * ((lane % cpr) ^ (swz_tr(px) & (cpr - 1)));
+    dch[j] = (isx ? c0 : k0) + 8 * ((lane % cpr) ^ (swz_st(px, cpr) & (cpr - 1)));
     dla[j] = isx ? piece * 1024 : S::XBYTES + (piece - S::XINS) * 1024;
   }
   const char* zb = reinterpret_cast<const char*>(&g_zero_chunk);
@@ -2083,7 +2092,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_dband_kernel(DbArgs p) {
   // transposed 8-byte read of the 4 x 4 block at (pixel row, element column col) of an image with cpr
   // 16-byte chunks per pixel
   auto rd = [&](const char* img, int cpr, int row, int col) __attribute__((always_inline)) {
-    const int byte = row * (cpr * 16) + ((((col * 2) >> 4) ^ (swz_tr(row) & (cpr - 1))) << 4) + ((col * 2) & 15);
+    const int byte = row * (cpr * 16) + ((((col * 2) >> 4) ^ (swz_st(row, cpr) & (cpr - 1))) << 4) + ((col * 2) & 15);
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(img + byte));
   };
   auto compute = [&](int buf) __attribute__((always_inline)) {
@@ -2321,15 +2330,6 @@ constexpr int stream_wk(int kb, int cb) {  // waves along K (of 8) minimizing th
     if (kb / wk + cb / wc < cost) cost = kb / wk + cb / wc, best = wk;
   }
   return best;
-}
-// The stream kernel's LDS swizzle: swz_tr, except for 8-chunk (128-byte, 64-channel) rows. A transposed
-// 64-bit read's 32-lane group covers rows 8 g + 4 h + q (g = 0, 1; q = 0..3) at two chunks each; with
-// 128-byte rows a row's bank half is row & 1, and swz_tr & 7 = 2 q drops g, so rows r and r + 8 hit the
-// same banks (2-way: PMC 0.288 of the kernel's LDS cycles were conflicts on ResNet-50's 64-channel
-// layers, profiles/r04/pmc_summary_resnet50_final.txt). Here the chunk pair of a row is 2 ((q >> 1) | 2 g):
-// with q & 1 picking the bank half, the 8 rows x 2 chunks cover 16 distinct 16-byte bank groups.
-__device__ __forceinline__ int swz_st(int row, int cpr) {
-  return cpr == 8 ? 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1)) : swz_tr(row);
 }
 template <int K, int C, int XF, int NBUF, int I8X = 0>
 __global__ __launch_bounds__(512, 1) void wgrad_stream_kernel(WgradArgs p) {
