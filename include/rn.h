@@ -645,6 +645,11 @@ const char* rn_last_error(void);
  *      within 2^-21 |v / unit| of a half-integer -- the same codes bit for bit, fewer instructions). */
 int rn_set_tuning(int32_t key, int32_t value);
 int32_t rn_version(void);
+/* Build id baked in at compile time: a hash of the sources (csrc/*.hip, csrc/*.h, include/rn.h) and the
+ * compiler flags this library was built from (rn/build.py: source_hash). The host refuses to run a library
+ * whose id differs from the tree's, so a stale prebuilt cannot be tested silently. Same role as the
+ * reference's pin to one MXNet fork build (README.md:7). */
+const char* rn_build_id(void);
 /* Number of compute units of the current device (for split heuristics / reporting). */
 int32_t rn_device_cu_count(void);
 

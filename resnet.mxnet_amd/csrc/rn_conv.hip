@@ -1417,7 +1417,7 @@ struct WgradArgs {
   int grouped, gk, gc, cblk;  // grouped: rows / channels per group, channels per row block
   int creal;                  // logical input channels (< C: padded stride, dw keeps c < creal)
   int nct, nkt;               // column tiles, k tiles (grid = splits * nkt * nct)
-  int diag_noepi;             // diagnostic (rn_set_tuning 6): skip the dW epilogue (wrong results)
+  int diag_noepi;             // diagnostic (rn_set_tuning 6, bits): 1 skip the dW epilogue, 2 / 4 (wgrad_big_kernel) no loop DMAs / waits
   int p4;                     // the stem's padded NHWC4 image (rn_stem_prepare_p4): column = (r*8 + s)*4 + c,
                               // r, s < 8; dW keeps r < R, s < S, c < creal ([K][R][S][creal])
   int gspread;                // (gdiag) the diagonal blocks spread over all four waves
@@ -1674,7 +1674,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
   }
 
   // epilogue: D[row = k][col] -> atomic add into dw
-  if (kRnDiag && p.diag_noepi) {  // keep the accumulators live without touching memory
+  if (kRnDiag && (p.diag_noepi & 1)) {  // keep the accumulators live without touching memory
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -1894,23 +1894,36 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
   };
 
   const int nstage = (mend - mbeg + BKM - 1) / BKM;
+  // diagnostic build only (rn_set_tuning 6, bit mask; wrong results): 1 no dW epilogue, 2 no DMAs inside
+  // the loop (the prologue's buffers are re-read), 4 no M-tile waits / barriers
+  const int diag = kRnDiag ? p.diag_noepi : 0;
 #pragma unroll
   for (int s = 0; s < NBUF - 1; ++s) issue(mbeg + s * BKM, s);
   for (int t = 0; t < nstage; ++t) {
-    if (NBUF == 3) wait_vmcnt<LPT>();  // the later M-tile's DMAs (real or past the range) may stay in flight
-    else wait_vmcnt<0>();
-    __syncthreads();
+    if (!(diag & 4)) {
+      if (NBUF == 3) wait_vmcnt<LPT>();  // the later M-tile's DMAs (real or past the range) may stay in flight
+      else wait_vmcnt<0>();
+      __syncthreads();
+    }
     compute(t % NBUF, 0);
     // unconditional (past the range every lane reads the zero chunk into a buffer nobody reads):
     // no branch, so the address arithmetic can interleave with slab 0's MFMAs
-    issue(mbeg + (t + NBUF - 1) * BKM, (t + NBUF - 1) % NBUF);
+    if (!(diag & 2)) issue(mbeg + (t + NBUF - 1) * BKM, (t + NBUF - 1) % NBUF);
     compute(t % NBUF, 1);
   }
   wait_vmcnt<0>();
 
   // D[row = k][col] -> fp32 atomic add into dw (dense, unpadded: ldw = ncol); padded channels (the
   // stem's 3 of 8) keep c < creal
-  if (kRnDiag && p.diag_noepi) return;  // diagnostic (rn_set_tuning 6): no dW epilogue (wrong results)
+  if (kRnDiag && (diag & 1)) {  // keep the accumulators live without touching memory
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+    if (s == 12345.678f) p.dw[0] = s;
+    return;
+  }
   if constexpr (I8X) {  // dW = unit * sum dy * code
     const float u = *p.xunit;
 #pragma unroll
@@ -1978,7 +1991,10 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
 // and ran at 6x these layers' memory time. 8 waves, wave (wk, wc) owns KB_W x CB_W 16-channel block
 // pairs over all 9 taps (18 accumulators). Each workgroup stores its partial dW slice into the slab
 // [split][K][9][C]; the split reduction pass sums them (deterministic order).
-// The stream and band weight-gradient kernels' LDS swizzle: swz_tr, except for 8-chunk (128-byte, 64-channel) rows. A transposed
+// The stream weight-gradient kernel's LDS swizzle: swz_tr, except for 8-chunk (128-byte, 64-channel) rows.
+// (The image-band weight gradient keeps swz_tr: this swizzle made its LDS conflict-free there too, 0.500 ->
+// 0.000, but measured 1.9 % slower in isolation and neutral in-step -- round 5, profiles/r05/ab/dband_swz --
+// so it was reverted in round 6: that kernel is not LDS-bound.) A transposed
 // 64-bit read's 32-lane group covers rows 8 g + 4 h + q (g = 0, 1; q = 0..3) at two chunks each; with
 // 128-byte rows a row's bank half is row & 1, and swz_tr & 7 = 2 q drops g, so rows r and r + 8 hit the
 // same banks (2-way: PMC 0.288 of the kernel's LDS cycles were conflicts on ResNet-50's 64-channel
@@ -2049,7 +2065,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_dband_kernel(DbArgs p) {
     const int px = isx ? piece * S::XPPI + lane / XCPR : (piece - S::XINS) * S::DPPI + lane / DCPR;
     dr[j] = isx ? px / WP : -1 - px / WP;  // (dy pieces: -1 - row)
     dc[j] = px % WP;
-    dch[j] = (isx ? c0 : k0) + 8 * ((lane % cpr) ^ (swz_st(px, cpr) & (cpr - 1)));
+    dch[j] = (isx ? c0 : k0) + 8 * ((lane % cpr) ^ (swz_tr(px) & (cpr - 1)));
     dla[j] = isx ? piece * 1024 : S::XBYTES + (piece - S::XINS) * 1024;
   }
   const char* zb = reinterpret_cast<const char*>(&g_zero_chunk);
@@ -2092,7 +2108,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_dband_kernel(DbArgs p) {
   // transposed 8-byte read of the 4 x 4 block at (pixel row, element column col) of an image with cpr
   // 16-byte chunks per pixel
   auto rd = [&](const char* img, int cpr, int row, int col) __attribute__((always_inline)) {
-    const int byte = row * (cpr * 16) + ((((col * 2) >> 4) ^ (swz_st(row, cpr) & (cpr - 1))) << 4) + ((col * 2) & 15);
+    const int byte = row * (cpr * 16) + ((((col * 2) >> 4) ^ (swz_tr(row) & (cpr - 1))) << 4) + ((col * 2) & 15);
     return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) v4s*)(img + byte));
   };
   auto compute = [&](int buf) __attribute__((always_inline)) {
@@ -2540,14 +2556,14 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_few_kernel(const float*
   for (int z = 0; z < 16; ++z)
     if (z < nsplit) v[z] = s4[(int64_t)z * n4 + col];
   float4 t = reinterpret_cast<const float4*>(dw)[col];
+  // each split as (0 + v), as the general kernel's group sum forms it: a -0 split adds +0, so the zero
+  // sign of the result matches for every nsplit <= 16 (its empty groups then add +0 to an already
+  // sign-normalised sum)
 #pragma unroll
   for (int z = 0; z < 16; ++z)
     if (z < nsplit) {
-      t.x += v[z].x; t.y += v[z].y; t.z += v[z].z; t.w += v[z].w;
+      t.x += 0.f + v[z].x; t.y += 0.f + v[z].y; t.z += 0.f + v[z].z; t.w += 0.f + v[z].w;
     }
-  if (nsplit < 16) {
-    t.x += 0.f; t.y += 0.f; t.z += 0.f; t.w += 0.f;
-  }
   reinterpret_cast<float4*>(dw)[col] = t;
 }
 

@@ -824,6 +824,12 @@ int rn_set_tuning(int32_t key, int32_t value) {
   return 0;
 }
 int32_t rn_version(void) { return 100; }
+#ifndef RN_BUILD_ID
+#define RN_BUILD_ID "unknown"
+#endif
+// the marker prefix lets rn/build.py read the id from the file without loading it
+static const char kBuildIdMarker[] = "RN_BUILD_ID=" RN_BUILD_ID;
+const char* rn_build_id(void) { return kBuildIdMarker + 12; }
 int32_t rn_device_cu_count(void) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return -1;

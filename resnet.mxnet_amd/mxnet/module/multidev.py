@@ -112,6 +112,10 @@ class _Worker:
         ex = self.mod.executor
         return {n: ex.get_param(n, grad=True) for n in ex.plan.param_names}
 
+    def env(self, name):
+        """The worker's own environment value (tests: the hardware-queue count rn/__init__ chose)."""
+        return os.environ.get(name)
+
     def input_slice(self):
         ex = self.mod.executor
         return ex._in_bufs[ex._in_idx].detach().cpu().numpy().copy()
@@ -162,18 +166,38 @@ class DeviceGroup:
     def __init__(self, symbol, contexts, names, precision):
         import torch.multiprocessing as mp
         ids = [c.device_id for c in contexts]
-        backend = os.environ.get("RN_DIST_BACKEND") or ("gloo" if dry_run() or len(set(ids)) < len(ids) else "nccl")
+        shared = len(set(ids)) < len(ids)
+        backend = os.environ.get("RN_DIST_BACKEND") or ("gloo" if dry_run() or shared else "nccl")
         ctx = mp.get_context("spawn")
         port = _free_port()
         env = {k: v for k, v in os.environ.items() if k.startswith(("RN_", "HSA_", "HIP_", "NCCL_", "RCCL_"))}
+        # A spawned worker imports rn (rn/__init__.py sets GPU_MAX_HW_QUEUES) while unpickling its target,
+        # before _worker_main applies `env`: what it must see then is set in os.environ around p.start()
+        # (spawn copies the parent's environment at that moment). Ranks sharing one GPU keep HIP's 4
+        # hardware queues -- 8 per process oversubscribe the queue slots there (rn/__init__.py) -- and the
+        # parent's own GPU_MAX_HW_QUEUES (raised to 8 by its `import rn`) must not leak into them.
+        # (explicit for distinct devices too: the worker may import rn only after it has set WORLD_SIZE, and
+        # a gloo backend over distinct GPUs is not a shared GPU)
+        start_env = ({"RN_HW_QUEUES": "4", "GPU_MAX_HW_QUEUES": "4"} if shared
+                     else {"RN_HW_QUEUES": os.environ.get("RN_HW_QUEUES", "8")})
+        env.update(RN_HW_QUEUES=start_env["RN_HW_QUEUES"])
+        saved = {k: os.environ.get(k) for k in start_env}
         self.conns, self.procs = [], []
-        for r in range(len(ids)):
-            a, b = ctx.Pipe()
-            p = ctx.Process(target=_worker_main, args=(r, len(ids), port, ids, symbol.tojson(), names, precision,
-                                                       backend, env, b), daemon=True)
-            p.start()
-            self.conns.append(a)
-            self.procs.append(p)
+        try:
+            os.environ.update(start_env)
+            for r in range(len(ids)):
+                a, b = ctx.Pipe()
+                p = ctx.Process(target=_worker_main, args=(r, len(ids), port, ids, symbol.tojson(), names, precision,
+                                                           backend, env, b), daemon=True)
+                p.start()
+                self.conns.append(a)
+                self.procs.append(p)
+        finally:
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
         self.backend = backend
         self._collect()  # every worker initialised its process group
         atexit.register(self.close)

@@ -2,9 +2,13 @@
 
 Each csrc/*.hip is compiled to an object in parallel with hipcc, then linked into
 resnet.mxnet_amd/rn/librn.so. The .so is git-ignored but travels to the GPU box with the
-gpurun snapshot. Rebuilds only when a source or header is newer than the library.
+gpurun snapshot. The library carries a build id -- a hash of the sources, include/rn.h and the compiler
+flags (source_hash) -- baked in with -DRN_BUILD_ID and exported as rn_build_id(); it is rebuilt whenever
+that id differs from the tree's, and rn.lib.load() refuses a library whose id does not match (a stale
+prebuilt after a checkout or copy fails loudly instead of being tested silently).
 """
 import concurrent.futures as cf
+import hashlib
 import os
 import subprocess
 import sys
@@ -39,11 +43,39 @@ def _deps():
     return deps
 
 
+def source_hash(diag=DIAG):
+    """16 hex digits over the library's inputs: every csrc/*.hip / *.h and include/*.h (name + bytes) and
+    the compile flags (the diagnostic build's -DRN_DIAG=1 included). Machine-independent: the same tree
+    gives the same id here and on the GPU box."""
+    h = hashlib.sha256()
+    flags = [f for f in CXXFLAGS if f != "-DRN_DIAG=1"] + (["-DRN_DIAG=1"] if diag else [])
+    h.update(" ".join(f for f in flags if f not in (INCLUDE, CSRC)).encode())
+    for path in sorted(_deps()):
+        if path == os.path.abspath(__file__):
+            continue
+        h.update(os.path.relpath(path, REPO).encode() + b"\0")
+        with open(path, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+_MARKER = b"RN_BUILD_ID="
+
+
+def library_build_id(path=None):
+    """The build id baked into a built library file (read from its bytes, without loading it), or None."""
+    path = path or LIB_PATH
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        data = f.read()
+    i = data.find(_MARKER)
+    return data[i + len(_MARKER):i + len(_MARKER) + 16].decode("ascii", "replace") if i >= 0 else None
+
+
 def needs_build():
-    if not os.path.exists(LIB_PATH):
-        return True
-    t = os.path.getmtime(LIB_PATH)
-    return any(os.path.getmtime(d) > t for d in _deps())
+    return library_build_id(LIB_PATH) != source_hash()
 
 
 def _compile(src, extra):
@@ -61,8 +93,9 @@ def build(force=False, verbose=True, extra=()):
     os.makedirs(BUILD_DIR, exist_ok=True)
     srcs = _sources()
     jobs = min(len(srcs), int(os.environ.get("MAX_JOBS", "8")), 16)
+    bid = [f'-DRN_BUILD_ID="{source_hash()}"'] if not extra else []  # (extra flags: an experiment, no id)
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
-        objs = list(ex.map(lambda s: _compile(s, list(extra)), srcs))
+        objs = list(ex.map(lambda s: _compile(s, bid + list(extra)), srcs))
     tmp = LIB_PATH + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -6,9 +6,12 @@ PyTorch fallback for any op of the training path.
 import ctypes as C
 import os
 
-from .build import LIB_PATH as _BUILT_LIB, build, needs_build
+from .build import LIB_PATH as _BUILT_LIB, build, library_build_id, needs_build, source_hash
 
-# RN_LIB_PATH: load another build of the library (A/B of two builds in one GPU call); default the in-tree one
+# RN_LIB_PATH: load another build of the library (A/B of two builds in one GPU call); default the in-tree one.
+# A library whose build id is not the tree's (rn/build.py: source_hash) is refused unless
+# RN_LIB_ALLOW_MISMATCH=1 says the A/B is deliberate; the diagnostic build (librn_diag.so) is checked
+# against the tree's diagnostic id.
 LIB_PATH = os.environ.get("RN_LIB_PATH") or _BUILT_LIB
 
 RN_BF16 = 0
@@ -129,6 +132,7 @@ SIGNATURES = {
     "rn_set_tuning": (_i32, [_i32, _i32]),
     "rn_last_error": (C.c_char_p, []),
     "rn_version": (_i32, []),
+    "rn_build_id": (C.c_char_p, []),
     "rn_device_cu_count": (_i32, []),
 }
 
@@ -160,6 +164,12 @@ def load(auto_build=True):
     # first pulls /opt/rocm's copy, torch then loads a second runtime, and librn's launches see no
     # device ("no ROCm-capable device is detected"). Importing torch does not initialise the GPU.
     import torch  # noqa: F401
+    expect = source_hash(diag=os.path.basename(LIB_PATH) == "librn_diag.so")
+    got = library_build_id(LIB_PATH)
+    if got != expect and os.environ.get("RN_LIB_ALLOW_MISMATCH", "0") != "1":
+        raise RuntimeError(f"{LIB_PATH} was built from other sources (build id {got}, tree {expect}): rebuild it "
+                           "(`python -c 'import __graft_entry__ as g; g.build()'`), or set RN_LIB_ALLOW_MISMATCH=1 "
+                           "for a deliberate A/B of another build")
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in list(SIGNATURES.items()) + list(DIAG_SIGNATURES.items()):
         if (name in DIAG_SIGNATURES or LIB_PATH != _BUILT_LIB) and not hasattr(lib, name):
@@ -171,16 +181,20 @@ def load(auto_build=True):
     # RN_DETERMINISTIC=1: bitwise reproducible weight gradients (rn_set_tuning 17)
     if os.environ.get("RN_DETERMINISTIC", "0") == "1":
         check(lib.rn_set_tuning(17, 1), "rn_set_tuning")
+        _DETERMINISTIC[0] = True
     # RN_TUNE="key=value,..." selects kernel variants (rn_set_tuning; A/B measurements)
     for kv in filter(None, os.environ.get("RN_TUNE", "").split(",")):
         k, v = kv.split("=")
         check(lib.rn_set_tuning(int(k), int(v)), "rn_set_tuning")
         USER_TUNED.add(int(k))
+        if int(k) == 17:
+            _DETERMINISTIC[0] = int(v) == 1
     return lib
 
 
 USER_TUNED = set()  # rn_set_tuning keys fixed by RN_TUNE: the executor leaves them alone
 WGRAD_SPLIT_OVERLAPPED = 45  # rn_set_tuning 21 with the weight gradients on the side stream (percent of the chip)
+_DETERMINISTIC = [False]  # rn_set_tuning 17 as set through this module (RN_DETERMINISTIC, RN_TUNE, call())
 
 
 def set_wgrad_split(overlapped, pct=None):
@@ -188,10 +202,14 @@ def set_wgrad_split(overlapped, pct=None):
     the executor runs them: `pct` (default 45 %) beside the data-gradient chain on the side stream
     (measured, DESIGN.md rounds 4-5), the whole chip when they run serialised on the compute stream
     (RN_WGRAD_STREAM=0). An RN_TUNE=21=... override wins. Launches clamp their split to the workspace the
-    plan sized."""
+    plan sized. The key is process-global and the split count fixes the fp32 summation order of the weight
+    gradients, so outside the deterministic mode a serialised step (bench.py's calibration) does not give
+    gradients bit-equal to an overlapped one; in the deterministic mode (rn_set_tuning 17) the key is
+    pinned to the whole chip for every executor and step, so the split -- and the bits -- never change."""
     lib = load()
     if 21 not in USER_TUNED:
-        check(lib.rn_set_tuning(21, (pct or WGRAD_SPLIT_OVERLAPPED) if overlapped else 100), "rn_set_tuning")
+        v = 100 if (_DETERMINISTIC[0] or not overlapped) else (pct or WGRAD_SPLIT_OVERLAPPED)
+        check(lib.rn_set_tuning(21, v), "rn_set_tuning")
 
 
 def check(ret, what=""):
@@ -203,7 +221,12 @@ def check(ret, what=""):
 
 def call(name, *args):
     lib = load()
-    return check(getattr(lib, name)(*args), name)
+    ret = check(getattr(lib, name)(*args), name)
+    if name == "rn_set_tuning" and int(args[0]) == 17:
+        _DETERMINISTIC[0] = int(args[1]) == 1
+        if 21 not in USER_TUNED:  # pinned to the whole chip in the mode (set_wgrad_split), else the library default
+            check(lib.rn_set_tuning(21, 100 if _DETERMINISTIC[0] else WGRAD_SPLIT_OVERLAPPED), "rn_set_tuning")
+    return ret
 
 
 def ptr(t):

@@ -3,6 +3,8 @@ import ctypes as C
 import os
 import re
 
+import pytest
+
 from rn import lib as L
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -106,3 +108,26 @@ def test_grouped_layout_is_fixed_at_descriptor_init():
         lib.rn_set_tuning(15, 0)
     d.groups = 1  # a dense conv is never direct
     assert lib.rn_conv_desc_init(C.byref(d)) == 0 and d.grouped_direct == 0
+
+
+def test_loaded_library_is_tied_to_the_tree(tmp_path, monkeypatch):
+    """the library carries a build id (a hash of csrc/*, include/rn.h and the flags,
+    exported as rn_build_id); rn.lib.load() refuses one whose id differs from the tree's, so a stale
+    prebuilt after a checkout or copy fails loudly. A touched source makes load(auto_build=False) fail."""
+    from rn import build as B
+    lib = L.load()
+    assert lib.rn_build_id().decode() == B.source_hash() == B.library_build_id(L.LIB_PATH)
+    assert not B.needs_build()
+    # a touched source: one more dependency with new bytes changes the tree's id
+    extra = tmp_path / "touched.h"
+    extra.write_text("// edited\n")
+    deps = B._deps
+    monkeypatch.setattr(B, "_deps", lambda: deps() + [str(extra)])
+    assert B.source_hash() != B.library_build_id(L.LIB_PATH) and B.needs_build()
+    monkeypatch.setattr(L, "_lib", None)
+    monkeypatch.delenv("RN_LIB_ALLOW_MISMATCH", raising=False)
+    with pytest.raises(RuntimeError, match="built from other sources"):
+        L.load(auto_build=False)
+    # an explicit A/B override loads it anyway
+    monkeypatch.setenv("RN_LIB_ALLOW_MISMATCH", "1")
+    assert L.load(auto_build=False) is not None

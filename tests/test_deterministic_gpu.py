@@ -62,7 +62,7 @@ def test_wgrad_deterministic(gpu, deterministic, dtype, case):
         L.call("rn_conv_bwd_filter_ws", C.byref(d), p(xd), p(dyd), p(dw), p(ws), need, stream())
         outs.append(dw)
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32)) and torch.equal(outs[0], outs[2])
     got = outs[0].cpu().numpy().reshape(k, r, r, c // g).transpose(0, 3, 1, 2)
     assert rel_err(got, dw_ref) < (2e-5 if dtype == F32 else 5e-3)
     # without a workspace the mode refuses instead of falling back to atomics
@@ -124,11 +124,16 @@ def test_resnet50_fp32_deterministic_unreplayed(gpu, deterministic):
     (4, 128, 14, 14, 128, 3, 1, 1, 32),
     (32, 2048, 1, 1, 1000, 1, 1, 0, 1),
     (64, 64, 56, 56, 64, 1, 1, 0, 1),      # many splits (> 16: the general kernel in both modes)
+    (16, 64, 14, 14, 64, 3, 1, 1, 1),      # image bands: one split per image, exactly 16
+    (16, 64, 14, 14, 64, 3, 1, 1, -1),     # the same onto a -0 start (zero signs compared too)
 ])
 def test_slab_reduce_few_splits_bitwise(gpu, deterministic, dtype, case):
     """rn_set_tuning 25: the few-split slab reduction (one thread per 16-byte column, <= 16 splits)
-    stores exactly the general kernel's sums (dw accumulated into: += onto a nonzero start)."""
+    stores exactly the general kernel's sums, bit for bit including the sign of zero (dw accumulated
+    into: += onto a nonzero start; g = -1: a -0 start)."""
     n, c, h, w, k, r, st, pd, g = case
+    negzero = g < 0
+    g = abs(g)
     rng = np.random.default_rng(11)
     x = rng.standard_normal((n, c, h, w))
     d = conv_desc(dtype, n, c, h, w, k, r, r, st, pd, groups=g)
@@ -140,6 +145,10 @@ def test_slab_reduce_few_splits_bitwise(gpu, deterministic, dtype, case):
     ws = torch.empty(need // 4, dtype=torch.float32, device=gpu)
     xd, dyd = to_nhwc(x, dtype, gpu), to_nhwc(dy, dtype, gpu)
     start = torch.tensor(rng.standard_normal(k * r * r * (c // g)), dtype=torch.float32, device=gpu)
+    if negzero:
+        start = torch.full_like(start, -0.0)
+    if dtype == BF16 and case[0] == 16 and case[1] == 64 and case[4] == 64:
+        assert need == 16 * k * r * r * c * 4  # 16 splits, the few-split kernel's limit
     outs = []
     try:
         for mode in (1, 0):
@@ -151,4 +160,4 @@ def test_slab_reduce_few_splits_bitwise(gpu, deterministic, dtype, case):
         torch.cuda.synchronize()
     finally:
         L.call("rn_set_tuning", 25, 0)
-    assert torch.equal(outs[0], outs[1])
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))

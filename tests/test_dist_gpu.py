@@ -120,13 +120,21 @@ def _run(graph, precision, mode, bucket_mb):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
+    saved = {k: os.environ.get(k) for k in ("RN_BUCKET_MB", "RN_HW_QUEUES", "GPU_MAX_HW_QUEUES")}
     os.environ["RN_BUCKET_MB"] = str(bucket_mb)  # inherited by the spawned ranks
     # two ranks on one GPU: HIP's 4 hardware queues each (8 per process oversubscribe the queue slots)
     os.environ["RN_HW_QUEUES"] = "4"
     os.environ["GPU_MAX_HW_QUEUES"] = "4"
     procs = [ctx.Process(target=_worker, args=(r, 2, port, graph, precision, mode, q)) for r in range(2)]
-    for p in procs:
-        p.start()
+    try:
+        for p in procs:
+            p.start()
+    finally:  # (the spawn copied them; this process keeps its own -- later tests read them)
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     res = {}
     try:
         for _ in range(2):

@@ -34,3 +34,25 @@ def _queues(**env):
 ])
 def test_hardware_queue_count(env, want):
     assert _queues(**env) == want
+
+
+@pytest.mark.parametrize("ids,want", [((0, 0), "4"), ((0, 1), "8")])
+def test_module_workers_queue_count(monkeypatch, ids, want):
+    """mx.mod.Module over repeated device ids (two contexts on one GPU) spawns workers that
+    import rn while unpickling, before the worker sets WORLD_SIZE: the shared-GPU queue count (4) must be
+    in the environment the spawn copies, and the parent's own 8 must not leak into them. Distinct
+    devices keep 8 per process."""
+    import mxnet as mx
+    from rn import graphs
+    monkeypatch.setenv("RN_DRY_RUN", "1")
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv("RN_DIST_BACKEND", raising=False)
+    monkeypatch.delenv("RN_HW_QUEUES", raising=False)
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "8")  # what the parent's `import rn` wrote
+    mod = mx.mod.Module(graphs.resnet20_cifar(), context=[mx.gpu(i) for i in ids])
+    try:
+        mod.bind(data_shapes=[("data", (4, 3, 32, 32))], label_shapes=[("softmax_label", (4,))])
+        assert mod._group.call("env", "GPU_MAX_HW_QUEUES") == [want, want]
+        assert os.environ["GPU_MAX_HW_QUEUES"] == "8" and "RN_DIST_BACKEND" not in os.environ  # parent unchanged
+    finally:
+        mod.close()

@@ -1885,3 +1885,47 @@ def test_conv3x3_band(gpu, case, persist):
         assert rel_err(from_nhwc(dx, c), dx_ref) < TOL[BF16]
     assert rel_err(from_nhwc(outs[1][0], k), from_nhwc(outs[0][0], k)) < 1e-2
     assert rel_err(from_nhwc(outs[1][1], c), from_nhwc(outs[0][1], c)) < 1e-2
+
+
+@pytest.mark.parametrize("case", [
+    (5, 64, 9, 13, 64, 3, 1, 1),     # ragged: odd rows, the last band has one output row
+    (40, 64, 20, 20, 64, 3, 1, 1),   # every workgroup walks several bands (double-buffered band loads)
+])
+def test_conv3x3_band_bnrelu_on_load(gpu, case):
+    """conv3x3c64_band_kernel<0, 1> (the producing BatchNorm+ReLU applied to each landed band in
+    LDS, the zero halo kept) == rn_bn_apply's output through the plain band kernel, BIT FOR BIT; the same
+    for the implicit-GEMM tile (rn_set_tuning 26 = 1), and the two forms within the bf16 bar of each other
+    and of the oracle on the bf16-rounded BN+ReLU output."""
+    n, c, h, w, k, r, st, pd = case
+    x, wt = _conv_data(case, 31)
+    rng = np.random.default_rng(32)
+    sc = rng.uniform(0.5, 1.5, c)
+    sh = rng.standard_normal(c) * 0.5
+    x, wt = bf16_round(x), bf16_round(wt)
+    xa = bf16_round(np.maximum(x * sc[None, :, None, None] + sh[None, :, None, None], 0))
+    y_ref = ops.conv2d_fwd(xa, wt, (st, st), (pd, pd))
+    d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd)
+    f = lambda a: torch.tensor(a, dtype=torch.float32, device=gpu)
+    scd, shd = f(sc), f(sh)
+    xd = to_nhwc(x, BF16, gpu)
+    bd = L.BNDesc(dtype=BF16, m=n * h * w, c=d.c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1)
+    xad = torch.zeros_like(xd)  # the unfused path: rn_bn_apply's stored BN+ReLU output
+    L.call("rn_bn_apply", C.byref(bd), p(xd), p(xad), p(scd), p(shd), stream())
+    wk = torch.zeros(k * r * r * d.c, dtype=torch.bfloat16, device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), p(wk), None, stream())
+    outs = []
+    try:
+        for mode in (0, 1):
+            L.call("rn_set_tuning", 26, mode)
+            y1 = torch.full((n, h, w, k), float("nan"), dtype=torch.bfloat16, device=gpu)
+            y0 = torch.full_like(y1, float("nan"))
+            L.call("rn_conv_fwd_x", C.byref(d), p(xd), p(wk), p(y1), BF16, None, None, p(scd), p(shd), None, stream())
+            L.call("rn_conv_fwd", C.byref(d), p(xad), p(wk), p(y0), BF16, None, None, stream())
+            torch.cuda.synchronize()
+            assert torch.equal(y1.view(torch.int16), y0.view(torch.int16)), mode
+            outs.append(y1)
+    finally:
+        L.call("rn_set_tuning", 26, 0)
+    for y in outs:
+        assert rel_err(from_nhwc(y, k), y_ref) < TOL[BF16]
+    assert rel_err(from_nhwc(outs[0], k), from_nhwc(outs[1], k)) < 1e-2

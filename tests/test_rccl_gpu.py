@@ -106,3 +106,62 @@ def test_bucketed_allreduce_over_rccl_world1(gpu):
         assert fro(g, p) < 1e-4, fro(g, p)
     for k in ref_args:  # weights after the first SGD step (update() waited for every bucket)
         assert fro(args[k], ref_args[k]) < 1e-3, k
+
+
+def _overlap_probe(main, side, cycles=200_000_000):
+    """A long spin on the compute stream, then a short op on the side stream enqueued while it runs: with
+    the two streams on different hardware queues the side op completes long before the spin ends; on one
+    queue (HIP runs a queue's packets in order) it completes after it. Returns (spin ms, side-done ms)."""
+    ev = lambda: torch.cuda.Event(enable_timing=True)
+    e0, e1, s1 = ev(), ev(), ev()
+    buf = torch.zeros(1024, device=main.device)
+    torch.cuda.synchronize()
+    e0.record(main)
+    with torch.cuda.stream(main):
+        torch.cuda._sleep(cycles)
+    e1.record(main)
+    with torch.cuda.stream(side):
+        buf.add_(1.0)
+    s1.record(side)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1), e0.elapsed_time(s1)
+
+
+def test_weight_gradient_stream_overlaps_with_rccl_hooks(gpu):
+    """with an RCCL process group and the bucketed all-reduce hooks on (the product's
+    data-parallel path, as bench.py RN_BENCH_ALLREDUCE=1 runs it at world 1) and the product's hardware-
+    queue count (rn/__init__.py), the executor's weight-gradient stream must not share the compute
+    stream's hardware queue. With HIP's 4 queues RCCL's pool streams moved it onto that queue and the
+    backward's two branches ran serialised (25.8 vs 20.4 ms per step, profiles/r05/streams): a side-stream
+    op enqueued behind a long compute-stream kernel then finishes only after it."""
+    import torch.distributed as dist
+    import mxnet as mx
+    from oracle import net as onet
+    from rn import dist as rdist, graphs
+    from rn.dist import BucketAllReducer
+    assert os.environ.get("GPU_MAX_HW_QUEUES") == "8"  # rn's import set it before this process's first HIP call
+    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1,
+                            device_id=gpu, **rdist.nccl_pg_kwargs())
+    try:
+        sym = graphs.resnet([3, 4, 6, 3], 4, [64, 256, 512, 1024, 2048], 16)
+        data, label = onet.synthetic_batch(8, (3, 64, 64), 16)
+        mod = mx.mod.Module(sym, context=[mx.gpu(0)], precision="bfloat16")
+        mod.bind(data_shapes=[("data", data.shape)], label_shapes=[("softmax_label", label.shape)], for_training=True)
+        mx.random.seed(3)
+        mod.init_params(mx.init.Xavier(rnd_type="gaussian", factor_type="in", magnitude=2))
+        mod.init_optimizer(kvstore="device", optimizer="sgd", optimizer_params={"learning_rate": 0.1})
+        ex = mod.executor
+        ex.bucket_bytes = 1 << 20
+        mod._reducer = BucketAllReducer(ex.grad, ex.buckets())
+        batch = mx.io.DataBatch(data=[mx.nd.array(data.astype(np.float32))], label=[mx.nd.array(label)])
+        for _ in range(2):  # RCCL has taken its streams and run its collectives beside both executor streams
+            mod.forward(batch, is_train=True)
+            mod.backward()
+            mod.update()
+        torch.cuda.synchronize()
+        assert ex._side_stream is not None and ex.side_enabled
+        spin, side_done = _overlap_probe(torch.cuda.current_stream(), ex._side_stream)
+    finally:
+        dist.destroy_process_group()
+    assert spin > 5.0, spin  # the probe's compute-stream kernel really ran long
+    assert side_done < 0.5 * spin, (side_done, spin)  # ... and the side stream did not wait behind it

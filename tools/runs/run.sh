@@ -31,7 +31,7 @@ for s in "$@"; do
     c2%*|c4%*|c5%*) m=${s%%\%*}; kv=${s#*%}; lab=$(echo "$kv" | tr '=,' '__')
       steps+=("200 env $(echo "$kv" | tr ',' ' ') python bench.py --model $(model_of $m) --no-cpu-baseline --pcie-steps 0 > gpurun_out/${tag}_${m}_${lab}.log 2>&1");;
     lib:*) m=${s#lib:}
-      steps+=("200 env RN_LIB_PATH=experiments/librn_base.so python bench.py --model $(model_of $m) --no-cpu-baseline --pcie-steps 0 > gpurun_out/${tag}_${m}_base.log 2>&1");;
+      steps+=("200 env RN_LIB_PATH=experiments/librn_base.so RN_LIB_ALLOW_MISMATCH=1 python bench.py --model $(model_of $m) --no-cpu-baseline --pcie-steps 0 > gpurun_out/${tag}_${m}_base.log 2>&1");;
     prof|prof:*|prof@*|prof:*@*) spec=${s#prof}; kv=""; [[ "$spec" == *@* ]] && kv=${spec#*@} && spec=${spec%%@*}
       m=$(model_of "${spec#:}"); lab=${m}$( [ -n "$kv" ] && echo "_$(echo "$kv" | tr '=,' '__')" )
       steps+=("300 env RN_TUNE=$kv bash tools/prof_bench.sh ${tag}_${lab} --model $m --steps 5 --warmup 2 --no-cpu-baseline --pcie-steps 0 > gpurun_out/${tag}_prof_${lab}.log 2>&1");;
