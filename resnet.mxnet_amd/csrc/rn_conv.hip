@@ -1418,6 +1418,7 @@ struct WgradArgs {
   int creal;                  // logical input channels (< C: padded stride, dw keeps c < creal)
   int nct, nkt;               // column tiles, k tiles (grid = splits * nkt * nct)
   int diag_noepi;             // diagnostic (rn_set_tuning 6, bits): 1 skip the dW epilogue, 2 / 4 (wgrad_big_kernel) no loop DMAs / waits
+  int x_bytes, dy_bytes;      // (wgrad_big_kernel) the operands' buffer descriptor sizes
   int p4;                     // the stem's padded NHWC4 image (rn_stem_prepare_p4): column = (r*8 + s)*4 + c,
                               // r, s < 8; dW keeps r < R, s < S, c < creal ([K][R][S][creal])
   int gspread;                // (gdiag) the diagonal blocks spread over all four waves
@@ -1737,7 +1738,10 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(WgradArgs p) {
 // ds_read_b64_tr_b8 -- lane i of a 16-lane group gets column i of an 8-row x 16-byte block, lane l
 // supplying row l / 2, bytes 8 (l % 2).. -- and widened to bf16 (exact: |code| <= 127); dW = unit *
 // sum dy * code, the unit applied once in the epilogue.
-template <int BMK, int NBUF, int BNC = 256, int XF = 0, int I8X = 0>
+// DIR (1x1, stride 1, pad 0: the gathered row of pixel m is x's row m): B rows addressed directly, no
+// coordinate divisions. Both operands are DMA'd through buffer descriptors (a masked lane's offset is past
+// the buffer: the hardware returns zeros), so a DMA is one v_cndmask, not an exec-masked pointer select.
+template <int BMK, int NBUF, int BNC = 256, int XF = 0, int I8X = 0, int DIR = 0>
 __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(WgradArgs p) {
   static_assert(!(XF && I8X), "int8 input: no input transform");
   constexpr int CE = I8X ? 16 : 8, BKM = 64, XES = I8X ? 1 : 2;  // B chunk channels, B bytes per element
@@ -1794,9 +1798,8 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
       b_h[j] = b_w[j] = 0;
     }
   }
-  const char* __restrict__ dyb = reinterpret_cast<const char*>(p.dy);
-  const char* __restrict__ xb = reinterpret_cast<const char*>(p.x);
-  const char* zb = reinterpret_cast<const char*>(&g_zero_chunk);
+  const v4i rs_dy = make_rsrc(p.dy, (uint32_t)p.dy_bytes);
+  const v4i rs_x = make_rsrc(p.x, (uint32_t)p.x_bytes);
   const uint32_t lds_a = __builtin_amdgcn_readfirstlane(lds_addr(smem) + wid * AR * 1024);  // this wave's pieces
   const uint32_t lds_b = __builtin_amdgcn_readfirstlane(lds_addr(smem) + A_SZ * 16 + wid * BR * 1024);
 
@@ -1808,21 +1811,25 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
     for (int j = 0; j < AR; ++j) {
       const int m = mb + a_row[j];
       const bool ok = a_col[j] >= 0 && m < mend;
-      const uint32_t off = (uint32_t)(m * p.ldy + a_col[j]) * 2u;
-      dma16_global(ok ? (const void*)(dyb + off) : (const void*)zb, lds_a + la + j * 1024);
+      dma16_asm(rs_dy, lds_a + la + j * 1024, ok ? (uint32_t)(m * p.ldy + a_col[j]) * 2u : kOob);
     }
 #pragma unroll
     for (int j = 0; j < BR; ++j) {
       const int m = mb + b_row[j];
-      const int n = fdiv(m, p.fdPQ);
-      const int rem = m - n * p.P * p.Q;
-      const int pp = fdiv(rem, p.fdQ);
-      const int qq = rem - pp * p.Q;
-      const int hin = pp * p.sh + b_h[j];
-      const int win = qq * p.sw + b_w[j];
-      const bool ok = b_ch[j] >= 0 && m < mend && (unsigned)hin < (unsigned)p.H && (unsigned)win < (unsigned)p.W;
-      const uint32_t off = (uint32_t)(((n * p.H + hin) * p.W + win) * p.C + b_ch[j]) * (uint32_t)XES;
-      dma16_global(ok ? (const void*)(xb + off) : (const void*)zb, lds_b + la + j * 1024);
+      if constexpr (DIR) {
+        const bool ok = b_ch[j] >= 0 && m < mend;
+        dma16_asm(rs_x, lds_b + la + j * 1024, ok ? (uint32_t)(m * p.C + b_ch[j]) * (uint32_t)XES : kOob);
+      } else {
+        const int n = fdiv(m, p.fdPQ);
+        const int rem = m - n * p.P * p.Q;
+        const int pp = fdiv(rem, p.fdQ);
+        const int qq = rem - pp * p.Q;
+        const int hin = pp * p.sh + b_h[j];
+        const int win = qq * p.sw + b_w[j];
+        const bool ok = b_ch[j] >= 0 && m < mend && (unsigned)hin < (unsigned)p.H && (unsigned)win < (unsigned)p.W;
+        dma16_asm(rs_x, lds_b + la + j * 1024,
+                  ok ? (uint32_t)(((n * p.H + hin) * p.W + win) * p.C + b_ch[j]) * (uint32_t)XES : kOob);
+      }
     }
   };
 
@@ -1932,20 +1939,44 @@ __global__ __launch_bounds__(BNC * 2, BNC == 256 ? 1 : 2) void wgrad_big_kernel(
       for (int j = 0; j < NI; ++j) acc[i][j] *= u;
   }
   const bool padded = p.creal != p.C;
-  if (p.slab && !padded) {  // plain stores of this split's partial tile (rows of 16 columns: 64-byte segments)
+  if (p.slab && !padded) {
+    // this split's partial tile, staged through LDS (the operand buffers are free now) so that each store
+    // instruction writes whole 256-byte rows (16 lanes x 16 bytes) instead of four 64-byte segments: per
+    // wave SR rows x 64 columns at a time (64 rows: 8 waves x 16 KB = the 128 KB of the two 256x256
+    // buffers; 32 where the int8-codes form's smaller buffers hold less). Column block j of staged row r
+    // sits at block j ^ ((r >> 2) & 3): the two 32-lane halves of a b32 write (rows r, r + 4) and the
+    // 16-lane groups of a b128 read (rows r, r + 1) meet no bank twice.
     float* dst = p.slab + (int64_t)zs * p.K * p.ldw;
+    constexpr int SR = NBUF * kStage * 16 >= NW * 64 * 64 * 4 ? 64 : 32;
+    static_assert(NW * SR * 64 * 4 <= NBUF * kStage * 16, "staging fits the operand buffers");
+    constexpr int IR = SR / 16;                        // accumulator rows i per round
+    constexpr int ROUNDS = (MI + IR - 1) / IR;
+    float* stg = reinterpret_cast<float*>(smem) + wid * (SR * 64);
+    __syncthreads();  // every wave is done reading the last M-tile's operands
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+    for (int hh = 0; hh < ROUNDS; ++hh) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int k = k0 + wm * (BMK / 2) + i * 16 + (lane >> 4) * 4 + e;
-        if (k >= p.K) continue;
+      for (int i = 0; i < IR; ++i) {
+        if (hh * IR + i >= MI) break;
 #pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          const int col = n0 + wn * 64 + j * 16 + (lane & 15);
-          if (col < p.ncol) dst[(int64_t)k * p.ldw + col] = acc[i][j][e];
+        for (int e = 0; e < 4; ++e) {
+          const int r = i * 16 + (lane >> 4) * 4 + e;
+#pragma unroll
+          for (int j = 0; j < NI; ++j) stg[r * 64 + ((j ^ ((r >> 2) & 3)) << 4) + (lane & 15)] = acc[hh * IR + i][j][e];
         }
       }
+      const int rows = (MI - hh * IR >= IR ? IR : MI - hh * IR) * 16;
+#pragma unroll
+      for (int t = 0; t < SR / 4; ++t) {
+        const int r = t * 4 + (lane >> 4);
+        if (r >= rows) break;
+        const int c4 = (lane & 15) * 4;  // columns c4 .. c4 + 3 of the wave's 64
+        const float4 v = *reinterpret_cast<const float4*>(stg + r * 64 + (((c4 >> 4) ^ ((r >> 2) & 3)) << 4) + (c4 & 15));
+        const int k = k0 + wm * (BMK / 2) + hh * SR + r;
+        const int col = n0 + wn * 64 + c4;
+        if (k < p.K && col < p.ncol) *reinterpret_cast<float4*>(dst + (int64_t)k * p.ldw + col) = v;
+      }
+    }
     return;
   }
   // (padded channels: the slab, in the deterministic mode, takes the same compacted indices)
@@ -4310,6 +4341,12 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
       a.gdiag = a.gk > 16 ? 2 : 1, a.gspread = g_tune[RN_TUNE_WGRAD_GD] != 2;
   }
   a.M = d->n * d->p * d->q;
+  // (wgrad_big_kernel) buffer descriptor sizes; its launches need both < 2^31 elements (checked below)
+  a.x_bytes = (int)(uint32_t)std::min<int64_t>((int64_t)d->n * d->h * d->w * d->c * (i8 ? 1 : 2), 0xFFFFFFFFll);
+  a.dy_bytes = (int)(uint32_t)std::min<int64_t>((int64_t)a.M * a.ldy * 2, 0xFFFFFFFFll);
+  // 1x1 / stride 1 / pad 0: x's row m is the gathered row m (wgrad_big_kernel DIR)
+  const bool dir = d->r == 1 && d->s == 1 && d->stride_h == 1 && d->stride_w == 1 && d->pad_h == 0 &&
+                   d->pad_w == 0 && d->c_real == d->c && d->groups <= 1;
   a.diag_noepi = g_tune[RN_TUNE_DIAG_WGRAD_NOEPI];
   a.fdQ = make_fastdiv(d->q); a.fdPQ = make_fastdiv(d->p * d->q);
   a.fdC = make_fastdiv(a.cblk); a.fdS = make_fastdiv(d->s);
@@ -4494,9 +4531,17 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     split = ceil_div(a.M, a.m_per_split);
     if (!launch) return finish(split, "wgrad_dma128");
     if (!use_slab(split)) return -1;
-    if (in_scale) hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128, 1>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
-    else if (i8) hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128, 0, 1>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128>), dim3((unsigned)(tiles * split)), dim3(256), 0, st, a);
+    const dim3 g128((unsigned)(tiles * split));
+#define RN_W128(DV)                                                                                        \
+  if (in_scale) hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128, 1, 0, DV>), g128, dim3(256), 0, st, a);   \
+  else if (i8) hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128, 0, 1, DV>), g128, dim3(256), 0, st, a);    \
+  else hipLaunchKernelGGL((wgrad_big_kernel<128, 2, 128, 0, 0, DV>), g128, dim3(256), 0, st, a);
+    if (dir) {
+      RN_W128(1)
+    } else {
+      RN_W128(0)
+    }
+#undef RN_W128
     return finish(split, "wgrad_dma128");
   }
   if (big256) {
@@ -4511,14 +4556,21 @@ int wgrad_dispatch(const rn_conv_desc* d, const void* x, const void* dy, float* 
     if (!launch) return finish(split, "wgrad_big");
     if (!use_slab(split)) return -1;
     dim3 grid((unsigned)(tiles * split));
-    if (in_scale) {
-      if (bmk == 256) hipLaunchKernelGGL((wgrad_big_kernel<256, 2, 256, 1>), grid, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((wgrad_big_kernel<128, 3, 256, 1>), grid, dim3(512), 0, st, a);
-    } else if (i8) {
-      if (bmk == 256) hipLaunchKernelGGL((wgrad_big_kernel<256, 2, 256, 0, 1>), grid, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((wgrad_big_kernel<128, 3, 256, 0, 1>), grid, dim3(512), 0, st, a);
-    } else if (bmk == 256) hipLaunchKernelGGL((wgrad_big_kernel<256, 2>), grid, dim3(512), 0, st, a);
-    else hipLaunchKernelGGL((wgrad_big_kernel<128, 3>), grid, dim3(512), 0, st, a);
+#define RN_W256(DV)                                                                                              \
+  if (in_scale) {                                                                                               \
+    if (bmk == 256) hipLaunchKernelGGL((wgrad_big_kernel<256, 2, 256, 1, 0, DV>), grid, dim3(512), 0, st, a);    \
+    else hipLaunchKernelGGL((wgrad_big_kernel<128, 3, 256, 1, 0, DV>), grid, dim3(512), 0, st, a);               \
+  } else if (i8) {                                                                                              \
+    if (bmk == 256) hipLaunchKernelGGL((wgrad_big_kernel<256, 2, 256, 0, 1, DV>), grid, dim3(512), 0, st, a);    \
+    else hipLaunchKernelGGL((wgrad_big_kernel<128, 3, 256, 0, 1, DV>), grid, dim3(512), 0, st, a);               \
+  } else if (bmk == 256) hipLaunchKernelGGL((wgrad_big_kernel<256, 2, 256, 0, 0, DV>), grid, dim3(512), 0, st, a); \
+  else hipLaunchKernelGGL((wgrad_big_kernel<128, 3, 256, 0, 0, DV>), grid, dim3(512), 0, st, a);
+    if (dir) {
+      RN_W256(1)
+    } else {
+      RN_W256(0)
+    }
+#undef RN_W256
     return finish(split, "wgrad_big");
   }
   if (i8) {  // (a plan-time query, launch == false, sets no error)
@@ -4709,6 +4761,8 @@ int rn_stem_conv_wgrad_p4(const rn_conv_desc* d, const void* x4, const void* dy,
   a.M = d->n * d->p * d->q;
   a.fdQ = make_fastdiv(d->q); a.fdPQ = make_fastdiv(d->p * d->q);
   a.fdC = make_fastdiv(4); a.fdS = make_fastdiv(8);
+  a.x_bytes = (int)((int64_t)d->n * hp * wp * 4 * 2);
+  a.dy_bytes = (int)((int64_t)a.M * a.ldy * 2);
   a.nct = 2;
   a.nkt = 1;
   const int64_t tiles = a.nct;

@@ -1929,3 +1929,4 @@ def test_conv3x3_band_bnrelu_on_load(gpu, case):
     for y in outs:
         assert rel_err(from_nhwc(y, k), y_ref) < TOL[BF16]
     assert rel_err(from_nhwc(outs[0], k), from_nhwc(outs[1], k)) < 1e-2
+
