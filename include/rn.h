@@ -638,6 +638,10 @@ const char* rn_last_error(void);
  *      the partials form at most 4 merge groups, bit-identical),
  * 25 = 1: the weight-gradient slab reduction always runs its general kernel (default 0: one thread per
  *      16-byte column with every split in flight where there are <= 16 splits; the same sums),
+ * 27 = 1: the 1x1 / stride-1 data gradients reducing over K = 64 or 128 into C >= 128 channels (the pre-activation
+ *      units' conv1) on the 224-row tiles (default 0: dgrad1x1_stream_kernel, which streams their rows with the
+ *      weights in registers -- with the BN-backward reduction, and with the BN backward applied);
+ *      27 = 2: that kernel with 32 channels per wave (default 64 where C % 256 == 0),
  * 26 = 1: the 3x3 / stride-1 / pad-1 64 -> 64 convolutions (forward, data gradient) on the implicit-GEMM
  *      tile (default 0: conv3x3c64_band_kernel, image bands and the nine taps' weights in LDS),
  * 22 = 1: the BatchNorm-folded int8 quantizers (rn_quant_int8_fwd_codes_bn[2]) form every quotient

@@ -120,7 +120,7 @@ __device__ __forceinline__ float quant_value(float v, float t, float qmax, int c
 }
 
 // ------------------------------------------------------------------ tuning knobs (rn_set_tuning)
-enum { RN_TUNE_WGRAD_DMA = 0, RN_TUNE_IGEMM_DMA = 1, RN_TUNE_WGRAD_BLOCKS_PER_CU = 2, RN_TUNE_DIAG_IGEMM_L1 = 3, RN_TUNE_IGEMM_BIG = 4, RN_TUNE_WGRAD_BIG = 5, RN_TUNE_DIAG_WGRAD_NOEPI = 6, RN_TUNE_IGEMM_SCHED = 7, RN_TUNE_IGEMM_MFMA = 8, RN_TUNE_IGEMM_ROWS = 9, RN_TUNE_IGEMM_PERSIST = 10, RN_TUNE_IGEMM_W4 = 11, RN_TUNE_POOL_BLOCK_BWD = 12, RN_TUNE_IGEMM_GD = 13, RN_TUNE_WGRAD_GD = 14, RN_TUNE_GROUP_DIRECT = 15, RN_TUNE_EPI_SYNC = 16, RN_TUNE_DETERMINISTIC = 17, RN_TUNE_BN_NT = 18, RN_TUNE_WGRAD_BAND = 19, RN_TUNE_IGEMM_PRIO = 20, RN_TUNE_WGRAD_SPLIT = 21, RN_TUNE_QUANT_DIV = 22, RN_TUNE_GBAND_SPLIT = 23, RN_TUNE_BN_MERGE = 24, RN_TUNE_SLAB_FEW = 25, RN_TUNE_CONV_BAND = 26, RN_TUNE_COUNT = 27 };
+enum { RN_TUNE_WGRAD_DMA = 0, RN_TUNE_IGEMM_DMA = 1, RN_TUNE_WGRAD_BLOCKS_PER_CU = 2, RN_TUNE_DIAG_IGEMM_L1 = 3, RN_TUNE_IGEMM_BIG = 4, RN_TUNE_WGRAD_BIG = 5, RN_TUNE_DIAG_WGRAD_NOEPI = 6, RN_TUNE_IGEMM_SCHED = 7, RN_TUNE_IGEMM_MFMA = 8, RN_TUNE_IGEMM_ROWS = 9, RN_TUNE_IGEMM_PERSIST = 10, RN_TUNE_IGEMM_W4 = 11, RN_TUNE_POOL_BLOCK_BWD = 12, RN_TUNE_IGEMM_GD = 13, RN_TUNE_WGRAD_GD = 14, RN_TUNE_GROUP_DIRECT = 15, RN_TUNE_EPI_SYNC = 16, RN_TUNE_DETERMINISTIC = 17, RN_TUNE_BN_NT = 18, RN_TUNE_WGRAD_BAND = 19, RN_TUNE_IGEMM_PRIO = 20, RN_TUNE_WGRAD_SPLIT = 21, RN_TUNE_QUANT_DIV = 22, RN_TUNE_GBAND_SPLIT = 23, RN_TUNE_BN_MERGE = 24, RN_TUNE_SLAB_FEW = 25, RN_TUNE_CONV_BAND = 26, RN_TUNE_DGRAD_STREAM = 27, RN_TUNE_COUNT = 28 };
 extern int g_tune[RN_TUNE_COUNT];
 // Diagnostic modes (tuning keys 3, 6, 7 and rn_sgd_mom_update_pack_checked) produce wrong results on
 // purpose (they isolate one cost of a kernel): compiled only into the diagnostic build (hipcc

@@ -4069,6 +4069,256 @@ int band_launch(const rn_conv_desc* d, const void* x, const void* w, void* y, in
   return rn_check_launch("conv3x3c64_band");
 }
 
+// ---- The data gradients of the pre-activation units' conv1 (symbol/resnet.py:17-20: a 1x1 / stride-1
+// convolution whose input has 2-4x its output's channels, so its data gradient reduces over K <= 128 channels
+// into C >= 256): streaming, not tiled. dx[m][c] = sum_k dy[m][k] w[c][k] (the CRSK copy) is memory-bound
+// (2 K MACs per 2 + 2 K / C bytes of dx), and on the 224-row tiles it ran in their epilogue bursts (the BN
+// input the reduction reads came in at ~3.5 TB/s). Here a 256-thread workgroup owns 224 rows (one BN-partial
+// block, the tiles' granularity) x 128 channels; wave w owns channels 32 w .. + 31 for all 224 rows, in steps of
+// 16 rows: v_mfma_f32_16x16x32_bf16 with the weights as the A operand (their fragments in registers for the
+// whole kernel) and dy as B, loaded straight from global memory (lane (g, i): 16 bytes of row i). The two MFMA
+// blocks interleave their rows' channels (block b, row r -> channel 8 (r >> 2) + 4 b + (r & 3)), so output lane
+// (g, i) holds channels 8 g .. 8 g + 7 of row i: every epilogue access is one 16-byte chunk per lane. The next
+// step's loads are issued before this step's MFMAs; the workgroups of one row block sit on one XCD (their dy
+// rows read into one L2). EPI 0: dx (+ add); 2: + the BatchNorm-backward reduction of the stored dx (as
+// igemm_big_kernel EPI 2: sum dz, sum dz (x - mean), dz = dx [x sc + sh > 0]); 3: dx = the BatchNorm backward
+// applied to the rounded gradient (EPI 3's formula) + add.
+struct D1Args {
+  const bf16_t* dy;  // [M][K]
+  const bf16_t* w;   // [C][K] (the CRSK copy of a 1x1 conv)
+  bf16_t* dx;        // [M][C], nullable with EPI 2 (reduction only)
+  const bf16_t* add; // nullable
+  const bf16_t* bn_x;
+  const float *bn_mean, *coef, *bn_sc, *bn_sh;
+  float* part;       // (EPI 2) [M / 224][C][2]
+  int M, C, K, relu, ncg;
+};
+// ADD: p.add is set (a compile-time branch: with a runtime one, hipcc (ROCm 7.2) let the epilogue's first VALU
+// read an MFMA result across the branch without the wait states it needs -- stale values in 1 of 8 channels,
+// run to run). NH: 32-channel halves per wave (NH = 2: a lane's two 16-byte chunks of a row are 64 bytes apart,
+// so each row's 128-byte lines are written whole by one wave).
+template <int KS, int EPI, int ADD, int NH>
+__global__ __launch_bounds__(256, 2) void dgrad1x1_stream_kernel(D1Args p) {
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, i = lane & 15;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int rb = lid / p.ncg, cg = lid - rb * p.ncg;
+  const int m0 = rb * 224, rows = min(224, p.M - m0);
+  const int cw = (cg * 4 + wid) * 32 * NH;  // this wave's 32 NH channels
+  int c8[NH];                                // this lane's 8-channel chunks
+#pragma unroll
+  for (int h = 0; h < NH; ++h) c8[h] = cw + 32 * h + 8 * g;
+  v8s wf[NH][2][KS];
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int ch = cw + 32 * h + 8 * (i >> 2) + 4 * b + (i & 3);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks)
+        wf[h][b][ks] = *reinterpret_cast<const v8s*>(p.w + (int64_t)ch * p.K + ks * 32 + 8 * g);
+    }
+  // per-channel constants of the lane's channels (EPI 2: mean, scale, shift; EPI 3: + A, mean dz, A2)
+  float mu[NH][8], sc[NH][8], sh[NH][8], ca[NH][8], cm[NH][8], c2[NH][8], s1[NH][8], s2[NH][8];
+#pragma unroll
+  for (int h = 0; h < NH; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int c = c8[h] + e;
+      s1[h][e] = s2[h][e] = 0.f;
+      mu[h][e] = sc[h][e] = sh[h][e] = ca[h][e] = cm[h][e] = c2[h][e] = 0.f;
+      if constexpr (EPI == 2) mu[h][e] = p.bn_mean[c];
+      if constexpr (EPI >= 2) {
+        sc[h][e] = p.bn_sc[c];
+        sh[h][e] = p.bn_sh[c];
+      }
+      if constexpr (EPI == 3) {
+        const float4 cf = reinterpret_cast<const float4*>(p.coef)[c];
+        ca[h][e] = cf.x; cm[h][e] = cf.y; c2[h][e] = cf.z; mu[h][e] = cf.w;
+      }
+    }
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  // buffer loads (a row past the block reads zeros through an offset past the buffer): no pointer selects,
+  // which hipcc turns into flat loads whose waits (vmcnt(0) with lgkmcnt) would also drain this step's stores
+  const __amdgpu_buffer_rsrc_t rs_dy = __builtin_amdgcn_make_buffer_rsrc((void*)p.dy, (short)0, p.M * p.K * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_x = __builtin_amdgcn_make_buffer_rsrc((void*)p.bn_x, (short)0, p.M * p.C * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs_a = __builtin_amdgcn_make_buffer_rsrc((void*)p.add, (short)0, p.M * p.C * 2, 0x00020000);
+  // dx through a buffer descriptor too: rows past the block store to an offset past it (dropped), and the
+  // reduction-only form (dx = NULL) gets an empty one -- so the step body has no branch
+  const __amdgpu_buffer_rsrc_t rs_dx =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.dx, (short)0, p.dx ? p.M * p.C * 2 : 0, 0x00020000);
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  auto ld = [&](__amdgpu_buffer_rsrc_t rs, uint32_t off) __attribute__((always_inline)) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  };
+  auto load = [&](int st, uint4 (&d)[KS], uint4 (&xv)[NH], uint4 (&av)[NH]) __attribute__((always_inline)) {
+    const int r = st * 16 + i;
+    const bool ok = r < rows;
+    const uint32_t m = (uint32_t)(m0 + r);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) d[ks] = ld(rs_dy, ok ? (m * p.K + ks * 32 + 8 * g) * 2u : kOob);
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      if constexpr (EPI >= 2) xv[h] = ld(rs_x, ok ? (m * p.C + c8[h]) * 2u : kOob);
+      if constexpr (ADD) av[h] = ld(rs_a, ok ? (m * p.C + c8[h]) * 2u : kOob);
+    }
+  };
+  const bool norelu = __builtin_amdgcn_readfirstlane(p.relu) == 0;
+  uint4 d0[KS], x0[NH], a0[NH];
+#pragma unroll
+  for (int h = 0; h < NH; ++h) x0[h] = a0[h] = z4;
+  load(0, d0, x0, a0);
+  // fully unrolled, branch-free (14 steps of 16 rows; a short last block's extra rows load zeros and store
+  // nothing): hipcc's wait counts then stay exact -- across a loop back-edge or a branch join they became
+  // vmcnt(0), draining the previous step's stores and the prefetched loads every step
+#pragma unroll
+  for (int st = 0; st < 14; ++st) {
+    uint4 d1[KS], x1[NH], a1[NH];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) d1[ks] = z4;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) x1[h] = a1[h] = z4;
+    if (st + 1 < 14) load(st + 1, d1, x1, a1);  // (compile-time)
+    v4f acc[NH][2];
+#pragma unroll
+    for (int h = 0; h < NH; ++h)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[h][b] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+          acc[h][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[h][b][ks], __builtin_bit_cast(v8s, d0[ks]), acc[h][b],
+                                                              0, 0, 0);
+    // the MFMA results' read wait states, explicitly (16 >= the 8-pass MFMA's VALU-read hazard), once per step
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7");
+    __builtin_amdgcn_sched_barrier(0);
+    const int r = st * 16 + i;
+    const bool ok = r < rows;
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      float v[8], xf[8], af[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[h][0][e];
+        v[4 + e] = acc[h][1][e];
+      }
+      chunk_to_f(x0[h], xf, (const bf16_t*)nullptr);
+      chunk_to_f(a0[h], af, (const bf16_t*)nullptr);
+      uint4 out;
+      if constexpr (EPI == 3) {
+        float gv[8];
+        chunk_to_f(f_to_chunk(v, (const bf16_t*)nullptr), gv, (const bf16_t*)nullptr);  // the gradient as stored
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float dz = norelu ? gv[e] : gv[e] * (fmaf(xf[e], sc[h][e], sh[h][e]) > 0.f ? 1.f : 0.f);
+          // spelled out as bn_bwd_apply_kernel is compiled (fma(A, dz - mean dz, -(A2 (x - mean)))): bit-identical
+          const float q = c2[h][e] * (xf[e] - mu[h][e]);
+          float w = fmaf(ca[h][e], dz - cm[h][e], -q);
+          if (ADD) w += af[e];
+          v[e] = w;
+        }
+        out = f_to_chunk(v, (const bf16_t*)nullptr);
+      } else {
+        if (ADD)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += af[e];
+        out = f_to_chunk(v, (const bf16_t*)nullptr);
+        if constexpr (EPI == 2) {
+          float gv[8];
+          chunk_to_f(out, gv, (const bf16_t*)nullptr);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const bool keep = ok & (norelu | (fmaf(xf[e], sc[h][e], sh[h][e]) > 0.f));  // (no short circuit: selects)
+            const float dz = keep ? gv[e] : 0.f;
+            s1[h][e] += dz;
+            s2[h][e] = fmaf(dz, xf[e] - mu[h][e], s2[h][e]);
+          }
+        }
+      }
+      __builtin_amdgcn_raw_buffer_store_b128(u32x4{out.x, out.y, out.z, out.w}, rs_dx,
+                                             ok ? ((uint32_t)(m0 + r) * p.C + c8[h]) * 2u : kOob, 0, 0);
+    }
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) d0[ks] = d1[ks];
+#pragma unroll
+    for (int h = 0; h < NH; ++h) {
+      x0[h] = x1[h];
+      a0[h] = a1[h];
+    }
+  }
+  if constexpr (EPI == 2) {  // the 16 rows lanes of each channel group: xor 1, 2, 4, 8; lane i = 0 stores
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s1[h][e] += __shfl_xor(s1[h][e], o, 64);
+          s2[h][e] += __shfl_xor(s2[h][e], o, 64);
+        }
+    if (i == 0)
+#pragma unroll
+      for (int h = 0; h < NH; ++h)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int64_t o = ((int64_t)rb * p.C + c8[h] + e) * 2;
+          p.part[o] = s1[h][e];
+          p.part[o + 1] = s2[h][e];
+        }
+  }
+}
+
+// dgrad1x1_stream_kernel for this data gradient? (rn_set_tuning 27 = 1: never -- the 224-row tiles)
+bool d1_stream_ok(const rn_conv_desc* d, const float* clip) {
+  // (224-row BN partial blocks, as the tiles' with rn_set_tuning 9 = 0)
+  return g_tune[RN_TUNE_DGRAD_STREAM] != 1 && g_tune[RN_TUNE_IGEMM_ROWS] != 1 && !clip && d->dtype == RN_BF16 &&
+         d->groups <= 1 && d->r == 1 &&
+         d->s == 1 && d->stride_h == 1 && d->stride_w == 1 && d->pad_h == 0 && d->pad_w == 0 &&
+         d->c == d->c_real && d->c % 128 == 0 && d->k == d->k_pad && (d->k == 64 || d->k == 128) &&
+         (int64_t)d->n * d->h * d->w * d->c < INT32_MAX;
+}
+int d1_stream_launch(const rn_conv_desc* d, int epi, const void* dy, const void* w, void* dx, const void* add,
+                     const void* bn_x, const float* mean, const float* coef, const float* sc, const float* sh,
+                     int relu, float* part, hipStream_t st) {
+  D1Args a{};
+  a.dy = (const bf16_t*)dy; a.w = (const bf16_t*)w; a.dx = (bf16_t*)dx; a.add = (const bf16_t*)add;
+  a.bn_x = (const bf16_t*)bn_x; a.bn_mean = mean; a.coef = coef; a.bn_sc = sc; a.bn_sh = sh; a.part = part;
+  // 64 channels per wave where C % 256 == 0 (rn_set_tuning 27 = 2: 32), except the apply form (EPI 3), whose
+  // per-channel coefficients need the registers
+  const int nh = (epi != 3 && d->c % 256 == 0 && g_tune[RN_TUNE_DGRAD_STREAM] != 2) ? 2 : 1;
+  a.M = d->n * d->h * d->w; a.C = d->c; a.K = d->k; a.relu = relu; a.ncg = d->c / (128 * nh);
+  const dim3 grid((unsigned)(ceil_div(a.M, 224) * a.ncg));
+#define RN_D1N(KSV, AV, NHV)                                                                                  \
+  if (epi == 0) hipLaunchKernelGGL((dgrad1x1_stream_kernel<KSV, 0, AV, NHV>), grid, dim3(256), 0, st, a);    \
+  else if (epi == 2) hipLaunchKernelGGL((dgrad1x1_stream_kernel<KSV, 2, AV, NHV>), grid, dim3(256), 0, st, a); \
+  else hipLaunchKernelGGL((dgrad1x1_stream_kernel<KSV, 3, AV, 1>), grid, dim3(256), 0, st, a);
+#define RN_D1(KSV, AV)     \
+  if (nh == 2) {           \
+    RN_D1N(KSV, AV, 2)     \
+  } else {                 \
+    RN_D1N(KSV, AV, 1)     \
+  }
+  if (d->k == 64) {
+    if (add) {
+      RN_D1(2, 1)
+    } else {
+      RN_D1(2, 0)
+    }
+  } else if (add) {
+    RN_D1(4, 1)
+  } else {
+    RN_D1(4, 0)
+  }
+#undef RN_D1
+#undef RN_D1N
+  return rn_check_launch("dgrad1x1_stream");
+}
+
 }  // namespace
 
 extern "C" {
@@ -4251,6 +4501,13 @@ int rn_conv_bwd_data_bnred_clip(const rn_conv_desc* d, const void* dy, const voi
     return gd_launch(d, 1, dy, w_crsk, dx, add_src, as_stream(stream), &r);
   }
   if (band_ok(d) && !part && !add_src && !clip && dx) return band_launch(d, dy, w_crsk, dx, 1, as_stream(stream));
+  // (with the BN reduction only: the plain form -- epilogue 0, kept in the kernel for tests -- measured slower
+  // than the tiles, 121.8 -> 182.4 us on stage 1's shape, profiles/r06/ab_dgrad_stream)
+  if (part && d1_stream_ok(d, clip)) {
+    RN_CHECK_ARG(bn_x && bn_mean && bn_scale && bn_shift, "BN reduction needs x, mean, scale, shift");
+    return d1_stream_launch(d, 2, dy, w_crsk, dx, add_src, bn_x, bn_mean, nullptr, bn_scale, bn_shift, relu, part,
+                            as_stream(stream));
+  }
   IgemmArgs a = make_igemm_args(d, 1);
   a.x = dy; a.w = w_crsk; a.y = dx; a.add = add_src; a.bias = nullptr;
   if (part) {
@@ -4289,6 +4546,9 @@ int rn_conv_bwd_data_bnapply(const rn_conv_desc* d, const void* dy, const void* 
   RN_CHECK_ARG(d && dy && w_crsk && dx && bn_x && coef && bn_scale && bn_shift, "null argument");
   RN_CHECK_ARG(d->dtype == RN_BF16 && d->c % 8 == 0 && d->c == d->c_real, "bf16, whole 8-channel chunks");
   RN_CHECK_ARG(rn_conv_tile(d, 1) >= 128, "BatchNorm-backward-apply dgrad needs the 224/256-row tile");
+  if (d1_stream_ok(d, nullptr))
+    return d1_stream_launch(d, 3, dy, w_crsk, dx, add_src, bn_x, nullptr, coef, bn_scale, bn_shift, relu, nullptr,
+                            as_stream(stream));
   IgemmArgs a = make_igemm_args(d, 1);
   a.x = dy; a.w = w_crsk; a.y = dx; a.add = add_src; a.bias = nullptr;
   a.bn_x = bn_x; a.bn_coef = coef; a.bn_sc = bn_scale; a.bn_sh = bn_shift; a.bn_relu = relu;

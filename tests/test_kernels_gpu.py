@@ -1930,3 +1930,70 @@ def test_conv3x3_band_bnrelu_on_load(gpu, case):
         assert rel_err(from_nhwc(y, k), y_ref) < TOL[BF16]
     assert rel_err(from_nhwc(outs[0], k), from_nhwc(outs[1], k)) < 1e-2
 
+
+
+@pytest.mark.parametrize("width", [0, 2], ids=["cpw64", "cpw32"])
+@pytest.mark.parametrize("mode", ["reduce", "reduce_add", "reduce_only", "norelu", "apply", "apply_add"])
+@pytest.mark.parametrize("case", [
+    (3, 256, 14, 14, 64, 1, 1, 0),     # stage-1 conv1's data gradient (K = 64 into 256)
+    (2, 512, 9, 11, 128, 1, 1, 0),     # stage-2 conv1 (K = 128 into 512), ragged last row block
+    (5, 128, 7, 9, 64, 1, 1, 0),       # one 128-channel group, fewer rows than a block
+])
+def test_dgrad1x1_stream(gpu, case, mode, width):
+    """dgrad1x1_stream_kernel (the pre-activation units' conv1 data gradients streamed with the weights in
+    registers, with the BN-backward reduction or the BN backward applied; rn_set_tuning 27 = 1: the 224-row
+    tiles, 27 = 2: 32 channels per wave) against the tiles: dx BIT FOR BIT (the same MFMA
+    sums), the BN-backward partials' per-channel totals within fp32 summation-order rounding, and the
+    oracle's conv dgrad + BN(+ReLU) backward within the bf16 bar."""
+    n, c, h, w, k, r, st, pd = case
+    rng = np.random.default_rng(51)
+    d = conv_desc(BF16, n, c, h, w, k, r, r, st, pd)
+    xb = bf16_round(rng.standard_normal((n, c, h, w)) * 1.5 + 0.3)
+    wt = bf16_round(rng.standard_normal((k, c, r, r)) / np.sqrt(c * r * r))
+    dy = bf16_round(rng.standard_normal((n, k, h, w)))
+    res = bf16_round(rng.standard_normal((n, c, h, w)) * 0.5)
+    lib = L.load()
+    wc = torch.zeros(d.c * d.k_pad, dtype=torch.bfloat16, device=gpu)
+    L.call("rn_conv_weight_pack", C.byref(d), p(_master_krsc(wt, gpu)), None, p(wc), stream())
+    f = lambda a: torch.tensor(np.asarray(a, np.float64), dtype=torch.float32, device=gpu)
+    mean, sc, sh = f(rng.standard_normal(c) * 0.2), f(rng.uniform(0.5, 1.5, c)), f(rng.standard_normal(c) * 0.3)
+    coef = f(np.stack([rng.uniform(0.5, 1.5, c), rng.standard_normal(c) * 0.1, rng.standard_normal(c) * 0.05,
+                       rng.standard_normal(c) * 0.2], 1).ravel())
+    xbd, dyd, resd = to_nhwc(xb, BF16, gpu), to_nhwc(dy, BF16, gpu), to_nhwc(res, BF16, gpu)
+    nrb = lib.rn_conv_bnred_blocks(C.byref(d))
+    assert nrb == -(-n * h * w // 224)
+    relu = 0 if mode == "norelu" else 1
+    add = resd if mode.endswith("_add") else None
+    outs = []
+    try:
+        for val in (1, width):  # the tiles, then the streaming kernel
+            L.call("rn_set_tuning", 27, val)
+            part = torch.full((nrb * d.c * 2,), float("nan"), dtype=torch.float32, device=gpu)
+            dx = None if mode == "reduce_only" else torch.full_like(xbd, float("nan"))
+            if mode.startswith("apply"):
+                L.call("rn_conv_bwd_data_bnapply", C.byref(d), p(dyd), p(wc), p(dx), p(add), p(xbd), p(coef), p(sc),
+                       p(sh), relu, stream())
+            else:
+                L.call("rn_conv_bwd_data_bnred", C.byref(d), p(dyd), p(wc), p(dx), p(add), p(xbd), p(mean), p(sc),
+                       p(sh), relu, p(part), stream())
+            torch.cuda.synchronize()
+            outs.append((dx, part))
+    finally:
+        L.call("rn_set_tuning", 27, 0)
+    (dx0, p0), (dx1, p1) = outs
+    if dx0 is not None:
+        assert not torch.isnan(dx1).any()
+        assert torch.equal(dx0.view(torch.int16), dx1.view(torch.int16))
+    if mode.startswith("reduce") or mode == "norelu":
+        assert not torch.isnan(p1).any()
+        t0 = p0.view(nrb, d.c, 2).double().sum(0)
+        t1 = p1.view(nrb, d.c, 2).double().sum(0)
+        assert torch.allclose(t0, t1, rtol=1e-4, atol=1e-4 * float(t0.abs().max()))
+        # the oracle: dz = bf16(dgrad (+ add)) [x sc + sh > 0], sums of dz and dz (x - mean)
+        dact, _ = ops.conv2d_bwd(xb, wt, dy, (1, 1), (0, 0))
+        g = bf16_round(dact + (res if add is not None else 0))
+        xs = xb * sc.cpu().numpy()[None, :, None, None] + sh.cpu().numpy()[None, :, None, None]
+        dz = g * (xs > 0) if relu else g
+        ref_s = dz.sum((0, 2, 3))
+        ref_q = (dz * (xb - mean.cpu().numpy()[None, :, None, None])).sum((0, 2, 3))
+        assert rel_err(t1[:, 0].cpu().numpy(), ref_s) < 1e-2 and rel_err(t1[:, 1].cpu().numpy(), ref_q) < 1e-2
