@@ -466,24 +466,9 @@ def main():
     pinned = mx.io.DataBatch(data=[mx.nd.array(data, ctx=mx.Context("cpu_pinned", 0))],
                              label=[mx.nd.array(label, ctx=mx.Context("cpu_pinned", 0))])
 
-    # RN_MAIN_PRIORITY=1: the data-gradient chain on a high-priority stream when the weight
-    # gradients run beside it, so the hardware prefers the chain's workgroups. Off by default: with
-    # the weight gradients' grids sized for part of the chip (rn_set_tuning 21) equal priorities
-    # measure faster (profiles/r04/priority: C2 -0.7 %, C4 -1.7 %, C5 -0.6 %)
-    main_stream = None
-    if getattr(ex, "_side_stream", None) is not None and os.environ.get("RN_MAIN_PRIORITY", "0") == "1":
-        lo, hi = torch.cuda.Stream.priority_range()
-        main_stream = torch.cuda.Stream(priority=min(lo, hi))
-        torch.cuda.synchronize()
-
-    def step(feed=pinned if a.host_input else None, on_current=False):
-        if main_stream is not None and not on_current:
-            with torch.cuda.stream(main_stream):
-                mod.forward(feed, is_train=True)
-                mod.backward()
-                mod.update()
-            torch.cuda.current_stream().wait_stream(main_stream)
-            return
+    # (the data-gradient chain on a high-priority stream -- RN_MAIN_PRIORITY, rounds 3-5 -- measured slower since the
+    # weight gradients' grids were sized for part of the chip, profiles/r04/priority: removed in round 6)
+    def step(feed=pinned if a.host_input else None):
         mod.forward(feed, is_train=True)
         mod.backward()
         mod.update()
@@ -516,19 +501,13 @@ def main():
         # the whole training step (forward, backward, SGD, weight repack) as ONE HIP graph:
         # removes the per-launch gaps between the ~580 kernels of a step; same kernels, same work
         graph = torch.cuda.CUDAGraph()
-        # (on the capture stream itself -- the high-priority one when there is one; the side stream
-        # joins the capture by the fork events)
-        with torch.cuda.graph(graph, stream=main_stream):
-            step(on_current=True)
+        # (a side stream joins the capture by the fork events)
+        with torch.cuda.graph(graph):
+            step()
         torch.cuda.synchronize()
 
         def replay():
-            if main_stream is not None:
-                with torch.cuda.stream(main_stream):
-                    graph.replay()
-                torch.cuda.current_stream().wait_stream(main_stream)
-            else:
-                graph.replay()
+            graph.replay()
         replay()  # one untimed replay
         torch.cuda.synchronize()
         run = replay

@@ -365,23 +365,11 @@ class Plan:
         # 22.17 ms per step on one box; RN_BN_APPLY_FUSION=0 writes act1 / act3
         if os.environ.get("RN_BN_APPLY_FUSION", "1") != "1":
             return
-        # the 3x3 stride-1 consumers too (act2 -> conv2, symbol/resnet.py:19-21) where the weight gradient
-        # is the image-band kernel (stage 1: C = K = 64), which transforms its staged x images in place;
-        # the forward's 64-column tile applies it on load from a register table (bf16).
-        # Opt-in (RN_BN_APPLY_FUSION_3X3=1). Round 4 measured the 64-column tile's per-K-tile transform 0.6 %
-        # slower per step, and stages 2-4 on the 224-row tiles and the band weight gradients 4 % slower
-        # (r04c); with round 5's image-band forward (conv3x3c64_band_kernel transforms each landed band once
-        # in LDS) it measures equal (20.04 / 20.03 / 20.01 vs 20.05 / 20.01 / 20.02 ms), so act2 stays written.
-        band3 = self.dtype == BF16 and os.environ.get("RN_BN_APPLY_FUSION_3X3", "0") == "1"
-
+        # (the 3x3 stride-1 consumers too -- act2 -> conv2 of stage 1, RN_BN_APPLY_FUSION_3X3, rounds 4-5 -- measured
+        # 0.6 % slower, then equal with the image-band forward: removed in round 6; the band kernels keep their
+        # BN+ReLU-on-load forms, kernel-tested)
         def xf_ok(u):
-            if u.groups != 1 or getattr(u, "qweight", None):
-                return False
-            if tuple(u.kernel) == (1, 1):
-                return True
-            c, k, w = u.x.c, u.y.c, u.x.w
-            return (band3 and tuple(u.kernel) == (3, 3) and tuple(u.stride) == (1, 1) and tuple(u.pad) == (1, 1)
-                    and c == k and u.x.cp == c and u.y.cp == k and c == 64 and w <= 56)
+            return u.groups == 1 and not getattr(u, "qweight", None) and tuple(u.kernel) == (1, 1)
         for bn in self.ops:
             if bn.kind != "bn" or not bn.relu or id(bn.y) in out_ids:
                 continue
@@ -1307,10 +1295,10 @@ class Executor:
         if getattr(op, "int8", False) and mode == 0:  # the int8 forward's tile (its dgrad is the bf16 one)
             x, y = op.x, op.y
             d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad, op.groups)
-            mc = min_cols if min_cols is not None else int(os.environ.get("RN_BN_FUSION_MIN_COLS", "128"))
+            mc = min_cols if min_cols is not None else 128
             return int(self.lib.rn_conv_tile(L.C.byref(d), 2)) >= mc
-        if min_cols is None:  # RN_BN_FUSION_MIN_COLS=64: also on the 64-column tile (opt-in: measured
-            min_cols = int(os.environ.get("RN_BN_FUSION_MIN_COLS", "128"))  # 0.6 % slower per step)
+        if min_cols is None:  # (64, the 64-column tile too -- RN_BN_FUSION_MIN_COLS -- measured 0.6 % slower per step)
+            min_cols = 128
         x, y = op.x, op.y
         d = self._conv_desc(x.n, x.h, x.w, x.cp, x.c, y.c, op.kernel, op.stride, op.pad, op.groups)
         return int(self.lib.rn_conv_tile(L.C.byref(d), mode)) >= min_cols
@@ -1432,18 +1420,6 @@ class Executor:
                               self.wgrad_ws_bytes, sp)
         return self._call("rn_conv_bwd_filter", L.C.byref(d), x, dy, dw, sp)
 
-    def _bn_recompute_ok(self, op, cop, cadd):
-        """May the BatchNorm `op`, whose output gradient the data gradient of conv `cop` completes, take
-        its backward from a recomputed dgrad (rn_conv_bwd_data_bnapply)? Where that dgrad is cheap: bf16,
-        a dense 1x1 stride-1 convolution reducing over at most half the BN's channels (the
-        pre-activation units' conv1, symbol/resnet.py:17-20), the only writer of the gradient (no fan-in
-        add), on the 224/256-row tile."""
-        d = cop.desc
-        return (self.dtype == L.RN_BF16 and cadd is None and not op.desc.clip and d.groups <= 1 and d.r == 1 and d.s == 1
-                and d.stride_h == 1 and d.stride_w == 1 and d.pad_h == 0 and d.pad_w == 0 and 2 * d.k <= d.c
-                and d.c == d.c_real and d.c % 8 == 0 and op.y.c == d.c
-                and int(self.lib.rn_conv_tile(L.C.byref(d), 1)) >= 128)
-
     def _quant_groups(self):
         """{id(bn): (bn, [quant ops])} for the BatchNorm+ReLU outputs that only activation quantizers
         (Quantization_int8 of data, the int8 graph) read -- one, or two (symbol/resnet_int8.py: a stage's
@@ -1487,8 +1463,6 @@ class Executor:
             if op.kind == "bn":
                 op.qpair = False
                 op.qorder = []  # the folded quantizers in backward order (their gradients' pending order)
-                op.qwriters = []  # (a pair) the last writer of each one's gradient (self._gw entries)
-                op.pair_fused = None
         for bn, qs in groups.values():
             if len(qs) == 1:
                 bn.desc.clip = self._ap(qs[0].q["minmax"]).value  # (the threshold the forward just updated)
@@ -1503,13 +1477,10 @@ class Executor:
                 op.pre_part = None  # set by the residual add's fused ReLU backward (this build)
         bwd_fusion = os.environ.get("RN_BN_BWD_FUSION", "1") in ("1", "2")
         bwd_all = os.environ.get("RN_BN_BWD_FUSION", "1") == "2"
-        # BN backward applied by a recomputed cheap dgrad (rn_conv_bwd_data_bnapply), opt-in
-        # (RN_BN_BWD_RECOMPUTE=1): bit-identical, but measured 22.18 vs 21.45 ms per step
-        recompute = os.environ.get("RN_BN_BWD_RECOMPUTE", "0") == "1"
-        # a quantizer pair's clips and BN reduction in the later data gradient's epilogue
-        # (rn_conv_bwd_data_bnred_clip2), opt-in (RN_QUANT_PAIR_FUSION=1): parity-green but measured
-        # neutral (C5 22.68 / 22.69 vs 22.69 / 22.68 ms) -- default rn_bn_bwd with dy / dy2
-        pair_fusion = bwd_fusion and os.environ.get("RN_QUANT_PAIR_FUSION", "0") == "1"
+        # (removed in round 6, each measured slower or neutral, their kernels kept and kernel-tested: the BN backward
+        # applied by a recomputed dgrad, RN_BN_BWD_RECOMPUTE -- rn_conv_bwd_data_bnapply; 19.78 vs 19.43 ms with the
+        # streamed conv1 data gradients --, and a quantizer pair's clips folded into the later data gradient,
+        # RN_QUANT_PAIR_FUSION -- rn_conv_bwd_data_bnred_clip2; C5 22.68 / 22.69 vs 22.69 / 22.68 ms)
         # one workspace for the weight gradients' split-M partial tiles (rn_conv_bwd_filter_ws),
         # sized for the largest layer. Shared safely because every call using it is a weight-gradient
         # call, and those all run in plan order on ONE stream (the side stream when it is on:
@@ -1562,19 +1533,6 @@ class Executor:
                 if len(pend) == 2:
                     op.desc.clip2 = self._ap(op.qorder[1].q["minmax"]).value
                     op.desc.dy2 = self._p(pend[1]).value
-                    ws_ = op.qwriters
-                    ok = pair_fusion and self.dtype == BF16 and op.relu and op.y.c % 8 == 0 and \
-                        op.y.c == op.y.cp and len(ws_) == 2 and \
-                        all(w and w[0] == "dgrad" and w[5] is None and w[4] is b for w, b in zip(ws_, pend))
-                    if ok:
-                        late = 0 if ws_[0][1] > ws_[1][1] else 1
-                        lw = ws_[late]
-                        ok = lw[2].desc.groups <= 1 and int(self.lib.rn_conv_tile(L.C.byref(lw[2].desc), 1)) >= 64
-                    if ok:
-                        # the later dgrad stores both clipped gradients' sum and reduces the BN from it
-                        op.pair_fused = (lw, ws_[1 - late], op.qorder[late], op.qorder[1 - late])
-                        dy = lw[4]
-                        op.desc.clip = op.desc.clip2 = op.desc.dy2 = 0
             else:
                 dy = gs.read(op.y) if op.kind != "softmax" else None
             if dy is None:
@@ -1690,19 +1648,6 @@ class Executor:
                                                 self._p(dy), self._p(out), self._p(add), self._pp(op.gamma),
                                                 self._ap(op.mean), self._ap(op.var), op.sc, op.sh,
                                                 self._gp(op.gamma), self._gp(op.beta), wsp, sp))
-                elif op.pair_fused is not None:
-                    lw, ew, lq, eq = op.pair_fused
-                    _, ci, cop, cdy, cout, _ = lw
-                    op.bnred_blocks = int(self.lib.rn_conv_bnred_blocks(L.C.byref(cop.desc)))
-                    op.bnred = self._zeros(op.bnred_blocks * op.y.cp * 2, self.torch.float32)
-                    self._bwd[ci] = self._call("rn_conv_bwd_data_bnred_clip2", L.C.byref(cop.desc), self._p(cdy),
-                                               self._p(cop.wc), self._p(cout), self._p(ew[4]), self._p(self.act(x)),
-                                               op.sm, op.sc, op.sh, self._ap(lq.q["minmax"]),
-                                               self._ap(eq.q["minmax"]), self._p(op.bnred), sp)
-                    self._bwd.append(self._call("rn_bn_bwd_part", L.C.byref(op.desc), self._p(op.bnred),
-                                                op.bnred_blocks, self._p(self.act(x)), self._p(dy), self._p(out),
-                                                self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc, op.sh,
-                                                self._gp(op.gamma), self._gp(op.beta), wsp, sp))
                 elif bwd_fusion and not op.desc.dy2 and w and w[0] == "dgrad" and dy is w[4] and \
                         op.y.c % 8 == 0 and op.y.c == op.y.cp and \
                         (bwd_all or self._big_tile(w[2], 1) or self._grouped_fuse(w[2], 1)) and \
@@ -1712,36 +1657,20 @@ class Executor:
                     _, ci, cop, cdy, cout, cadd = w
                     op.bnred_blocks = int(self.lib.rn_conv_bnred_blocks(L.C.byref(cop.desc)))
                     op.bnred = self._zeros(op.bnred_blocks * op.y.cp * 2, self.torch.float32)
-                    if recompute and self._bn_recompute_ok(op, cop, cadd):
-                        # the dgrad is cheap (1x1, reduction over fewer channels than the BN has): pass 1
-                        # only reduces (its BN-width output is never written), finalize, then the same
-                        # dgrad recomputed with the BN backward applied in its epilogue (bit-identical)
-                        op.coef = self._zeros(4 * op.y.cp, self.torch.float32)
-                        self._bwd[ci] = self._call("rn_conv_bwd_data_bnred", L.C.byref(cop.desc), self._p(cdy),
-                                                   self._p(cop.wc), None, None, self._p(self.act(x)), op.sm, op.sc,
-                                                   op.sh, int(op.relu), self._p(op.bnred), sp)
-                        self._bwd.append(self._call("rn_bn_bwd_finalize", L.C.byref(op.desc), self._p(op.bnred),
-                                                    op.bnred_blocks, self._pp(op.gamma), op.sm, op.si,
-                                                    self._gp(op.gamma), self._gp(op.beta), self._p(op.coef), sp))
-                        self._bwd.append(self._call("rn_conv_bwd_data_bnapply", L.C.byref(cop.desc), self._p(cdy),
-                                                    self._p(cop.wc), self._p(out), self._p(add), self._p(self.act(x)),
-                                                    self._p(op.coef), op.sc, op.sh, int(op.relu), sp))
-                        op.recomputed = True
+                    if op.desc.clip:  # (a folded quantizer straight-through clip)
+                        self._bwd[ci] = self._call("rn_conv_bwd_data_bnred_clip", L.C.byref(cop.desc),
+                                                   self._p(cdy), self._p(cop.wc), self._p(cout), self._p(cadd),
+                                                   self._p(self.act(x)), op.sm, op.sc, op.sh, int(op.relu),
+                                                   L.C.c_void_p(op.desc.clip), self._p(op.bnred), sp)
                     else:
-                        if op.desc.clip:  # (a folded quantizer straight-through clip)
-                            self._bwd[ci] = self._call("rn_conv_bwd_data_bnred_clip", L.C.byref(cop.desc),
-                                                       self._p(cdy), self._p(cop.wc), self._p(cout), self._p(cadd),
-                                                       self._p(self.act(x)), op.sm, op.sc, op.sh, int(op.relu),
-                                                       L.C.c_void_p(op.desc.clip), self._p(op.bnred), sp)
-                        else:
-                            self._bwd[ci] = self._call("rn_conv_bwd_data_bnred", L.C.byref(cop.desc), self._p(cdy),
-                                                       self._p(cop.wc), self._p(cout), self._p(cadd),
-                                                       self._p(self.act(x)), op.sm, op.sc, op.sh, int(op.relu),
-                                                       self._p(op.bnred), sp)
-                        self._bwd.append(self._call("rn_bn_bwd_part", L.C.byref(op.desc), self._p(op.bnred),
-                                                    op.bnred_blocks, self._p(self.act(x)), self._p(dy), self._p(out),
-                                                    self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc, op.sh,
-                                                    self._gp(op.gamma), self._gp(op.beta), wsp, sp))
+                        self._bwd[ci] = self._call("rn_conv_bwd_data_bnred", L.C.byref(cop.desc), self._p(cdy),
+                                                   self._p(cop.wc), self._p(cout), self._p(cadd),
+                                                   self._p(self.act(x)), op.sm, op.sc, op.sh, int(op.relu),
+                                                   self._p(op.bnred), sp)
+                    self._bwd.append(self._call("rn_bn_bwd_part", L.C.byref(op.desc), self._p(op.bnred),
+                                                op.bnred_blocks, self._p(self.act(x)), self._p(dy), self._p(out),
+                                                self._p(add), self._pp(op.gamma), op.sm, op.si, op.sc, op.sh,
+                                                self._gp(op.gamma), self._gp(op.beta), wsp, sp))
                 elif bwd_fusion and not op.desc.dy2 and not op.desc.clip and w and w[0] == "pool" and dy is w[4] and \
                         op.y.c == op.y.cp and self.dtype == BF16 and os.environ.get("RN_POOL_BN_FUSION", "1") == "1" and \
                         int(self.lib.rn_pool_bwd_bnred_blocks(L.C.byref(w[2].desc))) > 0:
@@ -1793,7 +1722,6 @@ class Executor:
                     bn = folds[id(op)]
                     bn.qorder.append(op)
                     if bn.qpair:
-                        bn.qwriters.append(self._gw.get(id(op.y)))
                         self._gw[id(op.x)] = ("other",)
                     elif id(op.y) in self._gw:
                         self._gw[id(op.x)] = self._gw[id(op.y)]

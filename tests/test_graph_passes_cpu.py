@@ -197,21 +197,12 @@ def test_int8_forward_plan(dry, monkeypatch):
     assert all(op.qsrc.codes_wgrad == (not (op.name.startswith("stage1") and op.name.endswith("conv2")))
                for op in ex.plan.ops if op.kind == "conv")
     assert "rn_conv_bwd_filter_i8" in ex.WGRAD_CALLS  # (routed to the side stream by name, _route_wgrads)
-    # the stage-first units' act1 quantizer pairs (stages 2-4; stage 1's dgrads run the 128-row kernel),
-    # opt-in RN_QUANT_PAIR_FUSION=1: both clips and the BN reduction in the later data gradient's
-    # epilogue, then rn_bn_bwd_part
-    monkeypatch.setenv("RN_QUANT_PAIR_FUSION", "1")
-    ex = _bind(graphs.resnet_int8(*R50_SMALL.values()), shape, precision="bfloat16").executor
-    bn = _call_names(ex._bwd)
-    pairs = [op for op in ex.plan.ops if op.kind == "bn" and op.qpair]
-    fused = [op for op in pairs if op.pair_fused is not None]
-    assert len(pairs) == 4 and len(fused) == 3 and bn.count("rn_conv_bwd_data_bnred_clip2") == 3
-    assert all(not op.desc.dy2 and not op.desc.clip for op in fused)
-    monkeypatch.setenv("RN_QUANT_PAIR_FUSION", "0")
+    # the stage-first units' act1 quantizer pairs: both clips folded into their BN's backward (rn_bn_desc.clip /
+    # clip2 / dy2; the opt-in fold into the later data gradient, RN_QUANT_PAIR_FUSION, was removed in round 6)
     ex0 = _bind(graphs.resnet_int8(*R50_SMALL.values()), shape, precision="bfloat16").executor
     assert "rn_conv_bwd_data_bnred_clip2" not in _call_names(ex0._bwd)
-    assert all(op.desc.dy2 for op in ex0.plan.ops if op.kind == "bn" and op.qpair)
-    monkeypatch.delenv("RN_QUANT_PAIR_FUSION")
+    pairs = [op for op in ex0.plan.ops if op.kind == "bn" and op.qpair]
+    assert len(pairs) == 4 and all(op.desc.dy2 for op in pairs)
     monkeypatch.setenv("RN_QUANT_CODES_WGRAD", "0")
     ex = _bind(graphs.resnet_int8(*R50_SMALL.values()), shape, precision="bfloat16").executor
     assert not any(op.codes_wgrad for op in ex.plan.ops if op.kind == "quant")

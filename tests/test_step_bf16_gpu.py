@@ -273,21 +273,6 @@ def _c5_layerwise(n, image):
     return ck
 
 
-def test_resnet50_bf16_layerwise_act2_on_load(gpu, monkeypatch):
-    """The opt-in act2 fusion (RN_BN_APPLY_FUSION_3X3=1: stage 1's bn2+ReLU applied on load by conv2's
-    image-band forward and its image-band weight gradient, act2 never written), per kernel at 8 images of
-    112x112 with the C2 bars."""
-    from rn import graphs
-    monkeypatch.setenv("RN_BN_APPLY_FUSION_3X3", "1")
-    ck = _layerwise(graphs.resnet50(), 8, 112, "bfloat16")
-    assert not ck.skipped, ck.skipped
-    fused = [op for op in ck.ex.plan.ops if op.kind == "bn" and op.name.startswith("stage1") and op.name.endswith("bn2")]
-    assert fused and all(op.apply_fused for op in fused)
-    assert ck.covered.get("rn_conv_bwd_filter_x", 0) >= 3 + 36  # the three fused conv2 weight gradients too
-    bad = ck.failures()
-    assert not bad, bad[:10]
-
-
 def test_resnext50_bf16_layerwise_small(gpu):
     """The C4 per-kernel checks at 8 images of 64x64 (a fast first gate before the full size)."""
     _c4_layerwise(8, 64)
@@ -296,15 +281,6 @@ def test_resnext50_bf16_layerwise_small(gpu):
 def test_resnet50_int8_layerwise_small(gpu):
     """The C5 per-kernel checks at 8 images of 64x64 (a fast first gate before the full size)."""
     _c5_layerwise(8, 64)
-
-
-def test_resnet50_int8_layerwise_pair_fusion(gpu, monkeypatch):
-    """The opt-in quantizer-pair fusion (RN_QUANT_PAIR_FUSION=1: the stage-first units' two act1
-    quantizers' clips and the BN reduction in the later data gradient's epilogue,
-    rn_conv_bwd_data_bnred_clip2), per kernel at 8 images of 112x112."""
-    monkeypatch.setenv("RN_QUANT_PAIR_FUSION", "1")
-    ck = _c5_layerwise(8, 112)
-    assert ck.covered.get("rn_conv_bwd_data_bnred_clip2", 0) == 3
 
 
 def test_resnet50_fp32_layerwise(gpu):

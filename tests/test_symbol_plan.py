@@ -113,7 +113,7 @@ def test_executor_dry_run(dtype):
     assert names.count("rn_stem_conv_wgrad_p4") == (0 if dtype == "float32" else 1)
     assert sum(n.startswith("rn_conv_bwd_data") for n in names) == 53
     # BN-backward reductions fused where the dgrad runs the 256-row tile (bf16 only)
-    # (the 224-row tiles' dgrads; RN_BN_FUSION_MIN_COLS=64 adds the 64-column tile's 3 stage-1 ones)
+    # (the 224-row tiles' dgrads)
     assert names.count("rn_conv_bwd_data_bnred") == (0 if dtype == "float32" else 41)
     assert names.count("rn_stem_shift_grad") == 1
     # every parameter's gradient has a producing call, buckets cover the flat buffer in order
