@@ -11,7 +11,8 @@ Rank 0 prints ONE JSON line (contract in the task statement), including
   roofline     : the dominant kernel family (most kernel time per step in a serialised calibration
                  step; every family's time is listed) -- algorithmic FLOP and bytes per launch /
                  average launch duration from HIP events around every launch of that family on the
-                 stream it runs on (eager mode: inside the timed region; HIP-graph mode: in one eager
+                 stream it runs on (eager mode: the last of the K timed steps -- the event packets cost
+                 ~1.7 % of a step, so the other K - 1 run without them; HIP-graph mode: in one eager
                  step right after it, graph nodes carry no timing events); "bound" from the family's
                  algorithmic FLOP/byte vs the 312.5 FLOP/B ridge (2.5 PF bf16 / 8 TB/s), both the MFMA
                  and the HBM fraction reported
@@ -512,19 +513,28 @@ def main():
         torch.cuda.synchronize()
         run = replay
     else:
-        for t in timers.values():  # HIP events around every launch of the reported families, in the timed region
-            t.wrap()
         run = step
 
     reducer = mod._reducer
-    if reducer is not None and not use_graph:
-        reducer.timing = True  # overlap evidence: HIP events at the backward's ends and each bucket
-        reducer.records = []
+
+    def instrument():
+        # HIP events around every launch of the reported families (and, with RCCL, at the backward's ends and
+        # each bucket: the overlap evidence) on the LAST timed step only: each event record is a packet of
+        # its own between two kernels, and on every step they cost ~0.34 ms (1.7 %) of a ResNet-50 step
+        # (profiles/r06/event_gaps: 19.26 ms eager without them, 19.60 with)
+        for t in timers.values():
+            t.wrap()
+        if reducer is not None:
+            reducer.timing = True
+            reducer.records = []
+
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for i in range(a.steps):
+        if i == a.steps - 1 and not use_graph:
+            instrument()
         run()
     torch.cuda.synchronize()
     if world > 1:
@@ -610,7 +620,9 @@ def main():
             "weight_gradients": roof.get(wg),
             "outputs_finite": finite,
             "hip_graph": bool(use_graph),
-            "inputs": "pinned host batch copied every step (PCIe-inclusive)" if a.host_input else
+            "family_timing": ("one eager step right after the timed region" if use_graph else
+                              "HIP events on the last of the %d timed steps" % a.steps),
+            "inputs":"pinned host batch copied every step (PCIe-inclusive)" if a.host_input else
                       "resident in HBM",
             "pcie_inclusive": pcie,
         }

@@ -75,7 +75,9 @@ def test_bench_gpus2_runs_two_ranks(gpu):
     for key in ("exposed_ms", "exposed_ms_max_over_ranks", "backward_ms", "comm_window_ms",
                 "bucket_launch_offsets_ms", "bus_gbs", "bytes_per_step", "steps_timed"):
         assert key in ar, key
-    assert ar["steps_timed"] == 3 and len(ar["bucket_launch_offsets_ms"]) == ar["buckets"]
+    # (the event records ride on the last timed step only: on every step they cost ~1.7 % of it)
+    assert ar["steps_timed"] == 1 and len(ar["bucket_launch_offsets_ms"]) == ar["buckets"]
+    assert out["family_timing"] == "HIP events on the last of the 3 timed steps"
     offs = ar["bucket_launch_offsets_ms"]
     # the first bucket leaves during the backward (the same step's: two ranks sharing one GPU vary a lot)
     assert offs == sorted(offs) and offs[0] < ar["backward_ms_last"]

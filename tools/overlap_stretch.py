@@ -30,7 +30,9 @@ def main(path):
     if not calib or not timed:
         print("no calibration / timed step found", len(steps))
         return
-    cal, last = calib[-1], timed[-1]
+    # (the step before the last timed one when there is one: bench.py's last timed step carries the HIP
+    # event packets that time the kernel families)
+    cal, last = calib[-1], timed[-2] if len(timed) >= 2 else timed[-1]
     qcount = defaultdict(int)
     for r in last:
         qcount[r["Queue_Id"]] += 1

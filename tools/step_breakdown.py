@@ -1,4 +1,4 @@
-"""Per-kernel breakdown of the LAST training step in a rocprofv3 kernel trace (steps end with the
+"""Per-kernel breakdown of the LAST uninstrumented training step in a rocprofv3 kernel trace (steps end with the
 SGD kernel). usage: python tools/step_breakdown.py gpurun_out/prof_<tag>/run_kernel_trace.csv"""
 import collections
 import csv
@@ -10,7 +10,10 @@ def main(path):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if "sgd_mom" in r["Kernel_Name"]]
-    a, b = idx[-2] + 1, idx[-1] + 1
+    # the step before the last when there is one: bench.py's last timed step carries the HIP event
+    # packets that time the kernel families (gaps of their own around every launch they wrap)
+    k = -2 if len(idx) >= 3 else -1
+    a, b = idx[k - 1] + 1, idx[k] + 1
     fam = collections.defaultdict(float)
     cnt = collections.Counter()
     for r in rows[a:b]:

@@ -1,4 +1,4 @@
-"""Per-queue busy time and idle gaps over the LAST training step of a rocprofv3 kernel trace (steps end
+"""Per-queue busy time and idle gaps over the LAST uninstrumented training step of a rocprofv3 kernel trace (steps end
 with the SGD kernel): how much of the step each HIP stream (queue) is busy, and the main queue's gaps.
 usage: python tools/stream_util.py gpurun_out/prof_<tag>/run_kernel_trace.csv"""
 import collections
@@ -11,7 +11,10 @@ def main(path):
     rows = list(csv.DictReader(open(path)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     idx = [i for i, r in enumerate(rows) if "sgd_mom" in r["Kernel_Name"]]
-    a, b = idx[-2] + 1, idx[-1] + 1
+    # the step before the last when there is one: bench.py's last timed step carries the HIP event
+    # packets that time the kernel families (gaps of their own around every launch they wrap)
+    k = -2 if len(idx) >= 3 else -1
+    a, b = idx[k - 1] + 1, idx[k] + 1
     step = rows[a:b]
     t0 = int(step[0]["Start_Timestamp"])
     t1 = max(int(r["End_Timestamp"]) for r in step)
