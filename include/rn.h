@@ -628,10 +628,11 @@ const char* rn_last_error(void);
  *      s_setprio 1 for the whole kernel; default off), 2 = the 224-row tiles issue the DMAs of the A
  *      rows past the tile too (default: skipped, those rows are never read),
  * 21 = the CUs the weight gradients size their split-M grids for, in percent of the device's (default
- *      45; 0 = 100): fewer splits, fewer partial slabs to reduce, for kernels that share the chip with
+ *      50; 0 = 100): fewer splits, fewer partial slabs to reduce, for kernels that share the chip with
  *      the data-gradient stream (measured, ResNet-50 at batch 256: 100 % 20.83 / 20.80 ms per step,
  *      75 % 20.74, 50 % 20.09 / 20.04, 25 % 23.85; on another box 55 % 21.01 / 21.03, 50 % 20.63 /
- *      20.60, 45 % 20.48 / 20.44, 40 % 20.67). Set before the workspaces are sized
+ *      20.60, 45 % 20.48 / 20.44, 40 % 20.67; round 6, timed without event packets: 50 % 18.82 / 18.83,
+ *      45 % 19.08 / 19.03, 55 % 18.95). Set before the workspaces are sized
  *      (rn_conv_wgrad_ws_bytes),
  * 23 = the same percent for the grouped image-band weight gradients only (0 = key 21's),
  * 24 = 1: rn_bn_fwd_train_part always merges and finalizes in two launches (default 0: one launch where

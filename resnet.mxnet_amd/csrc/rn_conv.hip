@@ -31,9 +31,10 @@ int chip_cus() {
   return cus;
 }
 // CUs the weight gradients size their split-M grids for: the chip, scaled by rn_set_tuning 21 (percent,
-// default 45; 0 = 100). They share the chip with the data-gradient chain on the other stream: half the
+// default 50; 0 = 100). They share the chip with the data-gradient chain on the other stream: half the
 // splits halve the partial slabs written and reduced, and the data gradients keep more of the CUs
-// (ResNet-50: 100 % 20.83, 50 % 20.09 ms per step, 45 % 0.8 % below 50; a quarter starves the weight
+// (ResNet-50: 100 % 20.83, 50 % 20.09 ms per step; 45 % 0.8 % below 50 with HIP events in every step, 1.2 %
+// above it without them, round 6; a quarter starves the weight
 // gradients: 23.85)
 int wgrad_cus() {
   const int pct = g_tune[RN_TUNE_WGRAD_SPLIT] > 0 ? g_tune[RN_TUNE_WGRAD_SPLIT] : 100;
@@ -2572,7 +2573,7 @@ __global__ __launch_bounds__(256) void wgrad_slab_reduce_kernel(const float* __r
   }
 }
 
-// The same sum for at most 16 splits (the split-M grids sized for 45 % of the chip give 1-16): one
+// The same sum for at most 16 splits (the split-M grids sized for 45-50 % of the chip give 1-16): one
 // thread per float4 column, every split's load in flight at once, added in split order onto dw --
 // the value wgrad_slab_reduce_kernel stores (its 16 group sums are then the splits themselves and
 // zeros; the one trailing + 0 reproduces its sign of a zero sum). The general kernel left 15/16 of its

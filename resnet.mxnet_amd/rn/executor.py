@@ -669,7 +669,8 @@ class Executor:
             self._side_stream = torch.cuda.Stream(device=self.device)
         # the weight gradients' split-M grids: part of the chip when they overlap the data-gradient chain,
         # all of it when they run serialised (before the plan sizes its workspace from the same key)
-        # (45 % for every graph: 40 % measured equal on ResNeXt-50, 27.47 vs 27.48 ms per step, round 5)
+        # (50 % for every graph; round 6, one box, timed steps without event packets: C2 18.82 / 18.83 vs
+        # 19.08 / 19.03 ms at 45 %, 55 % 18.95 / 18.98, 60 % 18.97, 70 % 19.00; C4 26.79 vs 27.01, C5 21.23 vs 21.32)
         self.wgrad_split_pct = L.WGRAD_SPLIT_OVERLAPPED
         L.set_wgrad_split(os.environ.get("RN_WGRAD_STREAM", "1") == "1", self.wgrad_split_pct)
         self._side_idx = set()

@@ -193,14 +193,14 @@ def load(auto_build=True):
 
 
 USER_TUNED = set()  # rn_set_tuning keys fixed by RN_TUNE: the executor leaves them alone
-WGRAD_SPLIT_OVERLAPPED = 45  # rn_set_tuning 21 with the weight gradients on the side stream (percent of the chip)
+WGRAD_SPLIT_OVERLAPPED = 50  # rn_set_tuning 21 with the weight gradients on the side stream (percent of the chip)
 _DETERMINISTIC = [False]  # rn_set_tuning 17 as set through this module (RN_DETERMINISTIC, RN_TUNE, call())
 
 
 def set_wgrad_split(overlapped, pct=None):
     """rn_set_tuning 21 -- the share of the chip the split-M weight gradients size their grids for -- by how
-    the executor runs them: `pct` (default 45 %) beside the data-gradient chain on the side stream
-    (measured, DESIGN.md rounds 4-5), the whole chip when they run serialised on the compute stream
+    the executor runs them: `pct` (default 50 %) beside the data-gradient chain on the side stream
+    (measured, DESIGN.md rounds 4-6), the whole chip when they run serialised on the compute stream
     (RN_WGRAD_STREAM=0). An RN_TUNE=21=... override wins. Launches clamp their split to the workspace the
     plan sized. The key is process-global and the split count fixes the fp32 summation order of the weight
     gradients, so outside the deterministic mode a serialised step (bench.py's calibration) does not give
