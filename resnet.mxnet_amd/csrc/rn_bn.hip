@@ -16,7 +16,7 @@
 // 16-byte chunk loads / stores of the streaming BatchNorm passes, NT = rn_set_tuning 18 bit mask:
 // 1 = nontemporal stores, 2 = nontemporal loads (the streaming hint: lines are evicted first, so
 // fewer dirty lines are left for the kernel-boundary L2 write-back and the other stream's tiles keep
-// their L2 share).
+// their L2 share); 4 = write-through stores instead (the apply passes with rn_set_tuning 18 bit 32).
 typedef unsigned int rn_u32x4 __attribute__((ext_vector_type(4)));
 template <int NT>
 __device__ __forceinline__ uint4 ld16(const void* p) {
@@ -29,7 +29,13 @@ __device__ __forceinline__ uint4 ld16(const void* p) {
 }
 template <int NT>
 __device__ __forceinline__ void st16(void* p, uint4 v) {
-  if constexpr ((NT & 1) != 0) {
+  if constexpr ((NT & 4) != 0) {
+    // write-through (sc1): the line leaves no dirty copy in the XCD's L2 for the end-of-kernel write-back
+    // (rn_set_tuning 18 bit 32). Asm the compiler does not see: the nop keeps its next instruction off the
+    // data registers until the store has read them
+    const rn_u32x4 w = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(w) : "memory");
+  } else if constexpr ((NT & 1) != 0) {
     const rn_u32x4 w = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(w, reinterpret_cast<rn_u32x4*>(p));
   } else {
@@ -809,13 +815,15 @@ template <typename T, bool RELU>
 void launch_apply(const rn_bn_desc* d, const void* x, void* y, const float* scale, const float* shift,
                   hipStream_t st) {
   Geo a = make_apply_geo<T>(d->m, d->c);
-  const int nt = g_tune[RN_TUNE_BN_NT] & 3;
+  const int nt = (g_tune[RN_TUNE_BN_NT] & 32) ? 4 | (g_tune[RN_TUNE_BN_NT] & 2) : g_tune[RN_TUNE_BN_NT] & 3;
 #define RN_APPLY(NT)                                                                                       \
   hipLaunchKernelGGL((bn_apply_kernel<T, RELU, NT>), dim3(a.gx, a.nrb), dim3(kThreads), 0, st, (const T*)x, \
                      (T*)y, scale, shift, d->m, d->c, a.ct, a.rows_per_block)
   if (nt == 1) RN_APPLY(1);
   else if (nt == 2) RN_APPLY(2);
   else if (nt == 3) RN_APPLY(3);
+  else if (nt == 4) RN_APPLY(4);
+  else if (nt == 6) RN_APPLY(6);
   else RN_APPLY(0);
 #undef RN_APPLY
 }
@@ -824,7 +832,7 @@ template <typename T, bool RELU>
 void launch_bwd_apply(const rn_bn_desc* d, const void* x, const void* dy, void* dx, const void* add,
                       const float* coef, const float* scale, const float* shift, hipStream_t st) {
   Geo a = make_apply_geo<T>(d->m, d->c);
-  const int nt = g_tune[RN_TUNE_BN_NT] & 3;
+  const int nt = (g_tune[RN_TUNE_BN_NT] & 32) ? 4 | (g_tune[RN_TUNE_BN_NT] & 2) : g_tune[RN_TUNE_BN_NT] & 3;
   if (RELU && d->dy2)
     hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true, true>), dim3(a.gx, a.nrb), dim3(kThreads), 0, st, (const T*)x,
                        (const T*)dy, (T*)dx, (const T*)add, coef, scale, shift, d->m, d->c, a.ct, a.rows_per_block,
@@ -837,6 +845,8 @@ void launch_bwd_apply(const rn_bn_desc* d, const void* x, const void* dy, void* 
     if (nt == 1) RN_BWD_APPLY(1);
     else if (nt == 2) RN_BWD_APPLY(2);
     else if (nt == 3) RN_BWD_APPLY(3);
+    else if (nt == 4) RN_BWD_APPLY(4);
+    else if (nt == 6) RN_BWD_APPLY(6);
     else RN_BWD_APPLY(0);
 #undef RN_BWD_APPLY
   }

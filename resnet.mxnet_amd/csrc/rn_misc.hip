@@ -809,7 +809,7 @@ __global__ void quant_state_multi_kernel(float* __restrict__ curmax, float* minm
 
 }  // namespace
 
-int g_tune[RN_TUNE_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512, 0, 0, 0, 0, 0, 0, 0, 23, 0, 0, 50, 0, 0, 0, 0, 0, 0};
+int g_tune[RN_TUNE_COUNT] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 512, 0, 0, 0, 0, 0, 0, 0, 55, 0, 0, 50, 0, 0, 0, 0, 0, 0};
 
 extern "C" {
 

@@ -145,7 +145,7 @@ BN_CASES = [(4, 64, 9, 9, False, True), (2, 24, 5, 7, True, False), (8, 256, 4, 
 def test_bn_streaming_hint_variants(gpu, dtype, relu):
     """rn_set_tuning 18 (nontemporal stores / loads in the BatchNorm passes) changes only the cache
     policy: rn_bn_fwd_train's y and rn_bn_bwd's reduction and dx (with the residual add) are
-    bit-identical for every mask value."""
+    bit-identical for every mask value (bit 32: the apply passes' write-through stores)."""
     n, c, h, w = 4, 200, 9, 13
     rng = np.random.default_rng(61)
     x = rng.standard_normal((n, c, h, w)) * 2 + 0.5
@@ -158,7 +158,7 @@ def test_bn_streaming_hint_variants(gpu, dtype, relu):
     ws = torch.zeros(L.load().rn_bn_workspace_bytes(C.byref(d)) // 4 + 16, dtype=torch.float32, device=gpu)
     outs = []
     try:
-        for mode in (0, 1, 2, 3, 6, 7):
+        for mode in (0, 1, 2, 3, 6, 7, 32, 34, 55):
             L.call("rn_set_tuning", 18, mode)
             g_d, b_d, mm, mv = f(gamma), f(beta), f(np.zeros(c)), f(np.ones(c))
             sm, si, sc, sh = [torch.zeros(c, dtype=torch.float32, device=gpu) for _ in range(4)]
@@ -171,7 +171,7 @@ def test_bn_streaming_hint_variants(gpu, dtype, relu):
             torch.cuda.synchronize()
             outs.append((yd.cpu(), dxd.cpu(), dg.cpu(), db.cpu()))
     finally:
-        L.call("rn_set_tuning", 18, 23)  # the default
+        L.call("rn_set_tuning", 18, 55)  # the default
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert torch.equal(a, b)
