@@ -407,6 +407,13 @@ typedef struct rn_pool_desc {
 int rn_pool_desc_init(rn_pool_desc* d);
 /* argmax: uint8 tap index per output element (max pool only; may be NULL for avg). */
 int rn_pool_fwd(const rn_pool_desc* d, const void* x, void* y, uint8_t* argmax, rn_stream_t stream);
+/* rn_pool_fwd over the output of the producing BatchNorm+ReLU (the stem's bn0 -> relu0 -> pool0 and the
+ * final bn1 -> relu1 -> global pool, symbol/resnet.py:94-97,111-113), applied while loading: x = the BN
+ * input, each element max(x * in_scale + in_shift, 0) rounded to the storage type as rn_bn_apply stores it,
+ * so y and argmax are bit-identical to rn_bn_apply followed by rn_pool_fwd, and the activation is never
+ * written or read back. */
+int rn_pool_fwd_x(const rn_pool_desc* d, const void* x, void* y, uint8_t* argmax, const float* in_scale,
+                  const float* in_shift, rn_stream_t stream);
 int rn_pool_bwd(const rn_pool_desc* d, const void* dy, const uint8_t* argmax, void* dx,
                 const void* add_src, rn_stream_t stream);
 /* rn_pool_bwd that also reduces the backward of the BatchNorm(+ReLU) whose output the pool read (the

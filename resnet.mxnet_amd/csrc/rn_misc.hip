@@ -36,10 +36,13 @@ struct PoolArgs {
 
 // forward: thread per (output pixel, chunk). Max: first maximal tap in (r, s) scan order,
 // which is the element MXNet's max-unpool gives the gradient to. Avg: count_include_pad
-// (divisor r*s), global pool divides by h*w.
-template <typename T>
+// (divisor r*s), global pool divides by h*w. XF: x is the input of the producing BatchNorm+ReLU, applied
+// per loaded element and rounded to T exactly as bn_apply_kernel stores it (max(x sc + sh, 0)), so the
+// pooled values and tap indices are bit-identical to pooling the stored activation, which is never written.
+template <typename T, bool XF = false>
 __global__ void pool_fwd_kernel(PoolArgs a, const T* __restrict__ x, T* __restrict__ y,
-                                uint8_t* __restrict__ argmax) {
+                                uint8_t* __restrict__ argmax, const float* __restrict__ in_sc = nullptr,
+                                const float* __restrict__ in_sh = nullptr) {
   constexpr int CE = 16 / sizeof(T);
   const int cpr = a.c / CE;
   const uint32_t total = (uint32_t)a.n * a.p * a.q * cpr;  // host-checked < 2^31
@@ -50,6 +53,18 @@ __global__ void pool_fwd_kernel(PoolArgs a, const T* __restrict__ x, T* __restri
     const int qq = (int)(pix - t * a.q);
     const uint32_t n = fdiv(t, a.fd_b);
     const int pp = (int)(t - n * a.p);
+    float xs[CE], xh[CE];
+    if constexpr (XF)
+#pragma unroll
+      for (int e = 0; e < CE; ++e) {
+        xs[e] = in_sc[cc * CE + e];
+        xh[e] = in_sh[cc * CE + e];
+      }
+    auto act = [&](float (&f)[CE]) __attribute__((always_inline)) {
+      if constexpr (XF)
+#pragma unroll
+        for (int e = 0; e < CE; ++e) f[e] = to_f(from_f<T>(fmaxf(fmaf(f[e], xs[e], xh[e]), 0.f)));
+    };
     float best[CE];
     int arg[CE];
 #pragma unroll
@@ -75,6 +90,7 @@ __global__ void pool_fwd_kernel(PoolArgs a, const T* __restrict__ x, T* __restri
       for (int t = 0; t < 9; ++t) {
         float f[CE];
         chunk_to_f(v[t], f, (const T*)nullptr);
+        act(f);
 #pragma unroll
         for (int e = 0; e < CE; ++e)
           if (ok[t] && f[e] > best[e]) {
@@ -92,6 +108,7 @@ __global__ void pool_fwd_kernel(PoolArgs a, const T* __restrict__ x, T* __restri
         float f[CE];
         chunk_to_f(*reinterpret_cast<const uint4*>(x + (((int64_t)n * a.h + hh) * a.w + ww) * a.c + cc * CE), f,
                    (const T*)nullptr);
+        act(f);
 #pragma unroll
         for (int e = 0; e < CE; ++e) {
           if (a.type == RN_POOL_MAX) {
@@ -855,7 +872,13 @@ int rn_pool_desc_init(rn_pool_desc* d) {
 }
 
 int rn_pool_fwd(const rn_pool_desc* d, const void* x, void* y, uint8_t* argmax, rn_stream_t stream) {
+  return rn_pool_fwd_x(d, x, y, argmax, nullptr, nullptr, stream);
+}
+
+int rn_pool_fwd_x(const rn_pool_desc* d, const void* x, void* y, uint8_t* argmax, const float* in_scale,
+                  const float* in_shift, rn_stream_t stream) {
   RN_CHECK_ARG(d && x && y, "null argument");
+  RN_CHECK_ARG((in_scale == nullptr) == (in_shift == nullptr), "in_scale / in_shift must both be set");
   PoolArgs a{d->n, d->h, d->w, d->c, d->r, d->s, d->stride_h, d->stride_w, d->pad_h, d->pad_w, d->p, d->q, d->type};
   a.fd_cpr = make_fastdiv(d->c / (d->dtype == RN_BF16 ? 8 : 4));
   a.fd_a = make_fastdiv(d->q);
@@ -863,12 +886,20 @@ int rn_pool_fwd(const rn_pool_desc* d, const void* x, void* y, uint8_t* argmax, 
   RN_CHECK_ARG((int64_t)d->n * d->h * d->w * d->c < INT32_MAX, "pooling tensor exceeds 2^31 elements");
   hipStream_t st = as_stream(stream);
   const int64_t total = (int64_t)d->n * d->p * d->q * d->c / 8;
-  if (d->dtype == RN_BF16)
-    hipLaunchKernelGGL(pool_fwd_kernel<bf16_t>, dim3(grid1d(total)), dim3(256), 0, st, a, (const bf16_t*)x,
-                       (bf16_t*)y, argmax);
-  else
+  if (d->dtype == RN_BF16) {
+    if (in_scale)
+      hipLaunchKernelGGL((pool_fwd_kernel<bf16_t, true>), dim3(grid1d(total)), dim3(256), 0, st, a, (const bf16_t*)x,
+                         (bf16_t*)y, argmax, in_scale, in_shift);
+    else
+      hipLaunchKernelGGL(pool_fwd_kernel<bf16_t>, dim3(grid1d(total)), dim3(256), 0, st, a, (const bf16_t*)x,
+                         (bf16_t*)y, argmax, nullptr, nullptr);
+  } else if (in_scale) {
+    hipLaunchKernelGGL((pool_fwd_kernel<float, true>), dim3(grid1d(total * 2)), dim3(256), 0, st, a, (const float*)x,
+                       (float*)y, argmax, in_scale, in_shift);
+  } else {
     hipLaunchKernelGGL(pool_fwd_kernel<float>, dim3(grid1d(total * 2)), dim3(256), 0, st, a, (const float*)x,
-                       (float*)y, argmax);
+                       (float*)y, argmax, nullptr, nullptr);
+  }
   return rn_check_launch("pool_fwd");
 }
 

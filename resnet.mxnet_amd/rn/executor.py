@@ -344,9 +344,10 @@ class Plan:
 
     def _fuse_bn_apply(self):
         """BatchNorm+ReLU whose output feeds ONLY 1x1 convolutions (act1 -> conv1 / sc, act3 -> conv3
-        of the pre-activation units, symbol/resnet.py:17-31): the convs stage max(x*sc+sh, 0) from
-        the BN input while loading (rn_conv_fwd_x / rn_conv_bwd_filter_x) and the BN+ReLU output is
-        never written or read back."""
+        of the pre-activation units, symbol/resnet.py:17-31) or poolings (relu0 -> pool0 of the stem and
+        relu1 -> the global pool, symbol/resnet.py:94-97,111-113): the consumers stage max(x*sc+sh, 0)
+        from the BN input while loading (rn_conv_fwd_x / rn_conv_bwd_filter_x / rn_pool_fwd_x) and the
+        BN+ReLU output is never written or read back."""
         for op in self.ops:
             op.xf = None
             if op.kind == "bn":
@@ -370,11 +371,14 @@ class Plan:
         # BN+ReLU-on-load forms, kernel-tested)
         def xf_ok(u):
             return u.groups == 1 and not getattr(u, "qweight", None) and tuple(u.kernel) == (1, 1)
+        # (the poolings: rn_pool_fwd_x; round 6, RN_POOL_XF=0 for the A/B)
+        pool_ok = os.environ.get("RN_POOL_XF", "1") == "1"
         for bn in self.ops:
             if bn.kind != "bn" or not bn.relu or id(bn.y) in out_ids:
                 continue
             users = refs.get(id(bn.y), [])
-            ok = users and all(u.kind == "conv" and key == "x" and xf_ok(u) for u, key in users)
+            ok = users and all(key == "x" and ((u.kind == "conv" and xf_ok(u)) or (u.kind == "pool" and pool_ok))
+                               for u, key in users)
             if not ok:
                 continue
             bn.apply_fused = True
@@ -1227,8 +1231,12 @@ class Executor:
                 op.desc = d
                 op.argmax = self.torch.zeros(max(y.rows * y.cp, 1), dtype=self.torch.uint8, device=self.device) \
                     if op.type == "max" else None
-                c = self._call("rn_pool_fwd", L.C.byref(d), self._p(self.act(x)), self._p(self.act(y)),
-                               self._p(op.argmax), sp)
+                if op.xf is not None:  # the producing BatchNorm+ReLU applied while loading
+                    c = self._call("rn_pool_fwd_x", L.C.byref(d), self._p(self.act(op.xf.x)), self._p(self.act(y)),
+                                   self._p(op.argmax), op.xf.sc, op.xf.sh, sp)
+                else:
+                    c = self._call("rn_pool_fwd", L.C.byref(d), self._p(self.act(x)), self._p(self.act(y)),
+                                   self._p(op.argmax), sp)
                 F.append(c)
                 I.append(c)
             elif op.kind == "fc":

@@ -134,6 +134,7 @@ SIGNATURES = {
     "rn_version": (_i32, []),
     "rn_build_id": (C.c_char_p, []),
     "rn_device_cu_count": (_i32, []),
+    "rn_pool_fwd_x": (_i32, [_P] * 7),
 }
 
 # include/rn.h's `#ifdef RN_DIAG` section: exported by the diagnostic build (librn_diag.so) only

@@ -278,6 +278,49 @@ def test_maxpool_and_gap(gpu, dtype):
 
 
 @pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("shape", [(3, 20, 11, 12), (2, 64, 56, 56), (4, 2048, 7, 7)])
+def test_pool_bnrelu_on_load(gpu, dtype, shape):
+    """rn_pool_fwd_x (the producing BatchNorm+ReLU applied to each loaded element: the stem's bn0 -> relu0
+    -> max pool and the final bn1 -> relu1 -> global pool, symbol/resnet.py:94-97,111-113) == rn_bn_apply
+    followed by rn_pool_fwd, BIT FOR BIT: the pooled values and the max pool's tap indices (many ReLU
+    zeros: the first-max rule on ties), padded channels included."""
+    n, c, h, w = shape
+    rng = np.random.default_rng(71)
+    x = rng.standard_normal((n, c, h, w)) * 1.5 + 0.2
+    cp = pad8(c)
+    sc = np.zeros(cp)
+    sh = np.zeros(cp)
+    sc[:c] = rng.uniform(0.3, 1.5, c) * np.where(rng.random(c) < 0.2, -1, 1)  # a few negative scales
+    sh[:c] = rng.standard_normal(c) * 0.5
+    f = lambda a: torch.tensor(a, dtype=torch.float32, device=gpu)
+    scd, shd = f(sc), f(sh)
+    xd = to_nhwc(x, dtype, gpu)
+    bd = L.BNDesc(dtype=dtype, m=n * h * w, c=cp, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1)
+    act = torch.zeros_like(xd)
+    L.call("rn_bn_apply", C.byref(bd), p(xd), p(act), p(scd), p(shd), stream())
+    for kind in ("max", "gap") if h * w <= 255 else ("max",):  # (the global pool's window: <= 255 taps)
+        if kind == "max":
+            d = L.PoolDesc(dtype=dtype, n=n, h=h, w=w, c=cp, r=3, s=3, stride_h=2, stride_w=2, pad_h=1, pad_w=1,
+                           type=L.RN_POOL_MAX, global_pool=0)
+        else:
+            d = L.PoolDesc(dtype=dtype, n=n, h=h, w=w, c=cp, type=L.RN_POOL_AVG, global_pool=1)
+        L.call("rn_pool_desc_init", C.byref(d))
+        y0 = torch.full((n, d.p, d.q, cp), float("nan"), dtype=tdt(dtype), device=gpu)
+        y1 = torch.full_like(y0, float("nan"))
+        a0 = torch.full((y0.numel(),), 255, dtype=torch.uint8, device=gpu)
+        a1 = torch.full_like(a0, 255)
+        am = (lambda t: p(t)) if kind == "max" else (lambda t: None)
+        L.call("rn_pool_fwd", C.byref(d), p(act), p(y0), am(a0), stream())
+        L.call("rn_pool_fwd_x", C.byref(d), p(xd), p(y1), am(a1), p(scd), p(shd), stream())
+        torch.cuda.synchronize()
+        iv = torch.int16 if dtype == BF16 else torch.int32
+        assert torch.equal(y0.view(iv), y1.view(iv)), kind
+        if kind == "max":
+            assert torch.equal(a0, a1)
+            assert (y1.float() == 0).any()  # ReLU zeros: ties in the windows
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
 def test_softmax_output(gpu, dtype):
     rng = np.random.default_rng(8)
     b, ncls, ld = 37, 1000, 1000

@@ -176,13 +176,20 @@ def test_plan_int8_quantization(monkeypatch):
 
 
 def test_plan_bn_apply_fusion_opt_in(monkeypatch):
-    """RN_BN_APPLY_FUSION=1: BN+ReLU outputs read only by 1x1 convs are applied on load."""
+    """RN_BN_APPLY_FUSION=1: BN+ReLU outputs read only by 1x1 convs or poolings are applied on load."""
     monkeypatch.setenv("RN_BN_APPLY_FUSION", "1")
     p = Plan(graphs.resnet50(), [("data", (2, 3, 224, 224))], [("softmax_label", (2,))])
     fused = [op for op in p.ops if op.kind == "bn" and op.apply_fused]
-    # bn1 of every unit (-> conv1, and sc in unit 1) and bn3 (-> conv3); not bn2 (3x3) / bn0 / bn1 final
-    assert len(fused) == 32
+    # bn1 of every unit (-> conv1, and sc in unit 1) and bn3 (-> conv3), bn0 (-> the stem's max pool) and
+    # the final bn1 (-> the global pool); not bn2 (3x3)
+    assert len(fused) == 34
     assert all(getattr(op, "xf", None) is not None for op in p.ops if op.kind == "conv" and op.kernel == (1, 1))
+    assert all(op.xf is not None and op.xf.apply_fused for op in p.ops if op.kind == "pool")
+    monkeypatch.setenv("RN_POOL_XF", "0")
+    p = Plan(graphs.resnet50(), [("data", (2, 3, 224, 224))], [("softmax_label", (2,))])
+    assert sum(1 for op in p.ops if op.kind == "bn" and op.apply_fused) == 32
+    assert all(op.xf is None for op in p.ops if op.kind == "pool")
+    monkeypatch.delenv("RN_POOL_XF")
     monkeypatch.setenv("RN_BN_APPLY_FUSION", "0")
     p = Plan(graphs.resnet50(), [("data", (2, 3, 224, 224))], [("softmax_label", (2,))])
     assert not any(op.apply_fused for op in p.ops if op.kind == "bn")
