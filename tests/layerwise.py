@@ -250,8 +250,8 @@ class Checker:
         return {"mismatch": float((dev != ref).double().mean()) if dev.numel() else 0.0}
 
     def conv_input(self, op):
-        """What the conv's kernel multiplies: its stored input, or relu(bn(x)) rounded to bf16 as the
-        BN+ReLU-on-load transform produces it."""
+        """What the conv's kernel multiplies (or the pooling reduces): its stored input, or relu(bn(x))
+        rounded to bf16 as the BN+ReLU-on-load transform produces it."""
         if op.xf is None:
             return self.act_nchw(op.x)
         return self.bn_relu_input(op.xf)
@@ -355,7 +355,7 @@ class Checker:
                         v = torch.relu(v)
                     self.add("bn_apply", op.name, self.act_nchw(op.y), v, bar)
             elif op.kind == "pool":
-                x = self.act_nchw(op.x)
+                x = self.conv_input(op)  # (rn_pool_fwd_x: relu(bn(x)) as the load transform rounds it)
                 if op.type == "max":
                     y = F.max_pool2d(x, op.kernel, op.stride, op.pad)
                 else:
