@@ -70,7 +70,7 @@ def conv_call_bytes(ex, name, args):
     return x + y + 2 * d.k * d.r * d.s * d.c_real * 4  # wgrad: fp32 dW read-modify-write (slabs not counted)
 
 
-PMC_ROUNDS = ("r05", "r04", "r03")  # newest first: the committed PMC summary of the latest round that has one
+PMC_ROUNDS = ("r06", "r05", "r04", "r03")  # newest first: the committed PMC summary of the latest round that has one
 
 
 def pmc_json_path(model="resnet50"):

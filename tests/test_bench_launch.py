@@ -134,7 +134,8 @@ def test_pmc_traffic_reads_the_committed_summary(tmp_path):
     import bench
     b, src = bench.pmc_traffic("igemm_big_kernel<224x256>")
     assert src is not None and src.startswith("profiles/")
-    assert 2.0e8 < b < 4.0e8, b  # ~275 MB per launch (r03)
+    # (~275 MB per launch in r03-r05; 185 MB in r06, whose streamed conv1 data gradients left the family)
+    assert 1.5e8 < b < 4.0e8, b
     flat = tmp_path / "flat.json"
     flat.write_text(json.dumps({"fam": {"launches": 3, "hbm_bytes": 123.0}}))
     assert bench.pmc_traffic("fam", str(flat))[0] == 123.0
