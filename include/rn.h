@@ -652,8 +652,10 @@ const char* rn_last_error(void);
  *      units' conv1) on the 224-row tiles (default 0: dgrad1x1_stream_kernel, which streams their rows with the
  *      weights in registers -- with the BN-backward reduction, and with the BN backward applied);
  *      27 = 2: that kernel with 32 channels per wave (default 64 where C % 256 == 0),
- * 26 = 1: the 3x3 / stride-1 / pad-1 64 -> 64 convolutions (forward, data gradient) on the implicit-GEMM
- *      tile (default 0: conv3x3c64_band_kernel, image bands and the nine taps' weights in LDS),
+ * 26 = 1: the 3x3 / stride-1 / pad-1 64 -> 64 convolutions (forward, data gradient) and the stem's 7x7 /
+ *      stride-2 64-channel forward (rn_stem_conv_fwd_p4) on the implicit-GEMM tile (default 0:
+ *      conv3x3c64_band_kernel and stem_band_kernel, image bands and the weights in LDS); 26 = 2: the stem
+ *      only on the tile,
  * 22 = 1: the BatchNorm-folded int8 quantizers (rn_quant_int8_fwd_codes_bn[2]) form every quotient
  *      v / unit by division (default 0: v * (1 / unit), the division only where that product lies
  *      within 2^-21 |v / unit| of a half-integer -- the same codes bit for bit, fewer instructions). */

@@ -4954,6 +4954,125 @@ int rn_conv_bwd_filter_i8(const rn_conv_desc* d, const void* x_codes, const floa
 
 // ---------------------------------------------------------------- stem over the padded NHWC4 image
 namespace {
+// The stem convolution (conv0: 7x7 / stride 2 over bn_data's output, symbol/resnet.py:90-93) over image
+// bands, as conv3x3c64_band_kernel does for stage 1's 3x3 layers. On the implicit-GEMM tile every output
+// row DMAs its 8 x 8 x 4 input patch on its own (a gather of 32 16-byte pieces per row, whose issue bounds
+// the launch: 198 us for a 411 MB output); here a band of 4 output rows takes its 14 input rows in one
+// contiguous DMA (the zero-bordered image needs no bounds), and every MFMA B fragment is one 16-byte LDS
+// read: k-step r (kernel row r, 32 k = taps s 0..7 x 4 channels), lane (q, c) supplies taps 2q, 2q + 1 of
+// output pixel c = input pixels 2 col + 2q, + 1, adjacent in the band row. The 64 x 256 weights stay in
+// LDS (rows XOR-swizzled by 16-byte chunk: the 16 lanes of a channel block read 16 distinct chunks). Seven
+// waves, wave w = 16-pixel blocks 4w..4w + 3 of the band's 4 Q <= 448 pixels, all 64 channels; operands
+// swapped so a lane's accumulator is 4 consecutive channels of one pixel (8-byte stores).
+struct StemBandArgs {
+  const void* x4;  // [N][hp][wp][4] bf16, zero-bordered
+  const void* w4;  // [64][8][8][4] bf16
+  void* y;         // [N][P][Q][64] bf16
+  int N, P, Q, hp, wp, pb, nbands, x_bytes, y_bytes;
+};
+constexpr int kStemInRows = 14;                  // 4 output rows at stride 2 + the 8-row kernel window - 2
+constexpr int kStemBandBytes = 26 * 1024;        // 26 whole 64-lane DMA instructions >= 14 rows x 232 px x 8 B
+__global__ __launch_bounds__(448, 1) void stem_band_kernel(StemBandArgs p) {
+  __shared__ __attribute__((aligned(16))) uint4 smem[(2 * kStemBandBytes + 64 * 512) / 16];  // 84 KB
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const v4i rs_x = make_rsrc(p.x4, (uint32_t)p.x_bytes);
+  const v4i rs_w = make_rsrc(p.w4, 64 * 512);
+  const __amdgpu_buffer_rsrc_t rs_y = __builtin_amdgcn_make_buffer_rsrc(p.y, (short)0, p.y_bytes, 0x00020000);
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  constexpr uint32_t kW = 2 * kStemBandBytes;
+  // the weights: 2048 chunks (channel o, phys chunk f) over waves 0-3, f holding logical chunk f ^ (o & 15)
+  if (wid < 4) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int ins = wid * 8 + j, chunk = ins * 64 + lane;
+      const int o = chunk >> 5, logical = (chunk & 31) ^ (o & 15);
+      dma16_asm(rs_w, lds0 + kW + ins * 1024, (uint32_t)((o * 256 + logical * 8) * 2));
+    }
+  }
+  // band b -> buffer bb: the 14 input rows from 2 p0 are one contiguous range of the image (26 pieces over
+  // waves 0-6); pieces past the image's last row read zeros
+  const uint32_t img_bytes = (uint32_t)p.hp * p.wp * 8;
+  auto issue_band = [&](int b, int bb) __attribute__((always_inline)) {
+    const int n = b / p.pb, p0 = (b - n * p.pb) * 4;
+    const uint32_t off0 = (uint32_t)(2 * p0) * p.wp * 8;
+    for (int ins = wid; ins < 26; ins += 7) {
+      const uint32_t off = off0 + (uint32_t)(ins * 64 + lane) * 16;
+      dma16_asm(rs_x, lds0 + bb * kStemBandBytes + ins * 1024, off < img_bytes ? (uint32_t)n * img_bytes + off : kOob);
+    }
+  };
+  // this lane's output pixels pp = (4 wid + i) 16 + c of the band = (orow, ocol); k-step r reads the band at
+  // byte ab[i] + r * wp * 8 (the 16 bytes of input pixels 2 ocol + 2q, + 1 of row 2 orow + r); channel block
+  // j's weights at wb[j] + chunk (4 r + q) ^ (o & 15)
+  const int q = lane >> 4, c = lane & 15;
+  int ab[4], orow[4], ocol[4], pp[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    pp[i] = (4 * wid + i) * 16 + c;
+    orow[i] = min(pp[i] / p.Q, 3);
+    ocol[i] = min(pp[i] - orow[i] * p.Q, p.Q - 1);
+    ab[i] = ((2 * orow[i]) * (p.wp >> 1) + ocol[i] + q) * 16;
+  }
+  int wb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) wb[j] = (int)kW + (16 * j + c) * 512;
+  const int rowb = p.wp * 8;
+  const char* lds = reinterpret_cast<const char*>(smem);
+  int it = 0;
+  int b = blockIdx.x;
+  if (b < p.nbands) issue_band(b, 0);
+  for (; b < p.nbands; b += gridDim.x, ++it) {
+    const int bb = it & 1;
+    if (it == 0) wait_vmcnt<0>();
+    else wait_vmcnt<16>();  // (the previous band's 16 stores may stay in flight)
+    __syncthreads();        // the band has landed for every wave; every wave is done with the other buffer
+    if (b + (int)gridDim.x < p.nbands) issue_band(b + gridDim.x, bb ^ 1);
+    v4f acc[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = v4f{0.f, 0.f, 0.f, 0.f};
+    const int boff = bb * kStemBandBytes;
+    uint4 fa[2][4], fb[2][4];
+    auto ld = [&](int r, int slot) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[slot][i] = *reinterpret_cast<const uint4*>(lds + boff + ab[i] + r * rowb);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[slot][j] = *reinterpret_cast<const uint4*>(lds + wb[j] + (((4 * r + q) ^ c) << 4));
+    };
+    ld(0, 0);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      if (r + 1 < 8) ld(r + 1, (r + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);  // (hipcc otherwise sinks every read next to its MFMA)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mfma_slab<bf16_t>(acc[i][j], fb[r & 1][j], fa[r & 1][i]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const int n = b / p.pb, p0 = (b - n * p.pb) * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int h = p0 + orow[i];
+      const bool ok = pp[i] < 4 * p.Q && h < p.P;
+      const int obase = (((n * p.P + h) * p.Q + ocol[i]) * 64 + 4 * q) * 2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t lo = (uint32_t)f2bf(acc[i][j][0]) | ((uint32_t)f2bf(acc[i][j][1]) << 16);
+        const uint32_t hi = (uint32_t)f2bf(acc[i][j][2]) | ((uint32_t)f2bf(acc[i][j][3]) << 16);
+        const uint32_t voff = ok ? (uint32_t)(obase + j * 32) : 0x80000000u;
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        __builtin_amdgcn_raw_buffer_store_b64(u32x2{lo, hi}, rs_y, voff, 0, 0);
+      }
+    }
+  }
+}
+// stem_band_kernel for this stem? (rn_set_tuning 26 = 1 or 2: the implicit-GEMM tile)
+bool stem_band_ok(const rn_conv_desc* d, int32_t hp, int32_t wp) {
+  return g_tune[RN_TUNE_CONV_BAND] == 0 && d->stride_h == 2 && d->stride_w == 2 && d->k == 64 && d->k_pad == 64 &&
+         wp % 2 == 0 && wp <= 232 && d->q <= 112 && (int64_t)d->n * d->p * d->q * 64 * 2 < INT32_MAX;
+}
+
 bool stem_p4_ok(const rn_conv_desc* d, int32_t hp, int32_t wp) {
   return d && d->dtype == RN_BF16 && d->groups == 1 && d->c_real <= 4 && d->k <= 64 && d->r <= 8 && d->s <= 8 &&
          hp >= (d->p - 1) * d->stride_h + 8 && wp >= (d->q - 1) * d->stride_w + 8 &&
@@ -4983,6 +5102,16 @@ int rn_stem_conv_fwd_p4(const rn_conv_desc* d, const void* x4, const void* w4, v
                         rn_stream_t stream) {
   RN_CHECK_ARG(x4 && w4 && y, "null argument");
   RN_CHECK_ARG(stem_p4_ok(d, hp, wp), "unsupported stem shape for the padded NHWC4 path");
+  if (stem_band_ok(d, hp, wp)) {
+    StemBandArgs s{};
+    s.x4 = x4; s.w4 = w4; s.y = y;
+    s.N = d->n; s.P = d->p; s.Q = d->q; s.hp = hp; s.wp = wp; s.pb = (d->p + 3) / 4; s.nbands = d->n * s.pb;
+    s.x_bytes = (int)((int64_t)d->n * hp * wp * 4 * 2);
+    s.y_bytes = (int)((int64_t)d->n * d->p * d->q * 64 * 2);
+    hipLaunchKernelGGL(stem_band_kernel, dim3((unsigned)std::min(s.nbands, chip_cus())), dim3(448), 0,
+                       as_stream(stream), s);
+    return rn_check_launch("stem_band");
+  }
   IgemmArgs a{};
   a.x = x4; a.w = w4; a.y = y;
   a.N = d->n; a.H = hp; a.W = wp; a.C = 4; a.P = d->p; a.Q = d->q; a.K = d->k; a.ldo = d->k_pad;

@@ -1169,6 +1169,43 @@ def test_stem_padded_nhwc4(gpu, mode, geom):
     assert rel_err(got, dw_ref) < 5e-3
 
 
+@pytest.mark.parametrize("geom", [(2, 224, 224), (3, 50, 38), (1, 31, 17)])
+def test_stem_band(gpu, geom):
+    """stem_band_kernel (the 7x7 / stride-2 stem over image bands in LDS: 14 input rows per 4 output rows,
+    the weights resident; rn_set_tuning 26 = 2: the implicit-GEMM tile) against the oracle and the tile:
+    the ResNet-50 stem at 224 (several bands per workgroup), a last band with fewer rows and 16-pixel
+    blocks across output rows (50 x 38 -> 25 x 19), a single ragged band."""
+    n, h, w = geom
+    c, k, r, st, pd = 3, 64, 7, 2, 3
+    rng = np.random.default_rng(29)
+    d = conv_desc(BF16, n, 8, h, w, k, r, r, st, pd, c_real=c)
+    hp = max(h + 2 * pd, (d.p - 1) * st + 8)
+    wp = max(w + 2 * pd, (d.q - 1) * st + 8)
+    hp, wp = hp + hp % 2, wp + wp % 2
+    img = np.zeros((n, hp, wp, 4), np.float32)
+    xin = bf16_round(rng.uniform(-2, 2, (n, c, h, w)))
+    img[:, pd:pd + h, pd:pd + w, :c] = xin.transpose(0, 2, 3, 1)
+    x4 = torch.tensor(img.reshape(-1), dtype=torch.bfloat16, device=gpu)
+    wt = bf16_round(rng.standard_normal((k, c, r, r)) * 0.1)
+    w4 = torch.zeros((k * 256,), dtype=torch.bfloat16, device=gpu)
+    L.call("rn_stem_weight_pack_p4", C.byref(d), p(_master_krsc(wt, gpu)), p(w4), stream())
+    outs = []
+    try:
+        for mode in (0, 2):
+            L.call("rn_set_tuning", 26, mode)
+            y = torch.full((n, d.p, d.q, d.k_pad), float("nan"), dtype=torch.bfloat16, device=gpu)
+            L.call("rn_stem_conv_fwd_p4", C.byref(d), p(x4), p(w4), p(y), hp, wp, stream())
+            torch.cuda.synchronize()
+            outs.append(y)
+    finally:
+        L.call("rn_set_tuning", 26, 0)
+    y_ref = ops.conv2d_fwd(xin.astype(np.float64), wt, (st, st), (pd, pd))
+    for y in outs:
+        assert not torch.isnan(y).any()
+        assert rel_err(from_nhwc(y, k), y_ref) < TOL[BF16]
+    assert rel_err(from_nhwc(outs[0], k), from_nhwc(outs[1], k)) < 1e-2
+
+
 @pytest.mark.parametrize("dtype", [F32, BF16])
 @pytest.mark.parametrize("case", [(2, 64, 14, 14, 128, 3, 1, 1), (2, 128, 14, 14, 256, 1, 2, 0),
                                   (3, 32, 13, 11, 48, 3, 2, 1), (3, 256, 20, 20, 128, 3, 2, 1),
