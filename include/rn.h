@@ -331,6 +331,14 @@ int32_t rn_stem_p4_supported(const rn_conv_desc* d, int32_t hp, int32_t wp);
 int rn_stem_weight_pack_p4(const rn_conv_desc* d, const float* w_master, void* w4, rn_stream_t stream);
 int rn_stem_conv_fwd_p4(const rn_conv_desc* d, const void* x4, const void* w4, void* y, int32_t hp, int32_t wp,
                         rn_stream_t stream);
+/* rn_stem_conv_fwd_p4 that also emits the statistics of y for the BatchNorm after the stem (bn0,
+ * symbol/resnet.py:94): part = float[rn_stem_bnstats_blocks(d, hp, wp)][3][64] (S1, S2, pivot per block, as
+ * rn_conv_fwd_bnstats), each block n*p*q / blocks rows, consumed by rn_bn_fwd_train_part with ld = 64.
+ * rn_stem_bnstats_blocks returns 0 where the band kernel cannot give every block the same rows (then the
+ * call is refused: run the statistics pass). */
+int rn_stem_conv_fwd_p4_bnstats(const rn_conv_desc* d, const void* x4, const void* w4, void* y, int32_t hp,
+                                int32_t wp, float* part, rn_stream_t stream);
+int64_t rn_stem_bnstats_blocks(const rn_conv_desc* d, int32_t hp, int32_t wp);
 int rn_stem_conv_wgrad_p4(const rn_conv_desc* d, const void* x4, const void* dy, float* dw, int32_t hp,
                           int32_t wp, rn_stream_t stream);
 

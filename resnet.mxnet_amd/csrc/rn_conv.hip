@@ -4968,12 +4968,16 @@ struct StemBandArgs {
   const void* x4;  // [N][hp][wp][4] bf16, zero-bordered
   const void* w4;  // [64][8][8][4] bf16
   void* y;         // [N][P][Q][64] bf16
+  float* part;     // (STATS) [workgroup][S1 | S2 | pivot][64]: bn0's statistics of the stored y, one block per
+                   // workgroup (its bands' rows, the same count for every workgroup), pivot = its first pixel
   int N, P, Q, hp, wp, pb, nbands, x_bytes, y_bytes;
 };
 constexpr int kStemInRows = 14;                  // 4 output rows at stride 2 + the 8-row kernel window - 2
 constexpr int kStemBandBytes = 26 * 1024;        // 26 whole 64-lane DMA instructions >= 14 rows x 232 px x 8 B
 __global__ __launch_bounds__(448, 1) void stem_band_kernel(StemBandArgs p) {
-  __shared__ __attribute__((aligned(16))) uint4 smem[(2 * kStemBandBytes + 64 * 512) / 16];  // 84 KB
+  const bool STATS = p.part != nullptr;  // (a runtime switch: this kernel has C linkage, no template)
+  // 84 KB: two band buffers, the weights; (STATS) the 7 waves' sums and the pivots
+  __shared__ __attribute__((aligned(16))) uint4 smem[(2 * kStemBandBytes + 64 * 512 + 7 * 64 * 8 + 64 * 4) / 16];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const v4i rs_x = make_rsrc(p.x4, (uint32_t)p.x_bytes);
   const v4i rs_w = make_rsrc(p.w4, 64 * 512);
@@ -5017,6 +5021,12 @@ __global__ __launch_bounds__(448, 1) void stem_band_kernel(StemBandArgs p) {
   for (int j = 0; j < 4; ++j) wb[j] = (int)kW + (16 * j + c) * 512;
   const int rowb = p.wp * 8;
   const char* lds = reinterpret_cast<const char*>(smem);
+  float* red = reinterpret_cast<float*>(reinterpret_cast<char*>(smem) + kW + 64 * 512);  // [wave][64][2]
+  float* piv = red + 7 * 64 * 2;                                                         // [64]
+  // (STATS) this lane's shifted sums of channels 16 j + 4 q + e (k = 4 j + e) over its valid pixels
+  float s1[16], s2[16], pv[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) s1[k] = s2[k] = pv[k] = 0.f;
   int it = 0;
   int b = blockIdx.x;
   if (b < p.nbands) issue_band(b, 0);
@@ -5051,6 +5061,18 @@ __global__ __launch_bounds__(448, 1) void stem_band_kernel(StemBandArgs p) {
       __builtin_amdgcn_sched_barrier(0);
     }
     const int n = b / p.pb, p0 = (b - n * p.pb) * 4;
+    if (STATS) {
+      if (it == 0) {  // the pivots: the stored values of the workgroup's first pixel (wave 0, block 0, lane c = 0)
+        if (wid == 0 && c == 0)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) piv[16 * j + 4 * q + e] = __uint_as_float((uint32_t)f2bf(acc[0][j][e]) << 16);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; ++k) pv[k] = piv[16 * (k >> 2) + 4 * q + (k & 3)];
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int h = p0 + orow[i];
@@ -5063,7 +5085,47 @@ __global__ __launch_bounds__(448, 1) void stem_band_kernel(StemBandArgs p) {
         const uint32_t voff = ok ? (uint32_t)(obase + j * 32) : 0x80000000u;
         typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
         __builtin_amdgcn_raw_buffer_store_b64(u32x2{lo, hi}, rs_y, voff, 0, 0);
+        if (STATS) {  // on the stored (rounded) values, as a statistics pass would read them
+          const uint32_t vw[4] = {lo << 16, lo & 0xFFFF0000u, hi << 16, hi & 0xFFFF0000u};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int k = 4 * j + e;
+            const float dv = ok ? __uint_as_float(vw[e]) - pv[k] : 0.f;
+            s1[k] += dv;
+            s2[k] = fmaf(dv, dv, s2[k]);
+          }
+        }
       }
+    }
+  }
+  if (STATS) {
+    // the 16 pixel lanes of each channel quad (xor 1, 2, 4, 8), then the 7 waves in order through LDS
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        s1[k] += __shfl_xor(s1[k], o, 64);
+        s2[k] += __shfl_xor(s2[k], o, 64);
+      }
+    if (c == 0)
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const int ch = 16 * (k >> 2) + 4 * q + (k & 3);
+        red[(wid * 64 + ch) * 2] = s1[k];
+        red[(wid * 64 + ch) * 2 + 1] = s2[k];
+      }
+    __syncthreads();
+    if (tid < 64) {
+      float a1 = red[tid * 2], a2 = red[tid * 2 + 1];
+#pragma unroll
+      for (int w = 1; w < 7; ++w) {
+        a1 += red[(w * 64 + tid) * 2];
+        a2 += red[(w * 64 + tid) * 2 + 1];
+      }
+      float* dst = p.part + (int64_t)blockIdx.x * 3 * 64 + tid;
+      dst[0] = a1;
+      dst[64] = a2;
+      dst[128] = piv[tid];
     }
   }
 }
@@ -5098,18 +5160,33 @@ int rn_stem_weight_pack_p4(const rn_conv_desc* d, const float* wm, void* w4, rn_
   return rn_check_launch("stem_weight_pack_p4");
 }
 
+int64_t rn_stem_bnstats_blocks(const rn_conv_desc* d, int32_t hp, int32_t wp) {
+  // the band kernel's workgroups when each takes the same number of whole bands (4 output rows each)
+  if (!d || !stem_p4_ok(d, hp, wp) || !stem_band_ok(d, hp, wp) || d->p % 4) return 0;
+  const int nb = d->n * (d->p / 4), g = chip_cus();
+  return nb <= g ? nb : (nb % g == 0 ? g : 0);
+}
+
 int rn_stem_conv_fwd_p4(const rn_conv_desc* d, const void* x4, const void* w4, void* y, int32_t hp, int32_t wp,
                         rn_stream_t stream) {
+  return rn_stem_conv_fwd_p4_bnstats(d, x4, w4, y, hp, wp, nullptr, stream);
+}
+
+int rn_stem_conv_fwd_p4_bnstats(const rn_conv_desc* d, const void* x4, const void* w4, void* y, int32_t hp,
+                                int32_t wp, float* part, rn_stream_t stream) {
   RN_CHECK_ARG(x4 && w4 && y, "null argument");
   RN_CHECK_ARG(stem_p4_ok(d, hp, wp), "unsupported stem shape for the padded NHWC4 path");
+  RN_CHECK_ARG(!part || rn_stem_bnstats_blocks(d, hp, wp) > 0,
+               "the stem's BatchNorm statistics need the band kernel with whole bands per workgroup "
+               "(rn_stem_bnstats_blocks)");
   if (stem_band_ok(d, hp, wp)) {
     StemBandArgs s{};
-    s.x4 = x4; s.w4 = w4; s.y = y;
+    s.x4 = x4; s.w4 = w4; s.y = y; s.part = part;
     s.N = d->n; s.P = d->p; s.Q = d->q; s.hp = hp; s.wp = wp; s.pb = (d->p + 3) / 4; s.nbands = d->n * s.pb;
     s.x_bytes = (int)((int64_t)d->n * hp * wp * 4 * 2);
     s.y_bytes = (int)((int64_t)d->n * d->p * d->q * 64 * 2);
-    hipLaunchKernelGGL(stem_band_kernel, dim3((unsigned)std::min(s.nbands, chip_cus())), dim3(448), 0,
-                       as_stream(stream), s);
+    const dim3 grid((unsigned)std::min(s.nbands, chip_cus()));
+    hipLaunchKernelGGL(stem_band_kernel, grid, dim3(448), 0, as_stream(stream), s);
     return rn_check_launch("stem_band");
   }
   IgemmArgs a{};

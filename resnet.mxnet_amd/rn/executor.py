@@ -979,6 +979,12 @@ class Executor:
                             (stats_mode == "2" or self._big_tile(src, 0) or self._grouped_fuse(src, 0)):
                         src.bnstats = True
                         op.part_src = src
+                    elif src is not None and src.kind == "stem" and src.y.cp == op.x.cp and \
+                            os.environ.get("RN_STEM_BN_STATS", "1") == "1":
+                        # (bn0's statistics from the stem band kernel: kept only where the stem runs it with
+                        # whole bands per workgroup, rn_stem_bnstats_blocks; decided when the stem is built)
+                        src.bnstats = True
+                        op.part_src = src
         for op in plan.ops:
             if op.kind == "bn":
                 d = L.BNDesc(dtype=self.dtype, m=op.x.rows, c=op.x.cp, c_real=op.x.c, eps=op.eps,
@@ -1085,11 +1091,24 @@ class Executor:
                         lst.append(self._call("rn_quant_int8_fwd", self.dtype, x.n * x.h * x.w * 8, self._p(op.x8),
                                               self._p(op.x8), self._ap(q["minmax"]), 0, tr, q["ema"], self._qfirst,
                                               q["nbits"], qwsp, sp))
+                nblk = int(self.lib.rn_stem_bnstats_blocks(L.C.byref(dfull), *op.p4)) if (op.p4 and op.bnstats) else 0
+                if op.bnstats and nblk <= 0:  # the BatchNorm runs its own statistics pass
+                    op.bnstats = False
+                    for o in plan.ops:
+                        if getattr(o, "part_src", None) is op:
+                            o.part_src = None
                 if op.p4:
                     c_ = self._call("rn_stem_conv_fwd_p4", L.C.byref(dfull), self._p(op.x8), self._p(op.wk),
                                     self._p(self.act(y)), op.p4[0], op.p4[1], sp)
                     I.append(c_)
-                    F.append(c_)
+                    if op.bnstats:  # + bn0's statistics of the stored output, one block per band workgroup
+                        op.part_blocks, op.part_rows = nblk, y.rows // nblk
+                        op.part = self._zeros(nblk * 3 * y.cp, self.torch.float32)
+                        F.append(self._call("rn_stem_conv_fwd_p4_bnstats", L.C.byref(dfull), self._p(op.x8),
+                                            self._p(op.wk), self._p(self.act(y)), op.p4[0], op.p4[1],
+                                            self._p(op.part), sp))
+                    else:
+                        F.append(c_)
                 else:
                     I.append(self._call("rn_conv_fwd", L.C.byref(dfull), self._p(op.x8), self._p(op.wk),
                                         self._p(self.act(y)), self.dtype, None, None, sp))

@@ -135,6 +135,8 @@ SIGNATURES = {
     "rn_build_id": (C.c_char_p, []),
     "rn_device_cu_count": (_i32, []),
     "rn_pool_fwd_x": (_i32, [_P] * 7),
+    "rn_stem_conv_fwd_p4_bnstats": (_i32, [_P, _P, _P, _P, _i32, _i32, _P, _P]),
+    "rn_stem_bnstats_blocks": (_i64, [_P, _i32, _i32]),
 }
 
 # include/rn.h's `#ifdef RN_DIAG` section: exported by the diagnostic build (librn_diag.so) only

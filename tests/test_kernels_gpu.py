@@ -1204,6 +1204,32 @@ def test_stem_band(gpu, geom):
         assert not torch.isnan(y).any()
         assert rel_err(from_nhwc(y, k), y_ref) < TOL[BF16]
     assert rel_err(from_nhwc(outs[0], k), from_nhwc(outs[1], k)) < 1e-2
+    # bn0's statistics from the band kernel's epilogue (rn_stem_conv_fwd_p4_bnstats; whole bands per workgroup)
+    lib = L.load()
+    nblk = lib.rn_stem_bnstats_blocks(C.byref(d), hp, wp)
+    assert (nblk > 0) == (d.p % 4 == 0)
+    if nblk <= 0:
+        assert lib.rn_stem_conv_fwd_p4_bnstats(C.byref(d), p(x4), p(w4), p(outs[0]), hp, wp, p(outs[0]), stream()) != 0
+        return
+    m = n * d.p * d.q
+    part = torch.full((nblk * 3 * 64,), float("nan"), dtype=torch.float32, device=gpu)
+    ys = torch.full_like(outs[0], float("nan"))
+    L.call("rn_stem_conv_fwd_p4_bnstats", C.byref(d), p(x4), p(w4), p(ys), hp, wp, p(part), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(ys.view(torch.int16), outs[0].view(torch.int16))  # the same stored output
+    gamma, beta = rng.uniform(0.5, 1.5, k), rng.standard_normal(k) * 0.1
+    f = lambda a: torch.tensor(np.asarray(a, np.float64), dtype=torch.float32, device=gpu)
+    g_d, b_d, mm, mv = f(gamma), f(beta), f(np.zeros(k)), f(np.ones(k))
+    sm, si, sc, sh = [torch.zeros(k, dtype=torch.float32, device=gpu) for _ in range(4)]
+    bd = L.BNDesc(dtype=BF16, m=m, c=k, c_real=k, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1)
+    ws = torch.zeros(lib.rn_bn_workspace_bytes(C.byref(bd)) // 4 + 16, dtype=torch.float32, device=gpu)
+    L.call("rn_bn_fwd_train_part", C.byref(bd), p(part), nblk, m // nblk, 64, p(ys), None, p(g_d), p(b_d), p(mm),
+           p(mv), p(sm), p(si), p(sc), p(sh), p(ws), stream())
+    torch.cuda.synchronize()
+    yv = ys.double().view(-1, 64)
+    mean, var = yv.mean(0), yv.var(0, unbiased=False)
+    assert rel_err(sm.cpu().numpy(), mean.cpu().numpy()) < 1e-5
+    assert rel_err((1.0 / si.double() ** 2 - 1e-5).cpu().numpy(), var.cpu().numpy()) < 1e-4
 
 
 @pytest.mark.parametrize("dtype", [F32, BF16])
