@@ -632,7 +632,9 @@ const char* rn_last_error(void);
  *      measured slower: C5 24.1 -> 25.1 ms per step), 16 = the 224/256-row conv tiles' output stores
  *      (rn_conv_fwd* / rn_conv_bwd_data*), 32 = the apply passes' stores write-through (sc1) instead of
  *      bit 1's hint (no dirty lines left in the XCD L2s; round 6, four pairs on one box: C2 18.85 ->
- *      18.82, 18.91 -> 18.86, 18.88 -> 18.82, 18.89 -> 18.85 ms; C4 26.75 -> 26.60, C5 21.21 -> 21.11).
+ *      18.82, 18.91 -> 18.86, 18.88 -> 18.82, 18.89 -> 18.85 ms; C4 26.75 -> 26.60, C5 21.21 -> 21.11),
+ *      64 = the int8 quantizer pass's stores (codes, fake-quantized copy) write-through (measured
+ *      slower, four pairs on one box: C5 21.16 -> 21.26, 21.14 -> 21.26, 21.21 -> 21.26, 21.12 -> 21.25 ms).
  *      Default 55. The same bits either way: only the cache policy changes,
  * 19 = the slice-resident weight gradients (rn_conv_bwd_filter[_ws / _x]; a workgroup keeps its dW
  *      slice for all of its images in registers, so dy and x are read once per slice; they need the

@@ -646,7 +646,8 @@ struct BnqTargets {
   float* unit[2];
   float qmax[2];
 };
-template <typename T, bool RELU, int NQ, bool NT = false>
+// NT: 1 = rn_set_tuning 18 bit 8's streaming hints, 4 = bit 64's write-through (sc1) stores
+template <typename T, bool RELU, int NQ, int NT = 0>
 __global__ __launch_bounds__(256) void bnq_codes_kernel(const T* __restrict__ x, const float* __restrict__ scale,
                                                         const float* __restrict__ shift, int64_t m, int c, int ct,
                                                         int64_t rows_per_block, BnqTargets tg,
@@ -675,7 +676,7 @@ __global__ __launch_bounds__(256) void bnq_codes_kernel(const T* __restrict__ x,
   for (int k = 0; k < NQ; ++k) inv[k] = unit[k] > 0.f ? 1.f / unit[k] : 0.f;
   for (int64_t r = r0 + tr; r < r1; r += rl) {
     float f[16];
-    bnq_load<T, RELU, NT>(x + r * c + cb, sc, sh, f);
+    bnq_load<T, RELU, (NT & 1) != 0>(x + r * c + cb, sc, sh, f);
     const int64_t off = r * c + cb;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
@@ -727,14 +728,25 @@ __global__ __launch_bounds__(256) void bnq_codes_kernel(const T* __restrict__ x,
 #pragma unroll
         for (int h = 0; h < 16 / CE; ++h) {
           const uint4 o = f_to_chunk(g + h * CE, (const T*)nullptr);
-          if constexpr (NT) {  // the fake-quantized copy is read only by the weight gradients, later
+          if constexpr ((NT & 4) != 0) {  // write-through: no dirty line left in the XCD L2 (as rn_bn.hip's st16)
+            const bnq_u32x4 w = {o.x, o.y, o.z, o.w};
+            asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(
+                             reinterpret_cast<bnq_u32x4*>(reinterpret_cast<T*>(tg.out[k]) + off) + h),
+                         "v"(w)
+                         : "memory");
+          } else if constexpr ((NT & 1) != 0) {  // the fake-quantized copy is read only by the weight gradients, later
             const bnq_u32x4 w = {o.x, o.y, o.z, o.w};
             __builtin_nontemporal_store(w, reinterpret_cast<bnq_u32x4*>(reinterpret_cast<T*>(tg.out[k]) + off) + h);
           } else {
             reinterpret_cast<uint4*>(reinterpret_cast<T*>(tg.out[k]) + off)[h] = o;
           }
         }
-      reinterpret_cast<uint4*>(tg.codes[k] + off)[0] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+      if constexpr ((NT & 4) != 0) {
+        const bnq_u32x4 w = {cw[0], cw[1], cw[2], cw[3]};
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(tg.codes[k] + off), "v"(w) : "memory");
+      } else {
+        reinterpret_cast<uint4*>(tg.codes[k] + off)[0] = make_uint4(cw[0], cw[1], cw[2], cw[3]);
+      }
     }
   }
 }
@@ -1371,8 +1383,11 @@ static void launch_quant_codes_bn(const rn_bn_desc* d, const void* x, const floa
   hipLaunchKernelGGL(quant_state_multi_kernel, dim3(1), dim3(1), 0, st, curmax, minmax[0], minmax[NQ - 1], NQ,
                      is_train, decay[0], decay[NQ - 1], first_batch, thr);
   const auto g = geo(8);
-  if (g_tune[RN_TUNE_BN_NT] & 8)
-    hipLaunchKernelGGL((bnq_codes_kernel<T, RELU, NQ, true>), dim3(gx, g.first), dim3(256), 0, st, (const T*)x, scale,
+  if (g_tune[RN_TUNE_BN_NT] & 64)
+    hipLaunchKernelGGL((bnq_codes_kernel<T, RELU, NQ, 4>), dim3(gx, g.first), dim3(256), 0, st, (const T*)x, scale,
+                       shift, d->m, d->c, ct, g.second, tg, thr, g_tune[RN_TUNE_QUANT_DIV] == 1 ? 1 : 0);
+  else if (g_tune[RN_TUNE_BN_NT] & 8)
+    hipLaunchKernelGGL((bnq_codes_kernel<T, RELU, NQ, 1>), dim3(gx, g.first), dim3(256), 0, st, (const T*)x, scale,
                        shift, d->m, d->c, ct, g.second, tg, thr, g_tune[RN_TUNE_QUANT_DIV] == 1 ? 1 : 0);
   else
     hipLaunchKernelGGL((bnq_codes_kernel<T, RELU, NQ>), dim3(gx, g.first), dim3(256), 0, st, (const T*)x, scale,
