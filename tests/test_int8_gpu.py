@@ -209,6 +209,37 @@ def test_quant_codes_bn_fused(gpu, dtype, relu, m, c):
 
 
 @pytest.mark.parametrize("dtype", [F32, BF16])
+@pytest.mark.parametrize("mode", [63, 119])
+def test_quant_codes_bn_store_hints(gpu, dtype, mode):
+    """rn_set_tuning 18 bit 8 (streaming hints) and bit 64 (write-through stores) change only the cache
+    policy of rn_quant_int8_fwd_codes_bn: values, codes and unit equal the default (55) bit for bit."""
+    m, c = 1001, 48
+    rng = np.random.default_rng(11)
+    x = torch.tensor(rng.standard_normal((m, c)) * 3.0, dtype=tdt(dtype), device=gpu)
+    sc = torch.tensor(rng.standard_normal(c) * 0.7, dtype=torch.float32, device=gpu)
+    sh = torch.tensor(rng.standard_normal(c) * 0.5, dtype=torch.float32, device=gpu)
+    d = L.BNDesc(dtype=dtype, m=m, c=c, c_real=c, eps=1e-5, momentum=0.9, fix_gamma=0, relu=1)
+    ws = torch.zeros(4096, dtype=torch.float32, device=gpu)
+    outs = []
+    try:
+        for md in (55, mode):
+            L.call("rn_set_tuning", 18, md)
+            out = torch.full_like(x, float("nan"))
+            codes = torch.zeros(m * c, dtype=torch.int8, device=gpu)
+            unit = torch.zeros(1, dtype=torch.float32, device=gpu)
+            mm = torch.tensor([2.5], dtype=torch.float32, device=gpu)
+            L.call("rn_quant_int8_fwd_codes_bn", C.byref(d), p(x), p(sc), p(sh), p(out), p(codes), p(unit), p(mm),
+                   1, 0.99, 0, 8, p(ws), stream())
+            torch.cuda.synchronize()
+            outs.append((out, codes, unit, mm))
+    finally:
+        L.call("rn_set_tuning", 18, 55)  # the default
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert not torch.isnan(outs[1][0].float()).any()
+
+
+@pytest.mark.parametrize("dtype", [F32, BF16])
 def test_quant_codes_bn_ties(gpu, dtype):
     """The fused quantizer forms the quotient v / unit as v * (1 / unit) and takes the exact division
     only near a half-integer: with unit = 2^-6 (threshold 127 * 2^-6, inference mode) every input
